@@ -1,0 +1,72 @@
+// Leveled logger, stall detector and scoped trace for the host runtime.
+//
+// Parity: srcs/go/log/logger.go:14-150 (levels from KUNGFU_CONFIG_LOG_LEVEL,
+// prefixes [D]/[I]/[W]/[E]/[F]); srcs/go/utils/stalldetector.go:9-46 (prints
+// "<name> stalled for <t>" every 3 s); srcs/cpp/include/kungfu/utils/trace.hpp
+// (TRACE_SCOPE; here it is always compiled and enabled by KUNGFU_CONFIG_ENABLE_TRACE,
+// printing per-scope count/total/mean at exit).
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdarg>
+#include <mutex>
+#include <string>
+#include <thread>
+
+namespace kungfu {
+
+enum class LogLevel : int { DEBUG = 0, INFO = 1, WARN = 2, ERROR = 3 };
+
+LogLevel log_level();
+void set_log_level(LogLevel l);
+void logf(LogLevel l, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+[[noreturn]] void fatalf(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define KF_DEBUG(...) ::kungfu::logf(::kungfu::LogLevel::DEBUG, __VA_ARGS__)
+#define KF_INFO(...) ::kungfu::logf(::kungfu::LogLevel::INFO, __VA_ARGS__)
+#define KF_WARN(...) ::kungfu::logf(::kungfu::LogLevel::WARN, __VA_ARGS__)
+#define KF_ERROR(...) ::kungfu::logf(::kungfu::LogLevel::ERROR, __VA_ARGS__)
+
+// Environment helpers shared by the runtime.
+std::string env_str(const char *key, const std::string &def = "");
+bool env_bool(const char *key, bool def = false);
+double env_duration_sec(const char *key, double def);  // "5m", "1s", "200ms", "3"
+
+bool stall_detection_enabled();
+
+// Prints "<name> stalled for <t>s" every `period` until destroyed.
+class StallDetector {
+  public:
+    explicit StallDetector(std::string name, double period_sec = 3.0);
+    ~StallDetector();
+
+  private:
+    std::string name_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool done_ = false;
+    std::thread th_;
+};
+
+// Scoped timer aggregated per name; report printed at process exit when
+// KUNGFU_CONFIG_ENABLE_TRACE is set.
+class TraceScope {
+  public:
+    explicit TraceScope(const char *name);
+    ~TraceScope();
+
+  private:
+    const char *name_;
+    std::chrono::steady_clock::time_point t0_;
+};
+
+bool trace_enabled();
+std::string trace_report();
+
+#define KF_TRACE_CAT2(a, b) a##b
+#define KF_TRACE_CAT(a, b) KF_TRACE_CAT2(a, b)
+#define KF_TRACE_SCOPE(name) ::kungfu::TraceScope KF_TRACE_CAT(_kf_trace_, __LINE__)(name)
+
+}  // namespace kungfu

@@ -1,0 +1,172 @@
+#include <kungfu/log.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <sstream>
+
+namespace kungfu {
+
+namespace {
+
+LogLevel parse_level(const std::string &s) {
+    if (s == "DEBUG" || s == "debug") return LogLevel::DEBUG;
+    if (s == "WARN" || s == "warn") return LogLevel::WARN;
+    if (s == "ERROR" || s == "error") return LogLevel::ERROR;
+    return LogLevel::INFO;
+}
+
+std::atomic<int> &level_ref() {
+    static std::atomic<int> lvl{static_cast<int>(parse_level(env_str("KUNGFU_CONFIG_LOG_LEVEL", "INFO")))};
+    return lvl;
+}
+
+const char *prefix(LogLevel l) {
+    switch (l) {
+    case LogLevel::DEBUG: return "[D]";
+    case LogLevel::INFO: return "[I]";
+    case LogLevel::WARN: return "[W]";
+    case LogLevel::ERROR: return "[E]";
+    }
+    return "[?]";
+}
+
+struct TraceStat {
+    uint64_t count = 0;
+    double total = 0;
+};
+
+std::mutex &trace_mu() {
+    static std::mutex m;
+    return m;
+}
+
+std::map<std::string, TraceStat> &trace_stats() {
+    static std::map<std::string, TraceStat> s;
+    return s;
+}
+
+struct TraceReporter {
+    ~TraceReporter() {
+        if (trace_enabled()) {
+            auto r = trace_report();
+            if (!r.empty()) std::fprintf(stderr, "%s", r.c_str());
+        }
+    }
+} g_trace_reporter;
+
+}  // namespace
+
+std::string env_str(const char *key, const std::string &def) {
+    const char *v = std::getenv(key);
+    return v ? std::string(v) : def;
+}
+
+bool env_bool(const char *key, bool def) {
+    const char *v = std::getenv(key);
+    if (!v) return def;
+    std::string s(v);
+    return s == "1" || s == "true" || s == "TRUE" || s == "True" || s == "yes" || s == "on";
+}
+
+double env_duration_sec(const char *key, double def) {
+    const char *v = std::getenv(key);
+    if (!v || !*v) return def;
+    std::string s(v);
+    try {
+        size_t pos = 0;
+        double x = std::stod(s, &pos);
+        std::string unit = s.substr(pos);
+        if (unit.empty() || unit == "s") return x;
+        if (unit == "ms") return x / 1000.0;
+        if (unit == "us") return x / 1e6;
+        if (unit == "m") return x * 60.0;
+        if (unit == "h") return x * 3600.0;
+    } catch (...) {
+    }
+    return def;
+}
+
+LogLevel log_level() { return static_cast<LogLevel>(level_ref().load()); }
+void set_log_level(LogLevel l) { level_ref().store(static_cast<int>(l)); }
+
+void logf(LogLevel l, const char *fmt, ...) {
+    if (static_cast<int>(l) < level_ref().load()) return;
+    char buf[4096];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    std::fprintf(stderr, "%s %s\n", prefix(l), buf);
+}
+
+void fatalf(const char *fmt, ...) {
+    char buf[4096];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    std::fprintf(stderr, "[F] %s\n", buf);
+    std::fflush(stderr);
+    std::abort();
+}
+
+bool stall_detection_enabled() {
+    static bool on = env_bool("KUNGFU_CONFIG_ENABLE_STALL_DETECTION", false);
+    return on;
+}
+
+StallDetector::StallDetector(std::string name, double period_sec) : name_(std::move(name)) {
+    if (!stall_detection_enabled()) return;
+    th_ = std::thread([this, period_sec] {
+        auto t0 = std::chrono::steady_clock::now();
+        std::unique_lock<std::mutex> lk(mu_);
+        while (!cv_.wait_for(lk, std::chrono::duration<double>(period_sec), [this] { return done_; })) {
+            double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            std::fprintf(stderr, "[W] %s stalled for %.1fs\n", name_.c_str(), dt);
+        }
+    });
+}
+
+StallDetector::~StallDetector() {
+    if (!th_.joinable()) return;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+}
+
+bool trace_enabled() {
+    static bool on = env_bool("KUNGFU_CONFIG_ENABLE_TRACE", false);
+    return on;
+}
+
+TraceScope::TraceScope(const char *name) : name_(name) {
+    if (trace_enabled()) t0_ = std::chrono::steady_clock::now();
+}
+
+TraceScope::~TraceScope() {
+    if (!trace_enabled()) return;
+    double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
+    std::lock_guard<std::mutex> lk(trace_mu());
+    auto &s = trace_stats()[name_];
+    s.count++;
+    s.total += dt;
+}
+
+std::string trace_report() {
+    std::lock_guard<std::mutex> lk(trace_mu());
+    std::ostringstream os;
+    for (auto &kv : trace_stats()) {
+        char buf[512];
+        std::snprintf(buf, sizeof(buf), "[trace] %-40s count=%llu total=%.6fs mean=%.3fms\n", kv.first.c_str(),
+                      static_cast<unsigned long long>(kv.second.count), kv.second.total,
+                      kv.second.count ? 1e3 * kv.second.total / kv.second.count : 0.0);
+        os << buf;
+    }
+    return os.str();
+}
+
+}  // namespace kungfu
