@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 SynchronousSGD training throughput on MI355X.
+
+Metric (BASELINE.json): images/sec ResNet-50 SynchronousSGD at 1/2/4/8 MI355X.
+The reference's comparable number is ~344 img/s/GPU (KungFu S-SGD, 256 images
+per GPU, 16 x V100); ``vs_baseline`` = value / (344.2 * n_gpus).
+
+Config: ResNet-50 (v1.5, 25.56 M params, random init), synthetic ImageNet-shaped
+data (224x224x3, 1000 classes), 256 images per GPU (weak scaling), bf16 autocast
+compute with f32 master weights, channels_last, SGD momentum 0.9 + wd 1e-4 via
+``kungfu_amd.optimizers.SynchronousSGDOptimizer`` (bucketed RCCL all-reduce
+overlapped with backward, fused HIP SGD step), one process per GPU.
+
+Usage:
+    python bench.py [--gpus 1] [--steps 20] [--warmup 5]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_PER_GPU = 5507.0 / 16  # KungFu S-SGD ResNet-50, global batch 4096 on 16 x V100
+METRIC = "images/sec/GPU ResNet-50 SynchronousSGD at 1/2/4/8 MI355X; scaling efficiency"
+
+
+def _setup_env():
+    # MIOpen tuning database shipped in-tree (find results for these shapes),
+    # so a fresh box skips the multi-minute exhaustive search.
+    tdir = os.path.join(ROOT, "kungfu_amd", "tuning", "miopen")
+    os.environ.setdefault("MIOPEN_USER_DB_PATH", tdir)
+    os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", tdir)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=8)
+    p.add_argument("--batch", type=int, default=256, help="images per GPU")
+    p.add_argument("--model", default="resnet50")
+    p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada"])
+    p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
+    p.add_argument("--bucket-mb", type=float, default=None)
+    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--json-out", default=None)
+    a = p.parse_args()
+    _setup_env()
+
+    import torch
+    import torch.nn.functional as F
+
+    import kungfu_amd as kf
+    from kungfu_amd.models import get_model
+
+    kf.init()
+    rank, size = kf.current_rank(), kf.current_cluster_size()
+    dev_idx = kf.get_hip_index()
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    torch.backends.cudnn.benchmark = False  # MIOpen immediate mode + in-tree find-db
+    torch.manual_seed(1234)
+
+    fused_bn = a.fused_bn
+    if fused_bn < 0:
+        from kungfu_amd.ops import fused_bn as fb
+
+        fused_bn = 1 if fb.available() else 0
+    model = get_model(a.model, fused_bn=bool(fused_bn)) if a.model.startswith("resnet") else get_model(a.model)
+    model = model.to(dev).to(memory_format=torch.channels_last)
+    base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+    if a.optimizer == "ssgd":
+        opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),
+                                                    bucket_mb=a.bucket_mb)
+    elif a.optimizer == "sma":
+        opt = kf.optimizers.SynchronousAveragingOptimizer(base, named_parameters=model.named_parameters())
+    elif a.optimizer == "pair":
+        opt = kf.optimizers.PairAveragingOptimizer(base, named_parameters=model.named_parameters())
+    else:
+        opt = kf.optimizers.AdaptiveSGDOptimizer(base, named_parameters=model.named_parameters(), change_step=10)
+    kf.broadcast_parameters(model.state_dict())
+
+    x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (a.batch,), device=dev)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    t_w0 = time.time()
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    warm_s = time.time() - t_w0
+
+    kf.run_barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    kf.run_barrier()
+    dt = time.perf_counter() - t0
+    # max over ranks
+    dt_t = torch.tensor([dt], dtype=torch.float64)
+    dt_max = float(kf.ops.all_reduce(dt_t, op="max")[0]) if size > 1 else dt
+    value = a.batch * size * a.steps / dt_max
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "images/sec (aggregate over n_gpus)",
+        "n_gpus": size,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(1000 * dt_max / a.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / (BASELINE_PER_GPU * size), 3),
+        "dtype": "bf16",
+        "data": "synthetic (random 224x224x3 images, random labels; random-init weights)",
+        "config": {
+            "model": a.model,
+            "global_batch": a.batch * size,
+            "per_gpu_batch": a.batch,
+            "seq_len": None,
+            "image_size": 224,
+            "parallelism": "dp%d" % size,
+            "optimizer": "%s(SGD momentum=0.9 wd=1e-4)" % a.optimizer,
+            "fused_bn_hip": bool(fused_bn),
+            "per_gpu_img_s": round(value / size, 2),
+            "baseline_per_gpu_img_s": round(BASELINE_PER_GPU, 1),
+            "warmup_s": round(warm_s, 1),
+            "final_loss": round(float(loss), 4),
+        },
+    }
+    if rank == 0:
+        line = json.dumps(res)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    kf.finalize()
+
+
+if __name__ == "__main__":
+    main()

@@ -138,6 +138,11 @@ Graph gen_star_bcast(int k, int r);
 void gen_circular_pair(int k, int r, Graph *reduce, Graph *bcast);
 // reverse(bcast) + self-loops on every node.
 Graph gen_default_reduce(const Graph &bcast);
+// Minimum spanning tree (Prim) over an n x n weight matrix (row-major), which
+// is symmetrised as w'[i][j] = w[i][j] + w[j][i].  Returns a father array
+// rooted at `root` (f[root] == root).  Parity: srcs/cpp/include/kungfu/mst.hpp:9-58.
+std::vector<int> minimum_spanning_tree(const std::vector<double> &w, int n, int root = 0);
+
 // Subgraphs over a subset of vertices vs (used for cross-host all-reduce).
 void gen_sub_circular_pair(int n, const std::vector<int> &vs, int r, Graph *reduce, Graph *bcast);
 Graph gen_sub_binary_tree(int n, const std::vector<int> &vs);

@@ -1,0 +1,357 @@
+// torch binding of the CDNA4 kernels and the RCCL controller: kungfu_amd._hip
+//
+// Every op enqueues on the current HIP stream of the tensor's device (or an
+// explicit stream handle) and never synchronises the host.
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/extension.h>
+
+#include "kernels.hpp"
+#include "rccl_comm.hpp"
+
+#include <memory>
+#include <vector>
+
+namespace {
+
+int dtype_code(const at::Tensor &t) {
+    switch (t.scalar_type()) {
+    case at::kByte: return 0;
+    case at::kChar: return 4;
+    case at::kInt: return 6;
+    case at::kLong: return 7;
+    case at::kHalf: return 8;
+    case at::kBFloat16: return 9;
+    case at::kFloat: return 10;
+    case at::kDouble: return 11;
+    case at::kBool: return 12;
+    default: TORCH_CHECK(false, "kungfu_amd._hip: unsupported dtype ", t.scalar_type());
+    }
+    return -1;
+}
+
+hipStream_t stream_of(const at::Tensor &t, int64_t stream) {
+    if (stream) return reinterpret_cast<hipStream_t>(stream);
+    return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_gpu(const at::Tensor &t, const char *name) {
+    TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void reduce_op(at::Tensor z, at::Tensor x, at::Tensor y, int64_t op) {
+    check_gpu(z, "z");
+    check_gpu(x, "x");
+    check_gpu(y, "y");
+    TORCH_CHECK(x.numel() == y.numel() && z.numel() == x.numel(), "reduce: size mismatch");
+    TORCH_CHECK(x.scalar_type() == y.scalar_type() && z.scalar_type() == x.scalar_type(), "reduce: dtype mismatch");
+    c10::DeviceGuard g(z.device());
+    kfk::launch_reduce(z.data_ptr(), x.data_ptr(), y.data_ptr(), x.numel(), dtype_code(x), static_cast<int>(op),
+                       stream_of(z, 0));
+}
+
+void sgd_step(at::Tensor w, at::Tensor g, c10::optional<at::Tensor> m, c10::optional<at::Tensor> shadow, double lr,
+              c10::optional<at::Tensor> lr_t, double mu, double damp, double wd, double gscale, bool nesterov,
+              bool first) {
+    check_gpu(w, "w");
+    check_gpu(g, "g");
+    TORCH_CHECK(w.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat, "sgd_step: f32 buffers required");
+    TORCH_CHECK(w.numel() == g.numel(), "sgd_step: size mismatch");
+    float *mp = nullptr;
+    if (m && m->defined()) {
+        check_gpu(*m, "m");
+        TORCH_CHECK(m->numel() == w.numel() && m->scalar_type() == at::kFloat, "sgd_step: bad momentum buffer");
+        mp = m->data_ptr<float>();
+    }
+    uint16_t *sp = nullptr;
+    if (shadow && shadow->defined()) {
+        TORCH_CHECK(shadow->scalar_type() == at::kBFloat16 && shadow->numel() == w.numel(), "sgd_step: bad shadow");
+        sp = reinterpret_cast<uint16_t *>(shadow->data_ptr());
+    }
+    const float *lrp = nullptr;
+    if (lr_t && lr_t->defined()) {
+        TORCH_CHECK(lr_t->is_cuda() && lr_t->scalar_type() == at::kFloat, "sgd_step: lr tensor must be f32 on GPU");
+        lrp = lr_t->data_ptr<float>();
+    }
+    c10::DeviceGuard gd(w.device());
+    kfk::launch_sgd(w.data_ptr<float>(), g.data_ptr<float>(), mp, sp, w.numel(), static_cast<float>(lr), lrp,
+                    static_cast<float>(mu), static_cast<float>(damp), static_cast<float>(wd),
+                    static_cast<float>(gscale), nesterov, first, stream_of(w, 0));
+}
+
+void adam_step(at::Tensor w, at::Tensor g, at::Tensor m, at::Tensor v, double lr, c10::optional<at::Tensor> lr_t,
+               double b1, double b2, double eps, double wd, bool adamw, double gscale, at::Tensor step) {
+    for (auto *t : {&w, &g, &m, &v}) {
+        check_gpu(*t, "adam buffer");
+        TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == w.numel(), "adam_step: f32 buffers of equal size");
+    }
+    TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat, "adam_step: step must be an f32 GPU tensor");
+    const float *lrp = (lr_t && lr_t->defined()) ? lr_t->data_ptr<float>() : nullptr;
+    c10::DeviceGuard gd(w.device());
+    kfk::launch_adam(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), w.numel(),
+                     static_cast<float>(lr), lrp, static_cast<float>(b1), static_cast<float>(b2),
+                     static_cast<float>(eps), static_cast<float>(wd), adamw, static_cast<float>(gscale),
+                     step.data_ptr<float>(), stream_of(w, 0));
+}
+
+void axpby(at::Tensor y, at::Tensor x, c10::optional<at::Tensor> z, double a, double b) {
+    check_gpu(y, "y");
+    check_gpu(x, "x");
+    TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "axpby: mismatch");
+    TORCH_CHECK(y.scalar_type() == at::kFloat || y.scalar_type() == at::kBFloat16, "axpby: f32/bf16 only");
+    void *zp = nullptr;
+    if (z && z->defined()) {
+        check_gpu(*z, "z");
+        TORCH_CHECK(z->numel() == y.numel() && z->scalar_type() == y.scalar_type(), "axpby: bad z");
+        zp = z->data_ptr();
+    }
+    c10::DeviceGuard gd(y.device());
+    kfk::launch_axpby(y.data_ptr(), x.data_ptr(), zp, y.numel(), static_cast<float>(a), static_cast<float>(b),
+                      dtype_code(y), stream_of(y, 0));
+}
+
+void scale_(at::Tensor x, double alpha) {
+    check_gpu(x, "x");
+    int dt = dtype_code(x);
+    TORCH_CHECK(dt == 8 || dt == 9 || dt == 10, "scale_: float types only");
+    c10::DeviceGuard gd(x.device());
+    kfk::launch_scale(x.data_ptr(), x.numel(), static_cast<float>(alpha), dt, stream_of(x, 0));
+}
+
+void square(at::Tensor dst, at::Tensor src) {
+    check_gpu(dst, "dst");
+    check_gpu(src, "src");
+    TORCH_CHECK(dst.scalar_type() == at::kFloat && dst.numel() == src.numel(), "square: f32 dst of equal size");
+    c10::DeviceGuard gd(dst.device());
+    kfk::launch_square(dst.data_ptr<float>(), src.data_ptr(), src.numel(), dtype_code(src), stream_of(dst, 0));
+}
+
+at::Tensor sumsq2(at::Tensor a, c10::optional<at::Tensor> b) {
+    check_gpu(a, "a");
+    int dt = dtype_code(a);
+    TORCH_CHECK(dt == 9 || dt == 10, "sumsq2: f32/bf16 only");
+    const void *bp = nullptr;
+    if (b && b->defined()) {
+        check_gpu(*b, "b");
+        TORCH_CHECK(b->numel() == a.numel() && b->scalar_type() == a.scalar_type(), "sumsq2: mismatch");
+        bp = b->data_ptr();
+    }
+    c10::DeviceGuard gd(a.device());
+    auto opts = a.options().dtype(at::kFloat);
+    auto partials = at::empty({2 * kfk::kMaxGridHost}, opts);
+    auto out = at::empty({2}, opts);
+    kfk::launch_sumsq2(a.data_ptr(), bp, a.numel(), dt, partials.data_ptr<float>(), out.data_ptr<float>(),
+                       stream_of(a, 0));
+    return out;
+}
+
+at::Tensor variance(at::Tensor s1, at::Tensor s2, double inv_np) {
+    check_gpu(s1, "s1");
+    check_gpu(s2, "s2");
+    TORCH_CHECK(s1.scalar_type() == at::kFloat && s2.scalar_type() == at::kFloat && s1.numel() == s2.numel(),
+                "variance: f32 buffers of equal size");
+    c10::DeviceGuard gd(s1.device());
+    auto opts = s1.options();
+    auto partials = at::empty({kfk::kMaxGridHost}, opts);
+    auto out = at::empty({1}, opts);
+    kfk::launch_variance(s1.data_ptr<float>(), s2.data_ptr<float>(), s1.numel(), static_cast<float>(inv_np),
+                         partials.data_ptr<float>(), out.data_ptr<float>(), stream_of(s1, 0));
+    return out;
+}
+
+void gns_update(at::Tensor sumsq_small, at::Tensor sumsq_big, double b_small, double b_big, double alpha,
+                at::Tensor state) {
+    TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kFloat && state.numel() >= 4, "gns_update: bad state");
+    c10::DeviceGuard gd(state.device());
+    kfk::launch_gns_update(sumsq_small.data_ptr<float>(), sumsq_big.data_ptr<float>(), static_cast<float>(b_small),
+                           static_cast<float>(b_big), static_cast<float>(alpha), state.data_ptr<float>(),
+                           stream_of(state, 0));
+}
+
+// desc: int64 GPU tensor [n, 3] of (ptr, offset, numel), sorted by offset.
+void pack(at::Tensor desc, int64_t n_tensors, int64_t src_dtype, at::Tensor flat, double scale) {
+    check_gpu(flat, "flat");
+    TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong, "pack: desc must be int64 on GPU");
+    c10::DeviceGuard gd(flat.device());
+    kfk::launch_pack(desc.data_ptr<int64_t>(), static_cast<int>(n_tensors), flat.numel(), flat.data_ptr(),
+                     dtype_code(flat), static_cast<int>(src_dtype), static_cast<float>(scale), stream_of(flat, 0));
+}
+
+void unpack(at::Tensor desc, int64_t n_tensors, int64_t dst_dtype, at::Tensor flat, double scale) {
+    check_gpu(flat, "flat");
+    TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong, "unpack: desc must be int64 on GPU");
+    c10::DeviceGuard gd(flat.device());
+    kfk::launch_unpack(desc.data_ptr<int64_t>(), static_cast<int>(n_tensors), flat.numel(), flat.data_ptr(),
+                       dtype_code(flat), static_cast<int>(dst_dtype), static_cast<float>(scale), stream_of(flat, 0));
+}
+
+// ---- fused BN(+add)+ReLU ----------------------------------------------------------
+
+kfk::BNShape bn_shape(const at::Tensor &x) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16, "bn: bf16 GPU tensor required");
+    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "bn: 4-D channels_last tensor required");
+    const int C = static_cast<int>(x.size(1));
+    TORCH_CHECK(kfk::bn_supported_channels(C), "bn: unsupported channel count ", C);
+    return kfk::BNShape{x.numel() / C, C};
+}
+
+// Returns (y, mean, invstd).
+std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
+                                   c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                                   double momentum, double eps, bool training, bool relu) {
+    auto sh = bn_shape(x);
+    const int C = sh.channels;
+    TORCH_CHECK(weight.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat && weight.numel() == C &&
+                    bias.numel() == C,
+                "bn: f32 weight/bias of size C required");
+    const uint16_t *rp = nullptr;
+    if (res && res->defined()) {
+        TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == at::kBFloat16 &&
+                        res->is_contiguous(at::MemoryFormat::ChannelsLast),
+                    "bn: residual must match x (bf16, channels_last)");
+        rp = reinterpret_cast<const uint16_t *>(res->data_ptr());
+    }
+    float *rm = nullptr, *rv = nullptr;
+    if (running_mean && running_mean->defined()) {
+        TORCH_CHECK(running_var && running_var->defined(), "bn: running_var missing");
+        rm = running_mean->data_ptr<float>();
+        rv = running_var->data_ptr<float>();
+    }
+    TORCH_CHECK(training || rm, "bn: eval mode needs running stats");
+    c10::DeviceGuard gd(x.device());
+    auto fopt = x.options().dtype(at::kFloat);
+    auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+    at::Tensor partial;
+    if (training) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    kfk::launch_bn_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, weight.data_ptr<float>(),
+                           bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()), sh, relu, training, rm,
+                           rv, static_cast<float>(momentum), static_cast<float>(eps),
+                           training ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), stream_of(x, 0));
+    return {y, mean, invstd};
+}
+
+// Returns (dx, dres or undefined, dweight, dbias).
+std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor y, at::Tensor mean, at::Tensor invstd,
+                                    at::Tensor weight, bool relu, bool training, bool want_dres) {
+    auto sh = bn_shape(x);
+    const int C = sh.channels;
+    if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == x.sizes(), "bn_backward: dy must match x");
+    c10::DeviceGuard gd(x.device());
+    auto fopt = x.options().dtype(at::kFloat);
+    auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    at::Tensor dres;
+    if (want_dres) dres = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
+    auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    kfk::launch_bn_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                            reinterpret_cast<const uint16_t *>(y.data_ptr()),
+                            reinterpret_cast<const uint16_t *>(x.data_ptr()), mean.data_ptr<float>(),
+                            invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, relu, training,
+                            partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                            coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
+                            want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0));
+    return {dx, dres, dw, db};
+}
+
+// ---- RCCL --------------------------------------------------------------------------
+
+class Comm {
+  public:
+    Comm(py::bytes id, int rank, int size, int device) : c_(new kfk::RcclComm(std::string(id), rank, size, device)) {}
+    int rank() const { return c_->rank(); }
+    int size() const { return c_->size(); }
+    bool valid() const { return c_->valid(); }
+    void all_reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t stream) {
+        check_gpu(in, "in");
+        check_gpu(out, "out");
+        TORCH_CHECK(in.numel() == out.numel(), "all_reduce: size mismatch");
+        c_->all_reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
+                       stream_of(in, stream));
+    }
+    void broadcast(at::Tensor t, int64_t root, int64_t stream) {
+        check_gpu(t, "t");
+        c_->broadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(root),
+                      stream_of(t, stream));
+    }
+    void reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t root, int64_t stream) {
+        check_gpu(in, "in");
+        c_->reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
+                   static_cast<int>(root), stream_of(in, stream));
+    }
+    void all_gather(at::Tensor in, at::Tensor out, int64_t stream) {
+        check_gpu(in, "in");
+        check_gpu(out, "out");
+        TORCH_CHECK(out.numel() == in.numel() * c_->size(), "all_gather: out must hold size*numel(in)");
+        c_->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), stream_of(in, stream));
+    }
+    void reduce_scatter(at::Tensor in, at::Tensor out, int64_t op, int64_t stream) {
+        check_gpu(in, "in");
+        check_gpu(out, "out");
+        TORCH_CHECK(in.numel() == out.numel() * c_->size(), "reduce_scatter: in must hold size*numel(out)");
+        c_->reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), dtype_code(in), static_cast<int>(op),
+                           stream_of(in, stream));
+    }
+    void send(at::Tensor t, int64_t peer, int64_t stream) {
+        check_gpu(t, "t");
+        c_->send(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
+    }
+    void recv(at::Tensor t, int64_t peer, int64_t stream) {
+        check_gpu(t, "t");
+        c_->recv(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
+    }
+    void destroy() { c_->destroy(); }
+    void abort() { c_->abort(); }
+
+  private:
+    std::unique_ptr<kfk::RcclComm> c_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "kungfu-amd CDNA4 kernels (gfx950) and RCCL controller";
+    m.def("reduce", &reduce_op, "K1: z = op(x, y)");
+    m.def("sgd_step", &sgd_step, "K8: fused SGD/momentum/nesterov/wd step on flat f32 buffers", py::arg("w"),
+          py::arg("g"), py::arg("m"), py::arg("shadow"), py::arg("lr"), py::arg("lr_t"), py::arg("mu"),
+          py::arg("damp"), py::arg("wd"), py::arg("gscale"), py::arg("nesterov"), py::arg("first"));
+    m.def("adam_step", &adam_step, "fused Adam/AdamW step on flat f32 buffers");
+    m.def("axpby", &axpby, "y = a*y + b*x (optionally also z = y)", py::arg("y"), py::arg("x"), py::arg("z"),
+          py::arg("a"), py::arg("b"));
+    m.def("scale_", &scale_, "x *= alpha");
+    m.def("square", &square, "dst = src^2");
+    m.def("sumsq2", &sumsq2, "[sum(a^2), sum(b^2)] in one pass", py::arg("a"), py::arg("b") = py::none());
+    m.def("variance", &variance, "sum |s2*inv - (s1*inv)^2|");
+    m.def("gns_update", &gns_update, "device-side gradient-noise-scale EMA update");
+    m.def("pack", &pack, "multi-tensor pack into a flat buffer");
+    m.def("unpack", &unpack, "multi-tensor unpack from a flat buffer");
+    m.def("bn_supported_channels", &kfk::bn_supported_channels);
+    m.def("bn_forward", &bn_forward, "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd)", py::arg("x"),
+          py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
+          py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"));
+    m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)");
+    m.def("rccl_unique_id", [] { return py::bytes(kfk::RcclComm::unique_id()); });
+    m.def("rccl_version", &kfk::RcclComm::version);
+    m.def("rccl_group_start", &kfk::RcclComm::group_start);
+    m.def("rccl_group_end", &kfk::RcclComm::group_end);
+    py::class_<Comm>(m, "RcclComm")
+        .def(py::init<py::bytes, int, int, int>())
+        .def("rank", &Comm::rank)
+        .def("size", &Comm::size)
+        .def("valid", &Comm::valid)
+        .def("all_reduce", &Comm::all_reduce, py::arg("input"), py::arg("output"), py::arg("op") = 0,
+             py::arg("stream") = 0)
+        .def("broadcast", &Comm::broadcast, py::arg("tensor"), py::arg("root") = 0, py::arg("stream") = 0)
+        .def("reduce", &Comm::reduce, py::arg("input"), py::arg("output"), py::arg("op") = 0, py::arg("root") = 0,
+             py::arg("stream") = 0)
+        .def("all_gather", &Comm::all_gather, py::arg("input"), py::arg("output"), py::arg("stream") = 0)
+        .def("reduce_scatter", &Comm::reduce_scatter, py::arg("input"), py::arg("output"), py::arg("op") = 0,
+             py::arg("stream") = 0)
+        .def("send", &Comm::send, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
+        .def("recv", &Comm::recv, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
+        .def("destroy", &Comm::destroy)
+        .def("abort", &Comm::abort);
+}

@@ -1,0 +1,80 @@
+// Shared device helpers for the kungfu-amd CDNA4 (gfx950) kernels.
+//
+// Conventions for every bandwidth-bound kernel here (cdna_hip_programming.md
+// §6 G11/G13, App. B):
+//   * 256-thread blocks (4 waves of 64), 16-byte vector loads/stores per lane,
+//   * grid = min(ceil(n / (256 * VEC)), 2048) with a grid-stride loop, so a
+//     launch fills all 256 CUs and long tensors amortise launch cost,
+//   * f32 accumulation for bf16/f16 data, round-to-nearest-even on store,
+//   * wave64 reductions via __shfl_xor (64-lane), then LDS across the 4 waves.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace kfk {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kMaxGrid = 2048;
+
+inline int grid_for(size_t n_vec) {
+    size_t g = (n_vec + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > static_cast<size_t>(kMaxGrid)) g = kMaxGrid;
+    return static_cast<int>(g);
+}
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    uint32_t u = __float_as_uint(f);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return static_cast<uint16_t>(u >> 16);
+}
+
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+    _Float16 x;
+    __builtin_memcpy(&x, &h, 2);
+    return static_cast<float>(x);
+}
+
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+    _Float16 x = static_cast<_Float16>(f);
+    uint16_t h;
+    __builtin_memcpy(&h, &x, 2);
+    return h;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum of up to two values; result valid in thread 0.
+template <int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], float (*lds)[kBlock / kWave]) {
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        v[i] = wave_sum(v[i]);
+        if (lane == 0) lds[i][wid] = v[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            float s = 0;
+#pragma unroll
+            for (int w = 0; w < kBlock / kWave; ++w) s += lds[i][w];
+            v[i] = s;
+        }
+    }
+}
+
+enum DT : int { DT_U8 = 0, DT_I32 = 6, DT_I64 = 7, DT_F16 = 8, DT_BF16 = 9, DT_F32 = 10, DT_F64 = 11 };
+enum OP : int { OP_SUM = 0, OP_MIN = 1, OP_MAX = 2, OP_PROD = 3 };
+
+}  // namespace kfk

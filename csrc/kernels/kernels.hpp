@@ -1,0 +1,82 @@
+// Host-side launchers of the kungfu-amd HIP kernels (no torch dependency).
+// Every launcher enqueues on `stream` and never synchronises, so it can be
+// captured into a hipGraph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace kfk {
+
+constexpr int kMaxGridHost = 2048;  // == kMaxGrid in common.hpp (partials scratch size)
+
+// K1: z = op(x, y) elementwise.  dtype/op codes as kungfu::DType / ReduceOp.
+void launch_reduce(void *z, const void *x, const void *y, size_t n, int dtype, int op, hipStream_t s);
+
+// K8: fused SGD step on flat f32 buffers (torch.optim.SGD semantics):
+//   d = g*gscale + wd*w ; m = first ? d : mu*m + (1-damp)*d ; d = nesterov ? d + mu*m : m ; w -= lr*d
+// lr is read from *lr_dev when lr_dev != nullptr (graph-capture friendly).
+// If shadow != nullptr the updated weights are also written as bf16 there.
+void launch_sgd(float *w, const float *g, float *m, uint16_t *shadow, size_t n, float lr, const float *lr_dev,
+                float mu, float damp, float wd, float gscale, bool nesterov, bool first, hipStream_t s);
+
+// Fused Adam / AdamW step on flat f32 buffers.  step_dev points at a float
+// step counter already incremented for this step (bias correction on device).
+void launch_adam(float *w, const float *g, float *m, float *v, size_t n, float lr, const float *lr_dev, float b1,
+                 float b2, float eps, float wd, bool adamw, float gscale, const float *step_dev, hipStream_t s);
+
+// K3/K4: y = a*y + b*x (f32 or bf16), optionally also writing the result to z.
+void launch_axpby(void *y, const void *x, void *z, size_t n, float a, float b, int dtype, hipStream_t s);
+
+// K2: x *= alpha (f32 / bf16 / f16).
+void launch_scale(void *x, size_t n, float alpha, int dtype, hipStream_t s);
+
+// K6 helper: dst = src^2 (f32 out, f32/bf16 in).
+void launch_square(float *dst, const void *src, size_t n, int dtype, hipStream_t s);
+
+// K5: out[0] = sum(a^2), out[1] = sum(b^2) in one pass (b may be null).
+// `partials` needs 2*kMaxGrid floats of scratch.
+void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s);
+
+// K6: out[0] = sum_i | s2[i]*inv - (s1[i]*inv)^2 |  (s1 = sum g, s2 = sum g^2 over np ranks)
+void launch_variance(const float *s1, const float *s2, size_t n, float inv_np, float *partials, float *out,
+                     hipStream_t s);
+
+// K5 epilogue on device: from sumsq(small-batch grad) and sumsq(big-batch grad)
+// compute biased G/S estimates, update their EMAs in state[0..1] and write the
+// noise scale S/G into state[2].  state[3] counts updates.
+void launch_gns_update(const float *sumsq_small, const float *sumsq_big, float b_small, float b_big, float alpha,
+                       float *state, hipStream_t s);
+
+// K7: multi-tensor pack/unpack.  desc is a device array of n_tensors
+// {ptr (int64), offset (elements), numel} triples; flat is contiguous.
+// pack:   flat[off:off+numel] = scale * src (dtype cast src_dtype -> flat_dtype)
+// unpack: dst = scale * flat[off:off+numel]
+void launch_pack(const int64_t *desc, int n_tensors, size_t total, void *flat, int flat_dtype, int src_dtype,
+                 float scale, hipStream_t s);
+void launch_unpack(const int64_t *desc, int n_tensors, size_t total, const void *flat, int flat_dtype,
+                   int dst_dtype, float scale, hipStream_t s);
+
+// Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
+// (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
+struct BNShape {
+    int64_t rows;  // N*H*W
+    int channels;
+};
+bool bn_supported_channels(int C);
+int bn_num_chunks(BNShape sh);  // partial scratch = 2 * nchunks * C floats
+// Training: batch stats -> mean/invstd, running stats update, coef = [scale; shift]
+// (2C floats), y = act(x*scale + shift [+ res]).  Eval: running stats.
+void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
+                       BNShape sh, bool relu, bool training, float *run_mean, float *run_var, float momentum,
+                       float eps, float *partial, float *mean, float *invstd, float *coef, hipStream_t s);
+// dz = relu ? dy*(y>0) : dy ; dgamma/dbeta (f32) ; dx = k1*dz + k2*x + k3 ; dres = dz.
+// coef scratch: 3C floats.
+void launch_bn_backward(const uint16_t *dy, const uint16_t *y, const uint16_t *x, const float *mean,
+                        const float *invstd, const float *gamma, BNShape sh, bool relu, bool training,
+                        float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres,
+                        hipStream_t s);
+
+}  // namespace kfk

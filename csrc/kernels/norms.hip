@@ -1,0 +1,181 @@
+// Reductions for the training monitors.
+//   K5 gradient noise scale: sum-of-squares of the local (small-batch) and the
+//      all-reduced (big-batch) gradient in ONE pass over both buffers, then a
+//      device-side epilogue computing G_biased / S_biased, their EMAs and S/G.
+//      Reference: srcs/python/kungfu/tensorflow/ops/monitor.py:6-17,
+//      srcs/cpp/src/tensorflow/ops/cpu/collective.cpp:212-260,
+//      srcs/python/kungfu/tensorflow/optimizers/grad_noise_scale.py:56-88.
+//   K6 gradient variance: sum_i |E[g^2]_i - E[g]_i^2| from the all-reduced
+//      sums of g and g^2.  Reference: optimizers/grad_variance.py:46-59.
+//
+// Structure: two-stage, deterministic (no float atomics): stage 1 grid-stride
+// with 16-byte loads, wave64 shuffle + LDS block reduce, one partial per block;
+// stage 2 a single block folds the partials.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace kfk {
+
+namespace {
+
+template <bool BF16, bool TWO>
+__global__ __launch_bounds__(kBlock) void sumsq2_stage1(const void *a, const void *b, size_t n, bool vec,
+                                                         float *partials) {
+    __shared__ float lds[2][kBlock / kWave];
+    float acc[2] = {0.f, 0.f};
+    size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (BF16) {
+        size_t n8 = vec ? n / 8 : 0;
+        const uint4 *a8 = static_cast<const uint4 *>(a), *b8 = static_cast<const uint4 *>(b);
+        for (size_t i = tid; i < n8; i += stride) {
+            uint4 va = a8[i];
+            const uint16_t *pa = reinterpret_cast<const uint16_t *>(&va);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                float x = bf16_to_f32(pa[k]);
+                acc[0] += x * x;
+            }
+            if (TWO) {
+                uint4 vb = b8[i];
+                const uint16_t *pb = reinterpret_cast<const uint16_t *>(&vb);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    float y = bf16_to_f32(pb[k]);
+                    acc[1] += y * y;
+                }
+            }
+        }
+        for (size_t i = n8 * 8 + tid; i < n; i += stride) {
+            float x = bf16_to_f32(static_cast<const uint16_t *>(a)[i]);
+            acc[0] += x * x;
+            if (TWO) {
+                float y = bf16_to_f32(static_cast<const uint16_t *>(b)[i]);
+                acc[1] += y * y;
+            }
+        }
+    } else {
+        size_t n4 = vec ? n / 4 : 0;
+        const float4 *a4 = static_cast<const float4 *>(a), *b4 = static_cast<const float4 *>(b);
+        for (size_t i = tid; i < n4; i += stride) {
+            float4 va = a4[i];
+            acc[0] += va.x * va.x + va.y * va.y + va.z * va.z + va.w * va.w;
+            if (TWO) {
+                float4 vb = b4[i];
+                acc[1] += vb.x * vb.x + vb.y * vb.y + vb.z * vb.z + vb.w * vb.w;
+            }
+        }
+        for (size_t i = n4 * 4 + tid; i < n; i += stride) {
+            float x = static_cast<const float *>(a)[i];
+            acc[0] += x * x;
+            if (TWO) {
+                float y = static_cast<const float *>(b)[i];
+                acc[1] += y * y;
+            }
+        }
+    }
+    block_sum<2>(acc, lds);
+    if (threadIdx.x == 0) {
+        partials[blockIdx.x] = acc[0];
+        partials[kMaxGrid + blockIdx.x] = acc[1];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fold2(const float *partials, int nparts, float *out) {
+    __shared__ float lds[2][kBlock / kWave];
+    float acc[2] = {0.f, 0.f};
+    for (int i = threadIdx.x; i < nparts; i += kBlock) {
+        acc[0] += partials[i];
+        acc[1] += partials[kMaxGrid + i];
+    }
+    block_sum<2>(acc, lds);
+    if (threadIdx.x == 0) {
+        out[0] = acc[0];
+        out[1] = acc[1];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void variance_stage1(const float4 *s1, const float4 *s2, const float *s1t,
+                                                          const float *s2t, size_t n, float inv, float *partials) {
+    __shared__ float lds[1][kBlock / kWave];
+    float acc[1] = {0.f};
+    size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    size_t tid = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    size_t n4 = s1 ? n / 4 : 0;
+    for (size_t i = tid; i < n4; i += stride) {
+        float4 a = s1[i], b = s2[i];
+        float m;
+        m = a.x * inv;
+        acc[0] += fabsf(b.x * inv - m * m);
+        m = a.y * inv;
+        acc[0] += fabsf(b.y * inv - m * m);
+        m = a.z * inv;
+        acc[0] += fabsf(b.z * inv - m * m);
+        m = a.w * inv;
+        acc[0] += fabsf(b.w * inv - m * m);
+    }
+    for (size_t i = n4 * 4 + tid; i < n; i += stride) {
+        float m = s1t[i] * inv;
+        acc[0] += fabsf(s2t[i] * inv - m * m);
+    }
+    block_sum<1>(acc, lds);
+    if (threadIdx.x == 0) partials[blockIdx.x] = acc[0];
+}
+
+__global__ void fold1(const float *partials, int nparts, float *out) {
+    __shared__ float lds[1][kBlock / kWave];
+    float acc[1] = {0.f};
+    for (int i = threadIdx.x; i < nparts; i += kBlock) acc[0] += partials[i];
+    block_sum<1>(acc, lds);
+    if (threadIdx.x == 0) out[0] = acc[0];
+}
+
+// state: [ema_G, ema_S, noise_scale, n_updates]
+__global__ void gns_update_kernel(const float *sumsq_small, const float *sumsq_big, float b_small, float b_big,
+                                  float alpha, float *state) {
+    float gs = *sumsq_small, gb = *sumsq_big;
+    float G = (b_big * gb - b_small * gs) / (b_big - b_small);
+    float S = (gs - gb) / (1.f / b_small - 1.f / b_big);
+    float cnt = state[3];
+    float eg = cnt == 0.f ? G : alpha * state[0] + (1.f - alpha) * G;
+    float es = cnt == 0.f ? S : alpha * state[1] + (1.f - alpha) * S;
+    state[0] = eg;
+    state[1] = es;
+    state[2] = eg != 0.f ? es / eg : 0.f;
+    state[3] = cnt + 1.f;
+}
+
+inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s) {
+    bool bf = dtype == DT_BF16;
+    size_t nvec = bf ? n / 8 : n / 4;
+    int g = grid_for(nvec ? nvec : 1);
+    bool aligned = al16(a) && (!b || al16(b));
+    if (bf) {
+        if (b) sumsq2_stage1<true, true><<<g, kBlock, 0, s>>>(a, b, n, aligned, partials);
+        else sumsq2_stage1<true, false><<<g, kBlock, 0, s>>>(a, a, n, aligned, partials);
+    } else {
+        if (b) sumsq2_stage1<false, true><<<g, kBlock, 0, s>>>(a, b, n, aligned, partials);
+        else sumsq2_stage1<false, false><<<g, kBlock, 0, s>>>(a, a, n, aligned, partials);
+    }
+    fold2<<<1, kBlock, 0, s>>>(partials, g, out);
+}
+
+void launch_variance(const float *s1, const float *s2, size_t n, float inv_np, float *partials, float *out,
+                     hipStream_t s) {
+    bool al = al16(s1) && al16(s2);
+    int g = grid_for(al ? (n / 4 ? n / 4 : 1) : (n ? n : 1));
+    variance_stage1<<<g, kBlock, 0, s>>>(al ? reinterpret_cast<const float4 *>(s1) : nullptr,
+                                         reinterpret_cast<const float4 *>(s2), s1, s2, n, inv_np, partials);
+    fold1<<<1, kBlock, 0, s>>>(partials, g, out);
+}
+
+void launch_gns_update(const float *sumsq_small, const float *sumsq_big, float b_small, float b_big, float alpha,
+                       float *state, hipStream_t s) {
+    gns_update_kernel<<<1, 1, 0, s>>>(sumsq_small, sumsq_big, b_small, b_big, alpha, state);
+}
+
+}  // namespace kfk

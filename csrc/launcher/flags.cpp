@@ -1,0 +1,234 @@
+// kungfu-run flag parsing and self-IP inference.  See launcher.hpp for parity.
+#include "launcher.hpp"
+
+#include <kungfu/log.hpp>
+
+#include <arpa/inet.h>
+#include <ifaddrs.h>
+#include <netinet/in.h>
+
+#include <cstdlib>
+#include <ctime>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <thread>
+
+namespace kungfu {
+namespace launcher {
+
+namespace {
+
+double parse_duration(const std::string &s) {
+    size_t pos = 0;
+    double x = std::stod(s, &pos);
+    std::string unit = s.substr(pos);
+    if (unit.empty() || unit == "s") return x;
+    if (unit == "ms") return x / 1000.0;
+    if (unit == "m") return x * 60.0;
+    if (unit == "h") return x * 3600.0;
+    // Go-style composite like "1m30s"
+    double total = 0;
+    std::string cur;
+    for (size_t i = 0; i < s.size(); ++i) {
+        char c = s[i];
+        if ((c >= '0' && c <= '9') || c == '.') {
+            cur.push_back(c);
+            continue;
+        }
+        std::string u(1, c);
+        if (c == 'm' && i + 1 < s.size() && s[i + 1] == 's') {
+            u = "ms";
+            ++i;
+        }
+        double v = std::stod(cur);
+        cur.clear();
+        if (u == "h") total += v * 3600;
+        else if (u == "m") total += v * 60;
+        else if (u == "s") total += v;
+        else if (u == "ms") total += v / 1000;
+        else throw std::invalid_argument("bad duration " + s);
+    }
+    return total;
+}
+
+bool parse_bool(const std::string &v) { return v == "1" || v == "true" || v == "True" || v == "t" || v == "T"; }
+
+}  // namespace
+
+std::string Flags::usage() {
+    return "usage: kungfu-run [flags] <prog> [args...]\n"
+           "  -np N                  number of peers (1)\n"
+           "  -H ip:slots[:pub],...  host list (127.0.0.1:<ncpu>)\n"
+           "  -hostfile PATH         OpenMPI-style hostfile (overrides -H)\n"
+           "  -u USER                ssh user (remote launch)\n"
+           "  -port-range A-B        worker ports (10000-11000)\n"
+           "  -self IPv4             this host's internal IPv4\n"
+           "  -nic NAME              infer self IPv4 from this interface\n"
+           "  -timeout DUR           kill the job after DUR (e.g. 30s, 5m)\n"
+           "  -v[=bool]              stream worker output (true)\n"
+           "  -q                     quiet launcher logs\n"
+           "  -allow-xgmi            keep all GPUs visible to every worker (alias -allow-nvlink)\n"
+           "  -strategy NAME         STAR|MULTI_STAR|RING|CLIQUE|TREE|BINARY_TREE|BINARY_TREE_STAR|"
+           "MULTI_BINARY_TREE_STAR|AUTO\n"
+           "  -port N                runner port (38080)\n"
+           "  -debug-port N          runner HTTP debug server port\n"
+           "  -w                     watch mode (elastic)\n"
+           "  -k                     keep runner alive after workers finish (watch mode)\n"
+           "  -init-version N        initial cluster version (-1: wait for a stage)\n"
+           "  -config-server URL     config server URL\n"
+           "  -builtin-config-port N run a config server in the launcher\n"
+           "  -t0 UNIX               job start timestamp\n"
+           "  -logfile PATH, -logdir DIR\n"
+           "  -delay DUR             delay start (testing)\n";
+}
+
+std::string Flags::parse(int argc, char **argv) {
+    job_start_time = static_cast<long>(std::time(nullptr));
+    host_list_str = "127.0.0.1:" + std::to_string(std::max(1u, std::thread::hardware_concurrency()));
+    int i = 1;
+    auto need = [&](const std::string &name) -> std::string {
+        if (i + 1 >= argc) throw std::invalid_argument("flag needs an argument: -" + name);
+        return argv[++i];
+    };
+    try {
+        for (; i < argc; ++i) {
+            std::string a = argv[i];
+            if (a == "--") {
+                ++i;
+                break;
+            }
+            if (a.size() < 2 || a[0] != '-') break;
+            std::string name = a.substr(a[1] == '-' ? 2 : 1), val;
+            bool has_val = false;
+            auto eq = name.find('=');
+            if (eq != std::string::npos) {
+                val = name.substr(eq + 1);
+                name = name.substr(0, eq);
+                has_val = true;
+            }
+            auto get = [&]() { return has_val ? val : need(name); };
+            auto getb = [&]() { return has_val ? parse_bool(val) : true; };
+            if (name == "np") np = std::stoi(get());
+            else if (name == "H") host_list_str = get();
+            else if (name == "hostfile") hostfile = get();
+            else if (name == "P") throw std::invalid_argument("-P is not supported (use -H)");
+            else if (name == "u") user = get();
+            else if (name == "port-range") port_range = PortRange::parse(get());
+            else if (name == "self") self = get();
+            else if (name == "timeout") timeout = parse_duration(get());
+            else if (name == "v") verbose = getb();
+            else if (name == "nic") nic = get();
+            else if (name == "allow-xgmi" || name == "allow-nvlink") allow_xgmi = getb();
+            else if (name == "strategy") {
+                auto s = get();
+                if (!parse_strategy(s, &strategy)) throw std::invalid_argument("invalid strategy " + s);
+            } else if (name == "port") port = std::stoi(get());
+            else if (name == "debug-port") debug_port = std::stoi(get());
+            else if (name == "w") watch = getb();
+            else if (name == "k") keep = getb();
+            else if (name == "init-version") init_version = std::stoi(get());
+            else if (name == "config-server") config_server = get();
+            else if (name == "t0") job_start_time = std::stol(get());
+            else if (name == "logfile") logfile = get();
+            else if (name == "logdir") logdir = get();
+            else if (name == "q") quiet = getb();
+            else if (name == "delay") delay = parse_duration(get());
+            else if (name == "builtin-config-port") builtin_config_port = std::stoi(get());
+            else if (name == "h" || name == "help") return usage();
+            else throw std::invalid_argument("unknown flag -" + name);
+        }
+        if (!hostfile.empty()) {
+            std::ifstream in(hostfile);
+            if (!in) throw std::invalid_argument("cannot open hostfile " + hostfile);
+            std::stringstream ss;
+            ss << in.rdbuf();
+            hosts = HostList::parse_hostfile(ss.str());
+        } else hosts = HostList::parse(host_list_str);
+    } catch (const std::exception &e) {
+        return e.what();
+    }
+    if (i >= argc) return "missing program name";
+    prog = argv[i++];
+    for (; i < argc; ++i) args.push_back(argv[i]);
+    return "";
+}
+
+uint32_t infer_self_ipv4(const std::string &self, const std::string &nic) {
+    if (!self.empty()) return parse_ipv4(self);
+    if (!nic.empty()) {
+        ifaddrs *ifa = nullptr;
+        if (getifaddrs(&ifa) != 0) throw std::runtime_error("getifaddrs failed");
+        uint32_t ip = 0;
+        for (auto *p = ifa; p; p = p->ifa_next) {
+            if (!p->ifa_addr || p->ifa_addr->sa_family != AF_INET || nic != p->ifa_name) continue;
+            ip = ntohl(reinterpret_cast<sockaddr_in *>(p->ifa_addr)->sin_addr.s_addr);
+            break;
+        }
+        freeifaddrs(ifa);
+        if (!ip) throw std::runtime_error("no ipv4 found on " + nic);
+        return ip;
+    }
+    return parse_ipv4("127.0.0.1");
+}
+
+std::vector<int> parse_visible_devices(const std::string &val, bool *ok) {
+    std::vector<int> ids;
+    *ok = true;
+    if (val.empty()) return ids;
+    std::stringstream ss(val);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        try {
+            int n = std::stoi(part);
+            if (n < 0) continue;
+            for (int x : ids)
+                if (x == n) *ok = false;
+            ids.push_back(n);
+        } catch (...) {
+            *ok = false;
+        }
+    }
+    if (!*ok) ids.clear();
+    return ids;
+}
+
+int gpu_index(int local_rank) {
+    const char *keys[] = {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"};
+    for (auto *k : keys) {
+        const char *v = std::getenv(k);
+        if (!v || !*v) continue;
+        bool ok = true;
+        auto ids = parse_visible_devices(v, &ok);
+        if (!ok) {
+            KF_WARN("invalid value of %s: %s", k, v);
+            return -1;
+        }
+        if (static_cast<int>(ids.size()) <= local_rank) {
+            KF_WARN("%s=%s is not enough for local rank %d", k, v, local_rank);
+            return -1;
+        }
+        return ids[local_rank];
+    }
+    return local_rank;
+}
+
+int GPUPool::get() {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (size_t i = 0; i < mask_.size(); ++i)
+        if (mask_[i]) {
+            mask_[i] = false;
+            return static_cast<int>(i);
+        }
+    return -1;
+}
+
+void GPUPool::put(int id) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (id < 0 || id >= static_cast<int>(mask_.size())) return;
+    if (mask_[id]) fatalf("GPU %d not allocated", id);
+    mask_[id] = true;
+}
+
+}  // namespace launcher
+}  // namespace kungfu

@@ -1,0 +1,54 @@
+// Job -> per-worker process specs (env contract).  See launcher.hpp for parity.
+#include "launcher.hpp"
+
+#include <kungfu/log.hpp>
+
+#include <ctime>
+
+namespace kungfu {
+namespace launcher {
+
+Proc Job::new_proc(const PeerID &peer, int gpu_id, int init_version, const Cluster &cluster) const {
+    Proc p;
+    p.name = format_ipv4(peer.ipv4) + "." + std::to_string(peer.port);
+    p.prog = prog;
+    p.args = args;
+    p.logdir = logdir;
+    auto &e = p.envs;
+    e[kEnvJobStartTimestamp] = std::to_string(start_time);
+    e[kEnvProcStartTimestamp] = std::to_string(static_cast<long>(std::time(nullptr)));
+    e[kEnvSelfSpec] = peer.str();
+    e[kEnvInitRunners] = cluster.runners.str();
+    e[kEnvParentID] = parent.str();
+    e[kEnvInitPeers] = cluster.workers.str();
+    e[kEnvInitClusterVersion] = std::to_string(init_version);
+    e[kEnvStrategy] = strategy_name(strategy);
+    if (!config_server.empty()) e[kEnvConfigServer] = config_server;
+    e["KUNGFU_ALLOW_XGMI"] = allow_xgmi ? "true" : "false";
+    int idx = gpu_index(gpu_id);
+    e["KUNGFU_HIP_VISIBLE_DEVICES"] = std::to_string(idx);
+    if (!allow_xgmi) {
+        // One GPU per worker.  HIP honours HIP_VISIBLE_DEVICES; the CUDA name is
+        // kept for frameworks that read it.
+        e["HIP_VISIBLE_DEVICES"] = std::to_string(idx);
+        e["CUDA_VISIBLE_DEVICES"] = std::to_string(idx);
+    }
+    if (!std::getenv("PYTHONUNBUFFERED")) e["PYTHONUNBUFFERED"] = "1";
+    // Keep dmabuf IPC (required for RCCL / HIP IPC on this platform).
+    if (!std::getenv("HSA_ENABLE_IPC_MODE_LEGACY")) e["HSA_ENABLE_IPC_MODE_LEGACY"] = "0";
+    for (auto &h : hosts)
+        if (h.ipv4 == peer.ipv4) p.hostname = h.public_addr;
+    return p;
+}
+
+std::vector<Proc> Job::create_procs(const Cluster &cluster, uint32_t host) const {
+    std::vector<Proc> ps;
+    for (auto &self : cluster.workers.on(host)) {
+        int local_rank = cluster.workers.local_rank(self);
+        ps.push_back(new_proc(self, local_rank, 0, cluster));
+    }
+    return ps;
+}
+
+}  // namespace launcher
+}  // namespace kungfu

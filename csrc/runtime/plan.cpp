@@ -535,6 +535,31 @@ Graph gen_default_reduce(const Graph &bcast) {
     return g;
 }
 
+std::vector<int> minimum_spanning_tree(const std::vector<double> &w, int n, int root) {
+    if (static_cast<int>(w.size()) != n * n) throw std::invalid_argument("mst: weight matrix must be n*n");
+    std::vector<int> father(n, root);
+    if (n == 0) return father;
+    std::vector<double> best(n, 1e300);
+    std::vector<bool> in(n, false);
+    best[root] = 0;
+    father[root] = root;
+    for (int it = 0; it < n; ++it) {
+        int u = -1;
+        for (int v = 0; v < n; ++v)
+            if (!in[v] && (u < 0 || best[v] < best[u])) u = v;
+        in[u] = true;
+        for (int v = 0; v < n; ++v) {
+            if (in[v]) continue;
+            double c = w[u * n + v] + w[v * n + u];
+            if (c < best[v]) {
+                best[v] = c;
+                father[v] = u;
+            }
+        }
+    }
+    return father;
+}
+
 void gen_sub_circular_pair(int n, const std::vector<int> &vs, int r, Graph *reduce, Graph *bcast) {
     *reduce = Graph(n);
     *bcast = Graph(n);

@@ -325,6 +325,9 @@ PYBIND11_MODULE(_kungfu, m) {
         d["roots"] = roots;
         return py::object(d);
     });
+    m.def("minimum_spanning_tree", [](const std::vector<double> &w, int n, int root) {
+        return minimum_spanning_tree(w, n, root);
+    }, py::arg("weights"), py::arg("n"), py::arg("root") = 0);
     m.def("cluster_resize", [](const std::string &cluster_json, int n) {
         return json::dump(Cluster::from_json(json::parse(cluster_json)).resize(n).to_json());
     });

@@ -1,0 +1,18 @@
+"""Multi-process host collectives through kungfu-run for np=1..4 x every
+strategy (parity: scripts/tests/run-integration-tests.sh:10-38)."""
+import pytest
+
+from conftest import kungfu_run, worker
+
+STRATEGIES = ["STAR", "MULTI_STAR", "RING", "CLIQUE", "TREE", "BINARY_TREE", "BINARY_TREE_STAR",
+              "MULTI_BINARY_TREE_STAR", "AUTO"]
+
+
+@pytest.mark.parametrize("np_", [1, 2, 3, 4])
+@pytest.mark.parametrize("strategy", STRATEGIES)
+def test_collectives(np_, strategy):
+    if np_ == 3 and strategy not in ("RING", "CLIQUE", "BINARY_TREE_STAR"):
+        pytest.skip("np=3 covered for a subset")
+    r = kungfu_run(np_, [worker("collectives.py")], strategy=strategy, timeout=180)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("COLLECTIVES_OK") == np_, r.stdout[-4000:]

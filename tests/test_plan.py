@@ -1,0 +1,107 @@
+"""Pure-logic tests of the native planning layer (parity: srcs/go/plan/*_test.go)."""
+import json
+
+import pytest
+
+from kungfu_amd._lib import runtime as K
+
+
+def peers(spec):
+    return ",".join(spec)
+
+
+def test_strategy_names():
+    names = K.strategy_names()
+    for s in ["STAR", "MULTI_STAR", "RING", "CLIQUE", "TREE", "BINARY_TREE", "BINARY_TREE_STAR",
+              "MULTI_BINARY_TREE_STAR", "AUTO"]:
+        assert s in names
+
+
+def _check_pair(reduce, bcast, n):
+    # every node reaches the bcast root; reduce has self loops where needed
+    rn, bn = reduce["nodes"], bcast["nodes"]
+    assert len(rn) == len(bn) == n
+    roots = [i for i, x in enumerate(bn) if not x["prevs"]]
+    assert len(roots) == 1, bcast["debug"]
+    for i, x in enumerate(bn):
+        assert len(x["prevs"]) <= 1
+
+
+@pytest.mark.parametrize("strategy", ["STAR", "MULTI_STAR", "RING", "CLIQUE", "TREE", "BINARY_TREE",
+                                      "BINARY_TREE_STAR", "MULTI_BINARY_TREE_STAR", "AUTO"])
+@pytest.mark.parametrize("hosts", [1, 2, 3])
+@pytest.mark.parametrize("per_host", [1, 2, 4])
+def test_strategy_graphs(strategy, hosts, per_host):
+    pl = ",".join("10.0.0.%d:%d" % (h + 1, 10000 + i) for h in range(hosts) for i in range(per_host))
+    n = hosts * per_host
+    gs = K.gen_strategy_graphs(pl, strategy)
+    assert len(gs) >= 1
+    for r, b in gs:
+        _check_pair(r, b, n)
+
+
+def test_ring_graph_shape():
+    pl = ",".join("127.0.0.1:%d" % (10000 + i) for i in range(4))
+    gs = K.gen_strategy_graphs(pl, "RING")
+    assert len(gs) == 4  # one per root
+    r, b = gs[0]
+    # reduce chain ends at root 0: 1->2->3->0 ; bcast chain 0->1->2->3
+    assert r["debug"] == "[4]{(0)(1)(2)(3)(1->2)(2->3)(3->0)}"
+    assert b["debug"] == "[4]{(0->1)(1->2)(2->3)}"
+
+
+def test_binary_tree_star_two_hosts():
+    pl = "10.0.0.1:10000,10.0.0.1:10001,10.0.0.2:10000,10.0.0.2:10001"
+    (r, b), = K.gen_strategy_graphs(pl, "BINARY_TREE_STAR")
+    assert b["debug"] == "[4]{(0->1)(0->2)(2->3)}"
+
+
+def test_forest():
+    g = K.graph_from_forest([0, 0, 1, 1])
+    assert g["roots"] == 1
+    assert g["nodes"][1]["prevs"] == [0]
+    assert K.graph_from_forest([1, 0]) is None  # cycle
+    assert K.graph_from_forest([0, 5]) is None  # out of range
+    assert K.graph_from_forest([0, 1, 1])["roots"] == 2
+
+
+def test_cluster_resize_validate():
+    c = {"Runners": ["10.0.0.1:38080", "10.0.0.2:38080"],
+         "Workers": ["10.0.0.1:10000", "10.0.0.1:10001", "10.0.0.2:10000"]}
+    cj = json.dumps(c)
+    assert K.cluster_validate(cj) == ""
+    grown = json.loads(K.cluster_resize(cj, 5))
+    assert grown["Workers"][:3] == c["Workers"]
+    assert grown["Workers"][3] == "10.0.0.2:10001"  # least-loaded host first
+    assert len(grown["Workers"]) == 5
+    shrunk = json.loads(K.cluster_resize(cj, 1))
+    assert shrunk["Workers"] == ["10.0.0.1:10000"]
+    bad = json.dumps({"Runners": ["10.0.0.1:38080"], "Workers": ["10.0.0.3:10000"]})
+    assert K.cluster_validate(bad) == "missing runner"
+    dup = json.dumps({"Runners": ["10.0.0.1:38080"], "Workers": ["10.0.0.1:10000", "10.0.0.1:10000"]})
+    assert K.cluster_validate(dup) == "duplicated port"
+
+
+def test_host_list_and_hostfile():
+    pl = K.gen_peer_list("192.168.1.1:2,192.168.1.2:2", 3, "10000-11000")
+    assert pl == "192.168.1.1:10000,192.168.1.1:10001,192.168.1.2:10000"
+    with pytest.raises(Exception):
+        K.gen_peer_list("127.0.0.1:2", 3, "10000-11000")
+    hl = K.parse_hostfile("# comment\n192.168.1.1 slots=4 public_addr=node1\n192.168.1.2\n")
+    assert hl == "192.168.1.1:4:node1,192.168.1.2:1:192.168.1.2"
+
+
+def test_partition_by_host():
+    masters, master_of = K.partition_by_host("10.0.0.1:1,10.0.0.2:1,10.0.0.1:2,10.0.0.2:2")
+    assert masters == [0, 1]
+    assert master_of == [0, 1, 0, 1]
+
+
+def test_even_partition():
+    assert K.even_partition(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    assert K.even_partition(2, 4) == [(0, 1), (1, 2), (2, 2), (2, 2)]
+
+
+def test_mst():
+    w = [0, 1, 5, 1, 0, 2, 5, 2, 0]
+    assert K.minimum_spanning_tree(w, 3, 0) == [0, 0, 1]
