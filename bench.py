@@ -48,7 +48,8 @@ def main():
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--batch", type=int, default=256, help="images per GPU")
     p.add_argument("--model", default="resnet50")
-    p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada"])
+    p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada", "local"])
+    p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--lr", type=float, default=0.1)
@@ -80,7 +81,11 @@ def main():
     base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
     if a.optimizer == "ssgd":
         opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),
-                                                    bucket_mb=a.bucket_mb)
+                                                    bucket_mb=a.bucket_mb, overlap=bool(a.overlap))
+    elif a.optimizer == "local":  # diagnostics only: fused flat SGD, no gradient exchange
+        from kungfu_amd.optimizers.core import KungFuOptimizer
+
+        opt = KungFuOptimizer(base, named_parameters=model.named_parameters())
     elif a.optimizer == "sma":
         opt = kf.optimizers.SynchronousAveragingOptimizer(base, named_parameters=model.named_parameters())
     elif a.optimizer == "pair":
@@ -144,7 +149,7 @@ def main():
             "per_gpu_img_s": round(value / size, 2),
             "baseline_per_gpu_img_s": round(BASELINE_PER_GPU, 1),
             "warmup_s": round(warm_s, 1),
-            "final_loss": round(float(loss), 4),
+            "final_loss": round(float(loss.detach()), 4),
         },
     }
     if rank == 0:

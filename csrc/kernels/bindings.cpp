@@ -160,6 +160,23 @@ at::Tensor variance(at::Tensor s1, at::Tensor s2, double inv_np) {
     return out;
 }
 
+// Per-tensor L2 norms of E[g^2]-E[g]^2 summed over tensors (the reference's
+// gradient variance, grad_variance.py:46-59).  seg_off: int64 GPU [nseg+1].
+at::Tensor seg_variance(at::Tensor s1, at::Tensor s2, at::Tensor seg_off, double inv_np) {
+    check_gpu(s1, "s1");
+    check_gpu(s2, "s2");
+    TORCH_CHECK(seg_off.is_cuda() && seg_off.scalar_type() == at::kLong && seg_off.numel() >= 2,
+                "seg_variance: int64 GPU offsets required");
+    TORCH_CHECK(s1.scalar_type() == at::kFloat && s2.scalar_type() == at::kFloat && s1.numel() == s2.numel(),
+                "seg_variance: f32 buffers of equal size");
+    c10::DeviceGuard gd(s1.device());
+    const int nseg = static_cast<int>(seg_off.numel() - 1);
+    auto out = at::zeros({nseg}, s1.options());
+    kfk::launch_seg_variance(s1.data_ptr<float>(), s2.data_ptr<float>(), s1.numel(), static_cast<float>(inv_np),
+                             seg_off.data_ptr<int64_t>(), nseg, out.data_ptr<float>(), stream_of(s1, 0));
+    return out.sqrt().sum();
+}
+
 void gns_update(at::Tensor sumsq_small, at::Tensor sumsq_big, double b_small, double b_big, double alpha,
                 at::Tensor state) {
     TORCH_CHECK(state.is_cuda() && state.scalar_type() == at::kFloat && state.numel() >= 4, "gns_update: bad state");
@@ -257,6 +274,42 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor y, a
     return {dx, dres, dw, db};
 }
 
+// ---- device model store: HIP IPC export / import ------------------------------------
+// A dedicated hipMalloc allocation (not a caching-allocator sub-block) so the
+// IPC handle maps exactly this buffer; peers open it and pull over xGMI with
+// no participation of the owner (one-sided, like the reference's P2P store).
+
+void hcheck(hipError_t e, const char *what) {
+    TORCH_CHECK(e == hipSuccess, "hip ", what, ": ", hipGetErrorString(e));
+}
+
+at::Tensor ipc_alloc(int64_t numel, int64_t device) {
+    c10::DeviceGuard gd(at::Device(at::kCUDA, device));
+    void *p = nullptr;
+    hcheck(hipMalloc(&p, std::max<int64_t>(numel, 1) * 4), "Malloc");
+    hcheck(hipMemset(p, 0, std::max<int64_t>(numel, 1) * 4), "Memset");
+    auto opts = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device);
+    return torch::from_blob(p, {numel}, [](void *q) { (void)hipFree(q); }, opts);
+}
+
+py::bytes ipc_handle(at::Tensor t) {
+    hipIpcMemHandle_t h;
+    hcheck(hipIpcGetMemHandle(&h, t.data_ptr()), "IpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char *>(&h), sizeof(h));
+}
+
+at::Tensor ipc_open(py::bytes handle, int64_t numel, int64_t device) {
+    std::string hs = handle;
+    TORCH_CHECK(hs.size() == sizeof(hipIpcMemHandle_t), "ipc_open: bad handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, hs.data(), sizeof(h));
+    c10::DeviceGuard gd(at::Device(at::kCUDA, device));
+    void *p = nullptr;
+    hcheck(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "IpcOpenMemHandle");
+    auto opts = at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, device);
+    return torch::from_blob(p, {numel}, [](void *q) { (void)hipIpcCloseMemHandle(q); }, opts);
+}
+
 // ---- RCCL --------------------------------------------------------------------------
 
 class Comm {
@@ -326,6 +379,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sumsq2", &sumsq2, "[sum(a^2), sum(b^2)] in one pass", py::arg("a"), py::arg("b") = py::none());
     m.def("variance", &variance, "sum |s2*inv - (s1*inv)^2|");
     m.def("gns_update", &gns_update, "device-side gradient-noise-scale EMA update");
+    m.def("seg_variance", &seg_variance, "sum_k ||E[g^2]-E[g]^2||_2 over flat tensor segments");
     m.def("pack", &pack, "multi-tensor pack into a flat buffer");
     m.def("unpack", &unpack, "multi-tensor unpack from a flat buffer");
     m.def("bn_supported_channels", &kfk::bn_supported_channels);
@@ -333,6 +387,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"));
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)");
+    m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
+    m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");
+    m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");
     m.def("rccl_unique_id", [] { return py::bytes(kfk::RcclComm::unique_id()); });
     m.def("rccl_version", &kfk::RcclComm::version);
     m.def("rccl_group_start", &kfk::RcclComm::group_start);

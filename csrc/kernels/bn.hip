@@ -49,6 +49,40 @@ struct Chunking {
     int nchunks;
 };
 
+constexpr int kMaxChunks = 512;
+constexpr int kFoldCh = 32;                   // channels per fold block
+constexpr int kFoldLanes = kBlock / kFoldCh;  // chunk lanes per channel
+
+// Fold partial[v][chunk][C] over chunks for kFoldCh channels per block:
+// 32 channel lanes x 8 chunk lanes, coalesced 128-B rows, f64 accumulation,
+// then an LDS reduce across chunk lanes.  Result valid for lane kl == 0.
+template <int NV>
+__device__ __forceinline__ void fold_partials(const float *partial, int nchunks, int C, int c, int kl,
+                                              double (&out)[NV]) {
+    __shared__ double red[NV][kFoldLanes][kFoldCh];
+    const int ci = threadIdx.x % kFoldCh;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        double s = 0;
+        if (c < C) {
+            const float *p = partial + static_cast<int64_t>(v) * nchunks * C + c;
+#pragma unroll 8
+            for (int k = kl; k < nchunks; k += kFoldLanes) s += p[static_cast<int64_t>(k) * C];
+        }
+        red[v][kl][ci] = s;
+    }
+    __syncthreads();
+    if (kl == 0) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            double s = 0;
+#pragma unroll
+            for (int j = 0; j < kFoldLanes; ++j) s += red[v][j][ci];
+            out[v] = s;
+        }
+    }
+}
+
 inline Chunking chunking(const BNShape &sh) {
     const int cvec = sh.channels / 8;
     const int rpi = kBlock / cvec;
@@ -56,8 +90,10 @@ inline Chunking chunking(const BNShape &sh) {
     int64_t rpc = (64 * 1024 + row_bytes - 1) / row_bytes;  // >= 64 KiB per block
     rpc = ((rpc + rpi - 1) / rpi) * rpi;
     int64_t n = (sh.rows + rpc - 1) / rpc;
-    if (n > kMaxGrid) {
-        rpc = (sh.rows + kMaxGrid - 1) / kMaxGrid;
+    // <= 2 blocks per CU: enough bytes in flight (4 x 16 B loads per lane per
+    // step) while keeping the partials fold short.
+    if (n > kMaxChunks) {
+        rpc = (sh.rows + kMaxChunks - 1) / kMaxChunks;
         rpc = ((rpc + rpi - 1) / rpi) * rpi;
         n = (sh.rows + rpc - 1) / rpc;
     }
@@ -104,7 +140,24 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const uint4 *__restric
     const int64_t r_begin = static_cast<int64_t>(blockIdx.x) * rows_per_chunk;
     int64_t r_end = r_begin + rows_per_chunk;
     if (r_end > rows) r_end = rows;
-    for (int64_t r = r_begin + r0; r < r_end; r += RPI) {
+    int64_t r = r_begin + r0;
+    // 4 independent 16-B loads in flight per lane
+    for (; r + 3 * RPI < r_end; r += 4 * RPI) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = x[(r + u * RPI) * CVEC + cv];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float f[8];
+            unpack8(v[u], f);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                acc[0][k] += f[k];
+                acc[1][k] += f[k] * f[k];
+            }
+        }
+    }
+    for (; r < r_end; r += RPI) {
         float f[8];
         unpack8(x[r * CVEC + cv], f);
 #pragma unroll
@@ -116,18 +169,17 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const uint4 *__restric
     reduce_to_partials<CVEC, 2>(acc, lds, partial, C, gridDim.x);
 }
 
-// One thread per channel: fold partials, emit mean/invstd, running stats and
+// Fold partials (parallel over chunks), emit mean/invstd, running stats and
 // the affine coefficients scale = gamma*invstd, shift = beta - mean*scale.
-__global__ void bn_stats_finalize(const float *partial, int nchunks, int C, int64_t rows, const float *gamma,
-                                  const float *beta, float *mean, float *invstd, float *run_mean, float *run_var,
-                                  float momentum, float eps, float *coef) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double s = 0, q = 0;
-    for (int k = 0; k < nchunks; ++k) {
-        s += partial[static_cast<int64_t>(k) * C + c];
-        q += partial[(static_cast<int64_t>(nchunks) + k) * C + c];
-    }
+__global__ __launch_bounds__(kBlock) void bn_stats_finalize(const float *partial, int nchunks, int C, int64_t rows,
+                                                            const float *gamma, const float *beta, float *mean,
+                                                            float *invstd, float *run_mean, float *run_var,
+                                                            float momentum, float eps, float *coef) {
+    const int c = blockIdx.x * kFoldCh + threadIdx.x % kFoldCh, kl = threadIdx.x / kFoldCh;
+    double sums[2];
+    fold_partials<2>(partial, nchunks, C, c, kl, sums);
+    if (kl != 0 || c >= C) return;
+    double s = sums[0], q = sums[1];
     double m = s / rows;
     double var = q / rows - m * m;
     if (var < 0) var = 0;
@@ -215,7 +267,37 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const uint4 *__re
     const int64_t r_begin = static_cast<int64_t>(blockIdx.x) * rows_per_chunk;
     int64_t r_end = r_begin + rows_per_chunk;
     if (r_end > rows) r_end = rows;
-    for (int64_t r = r_begin + r0; r < r_end; r += RPI) {
+    // Accumulate sum(dz) and sum(dz * x); dgamma = invstd*(sum(dz*x) - mean*sum(dz))
+    // is formed in the finalize (one FMA per element here instead of three).
+    int64_t r = r_begin + r0;
+    for (; r + RPI < r_end; r += 2 * RPI) {
+        uint4 vg[2], vx[2], vy[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t i = (r + u * RPI) * CVEC + cv;
+            vg[u] = dy[i];
+            vx[u] = x[i];
+            if (RELU) vy[u] = y[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float g[8], xv[8];
+            unpack8(vg[u], g);
+            unpack8(vx[u], xv);
+            if (RELU) {
+                float yv[8];
+                unpack8(vy[u], yv);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                acc[0][k] += g[k];
+                acc[1][k] += g[k] * xv[k];
+            }
+        }
+    }
+    for (; r < r_end; r += RPI) {
         const int64_t i = r * CVEC + cv;
         float g[8], xv[8];
         unpack8(dy[i], g);
@@ -229,23 +311,24 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const uint4 *__re
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             acc[0][k] += g[k];
-            acc[1][k] += g[k] * (xv[k] - mu[k]) * is[k];
+            acc[1][k] += g[k] * xv[k];
         }
     }
+    (void)mu;
+    (void)is;
     reduce_to_partials<CVEC, 2>(acc, lds, partial, C, gridDim.x);
 }
 
 // dbeta = sum dz, dgamma = sum dz*xhat; dx = k1*dz + k2*x + k3.
-__global__ void bn_bwd_finalize(const float *partial, int nchunks, int C, int64_t rows, const float *gamma,
-                                const float *mean, const float *invstd, float *dgamma, float *dbeta, float *coef,
-                                bool training) {
-    int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double db = 0, dg = 0;
-    for (int k = 0; k < nchunks; ++k) {
-        db += partial[static_cast<int64_t>(k) * C + c];
-        dg += partial[(static_cast<int64_t>(nchunks) + k) * C + c];
-    }
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize(const float *partial, int nchunks, int C, int64_t rows,
+                                                          const float *gamma, const float *mean, const float *invstd,
+                                                          float *dgamma, float *dbeta, float *coef, bool training) {
+    const int c = blockIdx.x * kFoldCh + threadIdx.x % kFoldCh, kl = threadIdx.x / kFoldCh;
+    double sums[2];
+    fold_partials<2>(partial, nchunks, C, c, kl, sums);
+    if (kl != 0 || c >= C) return;
+    // sums[1] = sum(dz * x)  ->  dgamma = invstd * (sum(dz*x) - mean * sum(dz))
+    double db = sums[0], dg = static_cast<double>(invstd[c]) * (sums[1] - static_cast<double>(mean[c]) * db);
     dgamma[c] = static_cast<float>(dg);
     dbeta[c] = static_cast<float>(db);
     float g = gamma ? gamma[c] : 1.f;
@@ -341,7 +424,8 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
             bn_stats_kernel<CV><<<ch.nchunks, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), sh.rows,
                                                               ch.rows_per_chunk, partial);
         });
-        bn_stats_finalize<<<(C + 255) / 256, 256, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, beta, mean, invstd,
+        bn_stats_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, beta,
+                                                                         mean, invstd,
                                                           run_mean, run_var, momentum, eps, coef);
     } else {
         bn_eval_coef<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, run_mean, run_var, eps, mean, invstd, coef);
@@ -380,8 +464,8 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *y, const uint16_t *x
             bn_bwd_reduce_kernel<CV, false><<<ch.nchunks, kBlock, 0, s>>>(d, yy, xx, mean, invstd, sh.rows,
                                                                           ch.rows_per_chunk, partial);
     });
-    bn_bwd_finalize<<<(C + 255) / 256, 256, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean, invstd, dgamma,
-                                                    dbeta, coef, training);
+    bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
+                                                                   invstd, dgamma, dbeta, coef, training);
     int g = apply_grid(nvec, cvec);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;

@@ -44,6 +44,12 @@ void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *par
 void launch_variance(const float *s1, const float *s2, size_t n, float inv_np, float *partials, float *out,
                      hipStream_t s);
 
+// K6 (reference form): out[k] += sum over tensor k of (s2*inv - (s1*inv)^2)^2;
+// seg_off is a device int64 array of nseg+1 tensor start offsets; out must be zeroed.
+// The gradient variance is then sum_k sqrt(out[k]).
+void launch_seg_variance(const float *s1, const float *s2, size_t n, float inv_np, const int64_t *seg_off, int nseg,
+                         float *out, hipStream_t s);
+
 // K5 epilogue on device: from sumsq(small-batch grad) and sumsq(big-batch grad)
 // compute biased G/S estimates, update their EMAs in state[0..1] and write the
 // noise scale S/G into state[2].  state[3] counts updates.

@@ -147,7 +147,53 @@ __global__ void gns_update_kernel(const float *sumsq_small, const float *sumsq_b
 
 inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Per-segment (per-tensor) sum of d^2, d = s2*inv - (s1*inv)^2, over a flat
+// buffer whose tensors start at seg_off[k].  Block b owns a contiguous chunk;
+// lanes stride by 256 inside it, so loads stay coalesced and each lane's
+// segment index only moves forward: one agent-scope float atomic per
+// (lane, segment) it touched.
+__global__ __launch_bounds__(kBlock) void seg_variance_kernel(const float *s1, const float *s2, int64_t n,
+                                                              float inv, const int64_t *seg_off, int nseg,
+                                                              int64_t chunk, float *out) {
+    const int64_t b0 = static_cast<int64_t>(blockIdx.x) * chunk;
+    int64_t b1 = b0 + chunk;
+    if (b1 > n) b1 = n;
+    int64_t i = b0 + threadIdx.x;
+    if (i >= b1) return;
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (seg_off[mid] <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    int seg = lo;
+    int64_t seg_end = seg_off[seg + 1];
+    float acc = 0.f;
+    for (; i < b1; i += kBlock) {
+        while (i >= seg_end) {
+            if (acc != 0.f) atomicAdd(out + seg, acc);
+            acc = 0.f;
+            ++seg;
+            seg_end = seg_off[seg + 1];
+        }
+        float m = s1[i] * inv;
+        float d = s2[i] * inv - m * m;
+        acc += d * d;
+    }
+    if (acc != 0.f) atomicAdd(out + seg, acc);
+}
+
 }  // namespace
+
+void launch_seg_variance(const float *s1, const float *s2, size_t n, float inv_np, const int64_t *seg_off, int nseg,
+                         float *out, hipStream_t s) {
+    if (n == 0 || nseg == 0) return;
+    int64_t blocks = static_cast<int64_t>((n + kBlock * 16 - 1) / (kBlock * 16));
+    if (blocks > kMaxGrid) blocks = kMaxGrid;
+    int64_t chunk = (static_cast<int64_t>(n) + blocks - 1) / blocks;
+    seg_variance_kernel<<<static_cast<int>(blocks), kBlock, 0, s>>>(s1, s2, static_cast<int64_t>(n), inv_np, seg_off,
+                                                                     nseg, chunk, out);
+}
 
 void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s) {
     bool bf = dtype == DT_BF16;

@@ -12,7 +12,8 @@ from .collective import (Handle, all_gather, all_reduce, all_reduce_fn, all_redu
                          monitored_all_reduce, monitored_all_reduce_, rank, reduce, wait_all_handles, wait_handle)
 from .fuse import defuse, fuse, split_like
 from .local import save_variable, save_variables
-from .monitor import egress_rates, global_gradient_noise_scale, global_noise_scale, gradient_variance, sum_squares
+from .monitor import (GlobalNoiseScale, egress_rates, global_gradient_noise_scale, global_noise_scale,
+                      gradient_variance, noise_scale_estimates, sum_squares)
 from .p2p import request_variable, request_variable_with_template
 from .state import Counter, ExponentialMovingAverage, counter, exponential_moving_average
 from .topology import (get_neighbour_mask, get_peer_latencies, global_minimum_spanning_tree, minimum_spanning_tree,

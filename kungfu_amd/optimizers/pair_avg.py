@@ -1,0 +1,187 @@
+"""PairAveragingOptimizer (AD-PSGD: asynchronous decentralized pair averaging).
+
+Parity: ``srcs/python/kungfu/tensorflow/optimizers/async_sgd.py:13-142``: each
+step pick a random peer != self, *pull* its (fused) model from its store,
+``v <- (v + v_peer) / 2``, apply local gradients, save the model to the own
+store; a save + barrier at step 0; no global synchronisation afterwards.
+
+MI355X design:
+* the model store is device resident: two dedicated HIP allocations per peer
+  (double buffer), exported with HIP IPC at start-up (handles exchanged once
+  through the host runtime's all-gather).  A pull is a one-sided device copy
+  from the peer's buffer over xGMI -- the owner does not participate -- then
+  one fused K4 kernel averages into the flat parameter buffer.
+* the owner publishes its model by a D2D copy into the buffer not currently
+  advertised, and advertises ``(buffer, version)`` in its host store one step
+  later (when that copy has certainly completed); readers fetch the 16-byte
+  record over the host P2P channel first.  A reader can only see a torn
+  buffer if its pull spans more than one full owner iteration (the reference
+  has an unguarded race on its blob instead).
+* peers on other hosts (no IPC) are pulled through the host P2P store
+  (device -> host snapshot on the owner, TCP pull on the reader).
+CPU tensors use the host P2P store for everything.
+"""
+from __future__ import annotations
+
+import random
+import struct
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import ops
+from .._lib import dtype_code, hip, runtime
+from .core import KungFuOptimizer
+
+_REC = "kf:pair:rec"
+
+
+class DeviceModelStore:
+    def __init__(self, numel: int, device: torch.device, name: str):
+        H = hip()
+        self.numel = numel
+        self.name = name
+        self.device = device
+        self.rank, self.size = runtime.rank(), runtime.size()
+        self.bufs = [H.ipc_alloc(numel, device.index), H.ipc_alloc(numel, device.index)]
+        hs = b"".join(H.ipc_handle(b) for b in self.bufs)
+        mine = torch.frombuffer(bytearray(hs), dtype=torch.uint8).clone()
+        allh = ops.all_gather(mine, name="kf:pair:handles:" + name)
+        hosts = runtime.peers().split(",")
+        my_host = hosts[self.rank].split(":")[0]
+        self.local: Dict[int, bool] = {}
+        self.peer_bufs: Dict[int, List[torch.Tensor]] = {}
+        for r in range(self.size):
+            if r == self.rank:
+                continue
+            same_host = hosts[r].split(":")[0] == my_host
+            self.local[r] = same_host
+            if same_host:
+                raw = bytes(allh[r].tolist())
+                self.peer_bufs[r] = [H.ipc_open(raw[i * 64:(i + 1) * 64], numel, device.index) for i in range(2)]
+        self.cross_host = not all(self.local.values()) if self.local else False
+        self.version = 0
+        self.write_idx = 0
+        self._pending: Optional[torch.cuda.Event] = None
+        self._pending_idx = 0
+        self._host_copy = None
+
+    def publish(self, flat: torch.Tensor):
+        """Snapshot ``flat`` into the non-advertised buffer (stream-ordered)."""
+        idx = self.write_idx
+        self.bufs[idx].copy_(flat, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending, self._pending_idx = ev, idx
+        self.write_idx ^= 1
+        if self.cross_host:
+            self._host_copy = flat.detach().to("cpu", non_blocking=False)
+
+    def advertise(self):
+        if self._pending is None:
+            return
+        self._pending.synchronize()  # issued one iteration ago: normally already complete
+        self.version += 1
+        rec = torch.tensor([self._pending_idx, self.version], dtype=torch.int64)
+        runtime.save(_REC + self.name, rec.data_ptr(), 16)
+        if self._host_copy is not None:
+            runtime.save("kf:pair:model:" + self.name, self._host_copy.data_ptr(), self.numel * 4)
+        self._pending = None
+
+    def pull(self, target: int, out: torch.Tensor) -> bool:
+        rec = torch.zeros(2, dtype=torch.int64)
+        if not runtime.request(target, "", _REC + self.name, rec.data_ptr(), 16):
+            return False
+        if self.local.get(target, False):
+            out.copy_(self.peer_bufs[target][int(rec[0])], non_blocking=True)
+            return True
+        h = torch.empty(self.numel, dtype=torch.float32)
+        if not runtime.request(target, "", "kf:pair:model:" + self.name, h.data_ptr(), self.numel * 4):
+            return False
+        out.copy_(h)
+        return True
+
+
+class _PairAveraging(KungFuOptimizer):
+    def __init__(self, optimizer, named_parameters=None, fuse_requests: bool = True,
+                 fused_model_name: str = "model", fused: bool = True, seed: Optional[int] = None):
+        super().__init__(optimizer, named_parameters, fused=fused)
+        self.fused_model_name = fused_model_name
+        self.fuse_requests = fuse_requests
+        self.rank, self.size = runtime.rank(), runtime.size()
+        self.rng = random.Random(self.rank if seed is None else seed + self.rank)
+        self.step_count = 0
+        self.last_target = -1
+        self.store: Optional[DeviceModelStore] = None
+        if self.space is not None and self.size > 1:
+            self.store = DeviceModelStore(self.space.numel, self.space.device, fused_model_name)
+            self._other = torch.empty_like(self.space.flat_param)
+
+    def random_peer(self) -> int:
+        t = self.rng.randrange(self.size)
+        return (t + 1) % self.size if t == self.rank else t
+
+    # -- CPU / host-store helpers --------------------------------------------
+    def _host_vars(self):
+        return [p for p in self.params if p.grad is not None]
+
+    def _host_save(self):
+        vs = self._host_vars()
+        if self.fuse_requests:
+            ops.save_variable(ops.fuse([v.detach() for v in vs]), name=self.fused_model_name)
+        else:
+            for i, v in enumerate(vs):
+                ops.save_variable(v, name="%s:%d" % (self.fused_model_name, i))
+
+    def _host_pull_average(self, target):
+        vs = self._host_vars()
+        with torch.no_grad():
+            if self.fuse_requests:
+                tmpl = ops.fuse([v.detach() for v in vs])
+                other = ops.request_variable(target, self.fused_model_name, tmpl.shape, tmpl.dtype)
+                if other is None:
+                    return
+                others = ops.split_like(other, [v.shape for v in vs])
+            else:
+                others = [ops.request_variable(target, "%s:%d" % (self.fused_model_name, i), v.shape, v.dtype)
+                          for i, v in enumerate(vs)]
+            for v, o in zip(vs, others):
+                if o is not None:
+                    v.add_(o.to(v.device)).mul_(0.5)
+
+    # -- algorithm ----------------------------------------------------------------
+    def _before_step(self):
+        if self.size == 1:
+            return
+        if self.step_count == 0:
+            if self.store is not None:
+                self.store.publish(self.space.flat_param)
+                self.store.advertise()
+            else:
+                self._host_save()
+            runtime.barrier()
+        target = self.random_peer()
+        self.last_target = target
+        if self.store is not None:
+            self.store.advertise()
+            if self.store.pull(target, self._other):
+                hip().axpby(self.space.flat_param, self._other, None, 0.5, 0.5)
+        else:
+            self._host_pull_average(target)
+
+    def _after_step(self):
+        self.step_count += 1
+        if self.size == 1:
+            return
+        if self.store is not None:
+            self.store.publish(self.space.flat_param)
+        else:
+            self._host_save()
+
+
+def PairAveragingOptimizer(optimizer, named_parameters=None, fuse_requests: bool = True,
+                           fused_model_name: str = "model", fused: bool = True, name=None, use_locking=False,
+                           with_keras=False):
+    """Wrap ``optimizer`` with AD-PSGD pair averaging (see module doc)."""
+    return _PairAveraging(optimizer, named_parameters, fuse_requests=fuse_requests,
+                          fused_model_name=fused_model_name, fused=fused)

@@ -13,6 +13,7 @@ path (the reference synchronises after every NCCL op).
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Optional
 
@@ -58,8 +59,10 @@ class DeviceComm:
         name = "kungfu::rccl_uid::%s::v%d" % (scope, self.version)
         uid = _bcast_bytes(uid, name) if scope == "global" else _local_bcast_bytes(uid, name)
         self.comm = H.RcclComm(uid, self.rank, self.size, self.device)
-        # High priority so bucket all-reduces are not starved by backward kernels.
-        self.stream = torch.cuda.Stream(device=self.device, priority=-1)
+        # Normal priority: a high-priority HIP stream measured 2x SLOWER for the
+        # whole ResNet-50 step on MI355X (63 vs 32 ms, 1 GPU, profiles/README.md).
+        prio = int(os.environ.get("KUNGFU_COMM_STREAM_PRIORITY", "0"))
+        self.stream = torch.cuda.Stream(device=self.device, priority=prio)
 
     # -- collectives on an explicit stream (default: the comm stream) ---------
     def _s(self, stream) -> int:

@@ -48,7 +48,9 @@ class Bucket:
 class GradReducer:
     def __init__(self, space: FlatParamSpace, op: str = "avg", bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
-                 skip_single: bool = False):
+                 skip_single: bool = True):
+        # skip_single: with one peer the average of the gradients IS the local
+        # gradient, so no collective is issued (the engine's hooks still run).
         self.space = space
         self.op = op
         cap_mb = float(os.environ.get("KUNGFU_BUCKET_MB", bucket_mb if bucket_mb is not None else 32.0))
@@ -91,6 +93,11 @@ class GradReducer:
         self._enabled = True
         self._hooks = []
         self._warned = False
+        # Optional callbacks (used by the monitoring optimizers):
+        #   pre_reduce(bucket, local_grad_view)  on the comm stream, before the all-reduce
+        #   post_finish()                        on the compute stream, after all buckets
+        self.pre_reduce = None
+        self.post_finish = None
         for i, p in enumerate(space.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         self._reset()
@@ -136,6 +143,9 @@ class GradReducer:
         ev.record(torch.cuda.current_stream(comm.device))
         comm.stream.wait_event(ev)
         g = self.space.flat_grad[b.start:b.end]
+        if self.pre_reduce is not None:
+            with torch.cuda.stream(comm.stream):
+                self.pre_reduce(b, g)
         if self.comm_dtype is not None and self.comm_dtype != g.dtype:
             with torch.cuda.stream(comm.stream):
                 c = g.to(self.comm_dtype)
@@ -160,6 +170,8 @@ class GradReducer:
         if self._expected is None and not self._warned:
             self._expected = list(self._fires)
         self._reset()
+        if self.post_finish is not None:
+            self.post_finish()
 
     def _reset(self):
         for b in self.buckets:

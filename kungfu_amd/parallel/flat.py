@@ -59,23 +59,47 @@ class FlatParamSpace:
         self.numel = off
         self.flat_param = torch.zeros(self.numel, dtype=dtype, device=dev)
         self.flat_grad = torch.zeros(self.numel, dtype=dtype, device=dev)
+        # Keep each parameter's memory layout (e.g. channels_last conv weights):
+        # the flat slot holds the parameter's dense storage order and the view
+        # re-applies its strides, so MIOpen sees the same NHWC weights.
+        self.strides = []
+        for p in ps:
+            st = p.stride() if self._dense(p) else torch.empty(p.shape).stride()
+            self.strides.append(st)
         with torch.no_grad():
-            for p, (o, n) in zip(ps, self.offsets):
-                self.flat_param[o:o + n].copy_(p.detach().reshape(-1).to(dtype))
-                p.data = self.flat_param[o:o + n].view_as(p)
-                p.grad = self.flat_grad[o:o + n].view_as(p)
+            for i, (p, (o, n)) in enumerate(zip(ps, self.offsets)):
+                v = self._view(self.flat_param, i)
+                v.copy_(p.detach())
+                p.data = v
+                p.grad = self._view(self.flat_grad, i)
         self._index = {id(p): i for i, p in enumerate(ps)}
+
+    @staticmethod
+    def _dense(p) -> bool:
+        """True if p's strides are a permutation of a contiguous layout."""
+        if p.numel() <= 1:
+            return True
+        dims = sorted((s, d) for d, s in zip(p.shape, p.stride()) if d != 1)
+        expect = 1
+        for s, d in dims:
+            if s != expect:
+                return False
+            expect *= d
+        return True
+
+    def _view(self, flat: torch.Tensor, i: int) -> torch.Tensor:
+        o, n = self.offsets[i]
+        p = self.params[i]
+        return torch.as_strided(flat, p.shape, self.strides[i], o)
 
     def index(self, p) -> int:
         return self._index[id(p)]
 
     def grad_view(self, i: int) -> torch.Tensor:
-        o, n = self.offsets[i]
-        return self.flat_grad[o:o + n].view_as(self.params[i])
+        return self._view(self.flat_grad, i)
 
     def param_view(self, i: int) -> torch.Tensor:
-        o, n = self.offsets[i]
-        return self.flat_param[o:o + n].view_as(self.params[i])
+        return self._view(self.flat_param, i)
 
     def zero_grad(self):
         self.flat_grad.zero_()

@@ -1,0 +1,58 @@
+"""Distributed optimizers on CPU through kungfu-run.
+
+S-SGD convergence regression (parity: tests/python/integration/test_mnist_slp.py
+and scripts/tests/run-train-tests.sh:76-81): with contiguous sharding and
+gradient averaging, training on np peers reproduces single-process training on
+the global batch, so weights and accuracy must not depend on np.  The
+reference pins exact MNIST accuracies (0.9137 / 0.8884 / 0.8845 / 0.8193 for
+global batch 50 / 500 / 600 / 6000); MNIST is not available offline, so the
+same property is checked on the deterministic synthetic set ("parity
+unpinned" for the absolute numbers; with KUNGFU_MNIST_DIR set the worker uses
+real MNIST).
+"""
+import re
+
+import pytest
+
+from conftest import kungfu_run, worker
+
+
+def results(out):
+    return re.findall(r"SLP_RESULT rank=(\d+) np=(\d+) acc=([\d.]+) w=(\S+)(.*)", out)
+
+
+@pytest.mark.parametrize("batch,nps", [(500, [1, 2, 4]), (600, [1, 3]), (6000, [1, 4])])
+def test_ssgd_np_invariance(batch, nps):
+    seen = {}
+    for np_ in nps:
+        r = kungfu_run(np_, [worker("slp_train.py"), "--batch", str(batch), "--epochs", "2"], timeout=240)
+        assert r.returncode == 0, r.stdout[-3000:]
+        res = results(r.stdout)
+        assert len(res) == np_, r.stdout[-3000:]
+        digests = {x[3] for x in res}
+        assert len(digests) == 1, res  # all peers hold the same model
+        seen[np_] = (float(res[0][2]), float(res[0][3]))
+    w0 = seen[nps[0]][1]
+    for np_, (acc, w) in seen.items():
+        assert abs(w - w0) <= 1e-5 * abs(w0), seen  # same model up to f32 summation order
+        assert abs(acc - seen[nps[0]][0]) <= 2e-3, seen
+
+
+@pytest.mark.parametrize("opt", ["sma", "pair", "ada", "gns", "var"])
+def test_other_optimizers_train(opt):
+    r = kungfu_run(2, [worker("slp_train.py"), "--batch", "50", "--epochs", "2", "--opt", opt], timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    res = results(r.stdout)
+    assert len(res) == 2, r.stdout[-3000:]
+    for _, _, acc, _, extra in res:
+        assert float(acc) > 0.3, res  # learns (chance = 0.1)
+    if opt in ("sma", "ada"):
+        # model averaging keeps replicas close but not identical until ADA switches
+        pass
+    if opt == "ada":
+        ws = [float(x[3]) for x in res]
+        assert abs(ws[0] - ws[1]) <= 1e-6 * abs(ws[0])  # after the switch + broadcast, S-SGD keeps them identical
+    if opt == "gns":
+        assert all("gns=" in x[4] and "None" not in x[4] for x in res)
+    if opt == "var":
+        assert all("var=" in x[4] for x in res)
