@@ -85,7 +85,9 @@ void pump(int fd, FILE *out, const std::string &prefix, const std::string &file,
 int run_once(const Proc &p, int color, bool verbose, const std::string &log_prefix, std::atomic<bool> *cancel,
              std::string *first_stderr) {
     int out_pipe[2], err_pipe[2];
-    if (::pipe(out_pipe) != 0 || ::pipe(err_pipe) != 0) return 127;
+    // O_CLOEXEC: workers forked later must not inherit these write ends, or
+    // this worker's output pumps would not see EOF until every sibling exits.
+    if (::pipe2(out_pipe, O_CLOEXEC) != 0 || ::pipe2(err_pipe, O_CLOEXEC) != 0) return 127;
     pid_t pid = ::fork();
     if (pid < 0) return 127;
     if (pid == 0) {

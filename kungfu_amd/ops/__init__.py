@@ -2,8 +2,9 @@
 (``srcs/python/kungfu/tensorflow/ops/__init__.py:1-83``) and ``kungfu.torch.ops``,
 re-implemented for PyTorch-ROCm tensors.
 """
-from .adapt import (calc_stats, check_interference, get_init_checkpoint, log_stats, print_strategy_stats, resize,
-                    resize_cluster_from_url, set_strategy, set_tree, step_based_schedule, StepBasedSchedule)
+from .adapt import (StepBasedSchedule, calc_stats, check_interference, get_init_checkpoint, log_stats,
+                    print_strategy_stats, resize, resize_cluster, resize_cluster_from_url, set_strategy, set_tree,
+                    step_based_schedule)
 from .collective import (Handle, all_gather, all_reduce, all_reduce_fn, all_reduce_with, barrier, broadcast,
                          broadcast_parameters, cluster_size, consensus, cross_all_reduce_, gather, group_all_reduce,
                          group_all_reduce_, group_hierarchical_nccl_all_reduce, group_nccl_all_reduce,

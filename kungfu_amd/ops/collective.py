@@ -35,10 +35,20 @@ _counters: Dict[str, itertools.count] = {}
 _clock = threading.Lock()
 
 
+_counter_version = [None]
+
+
 def _auto_name(kind: str) -> str:
+    """Per-cluster-version op counter: after an elastic resize every member of
+    the new cluster (old and newly spawned workers) counts from 0 again, so
+    auto-named collectives keep matching across peers."""
+    ver = runtime.cluster_version()
     with _clock:
+        if _counter_version[0] != ver:
+            _counters.clear()
+            _counter_version[0] = ver
         c = _counters.setdefault(kind, itertools.count())
-        return "kf:%s:%d" % (kind, next(c))
+        return "kf:%s:v%d:%d" % (kind, ver, next(c))
 
 
 def _gpu_host_staging() -> bool:

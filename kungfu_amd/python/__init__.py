@@ -196,8 +196,11 @@ def get_hip_index() -> int:
 
     Under ``kungfu-run`` the worker sees exactly its GPU (HIP_VISIBLE_DEVICES),
     so the index is 0 unless ``-allow-xgmi`` kept all GPUs visible; under
-    torchrun it is LOCAL_RANK.
+    torchrun it is LOCAL_RANK.  ``KUNGFU_FORCE_DEVICE`` overrides (tests that
+    co-locate several peers on one GPU).
     """
+    if "KUNGFU_FORCE_DEVICE" in os.environ:
+        return int(os.environ["KUNGFU_FORCE_DEVICE"])
     if "KUNGFU_SELF_SPEC" in os.environ:
         if os.environ.get("KUNGFU_ALLOW_XGMI", "false") == "true":
             return current_local_rank()

@@ -1,0 +1,250 @@
+"""GPU tests (run with -m gpu on an MI355X).  Every numerics test compares a
+HIP kernel with a float32 PyTorch reference of the same op."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT, kungfu_run, worker
+
+pytestmark = pytest.mark.gpu
+
+needs_gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+
+
+@pytest.fixture(scope="module")
+def H():
+    from kungfu_amd._lib import hip
+
+    return hip()
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12)).item()
+
+
+@needs_gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [1, 1000, (1 << 20) + 3])
+def test_reduce_kernel(H, dtype, n):
+    x = torch.randn(n, device="cuda").to(dtype)
+    y = torch.randn(n, device="cuda").to(dtype)
+    z = torch.empty_like(x)
+    for op, f in [(0, torch.add), (1, torch.minimum), (2, torch.maximum), (3, torch.mul)]:
+        H.reduce(z, x, y, op)
+        torch.testing.assert_close(z.float(), f(x.float(), y.float()).to(dtype).float(), rtol=0, atol=0)
+
+
+@needs_gpu
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_fused_sgd_matches_torch(H, nesterov):
+    from kungfu_amd.optimizers import FusedSGD
+    from kungfu_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    m1 = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 5)).cuda()
+    m2 = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.Flatten(), torch.nn.Linear(8 * 6 * 6, 5)).cuda()
+    m2.load_state_dict(m1.state_dict())
+    m2 = m2.to(memory_format=torch.channels_last)
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=nesterov)
+    o2 = FusedSGD(FlatParamSpace(m2.parameters()), lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=nesterov)
+    for _ in range(3):
+        x = torch.randn(4, 3, 8, 8, device="cuda")
+        for m, o in [(m1, o1), (m2, o2)]:
+            o.zero_grad()
+            m(x).square().sum().backward()
+            o.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@needs_gpu
+def test_fused_adam_matches_torch(H):
+    from kungfu_amd.optimizers import FusedAdam
+    from kungfu_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    m1 = torch.nn.Linear(37, 11).cuda()
+    m2 = torch.nn.Linear(37, 11).cuda()
+    m2.load_state_dict(m1.state_dict())
+    o1 = torch.optim.AdamW(m1.parameters(), lr=1e-2, weight_decay=0.01)
+    o2 = FusedAdam(FlatParamSpace(m2.parameters()), lr=1e-2, weight_decay=0.01, adamw=True)
+    for _ in range(4):
+        x = torch.randn(8, 37, device="cuda")
+        for m, o in [(m1, o1), (m2, o2)]:
+            o.zero_grad()
+            m(x).square().sum().backward()
+            o.step()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+
+
+@needs_gpu
+def test_norms_variance_axpby(H):
+    n = (1 << 21) + 5
+    a, b = torch.randn(n, device="cuda"), torch.randn(n, device="cuda")
+    s = H.sumsq2(a, b)
+    ref = torch.stack([a.double().pow(2).sum(), b.double().pow(2).sum()])
+    assert _rel(s.double(), ref) < 1e-5
+    sb = H.sumsq2(a.bfloat16(), None)
+    assert abs(sb[0].item() / a.bfloat16().double().pow(2).sum().item() - 1) < 1e-5
+    s1 = torch.randn(n, device="cuda")
+    s2 = s1 * s1 + torch.rand(n, device="cuda")
+    v = H.variance(s1, s2, 0.25)
+    vr = (s2.double() * 0.25 - (s1.double() * 0.25) ** 2).abs().sum()
+    assert abs(v.item() / vr.item() - 1) < 1e-4
+    offs = torch.tensor([0, 10, 1000, 100000, n], dtype=torch.int64, device="cuda")
+    sv = H.seg_variance(s1, s2, offs, 0.5).item()
+    d = s2.double() * 0.5 - (s1.double() * 0.5) ** 2
+    svr = sum(d[offs[i]:offs[i + 1]].norm().item() for i in range(4))
+    assert abs(sv / svr - 1) < 1e-4
+    y, x, z = torch.randn(n, device="cuda"), torch.randn(n, device="cuda"), torch.empty(n, device="cuda")
+    y0 = y.clone()
+    H.axpby(y, x, z, 0.9, 0.1)
+    torch.testing.assert_close(y, 0.9 * y0 + 0.1 * x)
+    torch.testing.assert_close(z, y)
+
+
+@needs_gpu
+def test_gns_update_device(H):
+    st = torch.zeros(4, device="cuda")
+    sq_small, sq_big = torch.tensor([4.0], device="cuda"), torch.tensor([1.0], device="cuda")
+    H.gns_update(sq_small, sq_big, 32.0, 256.0, 0.6, st)
+    G = (256 * 1.0 - 32 * 4.0) / (256 - 32)
+    S = (4.0 - 1.0) / (1 / 32 - 1 / 256)
+    assert abs(st[2].item() - S / G) / (S / G) < 1e-5 and st[3].item() == 1
+
+
+@needs_gpu
+def test_pack_unpack(H):
+    from kungfu_amd.ops import defuse, fuse
+
+    ts = [torch.randn(k, device="cuda") for k in [3, 100, 4097, 1, 65536]]
+    flat = fuse(ts, scale=2.0)
+    torch.testing.assert_close(flat, torch.cat(ts) * 2)
+    outs = [torch.empty_like(t) for t in ts]
+    defuse(flat, outs, scale=0.5)
+    for t, o in zip(ts, outs):
+        torch.testing.assert_close(o, t)
+    flat16 = fuse(ts, dtype=torch.bfloat16)
+    torch.testing.assert_close(flat16.float(), torch.cat(ts).bfloat16().float())
+
+
+@needs_gpu
+@pytest.mark.parametrize("shape", [(4, 64, 16, 16), (8, 256, 14, 14), (2, 2048, 7, 7), (3, 128, 5, 9)])
+@pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False)])
+def test_fused_bn(shape, relu, with_res):
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.fused_bn import bn_act
+
+    torch.manual_seed(1)
+    N, C, Hh, W = shape
+    x = (torch.randn(shape, device="cuda") * 2 + 0.5).bfloat16().to(memory_format=torch.channels_last)
+    res = torch.randn_like(x) if with_res else None
+    w, b = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    rm2, rv2 = rm.clone(), rv.clone()
+    xr = x.detach().float().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    resr = res.detach().float().requires_grad_() if with_res else None
+    yr = F.batch_norm(xr, rm2, rv2, wr, br, True, 0.1, 1e-5)
+    if with_res:
+        yr = yr + resr
+    if relu:
+        yr = F.relu(yr)
+    xa, wa, ba = x.detach().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    resa = res.detach().requires_grad_() if with_res else None
+    ya = bn_act(xa, wa, ba, rm, rv, True, 0.1, 1e-5, relu=relu, res=resa)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    ya.backward(g.bfloat16().to(memory_format=torch.channels_last))
+    for a, r in [(ya, yr), (xa.grad, xr.grad), (wa.grad, wr.grad), (ba.grad, br.grad), (rm, rm2), (rv, rv2)]:
+        assert _rel(a, r) < 3e-2
+    if with_res:
+        assert _rel(resa.grad, resr.grad) < 3e-2
+
+
+@needs_gpu
+def test_rccl_single_rank_and_ops():
+    import kungfu_amd as kf
+    from kungfu_amd.parallel.comm import get_device_comm
+
+    kf.init()
+    torch.cuda.set_device(0)
+    t = torch.arange(1000, device="cuda", dtype=torch.float32)
+    torch.testing.assert_close(kf.ops.all_reduce(t), t)
+    b = kf.ops.broadcast(t)
+    torch.testing.assert_close(b, t)
+    g = kf.ops.all_gather(t[:10])
+    assert g.shape == (1, 10)
+    comm = get_device_comm()
+    out = torch.empty(10, device="cuda")
+    comm.reduce_scatter(t[:10].clone(), out)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, t[:10])
+
+
+@needs_gpu
+def test_resnet_step_ssgd_fused_vs_plain():
+    """One ResNet-18 step through the engine (fused BN + flat SGD) vs plain torch."""
+    import torch.nn.functional as F
+
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet18
+
+    kf.init()
+    torch.manual_seed(0)
+    m1 = resnet18(fused_bn=False).cuda().to(memory_format=torch.channels_last)
+    m2 = resnet18(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    m2.load_state_dict(m1.state_dict())
+    o1 = torch.optim.SGD(m1.parameters(), lr=0.05, momentum=0.9)
+    o2 = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m2.parameters(), lr=0.05, momentum=0.9))
+    x = torch.randn(8, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (8,), device="cuda")
+    losses = []
+    for m, o in [(m1, o1), (m2, o2)]:
+        ls = []
+        for _ in range(3):
+            o.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            o.step()
+            ls.append(loss.item())
+        losses.append(ls)
+    for a, b in zip(*losses):
+        assert abs(a - b) < 0.05 * abs(a) + 0.05, losses
+
+
+@needs_gpu
+def test_pair_averaging_ipc_two_procs_one_gpu():
+    """Two peers on ONE GPU: the HIP-IPC device model store (one-sided pulls)."""
+    r = kungfu_run(2, [worker("pair_gpu.py")], timeout=300, extra=["-allow-xgmi"],
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"})
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("PAIR_GPU_OK") == 2, r.stdout[-4000:]
+
+
+@needs_gpu
+def test_smoke_entry():
+    r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0 and "smoke ok" in r.stdout, r.stdout[-3000:]
+
+
+@needs_gpu
+def test_bench_json():
+    import json
+
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "2", "--batch", "64"], cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"]:
+        assert k in d
+    assert d["value"] > 0 and d["n_gpus"] == 1

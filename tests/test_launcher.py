@@ -1,0 +1,122 @@
+"""kungfu-run launcher: simple mode, fail-fast, timeout, env contract, and
+watch-mode elastic resize with the builtin config server
+(parity: scripts/tests/run-tensorflow-resize-test.sh, runner/local/local.go:77-80)."""
+import os
+import re
+import subprocess
+import sys
+import textwrap
+
+from conftest import ROOT, free_port_block, kungfu_run, worker
+
+
+def _script(tmp_path, body):
+    p = tmp_path / "w.py"
+    p.write_text(textwrap.dedent(body))
+    return str(p)
+
+
+def test_env_contract(tmp_path):
+    s = _script(tmp_path, """
+        import os
+        keys = ["KUNGFU_SELF_SPEC", "KUNGFU_INIT_PEERS", "KUNGFU_INIT_RUNNERS", "KUNGFU_PARENT_ID",
+                "KUNGFU_INIT_CLUSTER_VERSION", "KUNGFU_ALLREDUCE_STRATEGY", "KUNGFU_JOB_START_TIMESTAMP",
+                "KUNGFU_PROC_START_TIMESTAMP", "KUNGFU_HIP_VISIBLE_DEVICES"]
+        assert all(k in os.environ for k in keys), [k for k in keys if k not in os.environ]
+        assert os.environ["KUNGFU_SELF_SPEC"] in os.environ["KUNGFU_INIT_PEERS"].split(",")
+        print("ENV_OK", os.environ["KUNGFU_SELF_SPEC"], os.environ["KUNGFU_ALLREDUCE_STRATEGY"])
+    """)
+    r = kungfu_run(3, [s], strategy="RING")
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count("ENV_OK") == 3 and "RING" in r.stdout
+
+
+def test_fail_fast(tmp_path):
+    s = _script(tmp_path, """
+        import os, sys, time
+        peers = os.environ["KUNGFU_INIT_PEERS"].split(",")
+        if peers.index(os.environ["KUNGFU_SELF_SPEC"]) == 1:
+            sys.exit(3)
+        time.sleep(60)
+    """)
+    r = kungfu_run(2, [s], timeout=60)
+    assert r.returncode != 0
+    assert "exited with error" in r.stdout
+
+
+def test_timeout(tmp_path):
+    s = _script(tmp_path, "import time; time.sleep(60)\n")
+    r = kungfu_run(1, [s], extra=["-timeout", "2s"], timeout=60)
+    assert r.returncode == 124
+
+
+def test_logdir_and_prefix(tmp_path):
+    s = _script(tmp_path, "print('hello-from-worker')\n")
+    logdir = tmp_path / "logs"
+    r = kungfu_run(2, [s], extra=["-logdir", str(logdir)])
+    assert r.returncode == 0
+    assert "::stdout] hello-from-worker" in r.stdout
+    files = os.listdir(logdir)
+    assert any(f.endswith(".stdout.log") for f in files), files
+
+
+def test_elastic_resize_watch_mode():
+    base = free_port_block(16)
+    cfg = base + 15
+    r = kungfu_run(1, [worker("elastic.py"), "--schedule", "1:3,2:3,3:3,1:3", "--max-step", "12"], timeout=240,
+                   port_base=base,
+                   extra=["-w", "-builtin-config-port", str(cfg), "-config-server",
+                          "http://127.0.0.1:%d/config" % cfg, "-H", "127.0.0.1:4"])
+    assert r.returncode == 0, r.stdout[-5000:]
+    done = re.findall(r"ELASTIC_DONE rank=(\d+) np=(\d+) step=(\d+) w=([\d.]+) v=(\d+)", r.stdout)
+    assert len(done) == 1, r.stdout[-5000:]
+    rank, np_, step, w, v = done[0]
+    assert (rank, np_, step) == ("0", "1", "12")
+    assert float(w) == 100.0  # rank 0's model survived every resize
+    assert int(v) == 3  # three membership changes
+    assert r.stdout.count("ELASTIC_DETACHED") == 2  # the two extra workers left at the 3 -> 1 shrink
+    assert "resize 1 -> 2" in r.stdout and "resize 2 -> 3" in r.stdout
+
+
+def test_config_server_rest():
+    from kungfu_amd._lib import runtime as K
+    import json
+
+    port = free_port_block(1)
+    s = K.ConfigServer(port)
+    s.start()
+    url = "http://127.0.0.1:%d/config" % port
+    st, body = K.http_request("GET", url, "")
+    assert st == 404
+    c = {"Runners": ["127.0.0.1:38080"], "Workers": ["127.0.0.1:10000", "127.0.0.1:10001"]}
+    st, _ = K.http_request("PUT", url, json.dumps(c))
+    assert st == 200
+    st, body = K.http_request("GET", url, "")
+    assert st == 200 and json.loads(body)["Workers"] == c["Workers"]
+    bad = {"Runners": ["127.0.0.1:38080"], "Workers": ["10.0.0.9:10000"]}
+    st, _ = K.http_request("PUT", url, json.dumps(bad))
+    assert st == 400
+    st, _ = K.http_request("DELETE", url, "")
+    assert st == 200
+    st, _ = K.http_request("GET", url, "")
+    assert st == 404
+    s.stop()
+
+
+def test_config_server_binary(tmp_path):
+    port = free_port_block(1)
+    p = subprocess.Popen([os.path.join(ROOT, "bin", "kungfu-config-server"), "-port", str(port), "-ttl", "20"])
+    try:
+        import time
+        from kungfu_amd._lib import runtime as K
+        for _ in range(50):
+            st, _ = K.http_request("GET", "http://127.0.0.1:%d/config" % port, "")
+            if st != -1:
+                break
+            time.sleep(0.1)
+        assert st == 404
+        K.http_request("GET", "http://127.0.0.1:%d/stop" % port, "")
+        assert p.wait(timeout=10) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
