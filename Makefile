@@ -96,3 +96,22 @@ $(HIP_MOD): $(HIP_OBJS) $(HIP_BIND)
 
 clean:
 	rm -rf $(BUILD) $(RT_LIB) $(PY_MOD) $(HIP_MOD) $(BINS)
+
+# ---- native tests (host only; sanitizer builds for race / memory checks) ----
+NT_SRCS := tests/native/test_runtime.cpp $(patsubst %,csrc/runtime/%.cpp,$(RT_SRCS))
+.PHONY: native-test native-test-asan native-test-tsan
+build/native_test: $(NT_SRCS) $(wildcard csrc/include/kungfu/*.hpp)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -g -o $@ $(NT_SRCS) $(LDFLAGS)
+build/native_test_asan: $(NT_SRCS) $(wildcard csrc/include/kungfu/*.hpp)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -o $@ $(NT_SRCS) $(LDFLAGS)
+build/native_test_tsan: $(NT_SRCS) $(wildcard csrc/include/kungfu/*.hpp)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -O1 -g -fsanitize=thread -o $@ $(NT_SRCS) $(LDFLAGS)
+native-test: build/native_test
+	./build/native_test
+native-test-asan: build/native_test_asan
+	./build/native_test_asan 42000
+native-test-tsan: build/native_test_tsan
+	TSAN_OPTIONS=halt_on_error=1 ./build/native_test_tsan 43000

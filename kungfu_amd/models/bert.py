@@ -1,0 +1,70 @@
+"""BERT-base encoder for masked-LM pre-training throughput (BASELINE.json config 5:
+"BERT-base SynchronousSGD + gradient-noise-scale monitor + elastic resize").
+12 layers, hidden 768, 12 heads, FFN 3072, vocab 30522, ~110 M parameters.
+Attention uses torch's scaled_dot_product_attention (flash kernels on ROCm)."""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class BertLayer(nn.Module):
+    def __init__(self, d=768, heads=12, ffn=3072, dropout=0.1):
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(d, 3 * d)
+        self.out = nn.Linear(d, d)
+        self.ln1 = nn.LayerNorm(d, eps=1e-12)
+        self.fc1 = nn.Linear(d, ffn)
+        self.fc2 = nn.Linear(ffn, d)
+        self.ln2 = nn.LayerNorm(d, eps=1e-12)
+        self.dropout = dropout
+
+    def forward(self, x, mask=None):
+        B, S, D = x.shape
+        q, k, v = self.qkv(x).view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
+                                           dropout_p=self.dropout if self.training else 0.0)
+        a = a.transpose(1, 2).reshape(B, S, D)
+        x = self.ln1(x + F.dropout(self.out(a), self.dropout, self.training))
+        h = self.fc2(F.gelu(self.fc1(x)))
+        return self.ln2(x + F.dropout(h, self.dropout, self.training))
+
+
+class BertForPreTraining(nn.Module):
+    def __init__(self, vocab=30522, d=768, layers=12, heads=12, ffn=3072, max_pos=512, type_vocab=2):
+        super().__init__()
+        self.tok = nn.Embedding(vocab, d)
+        self.pos = nn.Embedding(max_pos, d)
+        self.typ = nn.Embedding(type_vocab, d)
+        self.ln = nn.LayerNorm(d, eps=1e-12)
+        self.layers = nn.ModuleList([BertLayer(d, heads, ffn) for _ in range(layers)])
+        self.mlm_dense = nn.Linear(d, d)
+        self.mlm_ln = nn.LayerNorm(d, eps=1e-12)
+        self.mlm_bias = nn.Parameter(torch.zeros(vocab))
+        self.nsp = nn.Linear(d, 2)
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, ids, types=None):
+        B, S = ids.shape
+        pos = torch.arange(S, device=ids.device)
+        types = torch.zeros_like(ids) if types is None else types
+        x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ(types))
+        for layer in self.layers:
+            x = layer(x)
+        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
+        mlm = h @ self.tok.weight.t() + self.mlm_bias  # tied output embedding
+        return mlm, self.nsp(x[:, 0])
+
+
+def bert_base(**kw):
+    kw.pop("fused_bn", None)
+    return BertForPreTraining(**kw)

@@ -1,0 +1,113 @@
+"""Inception-v3 (the reference's third headline model),
+299x299 input, no auxiliary head (training throughput benchmark form)."""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class BasicConv2d(nn.Module):
+    def __init__(self, cin, cout, **kw):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
+        self.bn = nn.BatchNorm2d(cout, eps=0.001)
+
+    def forward(self, x):
+        return F.relu(self.bn(self.conv(x)), inplace=True)
+
+
+class InceptionA(nn.Module):
+    def __init__(self, cin, pool_features):
+        super().__init__()
+        self.b1 = BasicConv2d(cin, 64, kernel_size=1)
+        self.b5 = nn.Sequential(BasicConv2d(cin, 48, kernel_size=1), BasicConv2d(48, 64, kernel_size=5, padding=2))
+        self.b3 = nn.Sequential(BasicConv2d(cin, 64, kernel_size=1), BasicConv2d(64, 96, kernel_size=3, padding=1),
+                                BasicConv2d(96, 96, kernel_size=3, padding=1))
+        self.bp = BasicConv2d(cin, pool_features, kernel_size=1)
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+
+
+class InceptionB(nn.Module):
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = BasicConv2d(cin, 384, kernel_size=3, stride=2)
+        self.bd = nn.Sequential(BasicConv2d(cin, 64, kernel_size=1), BasicConv2d(64, 96, kernel_size=3, padding=1),
+                                BasicConv2d(96, 96, kernel_size=3, stride=2))
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.bd(x), F.max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionC(nn.Module):
+    def __init__(self, cin, c7):
+        super().__init__()
+        self.b1 = BasicConv2d(cin, 192, kernel_size=1)
+        self.b7 = nn.Sequential(BasicConv2d(cin, c7, kernel_size=1),
+                                BasicConv2d(c7, c7, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv2d(c7, 192, kernel_size=(7, 1), padding=(3, 0)))
+        self.bd = nn.Sequential(BasicConv2d(cin, c7, kernel_size=1),
+                                BasicConv2d(c7, c7, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv2d(c7, c7, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv2d(c7, c7, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv2d(c7, 192, kernel_size=(1, 7), padding=(0, 3)))
+        self.bp = BasicConv2d(cin, 192, kernel_size=1)
+
+    def forward(self, x):
+        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+
+
+class InceptionD(nn.Module):
+    def __init__(self, cin):
+        super().__init__()
+        self.b3 = nn.Sequential(BasicConv2d(cin, 192, kernel_size=1), BasicConv2d(192, 320, kernel_size=3, stride=2))
+        self.b7 = nn.Sequential(BasicConv2d(cin, 192, kernel_size=1),
+                                BasicConv2d(192, 192, kernel_size=(1, 7), padding=(0, 3)),
+                                BasicConv2d(192, 192, kernel_size=(7, 1), padding=(3, 0)),
+                                BasicConv2d(192, 192, kernel_size=3, stride=2))
+
+    def forward(self, x):
+        return torch.cat([self.b3(x), self.b7(x), F.max_pool2d(x, 3, 2)], 1)
+
+
+class InceptionE(nn.Module):
+    def __init__(self, cin):
+        super().__init__()
+        self.b1 = BasicConv2d(cin, 320, kernel_size=1)
+        self.b3_1 = BasicConv2d(cin, 384, kernel_size=1)
+        self.b3_2a = BasicConv2d(384, 384, kernel_size=(1, 3), padding=(0, 1))
+        self.b3_2b = BasicConv2d(384, 384, kernel_size=(3, 1), padding=(1, 0))
+        self.bd_1 = BasicConv2d(cin, 448, kernel_size=1)
+        self.bd_2 = BasicConv2d(448, 384, kernel_size=3, padding=1)
+        self.bd_3a = BasicConv2d(384, 384, kernel_size=(1, 3), padding=(0, 1))
+        self.bd_3b = BasicConv2d(384, 384, kernel_size=(3, 1), padding=(1, 0))
+        self.bp = BasicConv2d(cin, 192, kernel_size=1)
+
+    def forward(self, x):
+        b3 = self.b3_1(x)
+        bd = self.bd_2(self.bd_1(x))
+        return torch.cat([self.b1(x), self.b3_2a(b3), self.b3_2b(b3), self.bd_3a(bd), self.bd_3b(bd),
+                          self.bp(F.avg_pool2d(x, 3, 1, 1))], 1)
+
+
+class InceptionV3(nn.Module):
+    def __init__(self, num_classes: int = 1000):
+        super().__init__()
+        self.stem = nn.Sequential(
+            BasicConv2d(3, 32, kernel_size=3, stride=2), BasicConv2d(32, 32, kernel_size=3),
+            BasicConv2d(32, 64, kernel_size=3, padding=1), nn.MaxPool2d(3, 2),
+            BasicConv2d(64, 80, kernel_size=1), BasicConv2d(80, 192, kernel_size=3), nn.MaxPool2d(3, 2))
+        self.blocks = nn.Sequential(
+            InceptionA(192, 32), InceptionA(256, 64), InceptionA(288, 64), InceptionB(288),
+            InceptionC(768, 128), InceptionC(768, 160), InceptionC(768, 160), InceptionC(768, 192),
+            InceptionD(768), InceptionE(1280), InceptionE(2048))
+        self.fc = nn.Linear(2048, num_classes)
+
+    def forward(self, x):
+        x = self.blocks(self.stem(x))
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+
+def inception_v3(**kw):
+    kw.pop("fused_bn", None)
+    return InceptionV3(**kw)

@@ -36,11 +36,19 @@ def _norm_factory(fused: bool) -> Callable[[int, bool], nn.Module]:
 
         return lambda c, relu: BatchNormAct2d(c, relu=relu)
 
-    def plain(c: int, relu: bool) -> nn.Module:
-        bn = nn.BatchNorm2d(c)
-        return nn.Sequential(bn, nn.ReLU(inplace=True)) if relu else bn
+    return lambda c, relu: _BNReLU(c, relu)
 
-    return plain
+
+class _BNReLU(nn.BatchNorm2d):
+    """Plain PyTorch BN(+ReLU) with the same state_dict keys as the fused module."""
+
+    def __init__(self, c: int, relu: bool):
+        super().__init__(c)
+        self.relu = relu
+
+    def forward(self, x):
+        y = super().forward(x)
+        return torch.relu_(y) if self.relu else y
 
 
 class BasicBlock(nn.Module):
