@@ -52,6 +52,8 @@ def main():
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
     p.add_argument("--bucket-mb", type=float, default=None)
+    p.add_argument("--bf16-shadow", type=int, default=1,
+                   help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--json-out", default=None)
     a = p.parse_args()
@@ -93,6 +95,10 @@ def main():
     else:
         opt = kf.optimizers.AdaptiveSGDOptimizer(base, named_parameters=model.named_parameters(), change_step=10)
     kf.broadcast_parameters(model.state_dict())
+    if a.bf16_shadow and getattr(opt, "space", None) is not None:
+        from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+        enable_bf16_shadow(model, opt)
 
     x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (a.batch,), device=dev)
@@ -146,6 +152,7 @@ def main():
             "parallelism": "dp%d" % size,
             "optimizer": "%s(SGD momentum=0.9 wd=1e-4)" % a.optimizer,
             "fused_bn_hip": bool(fused_bn),
+            "bf16_shadow_weights": bool(a.bf16_shadow),
             "per_gpu_img_s": round(value / size, 2),
             "baseline_per_gpu_img_s": round(BASELINE_PER_GPU, 1),
             "warmup_s": round(warm_s, 1),

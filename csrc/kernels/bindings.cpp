@@ -203,6 +203,48 @@ void unpack(at::Tensor desc, int64_t n_tensors, int64_t dst_dtype, at::Tensor fl
                        dtype_code(flat), static_cast<int>(dst_dtype), static_cast<float>(scale), stream_of(flat, 0));
 }
 
+// flat[offsets[i] : offsets[i] + srcs[i].numel()] += scale * srcs[i] (memory order), batched into
+// launches of up to GradAccTable::kMax same-dtype tensors.  srcs must be dense (any stride
+// permutation); the caller guarantees the flat slot uses the same memory order.
+void grad_accumulate(at::Tensor flat, std::vector<at::Tensor> srcs, std::vector<int64_t> offsets, double scale) {
+    check_gpu(flat, "flat");
+    TORCH_CHECK(flat.scalar_type() == at::kFloat && flat.is_contiguous(), "grad_accumulate: flat must be f32");
+    TORCH_CHECK(srcs.size() == offsets.size(), "grad_accumulate: srcs/offsets length mismatch");
+    for (const auto &t : srcs)
+        TORCH_CHECK(dtype_code(t) == 9 || dtype_code(t) == 10,
+                    "grad_accumulate: bf16 or f32 sources only");
+    // Sources are consumed on the current stream, the one they were produced
+    // on, so the caching allocator's stream-ordered reuse keeps them valid.
+    c10::DeviceGuard gd(flat.device());
+    auto s = stream_of(flat, 0);
+    for (int dt : {9, 10}) {
+        kfk::GradAccTable tab;
+        tab.src_dtype = dt;
+        tab.scale = static_cast<float>(scale);
+        tab.blk_start[0] = 0;
+        auto flush = [&] {
+            kfk::launch_grad_accumulate(tab, flat.data_ptr<float>(), s);
+            tab.n = 0;
+        };
+        for (size_t i = 0; i < srcs.size(); ++i) {
+            const auto &t = srcs[i];
+            if (dtype_code(t) != dt) continue;
+            TORCH_CHECK(t.device() == flat.device(), "grad_accumulate: device mismatch");
+            TORCH_CHECK(t.is_non_overlapping_and_dense(), "grad_accumulate: source must be dense");
+            TORCH_CHECK(offsets[i] >= 0 && offsets[i] + t.numel() <= flat.numel(), "grad_accumulate: out of range");
+            if (t.numel() == 0) continue;
+            const int k = tab.n;
+            tab.src[k] = t.data_ptr();
+            tab.off[k] = offsets[i];
+            tab.numel[k] = t.numel();
+            tab.blk_start[k + 1] = tab.blk_start[k] + kfk::grad_accumulate_blocks(t.numel());
+            tab.n = k + 1;
+            if (tab.n == kfk::GradAccTable::kMax) flush();
+        }
+        flush();
+    }
+}
+
 // ---- fused BN(+add)+ReLU ----------------------------------------------------------
 
 kfk::BNShape bn_shape(const at::Tensor &x) {
@@ -213,15 +255,40 @@ kfk::BNShape bn_shape(const at::Tensor &x) {
     return kfk::BNShape{x.numel() / C, C};
 }
 
-// Returns (y, mean, invstd).
-std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
-                                   c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
-                                   double momentum, double eps, bool training, bool relu) {
-    auto sh = bn_shape(x);
-    const int C = sh.channels;
+struct BNCommon {
+    float *rm = nullptr, *rv = nullptr;
+    int64_t *nbt = nullptr;
+};
+
+BNCommon bn_common(int C, const at::Tensor &weight, const at::Tensor &bias,
+                   const c10::optional<at::Tensor> &running_mean, const c10::optional<at::Tensor> &running_var,
+                   const c10::optional<at::Tensor> &num_batches, bool training) {
     TORCH_CHECK(weight.scalar_type() == at::kFloat && bias.scalar_type() == at::kFloat && weight.numel() == C &&
                     bias.numel() == C,
                 "bn: f32 weight/bias of size C required");
+    BNCommon b;
+    if (running_mean && running_mean->defined()) {
+        TORCH_CHECK(running_var && running_var->defined(), "bn: running_var missing");
+        b.rm = running_mean->data_ptr<float>();
+        b.rv = running_var->data_ptr<float>();
+    }
+    TORCH_CHECK(training || b.rm, "bn: eval mode needs running stats");
+    if (training && num_batches && num_batches->defined()) {
+        TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1 && num_batches->is_cuda(),
+                    "bn: num_batches_tracked must be a 1-element int64 GPU tensor");
+        b.nbt = num_batches->data_ptr<int64_t>();
+    }
+    return b;
+}
+
+// Returns (y, mean, invstd, coef, mask-or-undefined).
+std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
+                                   c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
+                                   double momentum, double eps, bool training, bool relu,
+                                   c10::optional<at::Tensor> num_batches) {
+    auto sh = bn_shape(x);
+    const int C = sh.channels;
+    auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
     const uint16_t *rp = nullptr;
     if (res && res->defined()) {
         TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == at::kBFloat16 &&
@@ -229,34 +296,37 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                     "bn: residual must match x (bf16, channels_last)");
         rp = reinterpret_cast<const uint16_t *>(res->data_ptr());
     }
-    float *rm = nullptr, *rv = nullptr;
-    if (running_mean && running_mean->defined()) {
-        TORCH_CHECK(running_var && running_var->defined(), "bn: running_var missing");
-        rm = running_mean->data_ptr<float>();
-        rv = running_var->data_ptr<float>();
-    }
-    TORCH_CHECK(training || rm, "bn: eval mode needs running stats");
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
     auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+    at::Tensor mask;
+    if (rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
     at::Tensor partial;
     if (training) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     kfk::launch_bn_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, weight.data_ptr<float>(),
-                           bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()), sh, relu, training, rm,
-                           rv, static_cast<float>(momentum), static_cast<float>(eps),
+                           bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                           mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, sh, relu, training, b.rm, b.rv,
+                           static_cast<float>(momentum), static_cast<float>(eps),
                            training ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), coef.data_ptr<float>(), stream_of(x, 0));
-    return {y, mean, invstd};
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0));
+    return {y, mean, invstd, coef, mask};
 }
 
 // Returns (dx, dres or undefined, dweight, dbias).
-std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor y, at::Tensor mean, at::Tensor invstd,
-                                    at::Tensor weight, bool relu, bool training, bool want_dres) {
+std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd,
+                                    at::Tensor weight, at::Tensor fcoef, c10::optional<at::Tensor> mask, bool relu,
+                                    bool training, bool want_dres) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
     TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == x.sizes(), "bn_backward: dy must match x");
+    TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() == 2 * C, "bn_backward: fcoef must be 2C f32");
+    const uint8_t *mp = nullptr;
+    if (mask && mask->defined()) {
+        TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() == sh.rows * (C / 8), "bn_backward: bad mask");
+        mp = mask->data_ptr<uint8_t>();
+    }
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
     auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
@@ -265,13 +335,66 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor y, a
     auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
     auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     kfk::launch_bn_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
-                            reinterpret_cast<const uint16_t *>(y.data_ptr()),
-                            reinterpret_cast<const uint16_t *>(x.data_ptr()), mean.data_ptr<float>(),
-                            invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, relu, training,
-                            partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                            reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(), mp,
+                            mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, relu,
+                            training, partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
                             coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
                             want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0));
     return {dx, dres, dw, db};
+}
+
+// Stem BN+ReLU+MaxPool(3,2,1).  Returns (y_pool, mean, invstd, coef, argmax bytes).
+std::vector<at::Tensor> bn_pool_forward(at::Tensor x, at::Tensor weight, at::Tensor bias,
+                                        c10::optional<at::Tensor> running_mean,
+                                        c10::optional<at::Tensor> running_var, double momentum, double eps,
+                                        bool training, c10::optional<at::Tensor> num_batches) {
+    auto sh = bn_shape(x);
+    const int C = sh.channels;
+    const int H = static_cast<int>(x.size(2)), W = static_cast<int>(x.size(3));
+    TORCH_CHECK(kfk::bn_pool_supported(sh, H, W), "bn_pool: unsupported shape");
+    auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
+    c10::DeviceGuard gd(x.device());
+    auto fopt = x.options().dtype(at::kFloat);
+    const int OH = kfk::pool_out(H), OW = kfk::pool_out(W);
+    auto yp = at::empty({x.size(0), C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    auto arg = at::empty({x.size(0) * OH * OW * C}, x.options().dtype(at::kByte));
+    auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+    at::Tensor partial;
+    if (training) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    kfk::launch_bn_pool_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), weight.data_ptr<float>(),
+                                bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(yp.data_ptr()),
+                                arg.data_ptr<uint8_t>(), sh, H, W, training, b.rm, b.rv, static_cast<float>(momentum),
+                                static_cast<float>(eps), training ? partial.data_ptr<float>() : nullptr,
+                                mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt,
+                                stream_of(x, 0));
+    return {yp, mean, invstd, coef, arg};
+}
+
+// Returns (dx, dweight, dbias).
+std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Tensor x, at::Tensor mean,
+                                         at::Tensor invstd, at::Tensor weight, at::Tensor fcoef, bool training) {
+    auto sh = bn_shape(x);
+    const int C = sh.channels;
+    const int H = static_cast<int>(x.size(2)), W = static_cast<int>(x.size(3));
+    const int OH = kfk::pool_out(H), OW = kfk::pool_out(W);
+    if (!dyp.is_contiguous(at::MemoryFormat::ChannelsLast)) dyp = dyp.contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(dyp.scalar_type() == at::kBFloat16 && dyp.size(0) == x.size(0) && dyp.size(1) == C &&
+                    dyp.size(2) == OH && dyp.size(3) == OW,
+                "bn_pool_backward: dy shape mismatch");
+    TORCH_CHECK(arg.scalar_type() == at::kByte && arg.numel() == dyp.numel(), "bn_pool_backward: bad argmax");
+    TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() == 2 * C, "bn_pool_backward: fcoef must be 2C");
+    c10::DeviceGuard gd(x.device());
+    auto fopt = x.options().dtype(at::kFloat);
+    auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
+    auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    kfk::launch_bn_pool_backward(reinterpret_cast<const uint16_t *>(dyp.data_ptr()), arg.data_ptr<uint8_t>(),
+                                 reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(),
+                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, H, W,
+                                 training, partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                                 coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
+                                 stream_of(x, 0));
+    return {dx, dw, db};
 }
 
 // ---- device model store: HIP IPC export / import ------------------------------------
@@ -380,13 +503,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("variance", &variance, "sum |s2*inv - (s1*inv)^2|");
     m.def("gns_update", &gns_update, "device-side gradient-noise-scale EMA update");
     m.def("seg_variance", &seg_variance, "sum_k ||E[g^2]-E[g]^2||_2 over flat tensor segments");
+    m.def("grad_accumulate", &grad_accumulate, "flat[off_i:] += scale * src_i for a list of bf16/f32 tensors",
+          py::arg("flat"), py::arg("srcs"), py::arg("offsets"), py::arg("scale") = 1.0);
     m.def("pack", &pack, "multi-tensor pack into a flat buffer");
     m.def("unpack", &unpack, "multi-tensor unpack from a flat buffer");
     m.def("bn_supported_channels", &kfk::bn_supported_channels);
-    m.def("bn_forward", &bn_forward, "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd)", py::arg("x"),
+    m.def("bn_forward", &bn_forward,
+          "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd, coef, relu mask or None)", py::arg("x"),
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
-          py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"));
-    m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)");
+          py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
+          py::arg("num_batches") = py::none());
+    m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
+          py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
+          py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"));
+    m.def("bn_pool_supported", [](int64_t C, int64_t H, int64_t W) {
+        return kfk::bn_pool_supported(kfk::BNShape{H * W, static_cast<int>(C)}, static_cast<int>(H),
+                                      static_cast<int>(W));
+    });
+    m.def("bn_pool_forward", &bn_pool_forward,
+          "stem BN+ReLU+MaxPool(3,2,1) forward -> (y_pool, mean, invstd, coef, argmax)", py::arg("x"),
+          py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
+          py::arg("eps"), py::arg("training"), py::arg("num_batches") = py::none());
+    m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)");
     m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
     m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");
     m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");

@@ -1,11 +1,20 @@
-// Fused NHWC BatchNorm (+ residual add) (+ ReLU), forward and backward,
-// bf16 activations / f32 statistics and parameters, for gfx950.
+// Fused NHWC BatchNorm (+ residual add) (+ ReLU) (+ 3x3/s2 max-pool), forward and
+// backward, bf16 activations / f32 statistics and parameters, for gfx950.
 //
 // Why: on MI355X a channels_last bf16 ResNet-50 step spends ~55% of its time in
 // MIOpen batch-norm kernels plus separate PyTorch ReLU / residual-add /
-// threshold-backward kernels (profiles/r1_baseline_torch_resnet50_*.md), all
-// HBM-bound.  Fusing them cuts the bytes moved per BN layer by ~30-40% and
-// the launches by ~3x.
+// threshold-backward / max-pool kernels (profiles/r1_baseline_torch_resnet50_*.md),
+// all HBM-bound.  Every byte not moved is time saved, so:
+//
+//   * the ReLU mask is never re-read from y in backward: for BN+ReLU it is
+//     recomputed from x with the forward coefficients (x is read anyway), for
+//     BN+add+ReLU a 1-bit-per-element mask is written in forward (1/16 of y);
+//   * the ResNet stem BN+ReLU+MaxPool(3,2,1) is one forward kernel (the 112x112
+//     post-BN map is never written) and one backward gather (no scatter, no
+//     112x112 pool-gradient tensor);
+//   * statistics folds are wide (8 channels x 32 chunk lanes per block) so the
+//     tiny finalize kernels are not latency bound, and num_batches_tracked is
+//     bumped inside the finalize instead of by a separate launch.
 //
 // Layout: x is [rows = N*H*W, C] with C contiguous (channels_last).  Each lane
 // owns one 16-byte vector = 8 channels; CVEC = C/8 lanes cover a row and a
@@ -13,10 +22,9 @@
 // grid stride is a multiple of CVEC, a thread's channel group is fixed for the
 // whole kernel: per-channel coefficients live in registers, no LDS staging.
 //
-// Passes (bytes per element, bf16):
-//   forward   stats (read x: 2)  + apply (read x [+res], write y: 4 [6])
-//   backward  reduce (read dy, y, x: 6) + apply (read dy, y, x, write dx [+dres]: 8 [10])
-// vs. MIOpen BN + torch relu/add/threshold_backward: ~10 [16] forward, ~16 [19] backward.
+// Bytes per element (bf16 = 2):
+//   forward   stats (x: 2) + apply (x [+res] -> y [+mask]: 4 [6.125])
+//   backward  reduce (dy, x [+mask]: 4 [4.125]) + apply (dy, x -> dx [+dres]: 6 [8.125])
 //
 // Statistics are two-stage and deterministic: per-chunk partial sums (f32)
 // then a per-channel fold in f64 (no float atomics).
@@ -50,12 +58,13 @@ struct Chunking {
 };
 
 constexpr int kMaxChunks = 512;
-constexpr int kFoldCh = 32;                   // channels per fold block
-constexpr int kFoldLanes = kBlock / kFoldCh;  // chunk lanes per channel
+constexpr int kFoldCh = 8;                    // channels per fold block
+constexpr int kFoldLanes = kBlock / kFoldCh;  // chunk lanes per channel (32)
 
 // Fold partial[v][chunk][C] over chunks for kFoldCh channels per block:
-// 32 channel lanes x 8 chunk lanes, coalesced 128-B rows, f64 accumulation,
-// then an LDS reduce across chunk lanes.  Result valid for lane kl == 0.
+// 8 channel lanes x 32 chunk lanes (<= 16 independent loads per lane for 512
+// chunks), f64 accumulation, then an LDS reduce across chunk lanes.  Result
+// valid for lane kl == 0.
 template <int NV>
 __device__ __forceinline__ void fold_partials(const float *partial, int nchunks, int C, int c, int kl,
                                               double (&out)[NV]) {
@@ -66,20 +75,24 @@ __device__ __forceinline__ void fold_partials(const float *partial, int nchunks,
         double s = 0;
         if (c < C) {
             const float *p = partial + static_cast<int64_t>(v) * nchunks * C + c;
-#pragma unroll 8
+#pragma unroll 16
             for (int k = kl; k < nchunks; k += kFoldLanes) s += p[static_cast<int64_t>(k) * C];
         }
         red[v][kl][ci] = s;
     }
     __syncthreads();
+    // tree over the 32 chunk lanes
+#pragma unroll
+    for (int w = kFoldLanes / 2; w > 0; w >>= 1) {
+        if (kl < w) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) red[v][kl][ci] += red[v][kl + w][ci];
+        }
+        __syncthreads();
+    }
     if (kl == 0) {
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            double s = 0;
-#pragma unroll
-            for (int j = 0; j < kFoldLanes; ++j) s += red[v][j][ci];
-            out[v] = s;
-        }
+        for (int v = 0; v < NV; ++v) out[v] = red[v][0][ci];
     }
 }
 
@@ -174,10 +187,12 @@ __global__ __launch_bounds__(kBlock) void bn_stats_kernel(const uint4 *__restric
 __global__ __launch_bounds__(kBlock) void bn_stats_finalize(const float *partial, int nchunks, int C, int64_t rows,
                                                             const float *gamma, const float *beta, float *mean,
                                                             float *invstd, float *run_mean, float *run_var,
-                                                            float momentum, float eps, float *coef) {
+                                                            float momentum, float eps, float *coef,
+                                                            int64_t *num_batches) {
     const int c = blockIdx.x * kFoldCh + threadIdx.x % kFoldCh, kl = threadIdx.x / kFoldCh;
     double sums[2];
     fold_partials<2>(partial, nchunks, C, c, kl, sums);
+    if (num_batches && blockIdx.x == 0 && threadIdx.x == 0) num_batches[0] += 1;
     if (kl != 0 || c >= C) return;
     double s = sums[0], q = sums[1];
     double m = s / rows;
@@ -212,10 +227,12 @@ __global__ void bn_eval_coef(int C, const float *gamma, const float *beta, const
 
 // ---------------------------------------------------------------- forward apply
 
+// y = act(x*scale + shift [+ res]); with RES && RELU also a 1-bit mask per
+// element (one byte per 8-channel vector) for the backward.
 template <int CVEC, bool RES, bool RELU>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restrict__ x, const uint4 *__restrict__ res,
                                                           const float *__restrict__ coef, uint4 *__restrict__ y,
-                                                          int64_t nvec) {
+                                                          uint8_t *__restrict__ mask, int64_t nvec) {
     constexpr int C = CVEC * 8;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
@@ -231,65 +248,218 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
         unpack8(x[i], f);
         float rr[8];
         if (RES) unpack8(res[i], rr);
+        uint32_t m = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             float v = f[k] * sc[k] + sh[k];
             if (RES) v += rr[k];
-            if (RELU) v = v > 0.f ? v : 0.f;
+            if (RELU) {
+                m |= (v > 0.f ? 1u : 0u) << k;
+                v = v > 0.f ? v : 0.f;
+            }
             f[k] = v;
         }
         y[i] = pack8(f);
+        if (RES && RELU) mask[i] = static_cast<uint8_t>(m);
     }
 }
 
-// ---------------------------------------------------------------- backward
+// ---------------------------------------------------------------- stem: BN + ReLU + MaxPool(3, 2, 1)
 
-template <int CVEC, bool RELU>
-__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const uint4 *__restrict__ dy,
-                                                               const uint4 *__restrict__ y,
-                                                               const uint4 *__restrict__ x,
-                                                               const float *__restrict__ mean,
-                                                               const float *__restrict__ invstd, int64_t rows,
+// One lane per (pooled pixel, 8-channel vector): 9 window loads (served mostly
+// from L2 -- neighbouring outputs share 3-6 of them), BN+ReLU per element, max.
+// Emits the pooled bf16 map and the window argmax (0..8) per element as bytes.
+template <int CVEC>
+__global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__restrict__ x,
+                                                               const float *__restrict__ coef, uint4 *__restrict__ yp,
+                                                               uint2 *__restrict__ arg, int H, int W, int OH, int OW,
+                                                               int64_t nout_vec) {
+    constexpr int C = CVEC * 8;
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int cv = static_cast<int>(tid % CVEC);
+    float sc[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        sc[k] = coef[cv * 8 + k];
+        sh[k] = coef[C + cv * 8 + k];
+    }
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    for (int64_t i = tid; i < nout_vec; i += stride) {
+        const int64_t p = i / CVEC;
+        const int ow = static_cast<int>(p % OW);
+        const int64_t t = p / OW;
+        const int oh = static_cast<int>(t % OH);
+        const int64_t n = t / OH;
+        float best[8];
+        uint32_t a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            best[k] = -1.f;  // post-ReLU values are >= 0
+            a[k] = 0;
+        }
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int h = 2 * oh - 1 + kh;
+            if (h < 0 || h >= H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int w = 2 * ow - 1 + kw;
+                if (w < 0 || w >= W) continue;
+                float f[8];
+                unpack8(x[((n * H + h) * W + w) * CVEC + cv], f);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    float v = f[k] * sc[k] + sh[k];
+                    v = v > 0.f ? v : 0.f;
+                    if (v > best[k]) {
+                        best[k] = v;
+                        a[k] = kh * 3 + kw;
+                    }
+                }
+            }
+        }
+        yp[i] = pack8(best);
+        arg[i] = make_uint2(a[0] | (a[1] << 8) | (a[2] << 16) | (a[3] << 24),
+                            a[4] | (a[5] << 8) | (a[6] << 16) | (a[7] << 24));
+    }
+}
+
+// ---------------------------------------------------------------- backward gradient sources
+
+// dy read directly ([rows, C]).
+// Two-phase interface so the reduce loop can put several rows of loads in
+// flight before any arithmetic: fetch() issues the loads, get() unpacks.
+struct DirectGrad {
+    const uint4 *dy;
+    using Raw = uint4;
+    template <int CVEC>
+    __device__ __forceinline__ Raw fetch(int64_t i, int64_t /*row*/, int /*cv*/) const {
+        return dy[i];
+    }
+    __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const { unpack8(r, g); }
+};
+
+// dy of the BN output gathered from the max-pool gradient: input pixel (h, w)
+// receives dy_pool of every window (<= 2x2 of them) whose argmax it is.
+struct PoolGrad {
+    const uint4 *dyp;  // [N, OH, OW, C]
+    const uint2 *arg;  // [N, OH, OW, C] bytes
+    int H, W, OH, OW;
+    struct Raw {
+        float g[8];
+    };
+    __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = r.g[k];
+    }
+    template <int CVEC>
+    __device__ __forceinline__ Raw fetch(int64_t i, int64_t row, int cv) const {
+        Raw r;
+        load<CVEC>(i, row, cv, r.g);
+        return r;
+    }
+    // rows < 2^31 (checked on the host): 32-bit index math only.
+    template <int CVEC>
+    __device__ __forceinline__ void load(int64_t /*i*/, int64_t row64, int cv, float (&g)[8]) const {
+        const uint32_t row = static_cast<uint32_t>(row64);
+        const uint32_t hw = static_cast<uint32_t>(H) * static_cast<uint32_t>(W);
+        const uint32_t n = row / hw;
+        const uint32_t rem = row - n * hw;
+        const int h = static_cast<int>(rem / static_cast<uint32_t>(W));
+        const int w = static_cast<int>(rem) - h * W;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = 0.f;
+        const int oh_lo = h >> 1, oh_hi = (h + 1) >> 1;
+        const int ow_lo = w >> 1, ow_hi = (w + 1) >> 1;
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int oh = a ? oh_hi : oh_lo;
+            if ((a && oh_hi == oh_lo) || oh >= OH) continue;
+            const int kh = h + 1 - 2 * oh;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int ow = b ? ow_hi : ow_lo;
+                if ((b && ow_hi == ow_lo) || ow >= OW) continue;
+                const uint32_t kk = static_cast<uint32_t>(kh * 3 + (w + 1 - 2 * ow));
+                const uint32_t o = ((n * OH + oh) * OW + ow) * CVEC + cv;
+                const uint2 am = arg[o];
+                float d[8];
+                unpack8(dyp[o], d);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
+                    if (ak == kk) g[k] += d[k];
+                }
+            }
+        }
+    }
+};
+
+enum ReluMode : int { RM_NONE = 0, RM_COEF = 1, RM_BITS = 2 };
+
+// Zero g where the forward ReLU was inactive.
+template <int RM>
+__device__ __forceinline__ void relu_gate(float (&g)[8], const float (&xv)[8], const float (&sc)[8],
+                                          const float (&sh)[8], const uint8_t *mask, int64_t i) {
+    if (RM == RM_COEF) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = (xv[k] * sc[k] + sh[k]) > 0.f ? g[k] : 0.f;
+    } else if (RM == RM_BITS) {
+        const uint32_t m = mask[i];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = ((m >> k) & 1u) ? g[k] : 0.f;
+    }
+}
+
+template <int CVEC, int RM>
+__device__ __forceinline__ void load_fwd_coef(const float *fcoef, int cv, float (&sc)[8], float (&sh)[8]) {
+    constexpr int C = CVEC * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        sc[k] = RM == RM_COEF ? fcoef[cv * 8 + k] : 0.f;
+        sh[k] = RM == RM_COEF ? fcoef[C + cv * 8 + k] : 0.f;
+    }
+}
+
+// ---------------------------------------------------------------- backward reduce
+
+// Accumulate sum(dz) and sum(dz * x); dgamma = invstd*(sum(dz*x) - mean*sum(dz))
+// is formed in the finalize (one FMA per element here instead of three).
+template <int CVEC, int RM, class G>
+__global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(G grad, const uint4 *__restrict__ x,
+                                                               const float *__restrict__ fcoef,
+                                                               const uint8_t *__restrict__ mask, int64_t rows,
                                                                int64_t rows_per_chunk, float *partial) {
     constexpr int RPI = kBlock / CVEC;
     constexpr int C = CVEC * 8;
     __shared__ float lds[2 * RPI * C];
     const int tid = threadIdx.x, cv = tid % CVEC, r0 = tid / CVEC;
-    float mu[8], is[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        mu[k] = mean[cv * 8 + k];
-        is[k] = invstd[cv * 8 + k];
-    }
+    float sc[8], sh[8];
+    load_fwd_coef<CVEC, RM>(fcoef, cv, sc, sh);
     float acc[2][8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[0][k] = acc[1][k] = 0.f;
     const int64_t r_begin = static_cast<int64_t>(blockIdx.x) * rows_per_chunk;
     int64_t r_end = r_begin + rows_per_chunk;
     if (r_end > rows) r_end = rows;
-    // Accumulate sum(dz) and sum(dz * x); dgamma = invstd*(sum(dz*x) - mean*sum(dz))
-    // is formed in the finalize (one FMA per element here instead of three).
     int64_t r = r_begin + r0;
-    for (; r + RPI < r_end; r += 2 * RPI) {
-        uint4 vg[2], vx[2], vy[2];
+    // U rows per lane in flight (2 x 16-B loads each) before any arithmetic
+    constexpr int U = 4;
+    for (; r + (U - 1) * RPI < r_end; r += U * RPI) {
+        typename G::Raw gr[U];
+        uint4 xr[U];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int64_t i = (r + u * RPI) * CVEC + cv;
-            vg[u] = dy[i];
-            vx[u] = x[i];
-            if (RELU) vy[u] = y[i];
+        for (int u = 0; u < U; ++u) {
+            const int64_t row = r + u * RPI, i = row * CVEC + cv;
+            gr[u] = grad.template fetch<CVEC>(i, row, cv);
+            xr[u] = x[i];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < U; ++u) {
             float g[8], xv[8];
-            unpack8(vg[u], g);
-            unpack8(vx[u], xv);
-            if (RELU) {
-                float yv[8];
-                unpack8(vy[u], yv);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-            }
+            grad.get(gr[u], g);
+            unpack8(xr[u], xv);
+            relu_gate<RM>(g, xv, sc, sh, mask, (r + u * RPI) * CVEC + cv);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 acc[0][k] += g[k];
@@ -300,22 +470,15 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(const uint4 *__re
     for (; r < r_end; r += RPI) {
         const int64_t i = r * CVEC + cv;
         float g[8], xv[8];
-        unpack8(dy[i], g);
+        grad.get(grad.template fetch<CVEC>(i, r, cv), g);
         unpack8(x[i], xv);
-        if (RELU) {
-            float yv[8];
-            unpack8(y[i], yv);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-        }
+        relu_gate<RM>(g, xv, sc, sh, mask, i);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             acc[0][k] += g[k];
             acc[1][k] += g[k] * xv[k];
         }
     }
-    (void)mu;
-    (void)is;
     reduce_to_partials<CVEC, 2>(acc, lds, partial, C, gridDim.x);
 }
 
@@ -346,33 +509,31 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize(const float *partial, 
     }
 }
 
-template <int CVEC, bool RELU, bool DRES>
-__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(const uint4 *__restrict__ dy,
-                                                              const uint4 *__restrict__ y,
-                                                              const uint4 *__restrict__ x,
+// ---------------------------------------------------------------- backward apply
+
+template <int CVEC, int RM, bool DRES, class G>
+__global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint4 *__restrict__ x,
+                                                              const float *__restrict__ fcoef,
+                                                              const uint8_t *__restrict__ mask,
                                                               const float *__restrict__ coef, uint4 *__restrict__ dx,
                                                               uint4 *__restrict__ dres, int64_t nvec) {
     constexpr int C = CVEC * 8;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
-    float k1[8], k2[8], k3[8];
+    float k1[8], k2[8], k3[8], sc[8], sh[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         k1[k] = coef[cv * 8 + k];
         k2[k] = coef[C + cv * 8 + k];
         k3[k] = coef[2 * C + cv * 8 + k];
     }
+    load_fwd_coef<CVEC, RM>(fcoef, cv, sc, sh);
     const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
     for (int64_t i = tid; i < nvec; i += stride) {
         float g[8], xv[8];
-        unpack8(dy[i], g);
+        grad.get(grad.template fetch<CVEC>(i, i / CVEC, cv), g);
         unpack8(x[i], xv);
-        if (RELU) {
-            float yv[8];
-            unpack8(y[i], yv);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[k] = yv[k] > 0.f ? g[k] : 0.f;
-        }
+        relu_gate<RM>(g, xv, sc, sh, mask, i);
         if (DRES) dres[i] = pack8(g);
         float o[8];
 #pragma unroll
@@ -394,12 +555,72 @@ void dispatch_cvec(int cvec, F &&f) {
     }
 }
 
-int apply_grid(int64_t nvec, int cvec) {
+int apply_grid(int64_t nvec) {
     int64_t g = (nvec + kBlock - 1) / kBlock;
     if (g > kMaxGrid) g = kMaxGrid;
     if (g < 1) g = 1;
-    (void)cvec;  // kBlock is a multiple of every supported CVEC, so any grid keeps cv fixed
+    // kBlock is a multiple of every supported CVEC, so any grid keeps cv fixed
     return static_cast<int>(g);
+}
+
+void launch_stats(const uint16_t *x, BNShape sh, const float *gamma, const float *beta, float *run_mean,
+                  float *run_var, float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
+                  int64_t *num_batches, hipStream_t s) {
+    const int C = sh.channels, cvec = C / 8;
+    Chunking ch = chunking(sh);
+    dispatch_cvec(cvec, [&](auto cvc) {
+        constexpr int CV = decltype(cvc)::value;
+        bn_stats_kernel<CV><<<ch.nchunks, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), sh.rows,
+                                                          ch.rows_per_chunk, partial);
+    });
+    bn_stats_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, beta,
+                                                                     mean, invstd, run_mean, run_var, momentum, eps,
+                                                                     coef, num_batches);
+}
+
+template <class G>
+void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const uint8_t *mask, const float *mean,
+                          const float *invstd, const float *gamma, BNShape sh, int rm, bool training, float *partial,
+                          float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s) {
+    const int C = sh.channels, cvec = C / 8;
+    const int64_t nvec = sh.rows * cvec;
+    Chunking ch = chunking(sh);
+    const uint4 *xx = reinterpret_cast<const uint4 *>(x);
+    dispatch_cvec(cvec, [&](auto cvc) {
+        constexpr int CV = decltype(cvc)::value;
+        auto go = [&](auto rmc) {
+            constexpr int RM = decltype(rmc)::value;
+            bn_bwd_reduce_kernel<CV, RM, G>
+                <<<ch.nchunks, kBlock, 0, s>>>(grad, xx, fcoef, mask, sh.rows, ch.rows_per_chunk, partial);
+        };
+        if (rm == RM_COEF) go(std::integral_constant<int, RM_COEF>());
+        else if (rm == RM_BITS) go(std::integral_constant<int, RM_BITS>());
+        else go(std::integral_constant<int, RM_NONE>());
+    });
+    bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
+                                                                   invstd, dgamma, dbeta, coef, training);
+    const int g = apply_grid(nvec);
+    uint4 *o = reinterpret_cast<uint4 *>(dx), *r = reinterpret_cast<uint4 *>(dres);
+    dispatch_cvec(cvec, [&](auto cvc) {
+        constexpr int CV = decltype(cvc)::value;
+        auto go = [&](auto rmc, auto drc) {
+            constexpr int RM = decltype(rmc)::value;
+            constexpr bool DR = decltype(drc)::value;
+            bn_bwd_apply_kernel<CV, RM, DR, G><<<g, kBlock, 0, s>>>(grad, xx, fcoef, mask, coef, o, r, nvec);
+        };
+        using T = std::true_type;
+        using F = std::false_type;
+        if (rm == RM_COEF) {
+            if (dres) go(std::integral_constant<int, RM_COEF>(), T());
+            else go(std::integral_constant<int, RM_COEF>(), F());
+        } else if (rm == RM_BITS) {
+            if (dres) go(std::integral_constant<int, RM_BITS>(), T());
+            else go(std::integral_constant<int, RM_BITS>(), F());
+        } else {
+            if (dres) go(std::integral_constant<int, RM_NONE>(), T());
+            else go(std::integral_constant<int, RM_NONE>(), F());
+        }
+    });
 }
 
 }  // namespace
@@ -413,73 +634,78 @@ bool bn_supported_channels(int C) {
 int bn_num_chunks(BNShape sh) { return chunking(sh).nchunks; }
 
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
-                       BNShape sh, bool relu, bool training, float *run_mean, float *run_var, float momentum,
-                       float eps, float *partial, float *mean, float *invstd, float *coef, hipStream_t s) {
+                       uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
+                       float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
+                       int64_t *num_batches, hipStream_t s) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     if (training) {
-        Chunking ch = chunking(sh);
-        dispatch_cvec(cvec, [&](auto cvc) {
-            constexpr int CV = decltype(cvc)::value;
-            bn_stats_kernel<CV><<<ch.nchunks, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), sh.rows,
-                                                              ch.rows_per_chunk, partial);
-        });
-        bn_stats_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, beta,
-                                                                         mean, invstd,
-                                                          run_mean, run_var, momentum, eps, coef);
+        launch_stats(x, sh, gamma, beta, run_mean, run_var, momentum, eps, partial, mean, invstd, coef, num_batches,
+                     s);
     } else {
         bn_eval_coef<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, run_mean, run_var, eps, mean, invstd, coef);
     }
-    int g = apply_grid(nvec, cvec);
+    const int g = apply_grid(nvec);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
         const uint4 *xv = reinterpret_cast<const uint4 *>(x);
         const uint4 *rv = reinterpret_cast<const uint4 *>(res);
         uint4 *yv = reinterpret_cast<uint4 *>(y);
         if (res) {
-            if (relu) bn_apply_kernel<CV, true, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, nvec);
-            else bn_apply_kernel<CV, true, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, nvec);
+            if (relu) bn_apply_kernel<CV, true, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            else bn_apply_kernel<CV, true, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
         } else {
-            if (relu) bn_apply_kernel<CV, false, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, nvec);
-            else bn_apply_kernel<CV, false, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, nvec);
+            if (relu) bn_apply_kernel<CV, false, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            else bn_apply_kernel<CV, false, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
         }
     });
 }
 
-void launch_bn_backward(const uint16_t *dy, const uint16_t *y, const uint16_t *x, const float *mean,
-                        const float *invstd, const float *gamma, BNShape sh, bool relu, bool training,
-                        float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres,
-                        hipStream_t s) {
+void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
+                        const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
+                        bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
+                        uint16_t *dres, hipStream_t s) {
+    const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
+    launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy)}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
+                         training, partial, dgamma, dbeta, coef, dx, dres, s);
+}
+
+bool bn_pool_supported(BNShape sh, int H, int W) {
+    return bn_supported_channels(sh.channels) && H >= 2 && W >= 2 && sh.rows % (static_cast<int64_t>(H) * W) == 0 &&
+           sh.rows * (sh.channels / 8) < (int64_t(1) << 31);  // PoolGrad uses 32-bit index math
+}
+
+void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
+                            BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
+                            float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
+                            hipStream_t s) {
     const int C = sh.channels, cvec = C / 8;
-    const int64_t nvec = sh.rows * cvec;
-    Chunking ch = chunking(sh);
+    if (training) {
+        launch_stats(x, sh, gamma, beta, run_mean, run_var, momentum, eps, partial, mean, invstd, coef, num_batches,
+                     s);
+    } else {
+        bn_eval_coef<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, run_mean, run_var, eps, mean, invstd, coef);
+    }
+    const int OH = pool_out(H), OW = pool_out(W);
+    const int64_t N = sh.rows / (static_cast<int64_t>(H) * W);
+    const int64_t nout = N * OH * OW * cvec;
+    const int g = apply_grid(nout);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
-        const uint4 *d = reinterpret_cast<const uint4 *>(dy), *yy = reinterpret_cast<const uint4 *>(y),
-                    *xx = reinterpret_cast<const uint4 *>(x);
-        if (relu)
-            bn_bwd_reduce_kernel<CV, true><<<ch.nchunks, kBlock, 0, s>>>(d, yy, xx, mean, invstd, sh.rows,
-                                                                         ch.rows_per_chunk, partial);
-        else
-            bn_bwd_reduce_kernel<CV, false><<<ch.nchunks, kBlock, 0, s>>>(d, yy, xx, mean, invstd, sh.rows,
-                                                                          ch.rows_per_chunk, partial);
+        bn_pool_apply_kernel<CV><<<g, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), coef,
+                                                      reinterpret_cast<uint4 *>(yp), reinterpret_cast<uint2 *>(arg), H,
+                                                      W, OH, OW, nout);
     });
-    bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
-                                                                   invstd, dgamma, dbeta, coef, training);
-    int g = apply_grid(nvec, cvec);
-    dispatch_cvec(cvec, [&](auto cvc) {
-        constexpr int CV = decltype(cvc)::value;
-        const uint4 *d = reinterpret_cast<const uint4 *>(dy), *yy = reinterpret_cast<const uint4 *>(y),
-                    *xx = reinterpret_cast<const uint4 *>(x);
-        uint4 *o = reinterpret_cast<uint4 *>(dx), *r = reinterpret_cast<uint4 *>(dres);
-        if (relu) {
-            if (dres) bn_bwd_apply_kernel<CV, true, true><<<g, kBlock, 0, s>>>(d, yy, xx, coef, o, r, nvec);
-            else bn_bwd_apply_kernel<CV, true, false><<<g, kBlock, 0, s>>>(d, yy, xx, coef, o, r, nvec);
-        } else {
-            if (dres) bn_bwd_apply_kernel<CV, false, true><<<g, kBlock, 0, s>>>(d, yy, xx, coef, o, r, nvec);
-            else bn_bwd_apply_kernel<CV, false, false><<<g, kBlock, 0, s>>>(d, yy, xx, coef, o, r, nvec);
-        }
-    });
+}
+
+void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
+                             const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
+                             bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
+                             hipStream_t s) {
+    PoolGrad pg{reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint2 *>(arg), H, W, pool_out(H),
+                pool_out(W)};
+    launch_backward_impl(pg, x, fcoef, nullptr, mean, invstd, gamma, sh, RM_COEF, training, partial, dgamma, dbeta,
+                         coef, dx, nullptr, s);
 }
 
 }  // namespace kfk

@@ -65,6 +65,22 @@ void launch_pack(const int64_t *desc, int n_tensors, size_t total, void *flat, i
 void launch_unpack(const int64_t *desc, int n_tensors, size_t total, const void *flat, int flat_dtype,
                    int dst_dtype, float scale, hipStream_t s);
 
+// Bucket gradient accumulation: flat[off[t] + j] += scale * src[t][j], all
+// sources of one dtype (bf16 or f32), one launch per table.  blk_start is the
+// prefix sum of grad_accumulate_blocks(numel[t]) (blk_start[0] = 0).
+struct GradAccTable {
+    static constexpr int kMax = 48;
+    int n = 0;
+    int src_dtype = 0;
+    float scale = 1.f;
+    const void *src[kMax];
+    int64_t off[kMax];
+    int64_t numel[kMax];
+    int blk_start[kMax + 1];
+};
+int grad_accumulate_blocks(int64_t numel);
+void launch_grad_accumulate(const GradAccTable &tab, float *flat, hipStream_t s);
+
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
 struct BNShape {
@@ -75,14 +91,31 @@ bool bn_supported_channels(int C);
 int bn_num_chunks(BNShape sh);  // partial scratch = 2 * nchunks * C floats
 // Training: batch stats -> mean/invstd, running stats update, coef = [scale; shift]
 // (2C floats), y = act(x*scale + shift [+ res]).  Eval: running stats.
+// With res && relu, mask (rows*C/8 bytes) receives the ReLU bits for the backward.
+// num_batches (optional, int64 on device) is incremented in training mode.
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
-                       BNShape sh, bool relu, bool training, float *run_mean, float *run_var, float momentum,
-                       float eps, float *partial, float *mean, float *invstd, float *coef, hipStream_t s);
-// dz = relu ? dy*(y>0) : dy ; dgamma/dbeta (f32) ; dx = k1*dz + k2*x + k3 ; dres = dz.
+                       uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
+                       float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
+                       int64_t *num_batches, hipStream_t s);
+// dz = dy * relu'(.)  -- from mask bits if given, else recomputed as x*fcoef[0:C] + fcoef[C:2C] > 0
+// (fcoef = the forward's coef) ; dgamma/dbeta (f32) ; dx = k1*dz + k2*x + k3 ; dres = dz.
 // coef scratch: 3C floats.
-void launch_bn_backward(const uint16_t *dy, const uint16_t *y, const uint16_t *x, const float *mean,
-                        const float *invstd, const float *gamma, BNShape sh, bool relu, bool training,
-                        float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres,
-                        hipStream_t s);
+void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
+                        const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
+                        bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
+                        uint16_t *dres, hipStream_t s);
+
+// ResNet stem: y = maxpool3x3s2p1(relu(bn(x))), x = [N, H, W, C] (rows = N*H*W).
+// arg receives the window argmax (0..8) per pooled element (bytes).
+inline int pool_out(int h) { return (h + 2 - 3) / 2 + 1; }
+bool bn_pool_supported(BNShape sh, int H, int W);
+void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
+                            BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
+                            float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
+                            hipStream_t s);
+void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
+                             const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
+                             bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
+                             hipStream_t s);
 
 }  // namespace kfk

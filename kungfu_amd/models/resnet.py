@@ -150,7 +150,11 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.conv1(x)
+        if self._fused:
+            x = self.bn1.forward_pool(x)  # BN+ReLU+MaxPool(3,2,1) in one HIP pass
+        else:
+            x = self.maxpool(self.bn1(x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

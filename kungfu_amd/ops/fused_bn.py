@@ -1,7 +1,8 @@
-"""Fused NHWC BatchNorm(+residual)+ReLU modules backed by HIP kernels (bn.hip).
+"""Fused NHWC BatchNorm(+residual)+ReLU(+MaxPool) modules backed by HIP kernels (bn.hip).
 
 ``BatchNormAct2d``    y = relu(bn(x))               (relu optional)
 ``BatchNormAddAct2d`` y = relu(bn(x) + residual)    (ResNet bottleneck tail)
+``BatchNormAct2d.forward_pool``  y = maxpool3x3s2p1(relu(bn(x)))  (ResNet stem)
 
 Both subclass ``nn.BatchNorm2d`` (same parameters, buffers and state_dict
 keys).  The HIP path runs for bf16, 4-D, channels_last inputs on GPU with a
@@ -9,10 +10,10 @@ supported channel count (C/8 a power of two in [8, 256], i.e. C in
 {64, 128, ..., 2048}); anything else uses the PyTorch composition, so results
 are the same model either way.
 
-The fused path moves ~30-40% fewer bytes than MIOpen BN + separate
-ReLU/add/threshold-backward kernels and launches ~3x fewer kernels
-(profiles/r1_baseline_torch_resnet50_autocast_cl_b256.md shows those ops at
-~55% of a ResNet-50 step).
+What is saved for backward is chosen to minimise HBM traffic: x (already kept
+alive as the producing conv's output), the per-channel forward coefficients
+(the ReLU mask is recomputed from x), and for the residual variant a 1-bit
+ReLU mask.  y itself is never re-read.
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._lib import hip, hip_available
+from ..parallel.mixed import deliver, direct_target
 
 
 def available() -> bool:
@@ -40,34 +42,86 @@ def _fusable(x: torch.Tensor, res: Optional[torch.Tensor]) -> bool:
     return hip().bn_supported_channels(x.shape[1])
 
 
+def _param_grads(ctx, dw, db):
+    """Gamma/beta gradients: handed to the flat space's sink when the params
+    are registered for direct gradients (parallel/mixed.py), else returned."""
+    if ctx.direct is None:
+        return dw, db
+    tw, tb = ctx.direct
+    deliver(tw, dw)
+    deliver(tb, db)
+    return None, None
+
+
+def _direct(weight, bias):
+    tw, tb = direct_target(weight), direct_target(bias)
+    return (tw, tb) if tw is not None and tb is not None else None
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu):
-        H = hip()
-        y, mean, invstd = H.bn_forward(x, res, weight, bias, running_mean, running_var, momentum, eps, training,
-                                       relu)
-        ctx.save_for_backward(x, y, mean, invstd, weight)
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu, nbt):
+        y, mean, invstd, coef, mask = hip().bn_forward(x, res, weight, bias, running_mean, running_var, momentum, eps,
+                                                       training, relu, nbt)
+        ctx.save_for_backward(x, mean, invstd, weight, coef, mask)
         ctx.relu, ctx.training, ctx.has_res = relu, training, res is not None
+        ctx.direct = _direct(weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, weight = ctx.saved_tensors
-        dx, dres, dw, db = hip().bn_backward(dy, x, y, mean, invstd, weight, ctx.relu, ctx.training, ctx.has_res)
-        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None
+        x, mean, invstd, weight, coef, mask = ctx.saved_tensors
+        dx, dres, dw, db = hip().bn_backward(dy, x, mean, invstd, weight, coef, mask, ctx.relu, ctx.training,
+                                             ctx.has_res)
+        dw, db = _param_grads(ctx, dw, db)
+        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None, None
+
+
+class _BNActPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training, nbt):
+        y, mean, invstd, coef, arg = hip().bn_pool_forward(x, weight, bias, running_mean, running_var, momentum, eps,
+                                                           training, nbt)
+        ctx.save_for_backward(x, mean, invstd, weight, coef, arg)
+        ctx.training = training
+        ctx.direct = _direct(weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, invstd, weight, coef, arg = ctx.saved_tensors
+        dx, dw, db = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training)
+        dw, db = _param_grads(ctx, dw, db)
+        return dx, dw, db, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
-           relu: bool = True, res: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Functional fused BN(+res)(+ReLU); falls back to torch ops when not fusable."""
-    if _fusable(x, res) and weight is not None:
-        rm = running_mean if running_mean is not None else None
-        rv = running_var if running_var is not None else None
-        return _BNActFn.apply(x, res, weight, bias, rm, rv, momentum, eps, training, relu)
+           relu: bool = True, res: Optional[torch.Tensor] = None,
+           num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Functional fused BN(+res)(+ReLU); falls back to torch ops when not fusable.
+
+    ``num_batches_tracked`` (if given, training mode) is incremented on device."""
+    if _fusable(x, res) and weight is not None and momentum is not None:
+        return _BNActFn.apply(x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu,
+                              num_batches_tracked if training else None)
+    if training and num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
     y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
     if res is not None:
         y = y + res
     return F.relu(y) if relu else y
+
+
+def bn_act_pool(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
+                num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """maxpool3x3s2p1(relu(bn(x))) -- one HIP forward kernel pass, one gather backward."""
+    if (_fusable(x, None) and weight is not None and momentum is not None and
+            hip().bn_pool_supported(x.shape[1], x.shape[2], x.shape[3])):
+        return _BNActPoolFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, training,
+                                  num_batches_tracked if training else None)
+    y = bn_act(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=True,
+               num_batches_tracked=num_batches_tracked)
+    return F.max_pool2d(y, 3, 2, 1)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -75,18 +129,22 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps=eps, momentum=momentum)
         self.relu = relu
 
-    def _training_args(self):
+    def _args(self):
+        track = self.training and self.track_running_stats
         use_batch = self.training or self.running_mean is None
-        if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
-        return use_batch
+        stats = not self.training or self.track_running_stats
+        return (self.weight, self.bias, self.running_mean if stats else None, self.running_var if stats else None,
+                use_batch, self.momentum, self.eps), (self.num_batches_tracked if track else None)
 
     def forward(self, x):
-        use_batch = self._training_args()
-        return bn_act(x, self.weight, self.bias,
-                      self.running_mean if (not self.training or self.track_running_stats) else None,
-                      self.running_var if (not self.training or self.track_running_stats) else None,
-                      use_batch, self.momentum, self.eps, relu=self.relu)
+        a, nbt = self._args()
+        return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt)
+
+    def forward_pool(self, x):
+        """relu(bn(x)) followed by MaxPool2d(3, stride 2, padding 1), fused."""
+        assert self.relu
+        a, nbt = self._args()
+        return bn_act_pool(x, *a, num_batches_tracked=nbt)
 
 
 class BatchNormAddAct2d(BatchNormAct2d):
@@ -94,8 +152,5 @@ class BatchNormAddAct2d(BatchNormAct2d):
         super().__init__(num_features, relu=True, eps=eps, momentum=momentum)
 
     def forward(self, x, res):
-        use_batch = self._training_args()
-        return bn_act(x, self.weight, self.bias,
-                      self.running_mean if (not self.training or self.track_running_stats) else None,
-                      self.running_var if (not self.training or self.track_running_stats) else None,
-                      use_batch, self.momentum, self.eps, relu=True, res=res)
+        a, nbt = self._args()
+        return bn_act(x, *a, relu=True, res=res, num_batches_tracked=nbt)

@@ -37,12 +37,14 @@ from .flat import FlatParamSpace
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "launched")
+    __slots__ = ("index", "start", "end", "params", "pending", "launched", "staged", "staged_off")
 
     def __init__(self, index: int, start: int, end: int, params: List[int]):
         self.index, self.start, self.end, self.params = index, start, end, params
         self.pending = len(params)
         self.launched = False
+        self.staged: List[torch.Tensor] = []  # direct gradients waiting for the bucket
+        self.staged_off: List[int] = []
 
 
 class GradReducer:
@@ -100,6 +102,9 @@ class GradReducer:
         self.post_finish = None
         for i, p in enumerate(space.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+        # direct gradients (parallel/mixed.py) are delivered to put()
+        self._prev_sink = getattr(space, "sink", None)
+        space.sink = self
         self._reset()
 
     # ------------------------------------------------------------------ hooks
@@ -114,28 +119,56 @@ class GradReducer:
                 with torch.no_grad():
                     v.copy_(g)
                 p.grad = v
-            if not self._armed:
-                self._armed = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-            self._fires[i] += 1
-            if self._expected is None:
-                return
-            b = self.param_bucket[i]
-            if b.launched:
-                if not self._warned:
-                    self._warned = True
-                    print("[kungfu_amd] warning: parameter %s received a gradient after its bucket was "
-                          "reduced (dynamic graph); overlap disabled" % self.space.names[i])
-                self._expected = None
-                return
-            b.pending -= 1
-            if b.pending == 0:
-                self._launch_ready()
+            self._mark(i)
 
         return hook
 
+    def put(self, i: int, g: torch.Tensor):
+        """Sink for direct gradients: stage ``g`` (bf16/f32, the parameter's
+        memory layout) for parameter ``i``; it is added into the flat gradient
+        buffer by one multi-tensor kernel when its bucket launches."""
+        b = self.param_bucket[i]
+        o, n = self.space.offsets[i]
+        if (not self._enabled or b.launched or g.dtype not in (torch.bfloat16, torch.float32)
+                or g.stride() != self.space.strides[i] or not g.is_cuda):
+            with torch.no_grad():
+                self.space.grad_view(i).add_(g)
+        else:
+            b.staged.append(g)
+            b.staged_off.append(o)
+        if self._enabled:
+            self._mark(i)
+
+    def _mark(self, i: int):
+        if not self._armed:
+            self._armed = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
+        self._fires[i] += 1
+        if self._expected is None:
+            return
+        b = self.param_bucket[i]
+        if b.launched:
+            if not self._warned:
+                self._warned = True
+                print("[kungfu_amd] warning: parameter %s received a gradient after its bucket was "
+                      "reduced (dynamic graph); overlap disabled" % self.space.names[i])
+            self._expected = None
+            return
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch_ready()
+
+    def _land(self, b: Bucket):
+        """Add the bucket's staged direct gradients into the flat buffer (one kernel)."""
+        if b.staged:
+            from .._lib import hip
+
+            hip().grad_accumulate(self.space.flat_grad, b.staged, b.staged_off, 1.0)
+            b.staged, b.staged_off = [], []
+
     def _launch(self, b: Bucket):
         b.launched = True
+        self._land(b)
         if self.skip:
             return
         comm = self.comm
@@ -210,3 +243,5 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        if getattr(self.space, "sink", None) is self:
+            self.space.sink = self._prev_sink

@@ -73,6 +73,10 @@ class FlatParamSpace:
                 p.data = v
                 p.grad = self._view(self.flat_grad, i)
         self._index = {id(p): i for i, p in enumerate(ps)}
+        # bf16 compute copy of flat_param (see parallel/mixed.py) and the
+        # gradient sink that direct-gradient autograd functions deliver to.
+        self.flat_shadow: Optional[torch.Tensor] = None
+        self.sink = None
 
     @staticmethod
     def _dense(p) -> bool:
@@ -100,6 +104,25 @@ class FlatParamSpace:
 
     def param_view(self, i: int) -> torch.Tensor:
         return self._view(self.flat_param, i)
+
+    def enable_shadow(self):
+        if self.flat_shadow is None:
+            self.flat_shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            self.refresh_shadow()
+
+    @torch.no_grad()
+    def refresh_shadow(self):
+        """flat_shadow = bf16(flat_param): one cast kernel for the whole model."""
+        if self.flat_shadow is not None:
+            # Version counter preserved: shadow views saved by a still-pending
+            # backward (gradient accumulation over several forwards) stay valid;
+            # the master does not change between micro-batches, so the values
+            # they see are unchanged.
+            with torch.autograd._unsafe_preserve_version_counter(self.flat_shadow):
+                self.flat_shadow.copy_(self.flat_param)
+
+    def shadow_view(self, i: int) -> torch.Tensor:
+        return self._view(self.flat_shadow, i)
 
     def zero_grad(self):
         self.flat_grad.zero_()

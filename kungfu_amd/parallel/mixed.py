@@ -1,0 +1,163 @@
+"""bf16 compute weights over f32 master weights, with gradients landed directly
+in the flat f32 gradient buffer ("direct gradients").
+
+Under ``torch.autocast(dtype=bfloat16)`` a stock model pays, per conv/linear
+weight and per step: one f32->bf16 cast in forward, one bf16->f32 cast of the
+weight gradient in backward and one ``AccumulateGrad`` add into ``.grad`` --
+~3 x 53 small launches for ResNet-50 (profiles/r5_*.md: ~1.7 ms of a 29 ms
+step).  The MI355X-native arrangement instead:
+
+* keeps a bf16 *shadow* of the whole flat master buffer, refreshed by ONE
+  cast kernel at the start of every forward (a model forward pre-hook), and
+  hands conv/linear modules a bf16 view of it -- numerically identical to
+  autocast's own round-to-nearest-even weight cast;
+* routes the bf16 weight gradient (and the fused BN's f32 gamma/beta
+  gradients) to the space's *gradient sink* instead of ``AccumulateGrad``.
+  The default sink adds immediately; the S-SGD engine's
+  :class:`~kungfu_amd.parallel.ddp.GradReducer` stages them per bucket and
+  lands a whole bucket with ONE multi-tensor kernel
+  (``_hip.grad_accumulate``: flat += bf16/f32 sources) right before the
+  bucket's all-reduce.
+
+No reference counterpart: the reference trains in f32 TensorFlow and leaves
+precision to the framework; this is the MI355X data path for its S-SGD
+(``srcs/python/kungfu/tensorflow/optimizers/sync_sgd.py:78-109``).
+
+Usage::
+
+    opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(model.parameters(), ...))
+    kf.parallel.mixed.enable_bf16_shadow(model, opt)
+"""
+from __future__ import annotations
+
+import types
+from typing import Dict, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .flat import FlatParamSpace
+
+# id(param) -> (space, index) for parameters whose gradients go to space.sink
+_DIRECT: Dict[int, Tuple[FlatParamSpace, int]] = {}
+
+
+def direct_target(p: Optional[torch.Tensor]) -> Optional[Tuple[FlatParamSpace, int]]:
+    """(space, index) if ``p``'s gradient should be handed to ``space.sink``."""
+    if p is None:
+        return None
+    return _DIRECT.get(id(p))
+
+
+def deliver(target: Tuple[FlatParamSpace, int], g: torch.Tensor) -> None:
+    space, i = target
+    space.sink.put(i, g)
+
+
+def _bf16_autocast(dev: str) -> bool:
+    return torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
+
+
+class _ShadowWeight(torch.autograd.Function):
+    """Forward: the bf16 shadow view of a master weight (no kernel).
+    Backward: the bf16 weight gradient goes to the space's sink."""
+
+    @staticmethod
+    def forward(ctx, w, space, i):
+        ctx.target = (space, i)
+        return space.shadow_view(i)
+
+    @staticmethod
+    def backward(ctx, g):
+        deliver(ctx.target, g)
+        return None, None, None
+
+
+def shadow(p: torch.Tensor) -> torch.Tensor:
+    """bf16 compute copy of a registered master weight under bf16 autocast; ``p`` otherwise."""
+    t = _DIRECT.get(id(p)) if p is not None else None
+    if t is None or t[0].flat_shadow is None or not _bf16_autocast(p.device.type):
+        return p
+    return _ShadowWeight.apply(p, t[0], t[1])
+
+
+def _conv_forward(self, x):
+    return self._conv_forward(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
+
+
+def _linear_forward(self, x):
+    return F.linear(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
+
+
+class ImmediateSink:
+    """Default sink: add the gradient into the flat slot now (torch kernel)."""
+
+    def __init__(self, space: FlatParamSpace):
+        self.space = space
+
+    def put(self, i: int, g: torch.Tensor) -> None:
+        with torch.no_grad():
+            self.space.grad_view(i).add_(g)
+
+
+def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> int:
+    """Switch ``model``'s conv/linear weights to bf16 shadow compute and direct
+    gradients (and, with ``bn_direct``, the fused BN's gamma/beta gradients).
+
+    ``optimizer`` is a kungfu_amd optimizer with a flat space (or the space
+    itself).  Returns the number of parameters switched to direct gradients.
+    Modules outside the space keep the stock path.
+    """
+    space: FlatParamSpace = optimizer if isinstance(optimizer, FlatParamSpace) else optimizer.space
+    if space is None:
+        raise ValueError("enable_bf16_shadow: optimizer has no flat parameter space (CPU model?)")
+    space.enable_shadow()
+    if getattr(space, "sink", None) is None:
+        space.sink = ImmediateSink(space)
+    n = 0
+
+    def register(p):
+        nonlocal n
+        if p is None or not p.requires_grad:
+            return False
+        try:
+            i = space.index(p)
+        except KeyError:
+            return False
+        _DIRECT[id(p)] = (space, i)
+        n += 1
+        return True
+
+    from ..ops.fused_bn import BatchNormAct2d
+
+    for m in model.modules():
+        if type(m).forward in (nn.Conv1d.forward, nn.Conv2d.forward, nn.Conv3d.forward):
+            if register(m.weight):
+                if m.bias is not None:
+                    register(m.bias)
+                m.forward = types.MethodType(_conv_forward, m)
+        elif type(m).forward is nn.Linear.forward:
+            if register(m.weight):
+                if m.bias is not None:
+                    register(m.bias)
+                m.forward = types.MethodType(_linear_forward, m)
+        elif bn_direct and isinstance(m, BatchNormAct2d):
+            register(m.weight)
+            register(m.bias)
+    if getattr(model, "_kf_shadow_hook", None) is None:
+        model._kf_shadow_hook = model.register_forward_pre_hook(lambda mod, args: space.refresh_shadow())
+    return n
+
+
+def disable(model: nn.Module) -> None:
+    """Undo :func:`enable_bf16_shadow` for ``model`` (stock forwards, AccumulateGrad)."""
+    h = getattr(model, "_kf_shadow_hook", None)
+    if h is not None:
+        h.remove()
+        model._kf_shadow_hook = None
+    for m in model.modules():
+        if "forward" in m.__dict__:
+            del m.forward
+        for p in m.parameters(recurse=False):
+            _DIRECT.pop(id(p), None)

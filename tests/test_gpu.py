@@ -168,6 +168,50 @@ def test_fused_bn(shape, relu, with_res):
 
 
 @needs_gpu
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (2, 64, 15, 17), (3, 128, 8, 8)])
+def test_fused_bn_relu_maxpool(shape):
+    """Stem BN+ReLU+MaxPool(3,2,1) (one forward pass, gather backward) vs f32 torch."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.fused_bn import BatchNormAct2d, bn_act_pool
+
+    torch.manual_seed(2)
+    N, C, Hh, W = shape
+    x = (torch.randn(shape, device="cuda") * 2 + 0.3).bfloat16().to(memory_format=torch.channels_last)
+    w, b = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda")
+    w[::7] *= -1  # negative gamma: max must be taken after the affine map
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    rm2, rv2 = rm.clone(), rv.clone()
+    xr = x.detach().float().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    yr = F.max_pool2d(F.relu(F.batch_norm(xr, rm2, rv2, wr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    xa, wa, ba = x.detach().requires_grad_(), w.clone().requires_grad_(), b.clone().requires_grad_()
+    nbt = torch.zeros((), dtype=torch.long, device="cuda")
+    ya = bn_act_pool(xa, wa, ba, rm, rv, True, 0.1, 1e-5, num_batches_tracked=nbt)
+    assert ya.shape == yr.shape and ya.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    ya.backward(g.bfloat16().to(memory_format=torch.channels_last))
+    for a, r in [(ya, yr), (xa.grad, xr.grad), (wa.grad, wr.grad), (ba.grad, br.grad), (rm, rm2), (rv, rv2)]:
+        assert _rel(a, r) < 3e-2
+    assert int(nbt) == 1
+    m = BatchNormAct2d(C).cuda().eval()
+    torch.testing.assert_close(m.forward_pool(x).float(), F.max_pool2d(m(x), 3, 2, 1).float())
+
+
+@needs_gpu
+def test_fused_bn_num_batches_tracked():
+    from kungfu_amd.ops.fused_bn import BatchNormAct2d, BatchNormAddAct2d
+
+    x = torch.randn(2, 64, 8, 8, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    m1, m2 = BatchNormAct2d(64).cuda(), BatchNormAddAct2d(64).cuda()
+    for _ in range(3):
+        m1(x)
+        m2(x, x)
+    assert int(m1.num_batches_tracked) == 3 and int(m2.num_batches_tracked) == 3
+
+
+@needs_gpu
 def test_rccl_single_rank_and_ops():
     import kungfu_amd as kf
     from kungfu_amd.parallel.comm import get_device_comm
@@ -217,6 +261,73 @@ def test_resnet_step_ssgd_fused_vs_plain():
         losses.append(ls)
     for a, b in zip(*losses):
         assert abs(a - b) < 0.05 * abs(a) + 0.05, losses
+
+
+@needs_gpu
+def test_grad_accumulate_multi_tensor(H):
+    """_hip.grad_accumulate (flat += bf16/f32 sources, batched tables) vs torch f32."""
+    torch.manual_seed(3)
+    sizes = [1, 7, 64, 1000, 8192 * 3 + 5, 70000] + [33] * 60  # > one 48-entry table
+    srcs, offs, off = [], [], 0
+    for i, n in enumerate(sizes):
+        dt = torch.bfloat16 if i % 3 else torch.float32
+        srcs.append(torch.randn(n, device="cuda").to(dt))
+        offs.append(off)
+        off += (n + 63) // 64 * 64
+    flat = torch.randn(off, device="cuda")
+    ref = flat.clone()
+    for s, o in zip(srcs, offs):
+        ref[o:o + s.numel()] += 0.5 * s.float()
+    H.grad_accumulate(flat, srcs, offs, 0.5)
+    torch.testing.assert_close(flat, ref, rtol=1e-6, atol=1e-6)
+    # channels_last 4-D source lands in memory order
+    w = torch.randn(16, 8, 3, 3, device="cuda").to(memory_format=torch.channels_last).bfloat16()
+    flat2 = torch.zeros(w.numel(), device="cuda")
+    H.grad_accumulate(flat2, [w], [0])
+    torch.testing.assert_close(flat2, w.permute(0, 2, 3, 1).reshape(-1).float())
+
+
+@needs_gpu
+def test_resnet_ssgd_bf16_shadow_matches_autocast():
+    """bf16 shadow weights + direct bucket gradients vs stock autocast: same forward
+    (bit-identical loss) and first-step gradients within the run-to-run noise of the
+    stock path itself (MIOpen's weight-gradient kernels are not bitwise deterministic)."""
+    import torch.nn.functional as F
+
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet18
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+    x = torch.randn(8, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (8,), device="cuda")
+
+    def run(shadow):
+        torch.manual_seed(0)
+        m = resnet18(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+        o = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9))
+        if shadow:
+            assert enable_bf16_shadow(m, o) > 20
+        ls, g0 = [], None
+        for s in range(3):
+            o.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            if s == 0:
+                g0 = o.space.flat_grad.clone()
+            o.step()
+            ls.append(loss.item())
+        return ls, g0
+
+    l_a, g_a = run(False)
+    l_b, g_b = run(False)
+    l_s, g_s = run(True)
+    assert l_s[0] == l_a[0]
+    noise = _rel(g_b, g_a)
+    assert _rel(g_s, g_a) < 2 * noise + 1e-2, (noise, _rel(g_s, g_a))
+    for a, b in zip(l_a, l_s):
+        assert abs(a - b) < 0.05 * abs(a) + 0.05, (l_a, l_s)
 
 
 @needs_gpu
