@@ -23,7 +23,7 @@ TORCH_DIR  := $(shell $(PYTHON) -c "import os,torch;print(os.path.dirname(torch.
 CXXFLAGS   := -std=c++17 -O3 -fPIC -Wall -Wextra -Wno-unused-parameter -Icsrc/include -mavx2 -mf16c -pthread $(EXTRA_CXXFLAGS)
 LDFLAGS    := -pthread $(EXTRA_LDFLAGS)
 
-RT_SRCS    := base plan log monitor transport session http peer capi
+RT_SRCS    := base plan log monitor transport session http peer capi model_avg scheduler
 RT_OBJS    := $(patsubst %,$(BUILD)/rt/%.o,$(RT_SRCS))
 RT_LIB     := kungfu_amd/lib/libkungfu_amd.so
 PY_MOD     := kungfu_amd/_kungfu$(PYEXT)

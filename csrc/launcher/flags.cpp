@@ -5,6 +5,7 @@
 
 #include <arpa/inet.h>
 #include <ifaddrs.h>
+#include <netdb.h>
 #include <netinet/in.h>
 
 #include <cstdlib>
@@ -65,6 +66,7 @@ std::string Flags::usage() {
            "  -port-range A-B        worker ports (10000-11000)\n"
            "  -self IPv4             this host's internal IPv4\n"
            "  -nic NAME              infer self IPv4 from this interface\n"
+           "  -platform NAME         peer discovery from a platform's env (modelarts); or KUNGFU_PLATFORM\n"
            "  -timeout DUR           kill the job after DUR (e.g. 30s, 5m)\n"
            "  -v[=bool]              stream worker output (true)\n"
            "  -q                     quiet launcher logs\n"
@@ -135,10 +137,30 @@ std::string Flags::parse(int argc, char **argv) {
             else if (name == "q") quiet = getb();
             else if (name == "delay") delay = parse_duration(get());
             else if (name == "builtin-config-port") builtin_config_port = std::stoi(get());
+            else if (name == "platform") platform = get();
             else if (name == "h" || name == "help") return usage();
             else throw std::invalid_argument("unknown flag -" + name);
         }
-        if (!hostfile.empty()) {
+        if (platform.empty()) {
+            const char *e = std::getenv("KUNGFU_PLATFORM");
+            if (e) platform = e;
+        }
+        if (platform == "modelarts") {
+            // runner list, self and ports come from the platform's env (one runner per container)
+            auto info = parse_modelarts_env();
+            self = format_ipv4(info.self.ipv4);
+            port = info.self.port;
+            hosts.clear();
+            const int n = static_cast<int>(info.runners.size());
+            for (size_t k = 0; k < info.runners.size(); ++k) {
+                HostSpec h;
+                h.ipv4 = info.runners[k].ipv4;
+                h.slots = (np + n - 1) / n;
+                hosts.push_back(h);
+            }
+        } else if (!platform.empty()) {
+            throw std::invalid_argument("unknown platform " + platform);
+        } else if (!hostfile.empty()) {
             std::ifstream in(hostfile);
             if (!in) throw std::invalid_argument("cannot open hostfile " + hostfile);
             std::stringstream ss;
@@ -152,6 +174,47 @@ std::string Flags::parse(int argc, char **argv) {
     prog = argv[i++];
     for (; i < argc; ++i) args.push_back(argv[i]);
     return "";
+}
+
+// ModelArts (reference: srcs/go/platforms/modelarts/modelarts.go:14-115):
+// DLS_TASK_INDEX / DLS_TASK_NUMBER select this container among the
+// BATCH_CUSTOM<i>_HOSTS "host:port" entries (one runner per container); a
+// single-container job runs on 127.0.0.1:38888.
+ContainerInfo parse_modelarts_env() {
+    auto req_int = [](const char *k) {
+        const char *v = std::getenv(k);
+        if (!v || !*v) throw std::invalid_argument(std::string(k) + " not set");
+        return std::stoi(v);
+    };
+    int idx = req_int("DLS_TASK_INDEX");
+    const int num = req_int("DLS_TASK_NUMBER");
+    if (num < 1) throw std::invalid_argument("DLS_TASK_NUMBER must be >= 1");
+    ContainerInfo info;
+    if (num == 1) {
+        info.runners.push_back(PeerID{parse_ipv4("127.0.0.1"), 38888});
+    } else {
+        for (int i = 0; i < num; ++i) {
+            std::string key = "BATCH_CUSTOM" + std::to_string(i) + "_HOSTS";
+            const char *v = std::getenv(key.c_str());
+            if (!v || !*v) throw std::invalid_argument(key + " not set");
+            std::string hp = v;
+            auto colon = hp.rfind(':');
+            if (colon == std::string::npos) throw std::invalid_argument(key + ": host:port expected");
+            std::string host = hp.substr(0, colon);
+            int port = std::stoi(hp.substr(colon + 1));
+            addrinfo hints{}, *res = nullptr;
+            hints.ai_family = AF_INET;
+            if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res)
+                throw std::invalid_argument("cannot resolve " + host);
+            uint32_t ip = ntohl(reinterpret_cast<sockaddr_in *>(res->ai_addr)->sin_addr.s_addr);
+            freeaddrinfo(res);
+            info.runners.push_back(PeerID{ip, static_cast<uint16_t>(port)});
+        }
+    }
+    if (num == 1 && idx == 1) idx = 0;  // tolerated by the platform
+    if (idx < 0 || idx >= num) throw std::invalid_argument("DLS_TASK_INDEX out of range");
+    info.self = info.runners[idx];
+    return info;
 }
 
 uint32_t infer_self_ipv4(const std::string &self, const std::string &nic) {

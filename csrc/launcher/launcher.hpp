@@ -57,6 +57,7 @@ struct Flags {
     bool quiet = false;
     double delay = 0;
     int builtin_config_port = 0;
+    std::string platform;  // "" or "modelarts"
     std::string prog;
     std::vector<std::string> args;
 
@@ -67,6 +68,13 @@ struct Flags {
 };
 
 uint32_t infer_self_ipv4(const std::string &self, const std::string &nic);
+
+// Platform peer discovery (ModelArts DLS_* / BATCH_CUSTOM<i>_HOSTS env).
+struct ContainerInfo {
+    PeerID self;
+    PeerList runners;
+};
+ContainerInfo parse_modelarts_env();
 
 // GPU id of a local rank given the visible-devices env (HIP/ROCR/CUDA).
 int gpu_index(int local_rank);

@@ -7,6 +7,8 @@
 // srcs/cpp/include/kungfu/utils/handler_manager.hpp:9-84 — but waits block on
 // a condition variable instead of spinning).
 #include <kungfu/log.hpp>
+#include <kungfu/model_avg.hpp>
+#include <kungfu/scheduler.hpp>
 #include <kungfu/peer.hpp>
 #include <kungfu/runtime.hpp>
 
@@ -247,6 +249,55 @@ PYBIND11_MODULE(_kungfu, m) {
                         size_t nbytes) {
         py::gil_scoped_release r;
         return require_peer().request(rank, version, name, reinterpret_cast<void *>(buf), nbytes);
+    });
+
+    // ---- ordered collective scheduler -----------------------------------------
+    py::class_<OrderedScheduler>(m, "OrderedScheduler")
+        .def(py::init<int>())
+        .def("reset", &OrderedScheduler::reset)
+        .def("ready", &OrderedScheduler::ready)
+        .def("flush", &OrderedScheduler::flush)
+        .def("set_order", &OrderedScheduler::set_order)
+        .def("auto_order", [](OrderedScheduler &o) {
+            auto s = require_session();
+            py::gil_scoped_release r;
+            o.auto_order(*s);
+        })
+        .def("order", &OrderedScheduler::order)
+        .def("arrivals", &OrderedScheduler::arrivals)
+        .def("size", &OrderedScheduler::size);
+
+    // ---- model averaging (legacy pair-averaging ops) --------------------------
+    py::class_<ModelAverager>(m, "ModelAverager")
+        .def(py::init([](size_t count, const std::string &name, const std::string &selection) {
+                 return new ModelAverager(&require_peer(), count, name, selection);
+             }),
+             py::arg("count"), py::arg("name") = "kungfu-model", py::arg("selection") = "random")
+        .def("save", [](ModelAverager &a, uintptr_t p) {
+            py::gil_scoped_release r;
+            a.save(reinterpret_cast<const float *>(p));
+        })
+        .def("request", [](ModelAverager &a, uintptr_t p) {
+            py::gil_scoped_release r;
+            return a.request(reinterpret_cast<float *>(p));
+        })
+        .def("average", [](ModelAverager &a, uintptr_t p) {
+            py::gil_scoped_release r;
+            return a.average(reinterpret_cast<float *>(p));
+        })
+        .def("async_average", [](ModelAverager &a, uintptr_t p) {
+            py::gil_scoped_release r;
+            return a.async_average(reinterpret_cast<float *>(p));
+        })
+        .def("wait", &ModelAverager::wait, py::call_guard<py::gil_scoped_release>())
+        .def("count", &ModelAverager::count)
+        .def("pulls", &ModelAverager::pulls);
+    m.def("peer_selector_sequence", [](const std::string &kind, const std::vector<int> &ranks, uint64_t seed,
+                                       int n) {
+        PeerSelector s(kind, ranks, seed);
+        std::vector<int> out;
+        for (int i = 0; i < n; ++i) out.push_back(s.next());
+        return out;
     });
 
     // ---- elastic / adaptation ------------------------------------------------

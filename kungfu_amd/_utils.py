@@ -54,3 +54,25 @@ class EMA:
                     nv = lo if nv >= 0 else -lo
             self.value = nv
         return self.value
+
+
+Ki, Mi, Gi = 1024, 1024 ** 2, 1024 ** 3
+
+
+def show_size(s: float) -> str:
+    """Human-readable byte count (parity: v1/helpers/utils.py show_size)."""
+    if s > Gi:
+        return "%.2fGi" % (s / Gi)
+    if s > Mi:
+        return "%.2fMi" % (s / Mi)
+    if s > Ki:
+        return "%.2fKi" % (s / Ki)
+    return "%d" % s
+
+
+def show_rate(size: float, duration: float) -> str:
+    r = size / duration
+    for unit, k in (("GiB/s", Gi), ("MiB/s", Mi), ("KiB/s", Ki)):
+        if r >= k:
+            return "%.2f%s" % (r / k, unit)
+    return "%.2fB/s" % r

@@ -13,6 +13,8 @@ from .collective import (Handle, all_gather, all_reduce, all_reduce_fn, all_redu
                          monitored_all_reduce, monitored_all_reduce_, rank, reduce, wait_all_handles, wait_handle)
 from .fuse import defuse, fuse, split_like
 from .local import save_variable, save_variables
+from .model_avg import (ModelAveraging, async_model_averaging, model_averaging, request_model,
+                        save_model)
 from .monitor import (GlobalNoiseScale, egress_rates, global_gradient_noise_scale, global_noise_scale,
                       gradient_variance, noise_scale_estimates, sum_squares)
 from .p2p import request_variable, request_variable_with_template

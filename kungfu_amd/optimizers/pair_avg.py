@@ -104,8 +104,13 @@ class DeviceModelStore:
 
 class _PairAveraging(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, fuse_requests: bool = True,
-                 fused_model_name: str = "model", fused: bool = True, seed: Optional[int] = None):
+                 fused_model_name: str = "model", fused: bool = True, seed: Optional[int] = None,
+                 peer_selection: str = "random"):
         super().__init__(optimizer, named_parameters, fused=fused)
+        if peer_selection not in ("random", "roundrobin"):
+            raise ValueError("peer_selection must be 'random' or 'roundrobin'")
+        self.peer_selection = peer_selection
+        self._rr = 0
         self.fused_model_name = fused_model_name
         self.fuse_requests = fuse_requests
         self.rank, self.size = runtime.rank(), runtime.size()
@@ -120,6 +125,16 @@ class _PairAveraging(KungFuOptimizer):
     def random_peer(self) -> int:
         t = self.rng.randrange(self.size)
         return (t + 1) % self.size if t == self.rank else t
+
+    def next_peer(self) -> int:
+        """Peer for this step: uniform random (AD-PSGD) or round-robin over the others
+        (the reference's SelectionStrategy, ops/cpu/peer_to_peer.cpp:8-63)."""
+        if self.peer_selection == "random":
+            return self.random_peer()
+        others = [r for r in range(self.size) if r != self.rank]
+        t = others[self._rr % len(others)]
+        self._rr += 1
+        return t
 
     # -- CPU / host-store helpers --------------------------------------------
     def _host_vars(self):
@@ -160,7 +175,7 @@ class _PairAveraging(KungFuOptimizer):
             else:
                 self._host_save()
             runtime.barrier()
-        target = self.random_peer()
+        target = self.next_peer()
         self.last_target = target
         if self.store is not None:
             self.store.advertise()
@@ -181,7 +196,7 @@ class _PairAveraging(KungFuOptimizer):
 
 def PairAveragingOptimizer(optimizer, named_parameters=None, fuse_requests: bool = True,
                            fused_model_name: str = "model", fused: bool = True, name=None, use_locking=False,
-                           with_keras=False):
+                           with_keras=False, peer_selection: str = "random"):
     """Wrap ``optimizer`` with AD-PSGD pair averaging (see module doc)."""
     return _PairAveraging(optimizer, named_parameters, fuse_requests=fuse_requests,
-                          fused_model_name=fused_model_name, fused=fused)
+                          fused_model_name=fused_model_name, fused=fused, peer_selection=peer_selection)

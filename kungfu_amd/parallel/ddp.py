@@ -13,9 +13,11 @@ MI355X design:
 * a post-accumulate-grad hook counts ready grads per bucket; when a bucket is
   complete it is launched on the high-priority comm stream after an event on
   the compute stream, overlapping with the rest of backward.
-* buckets are launched strictly in index order (a ready bucket waits for its
-  predecessors), which gives every rank the same RCCL call order without the
-  reference's run-time order broadcast.
+* buckets are launched in one fixed order on every rank (a ready bucket waits
+  for its predecessors): index order first, then -- from the first step whose
+  bucket completions are known -- rank 0's observed completion order,
+  broadcast once (the reference scheduler's auto-order), decided by the native
+  ``kungfu::OrderedScheduler`` (csrc/runtime/scheduler.cpp).
 * an autograd end-of-backward callback launches any bucket whose params got
   no gradient (unused params keep zeros) and makes the compute stream wait
   for the comm stream, so ``loss.backward()`` returns with the reduced
@@ -90,7 +92,13 @@ class GradReducer:
         # every bucket at the end of backward; later steps overlap.
         self._expected: Optional[List[int]] = None
         self._fires = [0] * len(space.params)
-        self._next = 0
+        # Collective order (identical on every rank): bucket index order until
+        # the auto-order step, then rank 0's observed completion order --
+        # kungfu::OrderedScheduler in the C++ runtime.
+        from .._lib import runtime
+
+        self.sched = runtime.OrderedScheduler(len(self.buckets))
+        self._ordered = False
         self._armed = False
         self._enabled = True
         self._hooks = []
@@ -156,7 +164,8 @@ class GradReducer:
             return
         b.pending -= 1
         if b.pending == 0:
-            self._launch_ready()
+            for j in self.sched.ready(b.index):
+                self._launch(self.buckets[j])
 
     def _land(self, b: Bucket):
         """Add the bucket's staged direct gradients into the flat buffer (one kernel)."""
@@ -188,18 +197,17 @@ class GradReducer:
         else:
             comm.all_reduce(g, op=self.op)
 
-    def _launch_ready(self):
-        while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
-            self._launch(self.buckets[self._next])
-            self._next += 1
-
     def _finish(self):
-        for b in self.buckets[self._next:]:
-            if not b.launched:
-                self._launch(b)
-        self._next = len(self.buckets)
+        for j in self.sched.flush():
+            if not self.buckets[j].launched:
+                self._launch(self.buckets[j])
         if not self.skip:
             torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
+        if self._expected is not None and not self._ordered and not self.skip:
+            # first step with known bucket completion: every rank adopts rank 0's
+            # arrival order for its collectives from now on (native auto-order)
+            self.sched.auto_order()
+            self._ordered = True
         if self._expected is None and not self._warned:
             self._expected = list(self._fires)
         self._reset()
@@ -211,7 +219,7 @@ class GradReducer:
             b.pending = sum(self._expected[i] for i in b.params) if self._expected is not None else 1
             b.launched = False
         self._fires = [0] * len(self.space.params)
-        self._next = 0
+        self.sched.reset()
         self._armed = False
 
     # ------------------------------------------------------------------ API
@@ -224,8 +232,8 @@ class GradReducer:
     def reduce_all_now(self):
         """Reduce every bucket immediately (for grads computed without hooks)."""
         self._reset()
-        for b in self.buckets:
-            self._launch(b)
+        for j in self.sched.flush():
+            self._launch(self.buckets[j])
         if not self.skip:
             torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
 

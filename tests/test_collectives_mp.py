@@ -16,3 +16,10 @@ def test_collectives(np_, strategy):
     r = kungfu_run(np_, [worker("collectives.py")], strategy=strategy, timeout=180)
     assert r.returncode == 0, r.stdout[-4000:]
     assert r.stdout.count("COLLECTIVES_OK") == np_, r.stdout[-4000:]
+
+
+@pytest.mark.parametrize("np_", [2, 3])
+def test_model_averaging_ops(np_):
+    r = kungfu_run(np_, [worker("model_avg.py")], timeout=180)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("MODEL_AVG_OK") == np_, r.stdout[-4000:]

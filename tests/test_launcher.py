@@ -120,3 +120,23 @@ def test_config_server_binary(tmp_path):
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_modelarts_platform_discovery(tmp_path):
+    """-platform modelarts: runner list from DLS_TASK_* / BATCH_CUSTOM<i>_HOSTS (reference
+    srcs/go/platforms/modelarts/modelarts.go); a one-container job runs on 127.0.0.1."""
+    s = _script(tmp_path, """
+        import os
+        print("MA_OK", os.environ["KUNGFU_SELF_SPEC"], os.environ["KUNGFU_INIT_RUNNERS"])
+    """)
+    env = dict(os.environ, DLS_TASK_INDEX="0", DLS_TASK_NUMBER="1")
+    r = subprocess.run([os.path.join(ROOT, "bin", "kungfu-run"), "-platform", "modelarts", "-np", "2",
+                        sys.executable, s], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count("MA_OK") == 2 and "127.0.0.1:38888" in r.stdout
+    env = dict(os.environ, DLS_TASK_INDEX="0", DLS_TASK_NUMBER="2", BATCH_CUSTOM0_HOSTS="127.0.0.1:38888")
+    r = subprocess.run([os.path.join(ROOT, "bin", "kungfu-run"), "-platform", "modelarts", "-np", "2",
+                        sys.executable, s], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "BATCH_CUSTOM1_HOSTS not set" in r.stdout

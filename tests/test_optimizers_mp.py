@@ -38,12 +38,12 @@ def test_ssgd_np_invariance(batch, nps):
         assert abs(acc - seen[nps[0]][0]) <= 2e-3, seen
 
 
-@pytest.mark.parametrize("opt", ["sma", "pair", "ada", "gns", "var"])
+@pytest.mark.parametrize("opt", ["sma", "pair", "pair_rr", "ada", "gns", "var"])
 def test_other_optimizers_train(opt):
-    r = kungfu_run(2, [worker("slp_train.py"), "--batch", "50", "--epochs", "2", "--opt", opt], timeout=240)
+    r = kungfu_run(3 if opt == "pair_rr" else 2, [worker("slp_train.py"), "--batch", "50", "--epochs", "2", "--opt", opt], timeout=240)
     assert r.returncode == 0, r.stdout[-3000:]
     res = results(r.stdout)
-    assert len(res) == 2, r.stdout[-3000:]
+    assert len(res) == (3 if opt == "pair_rr" else 2), r.stdout[-3000:]
     for _, _, acc, _, extra in res:
         assert float(acc) > 0.3, res  # learns (chance = 0.1)
     if opt in ("sma", "ada"):

@@ -85,6 +85,19 @@ sd = {"a": torch.full((3,), float(r)), "b": torch.full((2, 2), r, dtype=torch.in
 ops.broadcast_parameters(sd)
 assert torch.equal(sd["a"], torch.zeros(3)) and torch.equal(sd["b"], torch.zeros(2, 2, dtype=torch.int32))
 
+# native ordered scheduler: ranks observe different completion orders, auto_order
+# makes every rank adopt rank 0's (the reference NCCLScheduler's auto-order)
+sched = kf._lib.runtime.OrderedScheduler(4)
+arr = [3, 1, 0, 2] if r == 0 else [0, 1, 2, 3]
+launched = []
+for i in arr:
+    launched += sched.ready(i)
+assert launched == [0, 1, 2, 3] and sched.arrivals() == arr
+sched.auto_order()
+assert sched.order() == [3, 1, 0, 2], sched.order()
+sched.reset()
+assert sched.ready(0) == [] and sched.ready(3) == [3] and sched.ready(1) == [1, 0] and sched.flush() == [2]
+
 lat = ops.get_peer_latencies()
 assert lat.shape == (n,) and (lat[torch.arange(n) != r] >= 0).all()
 print("COLLECTIVES_OK rank=%d np=%d strategy=%s" % (r, n, kf._lib.runtime.strategy()), flush=True)

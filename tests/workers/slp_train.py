@@ -33,6 +33,8 @@ elif a.opt == "sma":
     opt = kf.optimizers.SynchronousAveragingOptimizer(base, alpha=0.1)
 elif a.opt == "pair":
     opt = kf.optimizers.PairAveragingOptimizer(base)
+elif a.opt == "pair_rr":
+    opt = kf.optimizers.PairAveragingOptimizer(base, peer_selection="roundrobin")
 elif a.opt == "ada":
     opt = kf.optimizers.AdaptiveSGDOptimizer(base, change_step=5)
 elif a.opt == "gns":
