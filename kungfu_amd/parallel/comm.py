@@ -113,7 +113,100 @@ class DeviceComm:
             self.comm = None
 
 
-def get_device_comm(scope: str = "global") -> DeviceComm:
+class HostStagedComm:
+    """The DeviceComm interface over the host runtime (TCP/UDS graph collectives),
+    staging through pinned host memory.  Selected with ``KUNGFU_GPU_DATAPLANE=host``:
+    for ranks that share one GPU (RCCL refuses duplicate devices) and hosts
+    without a usable RCCL.  Every call synchronises its stream -- a functional
+    fallback, not a fast path.  Op names are sequence numbers, which match
+    across ranks because every rank issues the same collective sequence (the
+    ordered scheduler guarantees it for the bucket engine)."""
+
+    def __init__(self, scope: str = "global"):
+        self.scope = scope
+        self.version = runtime.cluster_version()
+        if scope == "global":
+            self.rank, self.size = runtime.rank(), runtime.size()
+        else:
+            self.rank, self.size = runtime.local_rank(), runtime.local_size()
+        self.device = torch.cuda.current_device()
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.comm = self  # "valid" marker for get_device_comm
+        self._seq = 0
+
+    def _name(self, kind):
+        self._seq += 1
+        return "kf:staged:%s:%s:v%d:%d" % (self.scope, kind, self.version, self._seq)
+
+    def _run(self, inp, out, stream, fn):
+        s = stream if stream is not None else self.stream
+        if not isinstance(s, torch.cuda.Stream):
+            s = torch.cuda.ExternalStream(int(s), device=self.device)
+        with torch.cuda.stream(s):
+            h = inp.detach().to("cpu").contiguous()  # synchronises s
+            fn(h)
+            (inp if out is None else out).copy_(h.view_as(inp))
+            s.synchronize()
+        return inp if out is None else out
+
+    def all_reduce(self, inp, out=None, op="sum", stream=None):
+        nm = self._name("ar")
+        red = op if op != "avg" else "sum"
+
+        def f(h):
+            args = (h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h))
+            if self.scope == "global":
+                runtime.all_reduce(*args, op_code(red), nm)
+            else:  # per-host: reduce to the local root, then broadcast back
+                runtime.local_reduce(*args, op_code(red), nm + ":r")
+                runtime.local_broadcast(*args, nm + ":b")
+            if op == "avg":
+                h.div_(self.size)
+
+        return self._run(inp, out, stream, f)
+
+    def broadcast(self, t, root: int = 0, stream=None):
+        if root != 0:
+            raise NotImplementedError("host-staged broadcast supports root 0")
+        nm = self._name("bc")
+        fn = runtime.broadcast if self.scope == "global" else runtime.local_broadcast
+        return self._run(t, None, stream, lambda h: fn(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), nm))
+
+    def reduce(self, inp, out=None, op="sum", root=0, stream=None):
+        return self.all_reduce(inp, out, op, stream)
+
+    def all_gather(self, inp, out, stream=None):
+        nm = self._name("ag")
+        s = stream if stream is not None else self.stream
+        with torch.cuda.stream(s if isinstance(s, torch.cuda.Stream) else torch.cuda.ExternalStream(int(s))):
+            h = inp.detach().to("cpu").contiguous()
+            ho = torch.empty((self.size,) + tuple(h.shape), dtype=h.dtype)
+            runtime.all_gather(h.data_ptr(), ho.data_ptr(), h.numel(), dtype_code(h), nm)
+            out.copy_(ho.view_as(out))
+        return out
+
+    def reduce_scatter(self, inp, out, op="sum", stream=None):
+        full = inp.detach().clone()
+        self.all_reduce(full, op=op, stream=stream)
+        n = out.numel()
+        out.copy_(full.view(-1)[self.rank * n:(self.rank + 1) * n].view_as(out))
+        return out
+
+    def group_start(self):
+        pass
+
+    def group_end(self):
+        pass
+
+    def destroy(self):
+        self.comm = None
+
+
+def _use_host_staging() -> bool:
+    return os.environ.get("KUNGFU_GPU_DATAPLANE", "rccl") == "host"
+
+
+def get_device_comm(scope: str = "global"):
     """Current communicator; rebuilt when the cluster version changed (resize)."""
     global _global, _local
     from ..python import _ensure
@@ -125,7 +218,7 @@ def get_device_comm(scope: str = "global") -> DeviceComm:
         if cur is None or cur.version != ver or cur.comm is None:
             if cur is not None:
                 cur.destroy()
-            cur = DeviceComm(scope)
+            cur = HostStagedComm(scope) if _use_host_staging() else DeviceComm(scope)
             if scope == "global":
                 _global = cur
             else:

@@ -290,7 +290,7 @@ def test_grad_accumulate_multi_tensor(H):
 @needs_gpu
 def test_resnet_ssgd_bf16_shadow_matches_autocast():
     """bf16 shadow weights + direct bucket gradients vs stock autocast: same forward
-    (bit-identical loss) and first-step gradients within the run-to-run noise of the
+    loss (to conv-algorithm rounding) and first-step gradients within the run-to-run noise of the
     stock path itself (MIOpen's weight-gradient kernels are not bitwise deterministic)."""
     import torch.nn.functional as F
 
@@ -323,11 +323,43 @@ def test_resnet_ssgd_bf16_shadow_matches_autocast():
     l_a, g_a = run(False)
     l_b, g_b = run(False)
     l_s, g_s = run(True)
-    assert l_s[0] == l_a[0]
+    # same math; conv kernels may pick other tiles/split-K for a differently aligned weight view
+    assert abs(l_s[0] - l_a[0]) <= max(2 * abs(l_b[0] - l_a[0]), 1e-3 * abs(l_a[0])), (l_a, l_b, l_s)
     noise = _rel(g_b, g_a)
     assert _rel(g_s, g_a) < 2 * noise + 1e-2, (noise, _rel(g_s, g_a))
     for a, b in zip(l_a, l_s):
         assert abs(a - b) < 0.05 * abs(a) + 0.05, (l_a, l_s)
+
+
+@needs_gpu
+def test_ssgd_engine_two_ranks_one_gpu_host_staged():
+    """Bucketed S-SGD with 2 ranks sharing the GPU (host-staged collectives): replicas
+    stay identical through broadcast + averaged gradients + auto-ordered buckets."""
+    r = kungfu_run(2, [worker("ssgd_gpu.py")], timeout=400, extra=["-allow-xgmi"],
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"})
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("SSGD_GPU_OK") == 2, r.stdout[-4000:]
+
+
+@needs_gpu
+def test_bench_torchrun_two_ranks_one_gpu_host_staged():
+    """bench.py through torch.distributed.run with 2 ranks (the driver's multi-GPU
+    launch path), host-staged collectives so both ranks can share one GPU."""
+    import json
+
+    env = dict(os.environ, KUNGFU_FORCE_DEVICE="0", KUNGFU_GPU_DATAPLANE="host", PYTHONPATH=ROOT)
+    from conftest import free_port_block
+
+    port = free_port_block(2)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "16"],
+                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["parallelism"] == "dp2"
 
 
 @needs_gpu
