@@ -325,8 +325,11 @@ def test_resnet_ssgd_bf16_shadow_matches_autocast():
     l_s, g_s = run(True)
     # same math; conv kernels may pick other tiles/split-K for a differently aligned weight view
     assert abs(l_s[0] - l_a[0]) <= max(2 * abs(l_b[0] - l_a[0]), 1e-3 * abs(l_a[0])), (l_a, l_b, l_s)
-    noise = _rel(g_b, g_a)
-    assert _rel(g_s, g_a) < 2 * noise + 1e-2, (noise, _rel(g_s, g_a))
+    def fro(a, b):
+        return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+    noise = fro(g_b, g_a)
+    assert fro(g_s, g_a) < max(3 * noise, 0.05), (noise, fro(g_s, g_a))
     for a, b in zip(l_a, l_s):
         assert abs(a - b) < 0.05 * abs(a) + 0.05, (l_a, l_s)
 
