@@ -245,6 +245,40 @@ void grad_accumulate(at::Tensor flat, std::vector<at::Tensor> srcs, std::vector<
     }
 }
 
+// ---- 3x3 implicit-GEMM convolution -------------------------------------------------
+
+at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3: x must be a 4-D channels_last bf16 GPU tensor");
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                    w.size(1) == x.size(1) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3: w must be [Cout, Cin, 3, 3] channels_last bf16");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+    TORCH_CHECK(kfk::conv3x3_supported(C, K, static_cast<int>(stride)), "conv3x3: unsupported channels/stride");
+    TORCH_CHECK(static_cast<int64_t>(N) * H * W * std::max(C, K) < (int64_t(1) << 31), "conv3x3: tensor too large");
+    const int OH = (H + 2 - 3) / stride + 1, OW = (W + 2 - 3) / stride + 1;
+    c10::DeviceGuard gd(x.device());
+    auto y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_conv3x3(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                        reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, static_cast<int>(stride),
+                        stream_of(x, 0), static_cast<int>(variant));
+    return y;
+}
+
+// [Cout, Cin, 3, 3] channels_last -> flipped/transposed [Cin, Cout, 3, 3] channels_last
+at::Tensor conv3x3_flip_weight(at::Tensor w) {
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3_flip_weight: [Cout, Cin, 3, 3] channels_last bf16 required");
+    const int K = w.size(0), C = w.size(1);
+    c10::DeviceGuard gd(w.device());
+    auto wt = at::empty({C, K, 3, 3}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_conv3x3_flip_weight(reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                                    reinterpret_cast<uint16_t *>(wt.data_ptr()), K, C, stream_of(w, 0));
+    return wt;
+}
+
 // ---- fused BN(+add)+ReLU ----------------------------------------------------------
 
 kfk::BNShape bn_shape(const at::Tensor &x) {
@@ -507,6 +541,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("flat"), py::arg("srcs"), py::arg("offsets"), py::arg("scale") = 1.0);
     m.def("pack", &pack, "multi-tensor pack into a flat buffer");
     m.def("unpack", &unpack, "multi-tensor unpack from a flat buffer");
+    m.def("conv3x3", &conv3x3, "3x3 pad-1 NHWC bf16 convolution (MFMA implicit GEMM)", py::arg("x"), py::arg("w"),
+          py::arg("stride") = 1, py::arg("variant") = -1);
+    m.def("conv3x3_variants", &kfk::conv3x3_variants);
+    m.def("conv3x3_flip_weight", &conv3x3_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,2-kh,2-kw] (data-gradient weights)");
+    m.def("conv3x3_supported", &kfk::conv3x3_supported);
     m.def("bn_supported_channels", &kfk::bn_supported_channels);
     m.def("bn_forward", &bn_forward,
           "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd, coef, relu mask or None)", py::arg("x"),

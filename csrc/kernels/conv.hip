@@ -1,0 +1,289 @@
+// 3x3 convolution (pad 1, stride 1 or 2), NHWC bf16, as an implicit GEMM on
+// CDNA4 matrix cores (v_mfma_f32_16x16x32_bf16), for gfx950.
+//
+//   y[m, co] = sum_{kh, kw, ci} x[n, oh*s + kh - 1, ow*s + kw - 1, ci] * w[co, kh, kw, ci]
+//   GEMM: M = N*OH*OW output pixels, N = Cout, K = 9 * Cin (tap-major, channel-minor)
+//
+// Why: ResNet-50 spends ~6.3 ms of a 28.6 ms step in its 16 3x3 convolutions at
+// ~450 TF/s through MIOpen/CK (profiles/README.md).  The K dimension of one
+// tap is a run of Cin contiguous channels, so every A-tile row is a 128-byte
+// segment of the input (or of a zero page at the padding border): the im2col
+// is done by the per-lane source address of global_load_lds, never in memory.
+//
+// Tiling: block = 4 waves (256 threads), wave tile 64x64 (4x4 MFMA 16x16
+// tiles, 64 accumulator VGPRs), block tile 128x128 (2x2 waves) or 256x64 (4x1,
+// for Cout = 64), BK = 64 channels of one tap per K-step.  A and B tiles are
+// staged global->LDS with 16-byte global_load_lds (no VGPR round trip),
+// double-buffered, with an XOR swizzle of the 16-byte chunk index by the row
+// (chunk ^ (row & 7)) applied on the source address and on the ds_read, so the
+// 16 rows a ds_read_b128 touches spread over 8 chunk positions.  Blocks are
+// remapped XCD-contiguously (consecutive tiles share input halo rows in L2).
+//
+// The same kernel computes the stride-1 data gradient: dx = conv3x3(dy, w')
+// with w'[ci, kh, kw, co] = w[co, 2-kh, 2-kw, ci] (conv3x3_flip_weight).
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace kfk {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kBK = 64;              // channels per K-step
+constexpr int kRowBytes = kBK * 2;   // 128 B per staged row
+
+__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ (row & 7); }
+
+// LDS byte address of (row, 16-B chunk) in a staged tile image.
+__device__ __forceinline__ int img_off(int row, int chunk) { return row * kRowBytes + (swz_chunk(row, chunk) << 4); }
+
+struct Geo {
+    int N, H, W, C, OH, OW, K, stride;
+    int M;       // N*OH*OW
+    int mtiles;  // ceil(M / BM)
+    int ntiles;  // K / BN
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
+template <int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(const uint16_t *__restrict__ x,
+                                                               const uint16_t *__restrict__ w,
+                                                               uint16_t *__restrict__ y,
+                                                               const uint16_t *__restrict__ zero, Geo g) {
+    constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+    constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
+    constexpr int STAGE = A_BYTES + B_BYTES;
+    constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
+    constexpr int B_INST = BN / 8 / NW;
+    constexpr int LOADS = A_INST + B_INST;
+    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    // XCD-aware bijective remap: blocks sharing an XCD get consecutive tile ids.
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int mt = wg / g.ntiles, nt = wg - mt * g.ntiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+
+    // ---- per-lane staging descriptors (fixed for the whole K loop)
+    // lane l of a glds instruction writes image bytes [l*16, l*16+16) of its
+    // 8-row slab: row = l/8, image chunk = l%8 -> logical chunk (l%8)^(l/8).
+    // A rows: 32-bit element offset of the tap-(0,0) input pixel (linear in the
+    // tap: + (kh*W + kw)*C) and a 9-bit in-bounds mask per row.
+    const int srow = lane >> 3;
+    const int schunk = (lane & 7) ^ srow;
+    int a_off[A_INST];
+    uint32_t a_ok[A_INST];
+#pragma unroll
+    for (int j = 0; j < A_INST; ++j) {
+        const int r = (wave * A_INST + j) * 8 + srow;
+        const int m = m0 + r;
+        a_off[j] = 0;
+        a_ok[j] = 0;
+        if (m < g.M) {
+            const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
+            const int ih0 = oh * g.stride - 1, iw0 = ow * g.stride - 1;
+            a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
+            uint32_t ok = 0;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw)
+                    if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
+                        static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
+                        ok |= 1u << (kh * 3 + kw);
+            a_ok[j] = ok;
+        }
+    }
+    int b_off[B_INST];
+#pragma unroll
+    for (int j = 0; j < B_INST; ++j) {
+        const int r = (wave * B_INST + j) * 8 + srow;
+        b_off[j] = (n0 + r) * 9 * g.C + schunk * 8;
+    }
+    const int csteps = g.C / kBK;
+    const int ksteps = 9 * csteps;
+
+    auto stage = [&](int ks, int buf) {
+        const int tap = ks / csteps, cc = ks - tap * csteps;
+        const int kh = tap / 3, kw = tap - kh * 3;
+        const int toff = (kh * g.W + kw) * g.C + cc * kBK;  // wave-uniform
+        uint8_t *abase = lds + buf * STAGE;
+        uint8_t *bbase = abase + A_BYTES;
+#pragma unroll
+        for (int j = 0; j < A_INST; ++j) {
+            const bool ok = (a_ok[j] >> tap) & 1u;
+            const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
+            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < B_INST; ++j) {
+            const uint16_t *src = w + static_cast<uint32_t>(b_off[j] + tap * g.C + cc * kBK);
+            __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
+        }
+    };
+
+    const int wm = wave / WN, wn = wave % WN;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+
+    // prologue: STAGES-1 tiles in flight
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p)
+        if (p < ksteps) stage(p, p);
+    int buf = 0;
+    for (int ks = 0; ks < ksteps; ++ks) {
+        // tile ks landed (this wave's loads); later tiles may stay in flight
+        if (ks + STAGES - 1 <= ksteps) wait_vmcnt<LOADS * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // raw barrier: keeps the other tiles' LDS-DMA in flight
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t *abase = lds + buf * STAGE;
+        const uint8_t *bbase = abase + A_BYTES;
+        // all 16 fragments of the K-step issued up front (substep 1 lands while
+        // substep 0's MFMAs run)
+        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ra = wm * 64 + i * 16 + (lane & 15), rb = wn * 64 + i * 16 + (lane & 15);
+            af0[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, lane >> 4));
+            bf0[i] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, lane >> 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int ra = wm * 64 + i * 16 + (lane & 15), rb = wn * 64 + i * 16 + (lane & 15);
+            af1[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, 4 + (lane >> 4)));
+            bf1[i] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, 4 + (lane >> 4)));
+        }
+        mfma_block(af0, bf0);
+        __builtin_amdgcn_sched_barrier(0);
+        // next tile's staging (VALU + LDS-DMA issue) between the two MFMA clusters
+        if (ks + STAGES - 1 < ksteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);  // the buffer read in iteration ks-1
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_block(af1, bf1);
+        buf = buf + 1 == STAGES ? 0 : buf + 1;
+    }
+    wait_vmcnt<0>();
+    __syncthreads();  // all ds_reads of the last tile done before the LDS is reused
+
+    // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
+    // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r.
+    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row
+    static_assert(BM * CROW <= STAGES * STAGE, "C tile fits the staging LDS");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                const int col = wn * 64 + j * 16 + (lane & 15);
+                *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(acc[i][j][r]);
+            }
+    __syncthreads();
+    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
+    for (int v = tid; v < BM * VPR; v += NT) {
+        const int row = v / VPR, cv = v - row * VPR;
+        const int m = m0 + row;
+        if (m < g.M)
+            *reinterpret_cast<uint4 *>(y + static_cast<int64_t>(m) * g.K + n0 + cv * 8) =
+                *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
+    }
+}
+
+// w'[ci, kh, kw, co] = w[co, 2-kh, 2-kw, ci]  (the stride-1 data-gradient weights)
+__global__ void conv3x3_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__restrict__ wt, int Cout, int Cin) {
+    const int64_t n = static_cast<int64_t>(Cout) * 9 * Cin;
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int co = static_cast<int>(i % Cout);
+        int64_t t = i / Cout;
+        const int tap = static_cast<int>(t % 9);
+        const int ci = static_cast<int>(t / 9);
+        wt[i] = w[(static_cast<int64_t>(co) * 9 + (8 - tap)) * Cin + ci];
+    }
+}
+
+}  // namespace
+
+bool conv3x3_supported(int Cin, int Cout, int stride) {
+    return Cin % 64 == 0 && Cout % 64 == 0 && (stride == 1 || stride == 2) && Cin >= 64;
+}
+
+// 256-byte zero page for padding rows (global_load_lds needs a real address).
+const void *zero_page() {
+    static void *p = [] {
+        void *q = nullptr;
+        (void)hipMalloc(&q, 256);
+        (void)hipMemset(q, 0, 256);
+        return q;
+    }();
+    return p;
+}
+
+template <int WM, int WN, int ST>
+void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, hipStream_t s) {
+    g.mtiles = (g.M + 64 * WM - 1) / (64 * WM);
+    g.ntiles = g.K / (64 * WN);
+    conv3x3_kernel<WM, WN, ST><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+        x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g);
+}
+
+int conv3x3_variants() { return 5; }
+
+void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
+                    int stride, hipStream_t s, int variant) {
+    Geo g;
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
+    g.OH = (H + 2 - 3) / stride + 1;
+    g.OW = (W + 2 - 3) / stride + 1;
+    g.M = N * g.OH * g.OW;
+    g.mtiles = g.ntiles = 0;
+    // default per shape class (tools/bench_conv3x3.py): 256x128/8 waves/3 stages when Cout
+    // allows, else 256x64/4 waves/2 stages
+    if (variant < 0) variant = Cout % 128 == 0 ? 1 : 2;
+    switch (variant) {
+    case 0: if (Cout % 128 == 0) { launch_variant<2, 2, 2>(x, w, y, g, s); break; }          // 128x128, 4 waves
+            [[fallthrough]];
+    case 1: if (Cout % 128 == 0) { launch_variant<4, 2, 3>(x, w, y, g, s); break; }          // 256x128, 8 waves
+            [[fallthrough]];
+    case 2: launch_variant<4, 1, 2>(x, w, y, g, s); break;                                   // 256x64, 4 waves
+    case 3: launch_variant<4, 1, 3>(x, w, y, g, s); break;                                   // 256x64, 3 stages
+    default: launch_variant<8, 1, 2>(x, w, y, g, s); break;                                  // 512x64, 8 waves
+    }
+}
+
+void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s) {
+    const int64_t n = static_cast<int64_t>(Cout) * 9 * Cin;
+    int grid = static_cast<int>((n + 255) / 256);
+    if (grid > 4096) grid = 4096;
+    conv3x3_flip_kernel<<<grid, 256, 0, s>>>(w, wt, Cout, Cin);
+}
+
+}  // namespace kfk

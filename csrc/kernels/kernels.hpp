@@ -81,6 +81,16 @@ struct GradAccTable {
 int grad_accumulate_blocks(int64_t numel);
 void launch_grad_accumulate(const GradAccTable &tab, float *flat, hipStream_t s);
 
+// 3x3 convolution, pad 1, stride 1|2, NHWC bf16 (x [N,H,W,Cin], w [Cout,3,3,Cin],
+// y [N,OH,OW,Cout]) as an MFMA implicit GEMM (conv.hip).  Cin, Cout multiples of 64.
+bool conv3x3_supported(int Cin, int Cout, int stride);
+// variant: tile/pipeline choice (-1 = default for the shape; 0..conv3x3_variants()-1 for tuning).
+void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
+                    int stride, hipStream_t s, int variant = -1);
+int conv3x3_variants();
+// wt[ci,kh,kw,co] = w[co,2-kh,2-kw,ci]: stride-1 data gradient = conv3x3(dy, wt).
+void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s);
+
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
 struct BNShape {

@@ -1,0 +1,97 @@
+"""3x3 convolutions on the hand-written MFMA implicit-GEMM kernel (csrc/kernels/conv.hip).
+
+``conv3x3(x, w, stride)`` computes ``F.conv2d(x, w, stride=stride, padding=1)`` for NHWC
+(channels_last) bf16 tensors with Cin, Cout multiples of 64:
+
+* forward: ``_hip.conv3x3`` (stride 1 or 2);
+* data gradient, stride 1: the same kernel on the flipped/transposed weights
+  (``dx = conv3x3(dy, w')``, ``w'[ci,co,kh,kw] = w[co,ci,2-kh,2-kw]``);
+  stride 2: MIOpen (``aten.convolution_backward``);
+* weight gradient: MIOpen.
+
+Measured per ResNet-50 shape against MIOpen in ``tools/bench_conv3x3.py`` (profiles/README.md).
+Set ``KUNGFU_CONV3X3=0`` to route everything through MIOpen.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from .._lib import hip, hip_available
+
+_ENABLED = os.environ.get("KUNGFU_CONV3X3", "1") != "0"
+
+
+def set_enabled(on: bool) -> bool:
+    """Turn the MFMA 3x3 path on/off at run time; returns the previous setting."""
+    global _ENABLED
+    old, _ENABLED = _ENABLED, bool(on)
+    return old
+
+
+def eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    if not _ENABLED or not x.is_cuda or groups != 1:
+        return False
+    st = stride if isinstance(stride, int) else (stride[0] if stride[0] == stride[1] else -1)
+    pd = padding if isinstance(padding, int) else (padding[0] if padding[0] == padding[1] else -1)
+    dl = dilation if isinstance(dilation, int) else (dilation[0] if dilation[0] == dilation[1] else -1)
+    if st not in (1, 2) or pd != 1 or dl != 1:
+        return False
+    if w.dim() != 4 or w.shape[2] != 3 or w.shape[3] != 3 or x.dim() != 4:
+        return False
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if not w.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if not hip_available():
+        return False
+    return hip().conv3x3_supported(int(x.shape[1]), int(w.shape[0]), int(st))
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride):
+        ctx.save_for_backward(x, w)
+        ctx.stride = stride
+        return hip().conv3x3(x, w, stride)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        s = ctx.stride
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        need_dx, need_dw = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if need_dx and s == 1:
+            dx = hip().conv3x3(dy, hip().conv3x3_flip_weight(w), 1)
+            need_dx = False
+        if need_dx or need_dw:
+            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                            [need_dx, need_dw, False])
+            if need_dx:
+                dx = gx
+            if need_dw:
+                dw = gw
+        return dx, dw, None
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> torch.Tensor:
+    """3x3, padding 1 convolution (MFMA kernel when eligible, else F.conv2d)."""
+    if eligible(x, w, stride, 1, 1, 1):
+        return _Conv3x3Fn.apply(x, w, int(stride if isinstance(stride, int) else stride[0]))
+    return F.conv2d(x, w, stride=stride, padding=1)
+
+
+def conv2d(x, w, bias, stride, padding, dilation, groups):
+    """F.conv2d with the 3x3 MFMA fast path (bias handled outside the kernel)."""
+    if eligible(x, w, stride, padding, dilation, groups):
+        y = _Conv3x3Fn.apply(x, w, int(stride if isinstance(stride, int) else stride[0]))
+        if bias is not None:
+            y = y + bias.view(1, -1, 1, 1).to(y.dtype)
+        return y
+    return F.conv2d(x, w, bias, stride, padding, dilation, groups)

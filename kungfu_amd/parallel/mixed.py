@@ -83,7 +83,14 @@ def shadow(p: torch.Tensor) -> torch.Tensor:
 
 
 def _conv_forward(self, x):
-    return self._conv_forward(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
+    w = shadow(self.weight)
+    b = shadow(self.bias) if self.bias is not None else None
+    if isinstance(self, nn.Conv2d) and self.padding_mode == "zeros" and x.dtype == torch.bfloat16:
+        # 3x3 convolutions take the hand-written MFMA implicit-GEMM kernel (ops/conv.py)
+        from ..ops import conv as _conv
+
+        return _conv.conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups)
+    return self._conv_forward(x, w, b)
 
 
 def _linear_forward(self, x):

@@ -264,6 +264,32 @@ def test_resnet_step_ssgd_fused_vs_plain():
 
 
 @needs_gpu
+@pytest.mark.parametrize("shape", [(2, 64, 56, 64, 1), (2, 128, 28, 256, 2), (3, 256, 14, 128, 1), (2, 512, 7, 512, 1),
+                                   (1, 64, 9, 128, 2), (2, 192, 5, 64, 1)])
+def test_conv3x3_mfma_matches_torch(shape):
+    """MFMA implicit-GEMM 3x3 conv (fwd, dgrad via flipped weights, wgrad) vs f32 torch."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.conv import _Conv3x3Fn, eligible
+
+    torch.manual_seed(4)
+    N, C, Hh, K, s = shape
+    x = (torch.randn(N, C, Hh, Hh + 1, device="cuda")).bfloat16().to(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 3, 3, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+    assert eligible(x, w, s, 1, 1, 1)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    yr = F.conv2d(xr, wr, stride=s, padding=1)
+    xa, wa = x.detach().requires_grad_(), w.detach().requires_grad_()
+    ya = _Conv3x3Fn.apply(xa, wa, s)
+    assert ya.shape == yr.shape and ya.is_contiguous(memory_format=torch.channels_last)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    ya.backward(g.bfloat16().to(memory_format=torch.channels_last))
+    for a, r in [(ya, yr), (xa.grad, xr.grad), (wa.grad, wr.grad)]:
+        assert ((a.float() - r).norm() / r.norm()).item() < 1e-2
+
+
+@needs_gpu
 def test_grad_accumulate_multi_tensor(H):
     """_hip.grad_accumulate (flat += bf16/f32 sources, batched tables) vs torch f32."""
     torch.manual_seed(3)
@@ -320,9 +346,15 @@ def test_resnet_ssgd_bf16_shadow_matches_autocast():
             ls.append(loss.item())
         return ls, g0
 
-    l_a, g_a = run(False)
-    l_b, g_b = run(False)
-    l_s, g_s = run(True)
+    from kungfu_amd.ops import conv as conv_ops
+
+    old = conv_ops.set_enabled(False)  # isolate the shadow/direct-gradient path from the conv kernels
+    try:
+        l_a, g_a = run(False)
+        l_b, g_b = run(False)
+        l_s, g_s = run(True)
+    finally:
+        conv_ops.set_enabled(old)
     # same math; conv kernels may pick other tiles/split-K for a differently aligned weight view
     assert abs(l_s[0] - l_a[0]) <= max(2 * abs(l_b[0] - l_a[0]), 1e-3 * abs(l_a[0])), (l_a, l_b, l_s)
     def fro(a, b):
