@@ -52,6 +52,9 @@ for ep in range(a.epochs):
         loss = F.cross_entropy(model(xb), yb)
         loss.backward()
         opt.step()
+# async optimizers (pair averaging) pull from peers' stores at any time: do not let a
+# fast peer exit (closing its store) while a slower one may still request from it
+kf.run_barrier()
 with torch.no_grad():
     acc = (model(data["test_x"].reshape(-1, 784)).argmax(1) == data["test_y"]).float().mean().item()
 digest = "%.6e" % model.fc.weight.detach().double().norm().item()
