@@ -266,6 +266,65 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
     return y;
 }
 
+// General 1x1 / 3x3 convolution with fused epilogues (conv.hip).
+// stats: f64 [kStatSlots*2*Cout] zero-initialised workspace receiving sum / sum of squares of the
+// bf16 outputs per channel (consumed and re-zeroed by bn_forward(..., sums=stats)).
+// out: accumulate target (y = out + conv(x, w), written in place and returned).
+at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
+                c10::optional<at::Tensor> out, int64_t variant) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv: x must be a 4-D channels_last bf16 GPU tensor");
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) && w.size(1) == x.size(1) &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == x.device(),
+                "conv: w must be [Cout, Cin, KS, KS] channels_last bf16 on x's device");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0), ks = w.size(2);
+    TORCH_CHECK(kfk::conv_supported(C, K, ks, static_cast<int>(stride)), "conv: unsupported channels/kernel/stride");
+    const int pad = (ks - 1) / 2;
+    const int OH = (H + 2 * pad - ks) / stride + 1, OW = (W + 2 * pad - ks) / stride + 1;
+    TORCH_CHECK(OH > 0 && OW > 0, "conv: empty output");
+    TORCH_CHECK(static_cast<int64_t>(N) * H * W * C < (int64_t(1) << 31) &&
+                    static_cast<int64_t>(N) * OH * OW * K < (int64_t(1) << 31),
+                "conv: tensor too large for 32-bit offsets");
+    c10::DeviceGuard gd(x.device());
+    double *sp = nullptr;
+    if (stats && stats->defined()) {
+        TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->numel() == 2 * K * kfk::kStatSlots &&
+                        stats->is_contiguous() && stats->device() == x.device(),
+                    "conv: stats must be a contiguous f64 [2*Cout] tensor on x's device");
+        sp = stats->data_ptr<double>();
+    }
+    at::Tensor y;
+    bool accum = false;
+    if (out && out->defined()) {
+        TORCH_CHECK(out->scalar_type() == at::kBFloat16 && out->dim() == 4 && out->size(0) == N && out->size(1) == K &&
+                        out->size(2) == OH && out->size(3) == OW &&
+                        out->is_contiguous(at::MemoryFormat::ChannelsLast) && out->device() == x.device(),
+                    "conv: out must be the [N, Cout, OH, OW] channels_last bf16 output");
+        y = *out;
+        accum = true;
+    } else {
+        y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    }
+    kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                     reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), sp,
+                     accum, stream_of(x, 0), static_cast<int>(variant));
+    return y;
+}
+
+// [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
+at::Tensor conv_flip_weight(at::Tensor w) {
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_flip_weight: [Cout, Cin, KS, KS] channels_last bf16 required");
+    const int K = w.size(0), C = w.size(1), ks = w.size(2);
+    c10::DeviceGuard gd(w.device());
+    auto wt = at::empty({C, K, ks, ks}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_conv_flip_weight(reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                                 reinterpret_cast<uint16_t *>(wt.data_ptr()), K, C, ks, stream_of(w, 0));
+    return wt;
+}
+
 // [Cout, Cin, 3, 3] channels_last -> flipped/transposed [Cin, Cout, 3, 3] channels_last
 at::Tensor conv3x3_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
@@ -319,7 +378,7 @@ BNCommon bn_common(int C, const at::Tensor &weight, const at::Tensor &bias,
 std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
                                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                    double momentum, double eps, bool training, bool relu,
-                                   c10::optional<at::Tensor> num_batches) {
+                                   c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> sums) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
@@ -336,14 +395,21 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
     auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
     at::Tensor mask;
     if (rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
+    double *sp = nullptr;
+    if (training && sums && sums->defined()) {
+        TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->numel() == 2 * C * kfk::kStatSlots &&
+                        sums->is_contiguous() && sums->device() == x.device(),
+                    "bn: sums must be the conv epilogue's f64 [2*C] workspace");
+        sp = sums->data_ptr<double>();
+    }
     at::Tensor partial;
-    if (training) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    if (training && !sp) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     kfk::launch_bn_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, weight.data_ptr<float>(),
                            bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()),
                            mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, sh, relu, training, b.rm, b.rv,
                            static_cast<float>(momentum), static_cast<float>(eps),
-                           training ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0));
+                           partial.defined() ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp);
     return {y, mean, invstd, coef, mask};
 }
 
@@ -544,6 +610,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv3x3", &conv3x3, "3x3 pad-1 NHWC bf16 convolution (MFMA implicit GEMM)", py::arg("x"), py::arg("w"),
           py::arg("stride") = 1, py::arg("variant") = -1);
     m.def("conv3x3_variants", &kfk::conv3x3_variants);
+    m.def("conv", &conv, "1x1/3x3 NHWC bf16 convolution (MFMA implicit GEMM) with fused BN-statistics and "
+          "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
+          py::arg("out") = py::none(), py::arg("variant") = -1);
+    m.def("conv_flip_weight", &conv_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,KS-1-kh,KS-1-kw] (data-gradient weights)");
+    m.def("conv_supported", &kfk::conv_supported);
+    m.attr("conv_stat_slots") = kfk::kStatSlots;
     m.def("conv3x3_flip_weight", &conv3x3_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,2-kh,2-kw] (data-gradient weights)");
     m.def("conv3x3_supported", &kfk::conv3x3_supported);
     m.def("bn_supported_channels", &kfk::bn_supported_channels);
@@ -551,7 +623,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd, coef, relu mask or None)", py::arg("x"),
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
-          py::arg("num_batches") = py::none());
+          py::arg("num_batches") = py::none(), py::arg("sums") = py::none());
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
           py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"));

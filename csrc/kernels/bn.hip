@@ -212,6 +212,40 @@ __global__ __launch_bounds__(kBlock) void bn_stats_finalize(const float *partial
     coef[C + c] = b - static_cast<float>(m) * sc;
 }
 
+// Same outputs from f64 per-channel sums produced by a convolution epilogue
+// (conv.hip, EPI bit 0): kStatSlots slots of [sum x (C), sum x^2 (C)]; the sums are
+// re-zeroed for the next producer (self-cleaning workspace, no memset launch).
+__global__ void bn_sums_finalize(double *sums, int C, int64_t rows, const float *gamma, const float *beta,
+                                 float *mean, float *invstd, float *run_mean, float *run_var, float momentum,
+                                 float eps, float *coef, int64_t *num_batches) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (num_batches && c == 0) num_batches[0] += 1;
+    if (c >= C) return;
+    double s = 0, q = 0;
+    for (int k = 0; k < kStatSlots; ++k) {
+        double *sl = sums + k * 2 * C;
+        s += sl[c];
+        q += sl[C + c];
+        sl[c] = 0.0;
+        sl[C + c] = 0.0;
+    }
+    const double m = s / rows;
+    double var = q / rows - m * m;
+    if (var < 0) var = 0;
+    const float is = rsqrtf(static_cast<float>(var) + eps);
+    mean[c] = static_cast<float>(m);
+    invstd[c] = is;
+    if (run_mean) {
+        const double unbiased = rows > 1 ? var * rows / (rows - 1) : var;
+        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * static_cast<float>(m);
+        run_var[c] = (1.f - momentum) * run_var[c] + momentum * static_cast<float>(unbiased);
+    }
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float sc = g * is;
+    coef[c] = sc;
+    coef[C + c] = b - static_cast<float>(m) * sc;
+}
+
 // Eval mode: coefficients from running stats.
 __global__ void bn_eval_coef(int C, const float *gamma, const float *beta, const float *run_mean,
                              const float *run_var, float eps, float *mean, float *invstd, float *coef) {
@@ -636,10 +670,13 @@ int bn_num_chunks(BNShape sh) { return chunking(sh).nchunks; }
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
-                       int64_t *num_batches, hipStream_t s) {
+                       int64_t *num_batches, hipStream_t s, double *sums) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
-    if (training) {
+    if (training && sums) {
+        bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
+                                                         run_var, momentum, eps, coef, num_batches);
+    } else if (training) {
         launch_stats(x, sh, gamma, beta, run_mean, run_var, momentum, eps, partial, mean, invstd, coef, num_batches,
                      s);
     } else {

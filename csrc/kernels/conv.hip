@@ -1,5 +1,6 @@
-// 3x3 convolution (pad 1, stride 1 or 2), NHWC bf16, as an implicit GEMM on
-// CDNA4 matrix cores (v_mfma_f32_16x16x32_bf16), for gfx950.
+// 3x3 (pad 1) and 1x1 (pad 0) convolutions, stride 1 or 2, NHWC bf16, as an implicit
+// GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x32_bf16), for gfx950, with optional
+// fused epilogues: BN batch statistics of the output, accumulate-into-destination.
 //
 //   y[m, co] = sum_{kh, kw, ci} x[n, oh*s + kh - 1, ow*s + kw - 1, ci] * w[co, kh, kw, ci]
 //   GEMM: M = N*OH*OW output pixels, N = Cout, K = 9 * Cin (tap-major, channel-minor)
@@ -52,12 +53,17 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
-template <int WM, int WN, int STAGES>
-__global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(const uint16_t *__restrict__ x,
-                                                               const uint16_t *__restrict__ w,
-                                                               uint16_t *__restrict__ y,
-                                                               const uint16_t *__restrict__ zero, Geo g) {
+// KS = 3 (pad 1) or 1 (pad 0); EPI bit 0: per-channel sum / sum-of-squares of the bf16
+// outputs accumulated (f64 atomics) into stats[2][K] (fused BN statistics); bit 1:
+// y += conv (accumulate into the existing bf16 tensor, e.g. a residual gradient).
+template <int KS, int WM, int WN, int STAGES, int EPI>
+__global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__restrict__ x,
+                                                            const uint16_t *__restrict__ w,
+                                                            uint16_t *__restrict__ y,
+                                                            const uint16_t *__restrict__ zero, Geo g,
+                                                            double *__restrict__ stats) {
     constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+    constexpr int TAPS = KS * KS, PAD = (KS - 1) / 2;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
     constexpr int STAGE = A_BYTES + B_BYTES;
     constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
@@ -92,16 +98,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(const uint16_t *_
         a_ok[j] = 0;
         if (m < g.M) {
             const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
-            const int ih0 = oh * g.stride - 1, iw0 = ow * g.stride - 1;
+            const int ih0 = oh * g.stride - PAD, iw0 = ow * g.stride - PAD;
             a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
             uint32_t ok = 0;
 #pragma unroll
-            for (int kh = 0; kh < 3; ++kh)
+            for (int kh = 0; kh < KS; ++kh)
 #pragma unroll
-                for (int kw = 0; kw < 3; ++kw)
+                for (int kw = 0; kw < KS; ++kw)
                     if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
                         static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
-                        ok |= 1u << (kh * 3 + kw);
+                        ok |= 1u << (kh * KS + kw);
             a_ok[j] = ok;
         }
     }
@@ -109,14 +115,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(const uint16_t *_
 #pragma unroll
     for (int j = 0; j < B_INST; ++j) {
         const int r = (wave * B_INST + j) * 8 + srow;
-        b_off[j] = (n0 + r) * 9 * g.C + schunk * 8;
+        b_off[j] = (n0 + r) * TAPS * g.C + schunk * 8;
     }
     const int csteps = g.C / kBK;
-    const int ksteps = 9 * csteps;
+    const int ksteps = TAPS * csteps;
 
     auto stage = [&](int ks, int buf) {
         const int tap = ks / csteps, cc = ks - tap * csteps;
-        const int kh = tap / 3, kw = tap - kh * 3;
+        const int kh = tap / KS, kw = tap - kh * KS;
         const int toff = (kh * g.W + kw) * g.C + cc * kBK;  // wave-uniform
         uint8_t *abase = lds + buf * STAGE;
         uint8_t *bbase = abase + A_BYTES;
@@ -207,26 +213,73 @@ __global__ __launch_bounds__(64 * WM * WN) void conv3x3_kernel(const uint16_t *_
                 *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(acc[i][j][r]);
             }
     __syncthreads();
+    if constexpr (EPI & 1) {
+        // fused BN statistics of the bf16-rounded tile (rows past M are zero rows)
+        constexpr int PARTS = NT / BN, RPP = BM / PARTS;
+        static_assert(PARTS * BN == NT && RPP * PARTS == BM, "stats split");
+        float *red = reinterpret_cast<float *>(lds + BM * CROW);
+        static_assert(BM * CROW + 2 * NT * 4 <= STAGES * STAGE, "stats scratch fits");
+        const int col = tid % BN, part = tid / BN;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll 8
+        for (int r = part * RPP; r < (part + 1) * RPP; ++r) {
+            const float v = bf16_to_f32(*reinterpret_cast<const uint16_t *>(lds + r * CROW + col * 2));
+            s1 += v;
+            s2 += v * v;
+        }
+        red[tid] = s1;
+        red[NT + tid] = s2;
+        __syncthreads();
+        if (part == 0) {
+            double t1 = 0, t2 = 0;
+#pragma unroll
+            for (int p = 0; p < PARTS; ++p) {
+                t1 += red[p * BN + col];
+                t2 += red[NT + p * BN + col];
+            }
+            double *sl = stats + (mt % kStatSlots) * 2 * g.K;  // spread atomics over slots
+            atomicAdd(sl + n0 + col, t1);
+            atomicAdd(sl + g.K + n0 + col, t2);
+        }
+    }
     constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     for (int v = tid; v < BM * VPR; v += NT) {
         const int row = v / VPR, cv = v - row * VPR;
         const int m = m0 + row;
-        if (m < g.M)
-            *reinterpret_cast<uint4 *>(y + static_cast<int64_t>(m) * g.K + n0 + cv * 8) =
-                *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
+        if (m < g.M) {
+            uint4 *dst = reinterpret_cast<uint4 *>(y + static_cast<int64_t>(m) * g.K + n0 + cv * 8);
+            uint4 val = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
+            if constexpr (EPI & 2) {
+                const uint4 old = *dst;
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(&val);
+                const uint32_t *b = reinterpret_cast<const uint32_t *>(&old);
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float lo = bf16_to_f32(static_cast<uint16_t>(a[k] & 0xffffu)) +
+                                     bf16_to_f32(static_cast<uint16_t>(b[k] & 0xffffu));
+                    const float hi = bf16_to_f32(static_cast<uint16_t>(a[k] >> 16)) +
+                                     bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
+                    o[k] = static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+                }
+                val = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            *dst = val;
+        }
     }
 }
 
-// w'[ci, kh, kw, co] = w[co, 2-kh, 2-kw, ci]  (the stride-1 data-gradient weights)
-__global__ void conv3x3_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__restrict__ wt, int Cout, int Cin) {
-    const int64_t n = static_cast<int64_t>(Cout) * 9 * Cin;
+// w'[ci, kh, kw, co] = w[co, KS-1-kh, KS-1-kw, ci]  (the stride-1 data-gradient weights)
+__global__ void conv_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__restrict__ wt, int Cout, int Cin,
+                                 int taps) {
+    const int64_t n = static_cast<int64_t>(Cout) * taps * Cin;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int co = static_cast<int>(i % Cout);
         int64_t t = i / Cout;
-        const int tap = static_cast<int>(t % 9);
-        const int ci = static_cast<int>(t / 9);
-        wt[i] = w[(static_cast<int64_t>(co) * 9 + (8 - tap)) * Cin + ci];
+        const int tap = static_cast<int>(t % taps);
+        const int ci = static_cast<int>(t / taps);
+        wt[i] = w[(static_cast<int64_t>(co) * taps + (taps - 1 - tap)) * Cin + ci];
     }
 }
 
@@ -234,6 +287,10 @@ __global__ void conv3x3_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__
 
 bool conv3x3_supported(int Cin, int Cout, int stride) {
     return Cin % 64 == 0 && Cout % 64 == 0 && (stride == 1 || stride == 2) && Cin >= 64;
+}
+
+bool conv_supported(int Cin, int Cout, int ks, int stride) {
+    return (ks == 1 || ks == 3) && conv3x3_supported(Cin, Cout, stride);
 }
 
 // 256-byte zero page for padding rows (global_load_lds needs a real address).
@@ -247,43 +304,72 @@ const void *zero_page() {
     return p;
 }
 
-template <int WM, int WN, int ST>
-void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, hipStream_t s) {
+template <int KS, int WM, int WN, int ST>
+void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, double *stats, bool accum,
+                    hipStream_t s) {
     g.mtiles = (g.M + 64 * WM - 1) / (64 * WM);
     g.ntiles = g.K / (64 * WN);
-    conv3x3_kernel<WM, WN, ST><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
-        x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g);
-}
-
-int conv3x3_variants() { return 5; }
-
-void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
-                    int stride, hipStream_t s, int variant) {
-    Geo g;
-    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
-    g.OH = (H + 2 - 3) / stride + 1;
-    g.OW = (W + 2 - 3) / stride + 1;
-    g.M = N * g.OH * g.OW;
-    g.mtiles = g.ntiles = 0;
-    // default per shape class (tools/bench_conv3x3.py): 256x128/8 waves/3 stages when Cout
-    // allows, else 256x64/4 waves/2 stages
-    if (variant < 0) variant = Cout % 128 == 0 ? 1 : 2;
-    switch (variant) {
-    case 0: if (Cout % 128 == 0) { launch_variant<2, 2, 2>(x, w, y, g, s); break; }          // 128x128, 4 waves
-            [[fallthrough]];
-    case 1: if (Cout % 128 == 0) { launch_variant<4, 2, 3>(x, w, y, g, s); break; }          // 256x128, 8 waves
-            [[fallthrough]];
-    case 2: launch_variant<4, 1, 2>(x, w, y, g, s); break;                                   // 256x64, 4 waves
-    case 3: launch_variant<4, 1, 3>(x, w, y, g, s); break;                                   // 256x64, 3 stages
-    default: launch_variant<8, 1, 2>(x, w, y, g, s); break;                                  // 512x64, 8 waves
+    const dim3 grid(g.mtiles * g.ntiles), block(64 * WM * WN);
+    const auto *z = reinterpret_cast<const uint16_t *>(zero_page());
+    const int epi = (stats ? 1 : 0) | (accum ? 2 : 0);
+    switch (epi) {
+    case 0: conv_kernel<KS, WM, WN, ST, 0><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
+    case 1: conv_kernel<KS, WM, WN, ST, 1><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
+    case 2: conv_kernel<KS, WM, WN, ST, 2><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
+    default: conv_kernel<KS, WM, WN, ST, 3><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
     }
 }
 
-void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s) {
-    const int64_t n = static_cast<int64_t>(Cout) * 9 * Cin;
+template <int KS>
+void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, double *stats, bool accum, hipStream_t s,
+               int variant) {
+    // default per shape class (tools/bench_conv3x3.py, tools/bench_conv.py): 3x3 -> 256x128 /
+    // 8 waves / 3 stages when Cout allows; 1x1 (1-16 K-steps) -> 128x128 / 4 waves / 2 stages
+    // (two blocks per CU keep more HBM traffic in flight); Cout = 64 -> 256x64 / 4 waves
+    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : 1) : 2;
+    switch (variant) {
+    case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2>(x, w, y, g, stats, accum, s); break; }  // 128x128
+            [[fallthrough]];
+    case 1: if (g.K % 128 == 0) { launch_variant<KS, 4, 2, 3>(x, w, y, g, stats, accum, s); break; }  // 256x128
+            [[fallthrough]];
+    case 2: launch_variant<KS, 4, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 256x64
+    case 3: launch_variant<KS, 4, 1, 3>(x, w, y, g, stats, accum, s); break;                          // 256x64 3st
+    case 4: launch_variant<KS, 8, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 512x64
+    case 5: launch_variant<KS, 2, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 128x64
+    default: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3>(x, w, y, g, stats, accum, s); break; } // 128x128 3st
+             launch_variant<KS, 2, 1, 3>(x, w, y, g, stats, accum, s); break;                         // 128x64 3st
+    }
+}
+
+int conv3x3_variants() { return 7; }
+
+void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
+                 int stride, double *stats, bool accumulate, hipStream_t s, int variant) {
+    Geo g;
+    const int pad = (ks - 1) / 2;
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
+    g.OH = (H + 2 * pad - ks) / stride + 1;
+    g.OW = (W + 2 * pad - ks) / stride + 1;
+    g.M = N * g.OH * g.OW;
+    g.mtiles = g.ntiles = 0;
+    if (ks == 1) launch_ks<1>(x, w, y, g, stats, accumulate, s, variant);
+    else launch_ks<3>(x, w, y, g, stats, accumulate, s, variant);
+}
+
+void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
+                    int stride, hipStream_t s, int variant) {
+    launch_conv(x, w, y, N, H, W, Cin, Cout, 3, stride, nullptr, false, s, variant);
+}
+
+void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s) {
+    const int64_t n = static_cast<int64_t>(Cout) * ks * ks * Cin;
     int grid = static_cast<int>((n + 255) / 256);
     if (grid > 4096) grid = 4096;
-    conv3x3_flip_kernel<<<grid, 256, 0, s>>>(w, wt, Cout, Cin);
+    conv_flip_kernel<<<grid, 256, 0, s>>>(w, wt, Cout, Cin, ks * ks);
+}
+
+void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s) {
+    launch_conv_flip_weight(w, wt, Cout, Cin, 3, s);
 }
 
 }  // namespace kfk

@@ -88,6 +88,18 @@ bool conv3x3_supported(int Cin, int Cout, int stride);
 void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
                     int stride, hipStream_t s, int variant = -1);
 int conv3x3_variants();
+// General KS x KS (KS = 1 or 3, pad (KS-1)/2) convolution with fused epilogues:
+// stats != nullptr: f64 atomics of per-output-channel sum / sum of squares of the bf16
+// outputs into stats[0..K) / stats[K..2K) (the caller zeroes them; bn_stats_from_sums
+// consumes and re-zeroes them); accumulate: y += conv(x, w) instead of y = conv(x, w).
+// The stats workspace is kStatSlots x [2][K] f64 (tiles add into slot tile % kStatSlots,
+// keeping atomic contention per address low); bn_forward(sums=...) folds the slots.
+constexpr int kStatSlots = 16;
+bool conv_supported(int Cin, int Cout, int ks, int stride);
+void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
+                 int stride, double *stats, bool accumulate, hipStream_t s, int variant = -1);
+// wt[ci,kh,kw,co] = w[co,KS-1-kh,KS-1-kw,ci]: stride-1 data gradient = conv(dy, wt).
+void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,2-kh,2-kw,ci]: stride-1 data gradient = conv3x3(dy, wt).
 void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s);
 
@@ -106,7 +118,8 @@ int bn_num_chunks(BNShape sh);  // partial scratch = 2 * nchunks * C floats
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
-                       int64_t *num_batches, hipStream_t s);
+                       int64_t *num_batches, hipStream_t s, double *sums = nullptr);
+// (sums: f64 [2C] batch sums from a conv epilogue -> no statistics pass; re-zeroed.)
 // dz = dy * relu'(.)  -- from mask bits if given, else recomputed as x*fcoef[0:C] + fcoef[C:2C] > 0
 // (fcoef = the forward's coef) ; dgamma/dbeta (f32) ; dx = k1*dz + k2*x + k3 ; dres = dz.
 // coef scratch: 3C floats.

@@ -12,7 +12,8 @@ MI355X-specific choices:
 * ``channels_last`` (NHWC) memory format end to end, so MIOpen picks its NHWC
   implicit-GEMM (MFMA) convolution solvers and batch-norm stays contiguous in C.
 * Optional fused BN(+residual)+ReLU epilogue from :mod:`kungfu_amd.ops.fused_bn`
-  (HIP kernel), selected with ``fused_bn=True``.
+  (HIP kernel), selected with ``fused_bn=True``; in training each bottleneck then runs
+  as one autograd node on the MFMA convolution kernels (:mod:`kungfu_amd.ops.fused_block`).
 """
 from __future__ import annotations
 
@@ -94,6 +95,13 @@ class Bottleneck(nn.Module):
             self.relu = nn.ReLU(inplace=True)
 
     def forward(self, x):
+        if self.fused_tail:
+            # training: the whole block as one node on the MFMA conv + fused BN kernels
+            # (conv epilogue BN statistics, in-place residual gradient; ops/fused_block.py)
+            from kungfu_amd.ops import fused_block
+
+            if fused_block.eligible(self, x):
+                return fused_block.bottleneck_forward(self, x)
         idt = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x))
         out = self.bn2(self.conv2(out))

@@ -1,0 +1,218 @@
+"""One autograd node per ResNet bottleneck block, sequenced by hand on the HIP kernels.
+
+Why a block-level node: with one node per conv / BN, autograd materialises every
+intermediate exactly as the modules produce it and sums the two gradients that reach
+each block input (identity + conv1 data gradient) with a separate elementwise add
+(16 per ResNet-50 step, 1.3 ms of 28 ms on MI355X, profiles/r7_*.md), and each BN
+re-reads its input for batch statistics.  Owning the block's forward and backward
+lets the MI355X kernels fuse across layer boundaries:
+
+forward (training)
+* every convolution (1x1 and 3x3, stride 1/2) runs on the MFMA implicit-GEMM kernel
+  (csrc/kernels/conv.hip) whose epilogue also accumulates the per-channel
+  sum / sum-of-squares of its bf16 output (slotted f64 atomics) -> the BN that follows
+  skips its statistics pass and only folds the sums (``bn_forward(..., sums=)``);
+* BN(+ReLU) and BN3 + residual + ReLU are the fused bn.hip kernels.
+
+backward
+* stride-1 data gradients are the same MFMA kernel on transposed/flipped weights;
+* the block-input gradient is formed IN PLACE: conv1's data-gradient kernel
+  accumulates into the identity gradient produced by the BN3+add+ReLU backward
+  (or into the downsample branch's data gradient) -- no elementwise add, no extra
+  pass over the largest activation of the block;
+* weight gradients use MIOpen (``aten.convolution_backward`` weight-only);
+* BN gamma/beta gradients go to the flat space's gradient sink when registered
+  (parallel/mixed.py), conv weight gradients flow to the bf16 shadow views.
+
+Saved tensors are the same as per-layer autograd would keep (conv inputs, BN inputs,
+per-channel coefficients, the 1-bit ReLU mask of the block tail).
+
+No reference counterpart: the reference trains ``tf.keras.applications`` ResNet-50
+with stock TF kernels (``benchmarks/system/benchmark_kungfu.py:96``).
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._lib import hip, hip_available
+from ..parallel.mixed import deliver, direct_target, shadow
+
+_ENABLED = os.environ.get("KUNGFU_FUSED_BLOCK", "1") != "0"
+
+
+def set_enabled(on: bool) -> bool:
+    global _ENABLED
+    old, _ENABLED = _ENABLED, bool(on)
+    return old
+
+
+def _cl(t: torch.Tensor) -> torch.Tensor:
+    return t if t.is_contiguous(memory_format=torch.channels_last) else t.contiguous(memory_format=torch.channels_last)
+
+
+def _sums(bn, dev) -> torch.Tensor:
+    """Per-BN f64 statistics workspace (kept zeroed by the finalize kernel)."""
+    ws = getattr(bn, "_kf_sums", None)
+    if ws is None or ws.device != dev:
+        ws = torch.zeros(hip().conv_stat_slots * 2 * bn.num_features, dtype=torch.float64, device=dev)
+        bn._kf_sums = ws
+    return ws
+
+
+def _wgrad(dy, x, w, stride, pad):
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None):
+    """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given)."""
+    H = hip()
+    if stride == 1:
+        return H.conv(dy, H.conv_flip_weight(w), 1, None, out)
+    dx = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                             [True, False, False])[0]
+    if out is not None:
+        out.add_(dx)
+        return out
+    return _cl(dx)
+
+
+class _Spec:
+    """Static description of one block (modules for running stats / workspaces)."""
+    __slots__ = ("bns", "stride", "ds", "dtypes", "direct")
+
+    def __init__(self, bns, stride, ds):
+        self.bns, self.stride, self.ds = bns, stride, ds
+        self.dtypes = None
+        self.direct = None
+
+
+class _BottleneckFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec: _Spec, x, *params):
+        H = hip()
+        dev = x.device
+        ws = [p for p in params]
+        ws_bf = [w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16) for w in ws[0::3]]
+        ws_bf = [_cl(w) for w in ws_bf]
+        gam, bet = ws[1::3], ws[2::3]
+        s = spec.stride
+        outs = []
+
+        def bn(i, y, res, relu):
+            m = spec.bns[i]
+            return H.bn_forward(y, res, gam[i], bet[i], m.running_mean, m.running_var, m.momentum, m.eps, True, relu,
+                                m.num_batches_tracked, _sums(m, dev))
+
+        y1 = H.conv(x, ws_bf[0], 1, _sums(spec.bns[0], dev))
+        z1, m1, i1, c1, _ = bn(0, y1, None, True)
+        y2 = H.conv(z1, ws_bf[1], s, _sums(spec.bns[1], dev))
+        z2, m2, i2, c2, _ = bn(1, y2, None, True)
+        y3 = H.conv(z2, ws_bf[2], 1, _sums(spec.bns[2], dev))
+        if spec.ds:
+            yd = H.conv(x, ws_bf[3], s, _sums(spec.bns[3], dev))
+            idt, md, idd, cd, _ = bn(3, yd, None, False)
+        else:
+            yd = md = idd = cd = None
+            idt = x
+        out, m3, i3, c3, mask3 = bn(2, y3, idt, True)
+        ctx.spec = spec
+        ctx.wdtypes = [w.dtype for w in ws[0::3]]
+        ctx.save_for_backward(x, y1, z1, y2, z2, y3, yd, *ws_bf, *gam, m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3,
+                              md, idd, cd)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        H = hip()
+        spec = ctx.spec
+        nb = 4 if spec.ds else 3
+        t = list(ctx.saved_tensors)
+        x, y1, z1, y2, z2, y3, yd = t[:7]
+        w = t[7:7 + nb]
+        g = t[7 + nb:7 + 2 * nb]
+        (m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3, md, idd, cd) = t[7 + 2 * nb:]
+        s = spec.stride
+        dout = _cl(dout)
+        dbn = [None] * nb  # (dgamma, dbeta)
+        dw = [None] * nb
+        dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, True)
+        dbn[2] = (dg3, db3)
+        dz2 = _dgrad(dy3, z2, w[2], 1, 0)
+        dw[2] = _wgrad(dy3, z2, w[2], 1, 0)
+        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False)
+        dbn[1] = (dg2, db2)
+        dz1 = _dgrad(dy2, z1, w[1], s, 1)
+        dw[1] = _wgrad(dy2, z1, w[1], s, 1)
+        dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False)
+        dbn[0] = (dg1, db1)
+        if spec.ds:
+            dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False)
+            dbn[3] = (dgd, dbd)
+            dx = _dgrad(dyd, x, w[3], s, 0)
+            dw[3] = _wgrad(dyd, x, w[3], s, 0)
+        else:
+            dx = didt  # the identity gradient: conv1's data gradient is accumulated into it
+        dx = _dgrad(dy1, x, w[0], 1, 0, out=dx)
+        dw[0] = _wgrad(dy1, x, w[0], 1, 0)
+        grads: List[Optional[torch.Tensor]] = []
+        for i in range(nb):
+            gw = dw[i]
+            if gw.dtype != ctx.wdtypes[i]:
+                gw = gw.to(ctx.wdtypes[i])
+            dgm, dbt = dbn[i]
+            tgt = spec.direct[i] if spec.direct is not None else None
+            if tgt is not None:
+                deliver(tgt[0], dgm)
+                deliver(tgt[1], dbt)
+                dgm = dbt = None
+            grads += [gw, dgm, dbt]
+        return (None, dx, *grads)
+
+
+def eligible(block, x: torch.Tensor) -> bool:
+    if not (_ENABLED and block.training and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last) or not hip_available():
+        return False
+    H = hip()
+    convs = [block.conv1, block.conv2, block.conv3] + ([block.downsample[0]] if block.downsample is not None else [])
+    for c in convs:
+        if c.bias is not None or c.groups != 1 or c.dilation != (1, 1):
+            return False
+        if not H.conv_supported(c.in_channels, c.out_channels, c.kernel_size[0], c.stride[0]):
+            return False
+    if block.conv2.kernel_size != (3, 3) or block.conv2.padding != (1, 1):
+        return False
+    if block.downsample is not None and block.downsample[0].kernel_size != (1, 1):
+        return False
+    bns = [block.bn1, block.bn2, block.bn3] + ([block.downsample[1]] if block.downsample is not None else [])
+    for b in bns:
+        if not (b.track_running_stats and b.momentum is not None and b.affine):
+            return False
+        if not H.bn_supported_channels(b.num_features):
+            return False
+    return True
+
+
+def bottleneck_forward(block, x: torch.Tensor) -> torch.Tensor:
+    """Training forward of a ResNet ``Bottleneck`` (fused tail) as one autograd node."""
+    ds = block.downsample is not None
+    convs = [block.conv1, block.conv2, block.conv3] + ([block.downsample[0]] if ds else [])
+    bns = [block.bn1, block.bn2, block.bn3] + ([block.downsample[1]] if ds else [])
+    spec = getattr(block, "_kf_spec", None)
+    if spec is None or spec.ds != ds:
+        spec = _Spec(bns, block.conv2.stride[0], ds)
+        block._kf_spec = spec
+    params = []
+    direct = []
+    for c, b in zip(convs, bns):
+        params += [shadow(c.weight), b.weight, b.bias]
+        tw, tb = direct_target(b.weight), direct_target(b.bias)
+        direct.append((tw, tb) if tw is not None and tb is not None else None)
+    spec.direct = direct if any(d is not None for d in direct) else None
+    return _BottleneckFn.apply(spec, x, *params)

@@ -54,7 +54,8 @@ class FusedSGD(torch.optim.Optimizer):
         lr, mu, damp, wd, nes = g["lr"], g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"]
         sp = self.space
         if self._gpu:
-            self._lr_t.fill_(lr)
+            if not torch.cuda.is_current_stream_capturing():  # replays get it from GraphedStep.pre_replay
+                self._lr_t.fill_(lr)
             hip().sgd_step(sp.flat_param, sp.flat_grad, self.momentum_buffer, self.shadow, lr, self._lr_t, mu, damp,
                            wd, self.grad_scale, nes, self._first)
         else:
@@ -120,7 +121,8 @@ class FusedAdam(torch.optim.Optimizer):
         sp = self.space
         self._step_t.add_(1.0)
         if self._gpu:
-            self._lr_t.fill_(lr)
+            if not torch.cuda.is_current_stream_capturing():
+                self._lr_t.fill_(lr)
             hip().adam_step(sp.flat_param, sp.flat_grad, self.exp_avg, self.exp_avg_sq, lr, self._lr_t, b1, b2, eps,
                             wd, self.adamw, self.grad_scale, self._step_t)
         else:

@@ -426,3 +426,109 @@ def test_bench_json():
               "vs_baseline", "dtype", "data", "config"]:
         assert k in d
     assert d["value"] > 0 and d["n_gpus"] == 1
+
+
+@needs_gpu
+@pytest.mark.parametrize("cin,stride,ds", [(256, 1, False), (64, 1, True), (256, 2, True)])
+def test_fused_bottleneck_matches_fp32(cin, stride, ds):
+    """One-node bottleneck (MFMA convs with BN-statistics epilogue, in-place residual
+    gradient) vs the float32 PyTorch composition of the same block; its error must be
+    within the bf16 error of the per-layer bf16 path (autocast + fused BN modules)."""
+    import copy
+
+    import torch.nn as nn
+
+    from kungfu_amd.models.resnet import Bottleneck, conv1x1
+    from kungfu_amd.ops import fused_block
+    from kungfu_amd.ops.fused_bn import BatchNormAct2d
+
+    torch.manual_seed(0)
+    planes = 64
+    norm = lambda c, relu: BatchNormAct2d(c, relu=relu)  # noqa: E731
+    down = nn.Sequential(conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4, relu=False)) if ds else None
+    blk = Bottleneck(cin, planes, stride, down, norm=norm, fused_tail=True).cuda().to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    ref, lay = copy.deepcopy(blk), copy.deepcopy(blk)
+    x = torch.randn(4, cin, 16, 16, device="cuda").to(memory_format=torch.channels_last)
+    gout = torch.randn(4, planes * 4, 16 // stride, 16 // stride, device="cuda")
+
+    def run(mod, xin, fused, autocast):
+        xin = xin.detach().clone().requires_grad_(True)
+        old = fused_block.set_enabled(fused)
+        try:
+            if fused:
+                assert fused_block.eligible(mod, xin)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+                out = mod(xin)
+            (out.float() * gout).sum().backward()
+        finally:
+            fused_block.set_enabled(old)
+        return out, xin.grad
+
+    xb = x.bfloat16()
+    out_f, gx_f = run(blk, xb, True, False)
+    out_r, gx_r = run(ref, xb.float(), False, False)
+    out_l, gx_l = run(lay, xb, False, True)
+
+    def r(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+    def close(a, b, c, what, floor):
+        ef, el = r(a, c), r(b, c)
+        assert ef <= max(1.5 * el, floor), (what, ef, el)
+
+    close(out_f, out_l, out_r, "out", 1e-2)
+    close(gx_f, gx_l, gx_r, "dx", 2e-2)
+    for (n, p), (_, q), (_, l) in zip(blk.named_parameters(), ref.named_parameters(), lay.named_parameters()):
+        assert p.grad is not None, n
+        close(p.grad, l.grad, q.grad, n, 2e-2)
+    for (n, b), (_, c) in zip(blk.named_buffers(), ref.named_buffers()):
+        if b.dtype.is_floating_point:
+            assert r(b, c) < 1e-2, (n, r(b, c))
+        else:
+            assert int(b) == int(c) == 1, n
+
+
+@needs_gpu
+def test_resnet50_fused_block_step_matches_layerwise():
+    """ResNet-50 S-SGD steps (bf16 shadow weights) with one-node fused bottlenecks: the
+    first-step loss is as close to the float32 model as the per-layer bf16 path's, and
+    training proceeds (finite, decreasing loss)."""
+    import torch.nn.functional as F
+
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet50
+    from kungfu_amd.ops import fused_block
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+    x = torch.randn(16, 3, 96, 96, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (16,), device="cuda")
+
+    def run(mode):
+        torch.manual_seed(0)
+        m = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+        o = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9))
+        if mode != "fp32":
+            enable_bf16_shadow(m, o)
+        old = fused_block.set_enabled(mode == "fused")
+        ls = []
+        try:
+            for _ in range(5):
+                o.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode != "fp32"):
+                    loss = F.cross_entropy(m(x).float(), y)
+                loss.backward()
+                o.step()
+                ls.append(loss.item())
+        finally:
+            fused_block.set_enabled(old)
+        return ls
+
+    l_r, l_l, l_f = run("fp32"), run("layer"), run("fused")
+    assert abs(l_f[0] - l_r[0]) <= max(1.5 * abs(l_l[0] - l_r[0]), 0.02 * abs(l_r[0])), (l_r, l_l, l_f)
+    assert all(map(lambda v: v == v and abs(v) < 1e4, l_f)), l_f
+    assert l_f[-1] < l_f[0], l_f
