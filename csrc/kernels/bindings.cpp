@@ -325,6 +325,41 @@ at::Tensor conv_flip_weight(at::Tensor w) {
     return wt;
 }
 
+// dsts[i] = conv_flip_weight(srcs[i]) for a list of bf16 conv weights, in as few launches as
+// possible (FlipTable::kMax per launch).  dsts must be preallocated [Cin, Cout, KS, KS] channels_last.
+void conv_flip_weights(std::vector<at::Tensor> srcs, std::vector<at::Tensor> dsts) {
+    TORCH_CHECK(srcs.size() == dsts.size(), "conv_flip_weights: length mismatch");
+    if (srcs.empty()) return;
+    c10::DeviceGuard gd(srcs[0].device());
+    auto s = stream_of(srcs[0], 0);
+    kfk::FlipTable tab;
+    tab.start[0] = 0;
+    for (size_t i = 0; i < srcs.size(); ++i) {
+        const auto &w = srcs[i];
+        const auto &d = dsts[i];
+        TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
+                        w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == srcs[0].device(),
+                    "conv_flip_weights: [Cout, Cin, KS, KS] channels_last bf16 sources on one device");
+        TORCH_CHECK(d.scalar_type() == at::kBFloat16 && d.dim() == 4 && d.size(0) == w.size(1) &&
+                        d.size(1) == w.size(0) && d.size(2) == w.size(2) && d.size(3) == w.size(3) &&
+                        d.is_contiguous(at::MemoryFormat::ChannelsLast) && d.device() == w.device(),
+                    "conv_flip_weights: destination must be [Cin, Cout, KS, KS] channels_last bf16");
+        const int k = tab.n;
+        tab.src[k] = reinterpret_cast<const uint16_t *>(w.data_ptr());
+        tab.dst[k] = reinterpret_cast<uint16_t *>(d.data_ptr());
+        tab.cout[k] = w.size(0);
+        tab.cin[k] = w.size(1);
+        tab.taps[k] = w.size(2) * w.size(3);
+        tab.start[k + 1] = tab.start[k] + w.numel();
+        tab.n = k + 1;
+        if (tab.n == kfk::FlipTable::kMax) {
+            kfk::launch_conv_flip_multi(tab, s);
+            tab.n = 0;
+        }
+    }
+    kfk::launch_conv_flip_multi(tab, s);
+}
+
 // [Cout, Cin, 3, 3] channels_last -> flipped/transposed [Cin, Cout, 3, 3] channels_last
 at::Tensor conv3x3_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 &&
@@ -615,6 +650,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("out") = py::none(), py::arg("variant") = -1);
     m.def("conv_flip_weight", &conv_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,KS-1-kh,KS-1-kw] (data-gradient weights)");
     m.def("conv_supported", &kfk::conv_supported);
+    m.def("conv_flip_weights", &conv_flip_weights, "multi-tensor conv_flip_weight into preallocated outputs");
     m.attr("conv_stat_slots") = kfk::kStatSlots;
     m.def("conv3x3_flip_weight", &conv3x3_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,2-kh,2-kw] (data-gradient weights)");
     m.def("conv3x3_supported", &kfk::conv3x3_supported);

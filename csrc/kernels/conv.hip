@@ -283,7 +283,34 @@ __global__ void conv_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__res
     }
 }
 
+__global__ void conv_flip_multi_kernel(FlipTable tab) {
+    const int64_t total = tab.start[tab.n];
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        int lo = 0, hi = tab.n - 1;  // last t with start[t] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tab.start[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t j = i - tab.start[lo];
+        const int Cout = tab.cout[lo], Cin = tab.cin[lo], taps = tab.taps[lo];
+        const int co = static_cast<int>(j % Cout);
+        const int64_t t = j / Cout;
+        const int tap = static_cast<int>(t % taps);
+        const int ci = static_cast<int>(t / taps);
+        tab.dst[lo][j] = tab.src[lo][(static_cast<int64_t>(co) * taps + (taps - 1 - tap)) * Cin + ci];
+    }
+}
+
 }  // namespace
+
+void launch_conv_flip_multi(const FlipTable &tab, hipStream_t s) {
+    if (tab.n == 0 || tab.start[tab.n] == 0) return;
+    int64_t grid = (tab.start[tab.n] + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    conv_flip_multi_kernel<<<static_cast<int>(grid), 256, 0, s>>>(tab);
+}
 
 bool conv3x3_supported(int Cin, int Cout, int stride) {
     return Cin % 64 == 0 && Cout % 64 == 0 && (stride == 1 || stride == 2) && Cin >= 64;

@@ -98,6 +98,16 @@ constexpr int kStatSlots = 16;
 bool conv_supported(int Cin, int Cout, int ks, int stride);
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
                  int stride, double *stats, bool accumulate, hipStream_t s, int variant = -1);
+// Multi-tensor flip (one launch for a whole model's conv weights).
+struct FlipTable {
+    static constexpr int kMax = 64;
+    int n = 0;
+    const uint16_t *src[kMax];
+    uint16_t *dst[kMax];
+    int cout[kMax], cin[kMax], taps[kMax];
+    int64_t start[kMax + 1];
+};
+void launch_conv_flip_multi(const FlipTable &tab, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,KS-1-kh,KS-1-kw,ci]: stride-1 data gradient = conv(dy, wt).
 void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,2-kh,2-kw,ci]: stride-1 data gradient = conv3x3(dy, wt).

@@ -68,11 +68,43 @@ def _wgrad(dy, x, w, stride, pad):
                                                [False, True, False])[1]
 
 
-def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None):
+class _FlipCache:
+    """Data-gradient weights (``conv_flip_weight``) of every registered bf16 shadow conv
+    weight of one flat space, produced by ONE multi-tensor kernel per shadow refresh
+    (i.e. per step) on first use in backward, instead of one launch per convolution."""
+
+    def __init__(self, space):
+        self.space = space
+        self.index = {}  # param index -> flipped tensor
+        self.gen = -1
+
+    def register(self, i: int, w: torch.Tensor):
+        if i not in self.index:
+            co, ci, kh, kw = w.shape
+            self.index[i] = torch.empty((ci, co, kh, kw), dtype=torch.bfloat16, device=w.device).contiguous(
+                memory_format=torch.channels_last)
+            self.gen = -1
+
+    def get(self, i: int) -> torch.Tensor:
+        if self.gen != self.space.shadow_gen:
+            idx = sorted(self.index)
+            hip().conv_flip_weights([self.space.shadow_view(j) for j in idx], [self.index[j] for j in idx])
+            self.gen = self.space.shadow_gen
+        return self.index[i]
+
+
+def _flip_cache(space) -> _FlipCache:
+    c = getattr(space, "_kf_flip", None)
+    if c is None:
+        c = space._kf_flip = _FlipCache(space)
+    return c
+
+
+def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: Optional[torch.Tensor] = None):
     """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given)."""
     H = hip()
     if stride == 1:
-        return H.conv(dy, H.conv_flip_weight(w), 1, None, out)
+        return H.conv(dy, flipped if flipped is not None else H.conv_flip_weight(w), 1, None, out)
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
     if out is not None:
@@ -83,12 +115,13 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None):
 
 class _Spec:
     """Static description of one block (modules for running stats / workspaces)."""
-    __slots__ = ("bns", "stride", "ds", "dtypes", "direct")
+    __slots__ = ("bns", "stride", "ds", "dtypes", "direct", "wsrc")
 
     def __init__(self, bns, stride, ds):
         self.bns, self.stride, self.ds = bns, stride, ds
         self.dtypes = None
         self.direct = None
+        self.wsrc = None  # per conv: (flip cache, param index) for bf16 shadow weights, else None
 
 
 class _BottleneckFn(torch.autograd.Function):
@@ -138,26 +171,31 @@ class _BottleneckFn(torch.autograd.Function):
         (m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3, md, idd, cd) = t[7 + 2 * nb:]
         s = spec.stride
         dout = _cl(dout)
+        fl = [None] * nb
+        if spec.wsrc is not None:
+            for k, src in enumerate(spec.wsrc):
+                if src is not None and (k != 1 or s == 1) and (k != 3 or s == 1):
+                    fl[k] = src[0].get(src[1])
         dbn = [None] * nb  # (dgamma, dbeta)
         dw = [None] * nb
         dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, True)
         dbn[2] = (dg3, db3)
-        dz2 = _dgrad(dy3, z2, w[2], 1, 0)
+        dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2])
         dw[2] = _wgrad(dy3, z2, w[2], 1, 0)
         dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False)
         dbn[1] = (dg2, db2)
-        dz1 = _dgrad(dy2, z1, w[1], s, 1)
+        dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1])
         dw[1] = _wgrad(dy2, z1, w[1], s, 1)
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False)
         dbn[0] = (dg1, db1)
         if spec.ds:
             dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False)
             dbn[3] = (dgd, dbd)
-            dx = _dgrad(dyd, x, w[3], s, 0)
+            dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
             dw[3] = _wgrad(dyd, x, w[3], s, 0)
         else:
             dx = didt  # the identity gradient: conv1's data gradient is accumulated into it
-        dx = _dgrad(dy1, x, w[0], 1, 0, out=dx)
+        dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0])
         dw[0] = _wgrad(dy1, x, w[0], 1, 0)
         grads: List[Optional[torch.Tensor]] = []
         for i in range(nb):
@@ -210,9 +248,19 @@ def bottleneck_forward(block, x: torch.Tensor) -> torch.Tensor:
         block._kf_spec = spec
     params = []
     direct = []
+    wsrc = []
     for c, b in zip(convs, bns):
-        params += [shadow(c.weight), b.weight, b.bias]
+        w = shadow(c.weight)
+        params += [w, b.weight, b.bias]
         tw, tb = direct_target(b.weight), direct_target(b.bias)
         direct.append((tw, tb) if tw is not None and tb is not None else None)
+        tc = direct_target(c.weight)
+        if tc is not None and w is not c.weight and w.dtype == torch.bfloat16:
+            fc = _flip_cache(tc[0])
+            fc.register(tc[1], w)
+            wsrc.append((fc, tc[1]))
+        else:
+            wsrc.append(None)
     spec.direct = direct if any(d is not None for d in direct) else None
+    spec.wsrc = wsrc if any(v is not None for v in wsrc) else None
     return _BottleneckFn.apply(spec, x, *params)

@@ -76,6 +76,7 @@ class FlatParamSpace:
         # bf16 compute copy of flat_param (see parallel/mixed.py) and the
         # gradient sink that direct-gradient autograd functions deliver to.
         self.flat_shadow: Optional[torch.Tensor] = None
+        self.shadow_gen = 0  # bumped by every refresh_shadow (caches derived from the shadow key on it)
         self.sink = None
 
     @staticmethod
@@ -120,6 +121,7 @@ class FlatParamSpace:
             # they see are unchanged.
             with torch.autograd._unsafe_preserve_version_counter(self.flat_shadow):
                 self.flat_shadow.copy_(self.flat_param)
+            self.shadow_gen += 1
 
     def shadow_view(self, i: int) -> torch.Tensor:
         return self._view(self.flat_shadow, i)

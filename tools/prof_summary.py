@@ -20,7 +20,9 @@ CATEGORIES = [
     ("conv bwd-weight", r"igemm_wrw|conv_bwd_weight|batched_gemm_xdl|ConvBwdWeight|wrw"),
     ("gemm (fc/linear)", r"Cijk_|gemm|hipblaslt"),
     ("fused BN (ours)", r"kfk::.*bn_"),
-    ("conv 3x3 MFMA (ours)", r"kfk::.*conv3x3"),
+    ("conv MFMA 1x1 (ours)", r"kfk::.*conv_kernel<1,"),
+    ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,"),
+    ("conv weight flip (ours)", r"kfk::.*conv_flip"),
     ("optimizer/flat (ours)", r"kfk::"),
     ("rccl", r"ncclDevKernel|oneRankReduce|rccl"),
     ("casts", r"bfloat16tofloat32_copy|bfloat16_copy|float_to|copy_kernel"),
