@@ -143,6 +143,35 @@ Graph gen_default_reduce(const Graph &bcast);
 // rooted at `root` (f[root] == root).  Parity: srcs/cpp/include/kungfu/mst.hpp:9-58.
 std::vector<int> minimum_spanning_tree(const std::vector<double> &w, int n, int root = 0);
 
+// ---- Round schedule of a graph all-reduce for a two-sided, group-batched device data
+// plane (RCCL send/recv over xGMI).  The host executor (session.cpp) walks the graphs
+// with blocking per-edge transfers; a GPU plane instead needs every rank to issue the same
+// sequence of batched send/recv groups.  Each strategy graph pair (reduce in-tree, bcast
+// out-tree) owns one chunk of the buffer (even partition, like the reference's
+// chunk->strategy map, srcs/go/kungfu/session/session.go:300-317).  Reduce round r
+// (1..H) moves every chunk one tree level up: nodes of height r-1 send to their reduce
+// father, fathers receive into scratch and reduce after the round; bcast round d moves
+// every chunk one level down.  All chunks share the rounds, so CLIQUE becomes a
+// link-parallel reduce-scatter + all-gather and RING the classic ring schedule.
+struct GraphXfer {
+    bool recv = false;
+    int peer = 0;
+    int64_t off = 0, len = 0;  // element range of the buffer
+    int64_t scratch = -1;      // recv only: >= 0 -> land in scratch[scratch..], then buf[off..] op= it
+};
+struct GraphRound {
+    std::vector<GraphXfer> ops;
+};
+struct GraphPlan {
+    std::vector<GraphRound> rounds;
+    int64_t scratch_elems = 0;
+};
+// pairs[c] = (reduce father array, bcast father array); f[i] == i marks the root.
+GraphPlan plan_graph_all_reduce(const std::vector<std::pair<std::vector<int>, std::vector<int>>> &pairs, int rank,
+                                int64_t count);
+// (reduce father, bcast father) of a strategy graph pair; throws if a graph is not a tree.
+std::pair<std::vector<int>, std::vector<int>> graph_pair_fathers(const Graph &reduce, const Graph &bcast);
+
 // Subgraphs over a subset of vertices vs (used for cross-host all-reduce).
 void gen_sub_circular_pair(int n, const std::vector<int> &vs, int r, Graph *reduce, Graph *bcast);
 Graph gen_sub_binary_tree(int n, const std::vector<int> &vs);

@@ -104,6 +104,8 @@ class Session {
     void simple_set_global_strategy(const std::vector<int> &forest);
     bool set_tree(const std::vector<int> &forest);  // consensus-checked swap
     std::vector<double> strategy_throughputs();
+    // (reduce father, bcast father) of every current global graph pair (device graph plane).
+    std::vector<std::pair<std::vector<int>, std::vector<int>>> global_strategy_pairs();
     void log_stats();
     // Vote: true if the majority observed a throughput drop below 0.8x ref.
     bool check_interference();

@@ -10,6 +10,7 @@
 #include "rccl_comm.hpp"
 
 #include <memory>
+#include <tuple>
 #include <vector>
 
 namespace {
@@ -614,6 +615,61 @@ class Comm {
         check_gpu(t, "t");
         c_->recv(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
     }
+    // Graph all-reduce on the device: one round = one grouped batch of send/recv
+    // (kungfu::plan_graph_all_reduce), then the K1 reduce kernel for every received
+    // partial (buf[off:off+len] = op(buf[...], scratch[sc:sc+len])).  Every rank must run
+    // its own plan of the same strategy graphs (same rounds, matched ops).
+    using Xfer = std::tuple<int, int, int64_t, int64_t, int64_t>;  // recv, peer, off, len, scratch
+    void graph_run(at::Tensor buf, c10::optional<at::Tensor> scratch, const std::vector<std::vector<Xfer>> &rounds,
+                   int64_t op, int64_t stream) {
+        check_gpu(buf, "buf");
+        TORCH_CHECK(buf.is_contiguous(), "graph_run: buf must be contiguous");
+        const int dt = dtype_code(buf);
+        const size_t esz = buf.element_size();
+        auto *base = static_cast<uint8_t *>(buf.data_ptr());
+        uint8_t *sbase = nullptr;
+        int64_t sn = 0;
+        if (scratch && scratch->defined()) {
+            TORCH_CHECK(scratch->is_cuda() && scratch->scalar_type() == buf.scalar_type() && scratch->is_contiguous() &&
+                            scratch->device() == buf.device(),
+                        "graph_run: scratch must be a contiguous tensor of buf's dtype on its device");
+            sbase = static_cast<uint8_t *>(scratch->data_ptr());
+            sn = scratch->numel();
+        }
+        const int64_t n = buf.numel();
+        // validate the whole plan before issuing anything
+        for (const auto &r : rounds)
+            for (const auto &x : r) {
+                const int64_t off = std::get<2>(x), len = std::get<3>(x), sc = std::get<4>(x);
+                const int peer = std::get<1>(x);
+                TORCH_CHECK(off >= 0 && len >= 0 && off + len <= n, "graph_run: range out of bounds");
+                TORCH_CHECK(peer >= 0 && peer < c_->size() && peer != c_->rank(), "graph_run: bad peer");
+                TORCH_CHECK(!std::get<0>(x) || sc < 0 || (sbase && sc + len <= sn), "graph_run: scratch too small");
+            }
+        c10::DeviceGuard gd(buf.device());
+        auto s = stream_of(buf, stream);
+        for (const auto &r : rounds) {
+            if (r.empty()) continue;
+            kfk::RcclComm::group_start();
+            for (const auto &x : r) {
+                const int peer = std::get<1>(x);
+                const int64_t off = std::get<2>(x), len = std::get<3>(x), sc = std::get<4>(x);
+                if (std::get<0>(x)) {
+                    uint8_t *dst = sc >= 0 ? sbase + sc * esz : base + off * esz;
+                    c_->recv(dst, len, dt, peer, s);
+                } else {
+                    c_->send(base + off * esz, len, dt, peer, s);
+                }
+            }
+            kfk::RcclComm::group_end();
+            for (const auto &x : r) {
+                const int64_t off = std::get<2>(x), len = std::get<3>(x), sc = std::get<4>(x);
+                if (std::get<0>(x) && sc >= 0)
+                    kfk::launch_reduce(base + off * esz, base + off * esz, sbase + sc * esz, len, dt,
+                                       static_cast<int>(op), s);
+            }
+        }
+    }
     void destroy() { c_->destroy(); }
     void abort() { c_->abort(); }
 
@@ -694,6 +750,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
              py::arg("stream") = 0)
         .def("send", &Comm::send, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
         .def("recv", &Comm::recv, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
+        .def("graph_run", &Comm::graph_run, "grouped send/recv rounds + K1 reduce (device graph all-reduce)",
+             py::arg("buf"), py::arg("scratch"), py::arg("rounds"), py::arg("op") = 0, py::arg("stream") = 0)
         .def("destroy", &Comm::destroy)
         .def("abort", &Comm::abort);
 }

@@ -581,4 +581,144 @@ Graph gen_sub_binary_tree(int n, const std::vector<int> &vs) {
     return g;
 }
 
+// ---------------------------------------------------------------- device graph rounds
+
+namespace {
+
+struct TreeInfo {
+    int root = -1;
+    std::vector<std::vector<int>> children;
+    std::vector<int> level;  // height (reduce) or depth (bcast)
+};
+
+TreeInfo tree_info(const std::vector<int> &f, bool heights) {
+    const int n = static_cast<int>(f.size());
+    TreeInfo t;
+    t.children.assign(n, {});
+    t.level.assign(n, 0);
+    for (int i = 0; i < n; ++i) {
+        if (f[i] < 0 || f[i] >= n) throw std::invalid_argument("graph plan: father out of range");
+        if (f[i] == i) {
+            if (t.root >= 0) throw std::invalid_argument("graph plan: forest with several roots");
+            t.root = i;
+        } else {
+            t.children[f[i]].push_back(i);
+        }
+    }
+    if (n > 0 && t.root < 0) throw std::invalid_argument("graph plan: no root");
+    // BFS order from the root (also detects cycles / unreachable nodes)
+    std::vector<int> order;
+    if (n > 0) order.push_back(t.root);
+    for (size_t k = 0; k < order.size(); ++k)
+        for (int c : t.children[order[k]]) order.push_back(c);
+    if (static_cast<int>(order.size()) != n) throw std::invalid_argument("graph plan: not a tree");
+    if (heights) {
+        for (auto it = order.rbegin(); it != order.rend(); ++it)
+            for (int c : t.children[*it]) t.level[*it] = std::max(t.level[*it], t.level[c] + 1);
+    } else {
+        for (int v : order)
+            for (int c : t.children[v]) t.level[c] = t.level[v] + 1;
+    }
+    return t;
+}
+
+}  // namespace
+
+std::pair<std::vector<int>, std::vector<int>> graph_pair_fathers(const Graph &reduce, const Graph &bcast) {
+    const int n = bcast.size();
+    std::vector<int> rf(n), bf(n);
+    for (int i = 0; i < n; ++i) {
+        std::vector<int> nx;
+        for (int j : reduce.nexts(i))
+            if (j != i) nx.push_back(j);
+        if (nx.size() > 1) throw std::invalid_argument("graph_pair_fathers: reduce graph is not an in-tree");
+        rf[i] = nx.empty() ? i : nx[0];
+        const auto &pv = bcast.prevs(i);
+        if (pv.size() > 1) throw std::invalid_argument("graph_pair_fathers: bcast graph is not an out-tree");
+        bf[i] = pv.empty() ? i : pv[0];
+    }
+    return {rf, bf};
+}
+
+GraphPlan plan_graph_all_reduce(const std::vector<std::pair<std::vector<int>, std::vector<int>>> &pairs, int rank,
+                                int64_t count) {
+    GraphPlan plan;
+    const size_t k = pairs.size();
+    if (k == 0 || count <= 0) return plan;
+    const auto parts = even_partition(static_cast<size_t>(count), k);
+    std::vector<TreeInfo> red(k), bc(k);
+    int hmax = 0, dmax = 0;
+    for (size_t c = 0; c < k; ++c) {
+        if (pairs[c].first.size() != pairs[c].second.size())
+            throw std::invalid_argument("graph plan: reduce/bcast sizes differ");
+        if (rank < 0 || rank >= static_cast<int>(pairs[c].first.size()))
+            throw std::invalid_argument("graph plan: rank out of range");
+        red[c] = tree_info(pairs[c].first, true);
+        bc[c] = tree_info(pairs[c].second, false);
+        if (red[c].root != bc[c].root) throw std::invalid_argument("graph plan: reduce and bcast roots differ");
+        hmax = std::max(hmax, red[c].level[red[c].root]);
+        for (int v : bc[c].level) dmax = std::max(dmax, v);
+    }
+    // reduce rounds
+    for (int r = 1; r <= hmax; ++r) {
+        GraphRound round;
+        int64_t scratch = 0;
+        for (size_t c = 0; c < k; ++c) {
+            const int64_t off = static_cast<int64_t>(parts[c].begin), len = static_cast<int64_t>(parts[c].len());
+            if (len == 0) continue;
+            const auto &t = red[c];
+            if (rank != t.root && t.level[rank] == r - 1) {
+                GraphXfer x;
+                x.recv = false;
+                x.peer = pairs[c].first[rank];
+                x.off = off;
+                x.len = len;
+                round.ops.push_back(x);
+            }
+            for (int ch : t.children[rank]) {
+                if (t.level[ch] != r - 1) continue;
+                GraphXfer x;
+                x.recv = true;
+                x.peer = ch;
+                x.off = off;
+                x.len = len;
+                x.scratch = scratch;
+                scratch += len;
+                round.ops.push_back(x);
+            }
+        }
+        plan.scratch_elems = std::max(plan.scratch_elems, scratch);
+        plan.rounds.push_back(std::move(round));
+    }
+    // bcast rounds
+    for (int d = 1; d <= dmax; ++d) {
+        GraphRound round;
+        for (size_t c = 0; c < k; ++c) {
+            const int64_t off = static_cast<int64_t>(parts[c].begin), len = static_cast<int64_t>(parts[c].len());
+            if (len == 0) continue;
+            const auto &t = bc[c];
+            if (t.level[rank] == d && rank != t.root) {
+                GraphXfer x;
+                x.recv = true;
+                x.peer = pairs[c].second[rank];
+                x.off = off;
+                x.len = len;
+                round.ops.push_back(x);
+            }
+            if (t.level[rank] == d - 1) {
+                for (int ch : t.children[rank]) {
+                    GraphXfer x;
+                    x.recv = false;
+                    x.peer = ch;
+                    x.off = off;
+                    x.len = len;
+                    round.ops.push_back(x);
+                }
+            }
+        }
+        plan.rounds.push_back(std::move(round));
+    }
+    return plan;
+}
+
 }  // namespace kungfu

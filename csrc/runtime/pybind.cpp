@@ -367,6 +367,26 @@ PYBIND11_MODULE(_kungfu, m) {
         for (auto &p : sl) out.append(py::make_tuple(graph_to_dict(p.reduce), graph_to_dict(p.bcast)));
         return out;
     });
+    m.def("strategy_pairs", [](const std::string &peers, const std::string &strategy) {
+        Strategy st;
+        if (!parse_strategy(strategy, &st)) throw std::invalid_argument("bad strategy " + strategy);
+        std::vector<std::pair<std::vector<int>, std::vector<int>>> out;
+        for (auto &p : make_strategies(PeerList::parse(peers), st)) out.push_back(graph_pair_fathers(p.reduce, p.bcast));
+        return out;
+    }, "(reduce father, bcast father) per graph pair of a strategy over a peer list");
+    m.def("global_strategy_pairs", [] { return require_session()->global_strategy_pairs(); },
+          "(reduce father, bcast father) per graph pair of the session's current global strategy");
+    m.def("plan_graph_all_reduce", [](const std::vector<std::pair<std::vector<int>, std::vector<int>>> &pairs, int rank,
+                                      int64_t count) {
+        auto plan = plan_graph_all_reduce(pairs, rank, count);
+        py::list rounds;
+        for (auto &r : plan.rounds) {
+            py::list ops;
+            for (auto &x : r.ops) ops.append(py::make_tuple(x.recv ? 1 : 0, x.peer, x.off, x.len, x.scratch));
+            rounds.append(ops);
+        }
+        return py::make_tuple(rounds, plan.scratch_elems);
+    }, "round schedule of a graph all-reduce: ([[(recv, peer, off, len, scratch), ...], ...], scratch elems)");
     m.def("graph_from_forest", [](const std::vector<int> &f) {
         Graph g;
         int roots = 0;

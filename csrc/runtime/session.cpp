@@ -474,4 +474,11 @@ std::vector<double> Session::peer_latencies() {
     return out;
 }
 
+std::vector<std::pair<std::vector<int>, std::vector<int>>> Session::global_strategy_pairs() {
+    std::lock_guard<std::mutex> lk(strat_mu_);
+    std::vector<std::pair<std::vector<int>, std::vector<int>>> out;
+    for (auto &p : global_) out.push_back(graph_pair_fathers(p.reduce, p.bcast));
+    return out;
+}
+
 }  // namespace kungfu

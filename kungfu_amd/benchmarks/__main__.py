@@ -14,7 +14,10 @@ from kungfu_amd.benchmarks.model_sizes import grad_sizes
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--method", default="CPU", choices=["CPU", "RCCL", "RCCL+CPU", "HIER"])
+    p.add_argument("--method", default="CPU", choices=["CPU", "RCCL", "RCCL+CPU", "HIER", "GRAPH"],
+                   help="CPU: host TCP graph plane; RCCL: RCCL all-reduce; RCCL+CPU: host-staged GPU; "
+                        "HIER: local RCCL reduce + host cross all-reduce + local bcast; GRAPH: the session's "
+                        "strategy graphs as device send/recv rounds (KUNGFU_ALLREDUCE_STRATEGY)")
     p.add_argument("--model", default="resnet50")
     p.add_argument("--fuse", action="store_true")
     p.add_argument("--max-count", type=int, default=0)
@@ -44,6 +47,9 @@ def main():
         if a.method == "HIER":
             for x in xs:
                 ops.hierarchical_all_reduce_(x)
+        elif a.method == "GRAPH":
+            for x in xs:
+                ops.monitored_all_reduce_(x)
         else:
             ops.group_all_reduce_(xs, names=["bench:%d" % i for i in range(len(xs))])
         if gpu:

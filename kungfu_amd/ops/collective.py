@@ -253,9 +253,18 @@ def group_nccl_all_reduce(tensors, op="sum"):
 
 def monitored_all_reduce_(x: torch.Tensor, tree: Optional[Sequence[int]] = None, name: Optional[str] = None,
                           op: str = "sum") -> torch.Tensor:
-    """Host all-reduce that records strategy throughput (see ``calc_stats``);
-    ``tree`` optionally gives a father array to reduce/broadcast along."""
+    """All-reduce along the strategy graphs (or along ``tree``, a father array), recording
+    strategy throughput on the host plane (see ``calc_stats``).  GPU tensors on the RCCL
+    plane run the same graphs on the device: grouped send/recv rounds over xGMI + the K1
+    reduce kernel (``DeviceComm.graph_all_reduce``)."""
     _ensure()
+    if x.is_cuda and not _gpu_host_staging():
+        c = x if x.is_contiguous() else x.contiguous()
+        pairs = [(list(tree), list(tree))] if tree else None
+        _dev_comm().graph_all_reduce(c, op=op, pairs=pairs, stream=_cs())
+        if c is not x:
+            x.copy_(c)
+        return x
 
     def run(h):
         runtime.monitored_all_reduce(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), op_code(op),

@@ -103,6 +103,30 @@ class DeviceComm:
     def group_end(self):
         hip().rccl_group_end()
 
+    def graph_all_reduce(self, t: torch.Tensor, op="sum", pairs=None, stream=None):
+        """In-place all-reduce along KungFu strategy graphs (default: the session's current
+        global strategy, which ``set_tree`` / ``set_strategy`` / adaptation swap) as grouped
+        RCCL send/recv rounds + the K1 reduce kernel (see ``plan_graph_all_reduce``)."""
+        if self.size == 1:
+            return t
+        if pairs is None:
+            pairs = runtime.global_strategy_pairs()
+        key = (tuple((tuple(a), tuple(b)) for a, b in pairs), t.numel())
+        cache = self.__dict__.setdefault("_graph_plans", {})
+        plan = cache.get(key)
+        if plan is None:
+            if len(cache) > 64:
+                cache.clear()
+            plan = runtime.plan_graph_all_reduce([(list(a), list(b)) for a, b in key[0]], self.rank, t.numel())
+            cache[key] = plan
+        rounds, nscratch = plan
+        scratch = torch.empty(max(int(nscratch), 1), dtype=t.dtype, device=t.device)
+        s = stream if stream is not None else self.stream
+        if hasattr(s, "cuda_stream") and s != torch.cuda.current_stream(t.device):
+            scratch.record_stream(s)
+        self.comm.graph_run(t, scratch, rounds, op_code(op), self._s(stream))
+        return t
+
     def destroy(self):
         if self.comm is not None:
             try:
@@ -164,6 +188,10 @@ class HostStagedComm:
                 h.div_(self.size)
 
         return self._run(inp, out, stream, f)
+
+    def graph_all_reduce(self, t, op="sum", pairs=None, stream=None):
+        # the host runtime executes the session's strategy graphs itself
+        return self.all_reduce(t, t, op=op, stream=stream)
 
     def broadcast(self, t, root: int = 0, stream=None):
         if root != 0:

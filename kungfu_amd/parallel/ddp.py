@@ -61,6 +61,10 @@ class GradReducer:
         esz = space.flat_grad.element_size()
         self.comm = get_device_comm()
         self.comm_dtype = comm_dtype
+        # KUNGFU_GPU_ALLREDUCE=graph: buckets follow the session's KungFu strategy graphs
+        # (set_tree / set_strategy / adaptation) as device send/recv rounds instead of RCCL's
+        # own all-reduce algorithm
+        self.graph = os.environ.get("KUNGFU_GPU_ALLREDUCE", "rccl") == "graph"
         self.skip = skip_single and self.comm.size == 1
         self.buckets: List[Bucket] = []
         cap = max(1, int(first_bucket_mb * (1 << 20) / esz))
@@ -191,11 +195,20 @@ class GradReducer:
         if self.comm_dtype is not None and self.comm_dtype != g.dtype:
             with torch.cuda.stream(comm.stream):
                 c = g.to(self.comm_dtype)
-                comm.all_reduce(c, op=self.op)
+                self._reduce(comm, c)
                 g.copy_(c)
                 c.record_stream(comm.stream)
         else:
+            self._reduce(comm, g)
+
+    def _reduce(self, comm, g):
+        if not self.graph:
             comm.all_reduce(g, op=self.op)
+            return
+        comm.graph_all_reduce(g, op="sum")
+        if self.op == "avg":
+            with torch.cuda.stream(comm.stream):
+                g.mul_(1.0 / comm.size)
 
     def _finish(self):
         for j in self.sched.flush():

@@ -532,3 +532,15 @@ def test_resnet50_fused_block_step_matches_layerwise():
     assert abs(l_f[0] - l_r[0]) <= max(1.5 * abs(l_l[0] - l_r[0]), 0.02 * abs(l_r[0])), (l_r, l_l, l_f)
     assert all(map(lambda v: v == v and abs(v) < 1e4, l_f)), l_f
     assert l_f[-1] < l_f[0], l_f
+
+
+@needs_gpu
+def test_device_graph_allreduce_two_ranks():
+    """KungFu strategy graphs executed on the device plane (RCCL send/recv rounds + K1)
+    with 2 ranks; skipped when RCCL refuses two ranks on one GPU."""
+    r = kungfu_run(2, [worker("graph_gpu.py")], timeout=300, extra=["-allow-xgmi"],
+                   env={"KUNGFU_FORCE_DEVICE": "0"})
+    if "GRAPH_GPU_SKIP" in r.stdout:
+        pytest.skip("RCCL refuses 2 ranks on one GPU: " + r.stdout[-300:])
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("GRAPH_GPU_OK") == 2, r.stdout[-4000:]

@@ -105,3 +105,90 @@ def test_even_partition():
 def test_mst():
     w = [0, 1, 5, 1, 0, 2, 5, 2, 0]
     assert K.minimum_spanning_tree(w, 3, 0) == [0, 0, 1]
+
+
+# ---- device graph all-reduce round schedule (plan_graph_all_reduce) -----------------
+
+def _simulate(pairs, n, count, rng):
+    """Run every rank's round schedule in lock step with matched send/recv per
+    (sender, receiver) in issue order -- the semantics of a grouped RCCL send/recv."""
+    import numpy as np
+
+    bufs = [rng.integers(-1000, 1000, size=count).astype(np.int64) for _ in range(n)]
+    want = sum(bufs)
+    plans = [K.plan_graph_all_reduce(pairs, r, count) for r in range(n)]
+    nrounds = {len(p[0]) for p in plans}
+    assert len(nrounds) == 1, "every rank runs the same number of rounds"
+    for ri in range(nrounds.pop()):
+        sends, recvs = {}, {}
+        for r in range(n):
+            for (is_recv, peer, off, ln, scratch) in plans[r][0][ri]:
+                if is_recv:
+                    recvs.setdefault((peer, r), []).append((off, ln, scratch))
+                else:
+                    sends.setdefault((r, peer), []).append(bufs[r][off:off + ln].copy())
+        assert sorted(sends) == sorted(recvs), ("unmatched ops in round", ri)
+        scratch = [np.zeros(max(plans[r][1], 1), dtype=np.int64) for r in range(n)]
+        pend = []
+        for (src, dst), rl in recvs.items():
+            sl = sends[(src, dst)]
+            assert len(sl) == len(rl)
+            for data, (off, ln, sc) in zip(sl, rl):
+                assert len(data) == ln
+                if sc >= 0:
+                    assert sc + ln <= plans[dst][1]
+                    scratch[dst][sc:sc + ln] = data
+                    pend.append((dst, off, ln, sc))
+                else:
+                    bufs[dst][off:off + ln] = data
+        for dst, off, ln, sc in pend:  # reduce kernels after the group
+            bufs[dst][off:off + ln] += scratch[dst][sc:sc + ln]
+    for r in range(n):
+        assert (bufs[r] == want).all(), ("rank", r)
+
+
+@pytest.mark.parametrize("strategy", ["STAR", "MULTI_STAR", "RING", "CLIQUE", "TREE", "BINARY_TREE",
+                                      "BINARY_TREE_STAR", "MULTI_BINARY_TREE_STAR", "AUTO"])
+@pytest.mark.parametrize("hosts", [[1], [2], [3], [8], [4, 4], [2, 3, 1]])
+def test_graph_round_plan_all_strategies(strategy, hosts):
+    import numpy as np
+
+    spec = []
+    for h, k in enumerate(hosts):
+        spec += ["10.0.0.%d:%d" % (h + 1, 10000 + i) for i in range(k)]
+    n = len(spec)
+    pairs = K.strategy_pairs(",".join(spec), strategy)
+    assert pairs
+    rng = np.random.default_rng(n)
+    for count in (1, 7, n * 5 + 3, 1000):
+        _simulate(pairs, n, count, rng)
+
+
+def test_graph_round_plan_shapes():
+    import numpy as np
+
+    n = 8
+    # CLIQUE on one host = link-parallel reduce-scatter + all-gather: 2 rounds, each rank
+    # talks to all 7 peers per round
+    pairs = K.strategy_pairs(",".join("127.0.0.1:%d" % (10000 + i) for i in range(n)), "CLIQUE")
+    rounds, scratch = K.plan_graph_all_reduce(pairs, 0, 800)
+    assert len(rounds) == 2 and scratch == 7 * 100
+    assert {op[1] for op in rounds[0]} == set(range(1, n))
+    # RING: 2 (n - 1) rounds with one send per round
+    pairs = K.strategy_pairs(",".join("127.0.0.1:%d" % (10000 + i) for i in range(n)), "RING")
+    rounds, _ = K.plan_graph_all_reduce(pairs, 3, 800)
+    assert len(rounds) == 2 * (n - 1)
+    assert all(sum(1 for op in r if op[0] == 0) == 1 for r in rounds)
+    # random set_tree forests (reduce along the tree, bcast down the same tree)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        m = int(rng.integers(1, 9))
+        root = int(rng.integers(0, m))
+        order = [root] + [i for i in rng.permutation(m).tolist() if i != root]
+        f = [0] * m
+        f[root] = root
+        for j in range(1, m):
+            f[order[j]] = order[int(rng.integers(0, j))]
+        _simulate([(f, f)], m, 37, rng)
+    with pytest.raises(Exception):
+        K.plan_graph_all_reduce([([1, 0], [1, 0])], 0, 10)  # cycle
