@@ -8,7 +8,7 @@
 #   kungfu_amd/lib/libkungfu_amd.so       C++ runtime + extern "C" ABI
 #   kungfu_amd/_kungfu$(PYEXT)            pybind11 binding of the runtime
 #   kungfu_amd/_hip$(PYEXT)               HIP/CDNA4 kernels + RCCL controller (torch extension)
-#   bin/kungfu-run, bin/kungfu-config-server, bin/kungfu-rrun, bin/kungfu-distribute
+#   bin/kungfu-run, bin/kungfu-config-server, bin/kungfu-rrun, bin/kungfu-distribute, bin/kungfu-test-util
 
 PYTHON     ?= python3
 CXX        ?= g++
@@ -21,7 +21,7 @@ PYEXT      := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_
 TORCH_DIR  := $(shell $(PYTHON) -c "import os,torch;print(os.path.dirname(torch.__file__))" 2>/dev/null)
 
 CXXFLAGS   := -std=c++17 -O3 -fPIC -Wall -Wextra -Wno-unused-parameter -Icsrc/include -mavx2 -mf16c -pthread $(EXTRA_CXXFLAGS)
-LDFLAGS    := -pthread $(EXTRA_LDFLAGS)
+LDFLAGS    := -pthread -ldl $(EXTRA_LDFLAGS)
 
 RT_SRCS    := base plan log monitor transport session http peer capi model_avg scheduler
 RT_OBJS    := $(patsubst %,$(BUILD)/rt/%.o,$(RT_SRCS))
@@ -30,7 +30,7 @@ PY_MOD     := kungfu_amd/_kungfu$(PYEXT)
 
 LAUNCH_SRCS := runner job configserver_main flags
 LAUNCH_OBJS := $(patsubst %,$(BUILD)/launcher/%.o,$(LAUNCH_SRCS))
-BINS       := bin/kungfu-run bin/kungfu-config-server bin/kungfu-rrun bin/kungfu-distribute
+BINS       := bin/kungfu-run bin/kungfu-config-server bin/kungfu-rrun bin/kungfu-distribute bin/kungfu-test-util
 
 HIP_SRCS   := $(wildcard csrc/kernels/*.hip)
 HIP_OBJS   := $(patsubst csrc/kernels/%.hip,$(BUILD)/hip/%.o,$(HIP_SRCS))
@@ -80,6 +80,10 @@ bin/kungfu-rrun: $(BUILD)/launcher/rrun.o $(LAUNCH_OBJS) $(RT_OBJS)
 	$(CXX) -o $@ $^ $(LDFLAGS)
 
 bin/kungfu-distribute: $(BUILD)/launcher/distribute.o $(LAUNCH_OBJS) $(RT_OBJS)
+	@mkdir -p bin
+	$(CXX) -o $@ $^ $(LDFLAGS)
+
+bin/kungfu-test-util: $(BUILD)/launcher/test_util.o $(RT_OBJS)
 	@mkdir -p bin
 	$(CXX) -o $@ $^ $(LDFLAGS)
 

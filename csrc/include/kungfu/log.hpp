@@ -62,8 +62,12 @@ class TraceScope {
     std::chrono::steady_clock::time_point t0_;
 };
 
-bool trace_enabled();
+bool trace_enabled();  // KUNGFU_CONFIG_ENABLE_TRACE
 std::string trace_report();
+// roctx range push/pop (no-ops unless tracing is enabled and libroctx64 is loadable)
+void trace_push(const char *name);
+void trace_pop();
+void trace_record(const std::string &name, double seconds);
 
 #define KF_TRACE_CAT2(a, b) a##b
 #define KF_TRACE_CAT(a, b) KF_TRACE_CAT2(a, b)

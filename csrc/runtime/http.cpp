@@ -24,7 +24,10 @@ std::string lower(std::string s) {
 }
 
 // Reads headers + body (by Content-Length).  Returns false on error.
-bool read_http(int fd, std::string *head, std::string *body) {
+// is_request: an HTTP/1.1 request without Content-Length has no body (a client such as
+// urllib or curl keeps its write side open waiting for the response); a response
+// without Content-Length is delimited by the connection close.
+bool read_http(int fd, std::string *head, std::string *body, bool is_request) {
     std::string buf;
     char tmp[4096];
     size_t hend = std::string::npos;
@@ -56,7 +59,7 @@ bool read_http(int fd, std::string *head, std::string *body) {
             body->append(tmp, static_cast<size_t>(n));
         }
         body->resize(clen);
-    } else {
+    } else if (!is_request) {
         // read until close (responses without Content-Length)
         for (;;) {
             ssize_t n = ::recv(fd, tmp, sizeof(tmp), 0);
@@ -121,7 +124,7 @@ void HttpServer::loop() {
             setsockopt(c, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
             std::string head, body;
             HttpResponse resp;
-            if (!read_http(c, &head, &body)) {
+            if (!read_http(c, &head, &body, /*is_request=*/true)) {
                 ::close(c);
                 return;
             }
@@ -210,7 +213,7 @@ int http_request(const std::string &method, const std::string &url, const std::s
         return -1;
     }
     std::string head, rbody;
-    bool ok = read_http(fd, &head, &rbody);
+    bool ok = read_http(fd, &head, &rbody, /*is_request=*/false);
     ::close(fd);
     if (!ok) return -1;
     int status = -1;

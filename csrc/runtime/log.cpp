@@ -1,5 +1,7 @@
 #include <kungfu/log.hpp>
 
+#include <dlfcn.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -36,14 +38,16 @@ struct TraceStat {
     double total = 0;
 };
 
+// Intentionally leaked: the at-exit reporter below runs during static destruction,
+// after function-local statics constructed later than it would already be gone.
 std::mutex &trace_mu() {
-    static std::mutex m;
-    return m;
+    static std::mutex *m = new std::mutex;
+    return *m;
 }
 
 std::map<std::string, TraceStat> &trace_stats() {
-    static std::map<std::string, TraceStat> s;
-    return s;
+    static auto *s = new std::map<std::string, TraceStat>;
+    return *s;
 }
 
 struct TraceReporter {
@@ -143,12 +147,56 @@ bool trace_enabled() {
     return on;
 }
 
+namespace {
+// roctx ranges (rocprofv3 --marker-trace shows them next to the kernels) loaded at run
+// time, so the runtime has no link dependency on the ROCm profiler libraries.
+struct Roctx {
+    int (*push)(const char *) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx() {
+        if (!trace_enabled()) return;
+        for (const char *lib : {"libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"}) {
+            void *h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+            if (!h) continue;
+            push = reinterpret_cast<int (*)(const char *)>(dlsym(h, "roctxRangePushA"));
+            pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+            if (push && pop) return;
+            push = nullptr;
+            pop = nullptr;
+        }
+    }
+};
+Roctx &roctx() {
+    static Roctx r;
+    return r;
+}
+}  // namespace
+
+void trace_push(const char *name) {
+    if (trace_enabled() && roctx().push) roctx().push(name);
+}
+
+void trace_pop() {
+    if (trace_enabled() && roctx().pop) roctx().pop();
+}
+
+void trace_record(const std::string &name, double seconds) {
+    std::lock_guard<std::mutex> lk(trace_mu());
+    auto &s = trace_stats()[name];
+    s.count++;
+    s.total += seconds;
+}
+
 TraceScope::TraceScope(const char *name) : name_(name) {
-    if (trace_enabled()) t0_ = std::chrono::steady_clock::now();
+    if (trace_enabled()) {
+        t0_ = std::chrono::steady_clock::now();
+        trace_push(name);
+    }
 }
 
 TraceScope::~TraceScope() {
     if (!trace_enabled()) return;
+    trace_pop();
     double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0_).count();
     std::lock_guard<std::mutex> lk(trace_mu());
     auto &s = trace_stats()[name_];

@@ -344,6 +344,10 @@ PYBIND11_MODULE(_kungfu, m) {
     m.def("monitor_enable", [](bool on) { Monitor::get().set_enabled(on); });
     m.def("metrics_text", [] { return Monitor::get().metrics_text(); });
     m.def("trace_report", [] { return trace_report(); });
+    m.def("trace_enabled", [] { return trace_enabled(); });
+    m.def("trace_push", [](const std::string &name) { trace_push(name.c_str()); });
+    m.def("trace_pop", [] { trace_pop(); });
+    m.def("trace_record", [](const std::string &name, double seconds) { trace_record(name, seconds); });
 
     // ---- host kernels ------------------------------------------------------------
     m.def("transform2", [](uintptr_t z, uintptr_t x, uintptr_t y, size_t n, int dt, int op) {

@@ -21,6 +21,7 @@ from typing import Iterable, Optional, Tuple
 import torch
 
 from ..parallel.flat import FlatParamSpace
+from ..utils import trace
 from .fused import FusedAdam, FusedSGD
 
 
@@ -100,9 +101,12 @@ class KungFuOptimizer(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        self._before_step()
-        self.inner.step()
-        self._after_step()
+        with trace.scope("optimizer::before_step"):
+            self._before_step()
+        with trace.scope("optimizer::apply"):
+            self.inner.step()
+        with trace.scope("optimizer::after_step"):
+            self._after_step()
         return loss
 
     # -- hooks for subclasses ------------------------------------------------

@@ -31,6 +31,7 @@ import torch
 
 from .. import ops
 from .._lib import dtype_code, hip, runtime
+from ..utils.trace import traced
 from .core import KungFuOptimizer
 
 _REC = "kf:pair:rec"
@@ -88,6 +89,7 @@ class DeviceModelStore:
             runtime.save("kf:pair:model:" + self.name, self._host_copy.data_ptr(), self.numel * 4)
         self._pending = None
 
+    @traced("pair::pull")
     def pull(self, target: int, out: torch.Tensor) -> bool:
         rec = torch.zeros(2, dtype=torch.int64)
         if not runtime.request(target, "", _REC + self.name, rec.data_ptr(), 16):

@@ -34,6 +34,7 @@ from typing import List, Optional
 
 import torch
 
+from ..utils.trace import traced
 from .comm import get_device_comm
 from .flat import FlatParamSpace
 
@@ -179,6 +180,7 @@ class GradReducer:
             hip().grad_accumulate(self.space.flat_grad, b.staged, b.staged_off, 1.0)
             b.staged, b.staged_off = [], []
 
+    @traced("ssgd::bucket_launch")
     def _launch(self, b: Bucket):
         b.launched = True
         self._land(b)

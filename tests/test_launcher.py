@@ -140,3 +140,76 @@ def test_modelarts_platform_discovery(tmp_path):
                         sys.executable, s], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                        text=True, timeout=120)
     assert r.returncode != 0 and "BATCH_CUSTOM1_HOSTS not set" in r.stdout
+
+
+def test_kill_peer_via_control_message(tmp_path):
+    """Fault injection (parity: kungfu-test-util -kill, tests/go/cmd/kungfu-test-util):
+    the "exit" control message ends a worker; the launcher then finishes."""
+    import subprocess
+    import sys
+    import time
+
+    from conftest import ROOT, free_port_block
+
+    s = _script(tmp_path, """
+        import os, sys, time
+        import kungfu_amd as kf
+        kf.init()
+        print("READY", os.environ["KUNGFU_SELF_SPEC"], flush=True)
+        time.sleep(120)
+        print("NOT_KILLED", flush=True)
+    """)
+    base = free_port_block(6)
+    cmd = [os.path.join(ROOT, "bin", "kungfu-run"), "-q", "-np", "2", "-H", "127.0.0.1:2",
+           "-port-range", "%d-%d" % (base + 1, base + 5), "-port", str(base), sys.executable, s]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    specs, lines = [], []
+    t0 = time.time()
+    try:
+        while len(specs) < 2 and time.time() - t0 < 60:
+            line = p.stdout.readline()
+            if not line:
+                break
+            lines.append(line)
+            if "READY" in line:
+                specs.append(line.split("READY", 1)[1].split()[0])
+        assert len(specs) == 2, "".join(lines)
+        k = subprocess.run([os.path.join(ROOT, "bin", "kungfu-test-util"), "-kill"] + specs,
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=30)
+        assert k.returncode == 0, k.stdout
+        out, _ = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert p.returncode == 0, out
+    assert "NOT_KILLED" not in out
+    assert time.time() - t0 < 90
+
+
+def test_monitoring_http_metrics(tmp_path):
+    """Net monitor (parity: tests/go/cmd/kungfu-test-monitor): egress counters exposed over
+    HTTP on port + 10000 and as the egress_rates op."""
+    s = _script(tmp_path, """
+        import os, time, urllib.request
+        import torch
+        import kungfu_amd as kf
+        from kungfu_amd import ops
+        kf.init()
+        for _ in range(5):
+            ops.all_reduce(torch.ones(1 << 16))
+        port = int(os.environ["KUNGFU_SELF_SPEC"].split(":")[1]) + 10000
+        opener = urllib.request.build_opener(urllib.request.ProxyHandler({}))
+        txt = opener.open("http://127.0.0.1:%d/metrics" % port, timeout=10).read().decode()
+        assert "egress_total_bytes" in txt, txt
+        vals = [float(l.split()[-1]) for l in txt.splitlines() if l.startswith("egress_total_bytes")]
+        assert vals and max(vals) > 0, txt
+        time.sleep(1.2)
+        r = ops.egress_rates()
+        assert r.shape == (kf.current_cluster_size(),)
+        kf.run_barrier()
+        print("MONITOR_OK", flush=True)
+    """)
+    r = kungfu_run(2, [s], timeout=120, env={"KUNGFU_CONFIG_ENABLE_MONITORING": "true"})
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert r.stdout.count("MONITOR_OK") == 2, r.stdout[-3000:]
