@@ -37,23 +37,38 @@ def _log_event(name: str):
 
 
 class EMA:
-    """Exponential moving average with optional scale cap (parity: kungfu.utils.ema)."""
+    """Exponential moving average with optional scale cap (parity: kungfu.utils.ema,
+    srcs/python/kungfu/utils/ema.py): the first update sets the value; later samples are
+    clamped to [value / cap, value * cap] before blending."""
 
-    def __init__(self, alpha: float = 0.9, max_scale: Optional[float] = None):
-        self.alpha, self.max_scale, self.value = alpha, max_scale, None
+    def __init__(self, alpha: float = 0.9, scale_cap: Optional[float] = None, max_scale: Optional[float] = None):
+        self.alpha = alpha
+        self.scale_cap = scale_cap if scale_cap is not None else max_scale
+        self.value = None
+
+    def _cap(self, x: float) -> float:
+        if self.scale_cap is None:
+            return x
+        up = self.value * self.scale_cap
+        if x > up:
+            return up
+        down = self.value / self.scale_cap
+        if x < down:
+            return down
+        return x
 
     def update(self, x: float) -> float:
         if self.value is None:
             self.value = x
         else:
-            nv = self.alpha * self.value + (1 - self.alpha) * x
-            if self.max_scale is not None and self.value != 0:
-                hi, lo = abs(self.value) * self.max_scale, abs(self.value) / self.max_scale
-                nv = max(min(nv, hi), -hi) if abs(nv) > hi else nv
-                if abs(nv) < lo:
-                    nv = lo if nv >= 0 else -lo
-            self.value = nv
+            self.value = self.alpha * self.value + (1 - self.alpha) * self._cap(x)
         return self.value
+
+    def get(self) -> Optional[float]:
+        return self.value
+
+    def reset(self) -> None:
+        self.value = None
 
 
 Ki, Mi, Gi = 1024, 1024 ** 2, 1024 ** 3

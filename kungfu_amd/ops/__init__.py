@@ -19,7 +19,7 @@ from .monitor import (GlobalNoiseScale, egress_rates, global_gradient_noise_scal
                       gradient_variance, noise_scale_estimates, sum_squares)
 from .p2p import request_variable, request_variable_with_template
 from .state import Counter, ExponentialMovingAverage, counter, exponential_moving_average
-from .topology import (get_neighbour_mask, get_peer_latencies, global_minimum_spanning_tree, minimum_spanning_tree,
+from .topology import (RoundRobin, get_neighbour_mask, get_peer_latencies, global_minimum_spanning_tree, minimum_spanning_tree, mst_father,
                        peer_info, round_robin)
 
 __all__ = [n for n in dir() if not n.startswith("_")]
