@@ -271,8 +271,13 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 // stats: f64 [kStatSlots*2*Cout] zero-initialised workspace receiving sum / sum of squares of the
 // bf16 outputs per channel (consumed and re-zeroed by bn_forward(..., sums=stats)).
 // out: accumulate target (y = out + conv(x, w), written in place and returned).
+// bn_x / bn_fcoef / bn_mask (backward): the output is the gradient of a BN(+ReLU) output whose
+// input is bn_x; stats then receive sum(dz), sum(dz * x) (dz = grad * relu') for
+// bn_backward(..., sums=stats).  bn_mask (1 bit per element) or bn_fcoef (forward
+// [scale; shift]) gives the ReLU gate.
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
-                c10::optional<at::Tensor> out, int64_t variant) {
+                c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
+                c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -307,9 +312,36 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
     } else {
         y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
     }
+    kfk::EpiArgs ea;
+    ea.stats = sp;
+    int epi = accum ? kfk::kEpiAccum : 0;
+    const bool bwd = bn_x && bn_x->defined();
+    if (bwd) {
+        TORCH_CHECK(sp, "conv: BN-backward statistics need the stats workspace");
+        TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->sizes() == y.sizes() &&
+                        bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) && bn_x->device() == x.device(),
+                    "conv: bn_x must be the BN input (bf16 channels_last, the output's shape)");
+        ea.bx = reinterpret_cast<const uint16_t *>(bn_x->data_ptr());
+        if (bn_mask && bn_mask->defined()) {
+            TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == y.numel() / 8 &&
+                            bn_mask->device() == x.device(),
+                        "conv: bn_mask must hold one byte per 8 output elements");
+            ea.bmask = bn_mask->data_ptr<uint8_t>();
+            epi |= kfk::kEpiBwdBits;
+        } else {
+            TORCH_CHECK(bn_fcoef && bn_fcoef->defined() && bn_fcoef->scalar_type() == at::kFloat &&
+                            bn_fcoef->numel() >= 2 * K && bn_fcoef->device() == x.device(),
+                        "conv: bn_fcoef (forward [scale; shift], f32) or bn_mask required");
+            ea.fcoef = bn_fcoef->data_ptr<float>();
+            epi |= kfk::kEpiBwdCoef;
+        }
+    } else if (sp) {
+        epi |= kfk::kEpiFwdStats;
+    }
+    TORCH_CHECK(!(epi & kfk::kEpiFwdStats) || !(epi & kfk::kEpiAccum), "conv: stats + accumulate unsupported");
     kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
-                     reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), sp,
-                     accum, stream_of(x, 0), static_cast<int>(variant));
+                     reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), ea, epi,
+                     stream_of(x, 0), static_cast<int>(variant));
     return y;
 }
 
@@ -452,7 +484,7 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
 // Returns (dx, dres or undefined, dweight, dbias).
 std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd,
                                     at::Tensor weight, at::Tensor fcoef, c10::optional<at::Tensor> mask, bool relu,
-                                    bool training, bool want_dres) {
+                                    bool training, bool want_dres, c10::optional<at::Tensor> sums) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -469,13 +501,21 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
     at::Tensor dres;
     if (want_dres) dres = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
-    auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    double *sp = nullptr;
+    if (sums && sums->defined()) {
+        TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->numel() == 2 * C * kfk::kStatSlots &&
+                        sums->is_contiguous() && sums->device() == x.device(),
+                    "bn_backward: sums must be the conv epilogue's f64 workspace");
+        sp = sums->data_ptr<double>();
+    }
+    at::Tensor partial;
+    if (!sp) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     kfk::launch_bn_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                             reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(), mp,
                             mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, relu,
-                            training, partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
-                            coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
-                            want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0));
+                            training, partial.defined() ? partial.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
+                            db.data_ptr<float>(), coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
+                            want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0), sp);
     return {dx, dres, dw, db};
 }
 
@@ -703,7 +743,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv3x3_variants", &kfk::conv3x3_variants);
     m.def("conv", &conv, "1x1/3x3 NHWC bf16 convolution (MFMA implicit GEMM) with fused BN-statistics and "
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
-          py::arg("out") = py::none(), py::arg("variant") = -1);
+          py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
+          py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none());
     m.def("conv_flip_weight", &conv_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,KS-1-kh,KS-1-kw] (data-gradient weights)");
     m.def("conv_supported", &kfk::conv_supported);
     m.def("conv_flip_weights", &conv_flip_weights, "multi-tensor conv_flip_weight into preallocated outputs");
@@ -718,7 +759,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("num_batches") = py::none(), py::arg("sums") = py::none());
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
-          py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"));
+          py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none());
     m.def("bn_pool_supported", [](int64_t C, int64_t H, int64_t W) {
         return kfk::bn_pool_supported(kfk::BNShape{H * W, static_cast<int>(C)}, static_cast<int>(H),
                                       static_cast<int>(W));

@@ -543,6 +543,38 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize(const float *partial, 
     }
 }
 
+// Same coefficients from the f64 slotted sums of a data-gradient conv epilogue
+// (conv.hip kEpiBwd*): sum dz, sum dz*x; the slots are re-zeroed.
+__global__ void bn_bwd_finalize_sums(double *sums, int C, int64_t rows, const float *gamma, const float *mean,
+                                     const float *invstd, float *dgamma, float *dbeta, float *coef, bool training) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s0 = 0, s1 = 0;
+    for (int k = 0; k < kStatSlots; ++k) {
+        double *sl = sums + k * 2 * C;
+        s0 += sl[c];
+        s1 += sl[C + c];
+        sl[c] = 0.0;
+        sl[C + c] = 0.0;
+    }
+    const double db = s0, dg = static_cast<double>(invstd[c]) * (s1 - static_cast<double>(mean[c]) * db);
+    dgamma[c] = static_cast<float>(dg);
+    dbeta[c] = static_cast<float>(db);
+    const float g = gamma ? gamma[c] : 1.f;
+    const float a = g * invstd[c];
+    if (training) {
+        const float inv_m = 1.f / static_cast<float>(rows);
+        const float k2 = -a * static_cast<float>(dg) * invstd[c] * inv_m;
+        coef[c] = a;
+        coef[C + c] = k2;
+        coef[2 * C + c] = -a * static_cast<float>(db) * inv_m - k2 * mean[c];
+    } else {
+        coef[c] = a;
+        coef[C + c] = 0.f;
+        coef[2 * C + c] = 0.f;
+    }
+}
+
 // ---------------------------------------------------------------- backward apply
 
 template <int CVEC, int RM, bool DRES, class G>
@@ -615,11 +647,16 @@ void launch_stats(const uint16_t *x, BNShape sh, const float *gamma, const float
 template <class G>
 void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const uint8_t *mask, const float *mean,
                           const float *invstd, const float *gamma, BNShape sh, int rm, bool training, float *partial,
-                          float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s) {
+                          float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s,
+                          double *sums = nullptr) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     Chunking ch = chunking(sh);
     const uint4 *xx = reinterpret_cast<const uint4 *>(x);
+    if (sums) {
+        bn_bwd_finalize_sums<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, mean, invstd, dgamma, dbeta,
+                                                             coef, training);
+    } else {
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
         auto go = [&](auto rmc) {
@@ -633,6 +670,7 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
     });
     bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
                                                                    invstd, dgamma, dbeta, coef, training);
+    }
     const int g = apply_grid(nvec);
     uint4 *o = reinterpret_cast<uint4 *>(dx), *r = reinterpret_cast<uint4 *>(dres);
     dispatch_cvec(cvec, [&](auto cvc) {
@@ -701,10 +739,10 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
 void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                        uint16_t *dres, hipStream_t s) {
+                        uint16_t *dres, hipStream_t s, double *sums) {
     const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
     launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy)}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
-                         training, partial, dgamma, dbeta, coef, dx, dres, s);
+                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums);
 }
 
 bool bn_pool_supported(BNShape sh, int H, int W) {

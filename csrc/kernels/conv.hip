@@ -25,12 +25,23 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <stdexcept>
+
 namespace kfk {
 
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+__device__ __forceinline__ void unpack_bf16x8(const uint4 &v, float (&f)[8]) {
+    const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f[2 * k] = __uint_as_float(u[k] << 16);
+        f[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+    }
+}
 
 constexpr int kBK = 64;              // channels per K-step
 constexpr int kRowBytes = kBK * 2;   // 128 B per staged row
@@ -53,15 +64,19 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
-// KS = 3 (pad 1) or 1 (pad 0); EPI bit 0: per-channel sum / sum-of-squares of the bf16
-// outputs accumulated (f64 atomics) into stats[2][K] (fused BN statistics); bit 1:
-// y += conv (accumulate into the existing bf16 tensor, e.g. a residual gradient).
+// KS = 3 (pad 1) or 1 (pad 0).  EPI flags (kernels.hpp ConvEpi):
+//   kEpiAccum     y += conv (accumulate into the existing bf16 tensor, a residual gradient);
+//   kEpiFwdStats  per-channel sum / sum-of-squares of the bf16 outputs (the following BN's
+//                 batch statistics) -> f64 atomics into ea.stats[slot][2][K];
+//   kEpiBwdCoef / kEpiBwdBits  the output is the gradient of a BN(+ReLU) output whose input
+//                 is ea.bx: sum(dz) and sum(dz * x) with dz = grad * relu' from the forward
+//                 coefficients ea.fcoef (recomputed) or from the 1-bit mask ea.bmask.
 template <int KS, int WM, int WN, int STAGES, int EPI>
 __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__restrict__ x,
                                                             const uint16_t *__restrict__ w,
                                                             uint16_t *__restrict__ y,
                                                             const uint16_t *__restrict__ zero, Geo g,
-                                                            double *__restrict__ stats) {
+                                                            EpiArgs ea) {
     constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
     constexpr int TAPS = KS * KS, PAD = (KS - 1) / 2;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
@@ -213,43 +228,30 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(acc[i][j][r]);
             }
     __syncthreads();
-    if constexpr (EPI & 1) {
-        // fused BN statistics of the bf16-rounded tile (rows past M are zero rows)
-        constexpr int PARTS = NT / BN, RPP = BM / PARTS;
-        static_assert(PARTS * BN == NT && RPP * PARTS == BM, "stats split");
-        float *red = reinterpret_cast<float *>(lds + BM * CROW);
-        static_assert(BM * CROW + 2 * NT * 4 <= STAGES * STAGE, "stats scratch fits");
-        const int col = tid % BN, part = tid / BN;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll 8
-        for (int r = part * RPP; r < (part + 1) * RPP; ++r) {
-            const float v = bf16_to_f32(*reinterpret_cast<const uint16_t *>(lds + r * CROW + col * 2));
-            s1 += v;
-            s2 += v * v;
-        }
-        red[tid] = s1;
-        red[NT + tid] = s2;
-        __syncthreads();
-        if (part == 0) {
-            double t1 = 0, t2 = 0;
+    // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
+    // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
+    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
+    static_assert(NT % VPR == 0, "fixed channel group per thread");
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
+    const int cv = tid % VPR;
+    float s1[8], s2[8], sc[8], sh[8];
 #pragma unroll
-            for (int p = 0; p < PARTS; ++p) {
-                t1 += red[p * BN + col];
-                t2 += red[NT + p * BN + col];
-            }
-            double *sl = stats + (mt % kStatSlots) * 2 * g.K;  // spread atomics over slots
-            atomicAdd(sl + n0 + col, t1);
-            atomicAdd(sl + g.K + n0 + col, t2);
+    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+    if constexpr ((EPI & kEpiBwdCoef) != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sc[k] = ea.fcoef[n0 + cv * 8 + k];
+            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
         }
     }
-    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     for (int v = tid; v < BM * VPR; v += NT) {
-        const int row = v / VPR, cv = v - row * VPR;
+        const int row = v / VPR;
         const int m = m0 + row;
         if (m < g.M) {
-            uint4 *dst = reinterpret_cast<uint4 *>(y + static_cast<int64_t>(m) * g.K + n0 + cv * 8);
+            const int64_t e = static_cast<int64_t>(m) * g.K + n0 + cv * 8;
+            uint4 *dst = reinterpret_cast<uint4 *>(y + e);
             uint4 val = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
-            if constexpr (EPI & 2) {
+            if constexpr ((EPI & kEpiAccum) != 0) {
                 const uint4 old = *dst;
                 const uint32_t *a = reinterpret_cast<const uint32_t *>(&val);
                 const uint32_t *b = reinterpret_cast<const uint32_t *>(&old);
@@ -265,6 +267,58 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 val = make_uint4(o[0], o[1], o[2], o[3]);
             }
             *dst = val;
+            if constexpr (STATS) {
+                float f[8];
+                unpack_bf16x8(val, f);
+                if constexpr ((EPI & kEpiFwdStats) != 0) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        s1[k] += f[k];
+                        s2[k] += f[k] * f[k];
+                    }
+                } else {
+                    // BN backward sums of the BN whose input is ea.bx:
+                    //   dz = grad * relu'(.) ; s1 += dz ; s2 += dz * x
+                    float xv[8];
+                    unpack_bf16x8(*reinterpret_cast<const uint4 *>(ea.bx + e), xv);
+                    uint32_t mbits = 0xffu;
+                    if constexpr ((EPI & kEpiBwdBits) != 0) mbits = ea.bmask[e >> 3];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        bool on;
+                        if constexpr ((EPI & kEpiBwdBits) != 0) on = (mbits >> k) & 1u;
+                        else on = xv[k] * sc[k] + sh[k] > 0.f;
+                        const float dz = on ? f[k] : 0.f;
+                        s1[k] += dz;
+                        s2[k] += dz * xv[k];
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (STATS) {
+        // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
+        constexpr int GROUPS = NT / VPR;
+        float *red = reinterpret_cast<float *>(lds + BM * CROW);
+        static_assert(BM * CROW + 2 * GROUPS * BN * 4 <= STAGES * STAGE, "stats scratch fits");
+        __syncthreads();
+        const int grp = tid / VPR;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            red[grp * BN + cv * 8 + k] = s1[k];
+            red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
+        }
+        __syncthreads();
+        for (int col = tid; col < BN; col += NT) {
+            double t1 = 0, t2 = 0;
+#pragma unroll 4
+            for (int p = 0; p < GROUPS; ++p) {
+                t1 += red[p * BN + col];
+                t2 += red[(GROUPS + p) * BN + col];
+            }
+            double *sl = ea.stats + (mt % kStatSlots) * 2 * g.K;  // spread atomics over slots
+            atomicAdd(sl + n0 + col, t1);
+            atomicAdd(sl + g.K + n0 + col, t2);
         }
     }
 }
@@ -331,47 +385,60 @@ const void *zero_page() {
     return p;
 }
 
-template <int KS, int WM, int WN, int ST>
-void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, double *stats, bool accum,
-                    hipStream_t s) {
+template <int KS, int WM, int WN, int ST, int EPI>
+void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
     g.mtiles = (g.M + 64 * WM - 1) / (64 * WM);
     g.ntiles = g.K / (64 * WN);
-    const dim3 grid(g.mtiles * g.ntiles), block(64 * WM * WN);
-    const auto *z = reinterpret_cast<const uint16_t *>(zero_page());
-    const int epi = (stats ? 1 : 0) | (accum ? 2 : 0);
-    switch (epi) {
-    case 0: conv_kernel<KS, WM, WN, ST, 0><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
-    case 1: conv_kernel<KS, WM, WN, ST, 1><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
-    case 2: conv_kernel<KS, WM, WN, ST, 2><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
-    default: conv_kernel<KS, WM, WN, ST, 3><<<grid, block, 0, s>>>(x, w, y, z, g, stats); break;
+    conv_kernel<KS, WM, WN, ST, EPI><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+        x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
+}
+
+// Tuning-only tile variants instantiate the plain epilogue; the defaults every fused one.
+template <int KS, int WM, int WN, int ST, bool ALL>
+void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
+                    hipStream_t s) {
+    if constexpr (!ALL) {
+        if (epi != 0) throw std::invalid_argument("conv: fused epilogues need the default tile variant");
+        launch_epi<KS, WM, WN, ST, 0>(x, w, y, g, ea, s);
+    } else {
+        switch (epi) {
+        case 0: launch_epi<KS, WM, WN, ST, 0>(x, w, y, g, ea, s); break;
+        case kEpiFwdStats: launch_epi<KS, WM, WN, ST, kEpiFwdStats>(x, w, y, g, ea, s); break;
+        case kEpiAccum: launch_epi<KS, WM, WN, ST, kEpiAccum>(x, w, y, g, ea, s); break;
+        case kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiBwdCoef>(x, w, y, g, ea, s); break;
+        case kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiBwdBits>(x, w, y, g, ea, s); break;
+        case kEpiAccum | kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdBits>(x, w, y, g, ea, s); break;
+        case kEpiAccum | kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdCoef>(x, w, y, g, ea, s); break;
+        default: throw std::invalid_argument("conv: unsupported epilogue combination");
+        }
     }
 }
 
 template <int KS>
-void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, double *stats, bool accum, hipStream_t s,
+void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi, hipStream_t s,
                int variant) {
     // default per shape class (tools/bench_conv3x3.py, tools/bench_conv.py): 3x3 -> 256x128 /
     // 8 waves / 3 stages when Cout allows; 1x1 (1-16 K-steps) -> 128x128 / 4 waves / 2 stages
     // (two blocks per CU keep more HBM traffic in flight); Cout = 64 -> 256x64 / 4 waves
     if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : 1) : 2;
     switch (variant) {
-    case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2>(x, w, y, g, stats, accum, s); break; }  // 128x128
+    case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
             [[fallthrough]];
-    case 1: if (g.K % 128 == 0) { launch_variant<KS, 4, 2, 3>(x, w, y, g, stats, accum, s); break; }  // 256x128
+    case 1: if (g.K % 128 == 0) { launch_variant<KS, 4, 2, 3, true>(x, w, y, g, ea, epi, s); break; }  // 256x128
             [[fallthrough]];
-    case 2: launch_variant<KS, 4, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 256x64
-    case 3: launch_variant<KS, 4, 1, 3>(x, w, y, g, stats, accum, s); break;                          // 256x64 3st
-    case 4: launch_variant<KS, 8, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 512x64
-    case 5: launch_variant<KS, 2, 1, 2>(x, w, y, g, stats, accum, s); break;                          // 128x64
-    default: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3>(x, w, y, g, stats, accum, s); break; } // 128x128 3st
-             launch_variant<KS, 2, 1, 3>(x, w, y, g, stats, accum, s); break;                         // 128x64 3st
+    case 2: launch_variant<KS, 4, 1, 2, true>(x, w, y, g, ea, epi, s); break;                          // 256x64
+    case 3: launch_variant<KS, 4, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 256x64 3st
+    case 4: launch_variant<KS, 8, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 512x64
+    case 5: launch_variant<KS, 2, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 128x64
+    default: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
+             launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                        // 128x64 3st
     }
 }
 
 int conv3x3_variants() { return 7; }
 
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
-                 int stride, double *stats, bool accumulate, hipStream_t s, int variant) {
+                 int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant) {
     Geo g;
     const int pad = (ks - 1) / 2;
     g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
@@ -379,13 +446,13 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.OW = (W + 2 * pad - ks) / stride + 1;
     g.M = N * g.OH * g.OW;
     g.mtiles = g.ntiles = 0;
-    if (ks == 1) launch_ks<1>(x, w, y, g, stats, accumulate, s, variant);
-    else launch_ks<3>(x, w, y, g, stats, accumulate, s, variant);
+    if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
+    else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
 }
 
 void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
                     int stride, hipStream_t s, int variant) {
-    launch_conv(x, w, y, N, H, W, Cin, Cout, 3, stride, nullptr, false, s, variant);
+    launch_conv(x, w, y, N, H, W, Cin, Cout, 3, stride, EpiArgs{}, 0, s, variant);
 }
 
 void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s) {

@@ -96,8 +96,15 @@ int conv3x3_variants();
 // keeping atomic contention per address low); bn_forward(sums=...) folds the slots.
 constexpr int kStatSlots = 16;
 bool conv_supported(int Cin, int Cout, int ks, int stride);
+enum ConvEpi : int { kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8 };
+struct EpiArgs {
+    double *stats = nullptr;         // kStatSlots x [2][K] f64 (zeroed; consumed + re-zeroed by the BN)
+    const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output
+    const float *fcoef = nullptr;    // bwd coef: forward [scale(K); shift(K)]
+    const uint8_t *bmask = nullptr;  // bwd bits: ReLU mask, one byte per 8 channels
+};
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
-                 int stride, double *stats, bool accumulate, hipStream_t s, int variant = -1);
+                 int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);
 // Multi-tensor flip (one launch for a whole model's conv weights).
 struct FlipTable {
     static constexpr int kMax = 64;
@@ -136,7 +143,8 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
 void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                        uint16_t *dres, hipStream_t s);
+                        uint16_t *dres, hipStream_t s, double *sums = nullptr);
+// (sums: f64 kStatSlots x [sum dz; sum dz*x] from a conv epilogue -> no reduce pass; re-zeroed.)
 
 // ResNet stem: y = maxpool3x3s2p1(relu(bn(x))), x = [N, H, W, C] (rows = N*H*W).
 // arg receives the window argmax (0..8) per pooled element (bytes).

@@ -15,7 +15,11 @@ forward (training)
 * BN(+ReLU) and BN3 + residual + ReLU are the fused bn.hip kernels.
 
 backward
-* stride-1 data gradients are the same MFMA kernel on transposed/flipped weights;
+* stride-1 data gradients are the same MFMA kernel on transposed/flipped weights, whose
+  epilogue also accumulates the backward sums (sum dz, sum dz*x under the ReLU gate) of the
+  BN that produced the conv input -> that BN's backward skips its reduction pass; across
+  blocks, the next block's conv1 data gradient does this for the previous block's BN3
+  (``_TailSlot``);
 * the block-input gradient is formed IN PLACE: conv1's data-gradient kernel
   accumulates into the identity gradient produced by the BN3+add+ReLU backward
   (or into the downsample branch's data gradient) -- no elementwise add, no extra
@@ -100,17 +104,42 @@ def _flip_cache(space) -> _FlipCache:
     return c
 
 
-def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: Optional[torch.Tensor] = None):
-    """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given)."""
+def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: Optional[torch.Tensor] = None,
+           bn=None):
+    """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given).
+
+    ``bn = (ws, bn_x, fcoef, mask)``: the result is the gradient of a BN(+ReLU) output whose
+    input is ``bn_x``; the kernel epilogue also accumulates that BN's backward sums into
+    ``ws`` (only on the MFMA path -- returns whether it did via ``_dgrad.fused``)."""
     H = hip()
     if stride == 1:
-        return H.conv(dy, flipped if flipped is not None else H.conv_flip_weight(w), 1, None, out)
+        wt = flipped if flipped is not None else H.conv_flip_weight(w)
+        if bn is not None:
+            ws, bx, fc, mk = bn
+            _dgrad.fused = True
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk)
+        return H.conv(dy, wt, 1, None, out)
+    _dgrad.fused = False
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
     if out is not None:
         out.add_(dx)
         return out
     return _cl(dx)
+
+
+class _TailSlot:
+    """Link from a block's output to the NEXT block's backward: that block's conv1 data
+    gradient IS the gradient of this output, so its epilogue can also produce this block's
+    BN3 backward sums (sum dz, sum dz*y3 under the 1-bit ReLU mask).  ``dx_ptr`` lets this
+    block's backward check that the gradient it receives is exactly that tensor (no other
+    consumer added to it); otherwise the sums are discarded and recomputed."""
+    __slots__ = ("ws", "y3", "mask", "ready", "dx_ptr")
+
+    def __init__(self, ws, y3, mask):
+        self.ws, self.y3, self.mask = ws, y3, mask
+        self.ready = False
+        self.dx_ptr = 0
 
 
 class _Spec:
@@ -153,6 +182,9 @@ class _BottleneckFn(torch.autograd.Function):
             yd = md = idd = cd = None
             idt = x
         out, m3, i3, c3, mask3 = bn(2, y3, idt, True)
+        # cross-block BN3 backward fusion: the previous block's tail (if x is its output)
+        ctx.prev = getattr(x, "_kf_tail", None)
+        ctx.tail = _TailSlot(_sums(spec.bns[2], dev), y3, mask3)
         ctx.spec = spec
         ctx.wdtypes = [w.dtype for w in ws[0::3]]
         ctx.save_for_backward(x, y1, z1, y2, z2, y3, yd, *ws_bf, *gam, m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3,
@@ -178,15 +210,24 @@ class _BottleneckFn(torch.autograd.Function):
                     fl[k] = src[0].get(src[1])
         dbn = [None] * nb  # (dgamma, dbeta)
         dw = [None] * nb
-        dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, True)
+        ws = [_sums(b, dout.device) for b in spec.bns]
+        tail = ctx.tail
+        use3 = tail.ready and dout.data_ptr() == tail.dx_ptr
+        if tail.ready and not use3:
+            tail.ws.zero_()  # sums of a gradient that is not the one we got: discard
+        tail.ready, tail.y3, tail.mask = False, None, None
+        dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, True,
+                                            ws[2] if use3 else None)
         dbn[2] = (dg3, db3)
-        dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2])
+        dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None))
         dw[2] = _wgrad(dy3, z2, w[2], 1, 0)
-        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False)
+        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1])
         dbn[1] = (dg2, db2)
-        dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1])
+        dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None))
+        fused1 = _dgrad.fused
         dw[1] = _wgrad(dy2, z1, w[1], s, 1)
-        dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False)
+        dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
+                                         ws[0] if fused1 else None)
         dbn[0] = (dg1, db1)
         if spec.ds:
             dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False)
@@ -195,7 +236,14 @@ class _BottleneckFn(torch.autograd.Function):
             dw[3] = _wgrad(dyd, x, w[3], s, 0)
         else:
             dx = didt  # the identity gradient: conv1's data gradient is accumulated into it
-        dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0])
+        prev = ctx.prev
+        if prev is not None and prev.y3 is not None and prev.y3.shape == dx.shape:
+            # conv1's data gradient completes the gradient of the previous block's output:
+            # its epilogue also accumulates that block's BN3 backward sums
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask))
+            prev.ready, prev.dx_ptr = True, dx.data_ptr()
+        else:
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0])
         dw[0] = _wgrad(dy1, x, w[0], 1, 0)
         grads: List[Optional[torch.Tensor]] = []
         for i in range(nb):
@@ -263,4 +311,7 @@ def bottleneck_forward(block, x: torch.Tensor) -> torch.Tensor:
             wsrc.append(None)
     spec.direct = direct if any(d is not None for d in direct) else None
     spec.wsrc = wsrc if any(v is not None for v in wsrc) else None
-    return _BottleneckFn.apply(spec, x, *params)
+    out = _BottleneckFn.apply(spec, x, *params)
+    if out.grad_fn is not None:
+        out._kf_tail = out.grad_fn.tail  # the next block's backward fills our BN3 sums
+    return out

@@ -429,8 +429,9 @@ def test_bench_json():
 
 
 @needs_gpu
-@pytest.mark.parametrize("cin,stride,ds", [(256, 1, False), (64, 1, True), (256, 2, True)])
-def test_fused_bottleneck_matches_fp32(cin, stride, ds):
+@pytest.mark.parametrize("cin,stride,ds,nblk", [(256, 1, False, 1), (64, 1, True, 1), (256, 2, True, 1),
+                                                (64, 1, True, 3), (256, 2, True, 2)])
+def test_fused_bottleneck_matches_fp32(cin, stride, ds, nblk):
     """One-node bottleneck (MFMA convs with BN-statistics epilogue, in-place residual
     gradient) vs the float32 PyTorch composition of the same block; its error must be
     within the bf16 error of the per-layer bf16 path (autocast + fused BN modules)."""
@@ -446,7 +447,11 @@ def test_fused_bottleneck_matches_fp32(cin, stride, ds):
     planes = 64
     norm = lambda c, relu: BatchNormAct2d(c, relu=relu)  # noqa: E731
     down = nn.Sequential(conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4, relu=False)) if ds else None
-    blk = Bottleneck(cin, planes, stride, down, norm=norm, fused_tail=True).cuda().to(memory_format=torch.channels_last)
+    blocks = [Bottleneck(cin, planes, stride, down, norm=norm, fused_tail=True)]
+    # following identity blocks: their conv1 data gradients also produce the previous
+    # block's BN3 backward sums (cross-block fusion)
+    blocks += [Bottleneck(planes * 4, planes, 1, None, norm=norm, fused_tail=True) for _ in range(nblk - 1)]
+    blk = nn.Sequential(*blocks).cuda().to(memory_format=torch.channels_last)
     for m in blk.modules():
         if isinstance(m, nn.BatchNorm2d):
             nn.init.uniform_(m.weight, 0.5, 1.5)
@@ -460,7 +465,7 @@ def test_fused_bottleneck_matches_fp32(cin, stride, ds):
         old = fused_block.set_enabled(fused)
         try:
             if fused:
-                assert fused_block.eligible(mod, xin)
+                assert fused_block.eligible(mod[0], xin)
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
                 out = mod(xin)
             (out.float() * gout).sum().backward()
