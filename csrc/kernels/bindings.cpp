@@ -345,6 +345,52 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
     return y;
 }
 
+// Weight gradient of conv(x, w, stride, pad (ks-1)/2): dw [Cout, Cin, ks, ks] channels_last
+// (memory [Cout][ks][ks][Cin]).  out: bf16 or f32 destination of that shape/layout (written,
+// or added to with accumulate); otherwise a new bf16 tensor.  variant / splits: -1 = planner.
+at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c10::optional<at::Tensor> out,
+                      bool accumulate, int64_t variant, int64_t splits) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_wgrad: x must be a 4-D channels_last bf16 GPU tensor");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+    const int pad = static_cast<int>((ks - 1) / 2);
+    const int OH = (H + 2 * pad - static_cast<int>(ks)) / static_cast<int>(stride) + 1;
+    const int OW = (W + 2 * pad - static_cast<int>(ks)) / static_cast<int>(stride) + 1;
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                    dy.size(2) == OH && dy.size(3) == OW && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dy.device() == x.device(),
+                "conv_wgrad: dy must be the [N, Cout, OH, OW] channels_last bf16 output gradient");
+    const int K = dy.size(1);
+    TORCH_CHECK(kfk::conv_wgrad_supported(C, K, static_cast<int>(ks), static_cast<int>(stride)),
+                "conv_wgrad: unsupported channels/kernel/stride");
+    TORCH_CHECK(static_cast<int64_t>(N) * H * W * C < (int64_t(1) << 31) &&
+                    static_cast<int64_t>(N) * OH * OW * K < (int64_t(1) << 31),
+                "conv_wgrad: tensor too large for 32-bit offsets");
+    c10::DeviceGuard gd(x.device());
+    at::Tensor dw;
+    if (out && out->defined()) {
+        TORCH_CHECK((out->scalar_type() == at::kBFloat16 || out->scalar_type() == at::kFloat) && out->dim() == 4 &&
+                        out->size(0) == K && out->size(1) == C && out->size(2) == ks && out->size(3) == ks &&
+                        out->is_contiguous(at::MemoryFormat::ChannelsLast) && out->device() == x.device(),
+                    "conv_wgrad: out must be [Cout, Cin, ks, ks] channels_last bf16/f32 on x's device");
+        dw = *out;
+    } else {
+        TORCH_CHECK(!accumulate, "conv_wgrad: accumulate needs out");
+        dw = at::empty({K, C, ks, ks}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    }
+    const auto plan = kfk::conv_wgrad_plan(N, H, W, C, K, static_cast<int>(ks), static_cast<int>(stride),
+                                           static_cast<int>(variant), static_cast<int>(splits));
+    at::Tensor ws;
+    if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, x.options().dtype(at::kFloat));
+    kfk::launch_conv_wgrad(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                           reinterpret_cast<const uint16_t *>(x.data_ptr()), dw.data_ptr(),
+                           plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, N, H, W, C, K, static_cast<int>(ks),
+                           static_cast<int>(stride), plan, dw.scalar_type() == at::kFloat, accumulate,
+                           stream_of(x, 0));
+    return dw;
+}
+
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
@@ -745,6 +791,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none());
+    m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
+          py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
+          py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
+    m.def("conv_wgrad_supported", &kfk::conv_wgrad_supported);
+    m.def("conv_wgrad_variants", &kfk::conv_wgrad_variants);
+    m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
+        const auto p = kfk::conv_wgrad_plan(N, H, W, Cin, Cout, ks, stride, variant, splits);
+        return py::make_tuple(p.variant, p.splits, p.kps, p.ws_floats);
+    }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("Cin"), py::arg("Cout"), py::arg("ks"), py::arg("stride"),
+          py::arg("variant") = -1, py::arg("splits") = -1);
     m.def("conv_flip_weight", &conv_flip_weight, "w[co,ci,kh,kw] -> w[ci,co,KS-1-kh,KS-1-kw] (data-gradient weights)");
     m.def("conv_supported", &kfk::conv_supported);
     m.def("conv_flip_weights", &conv_flip_weights, "multi-tensor conv_flip_weight into preallocated outputs");

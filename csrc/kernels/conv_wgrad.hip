@@ -1,0 +1,453 @@
+// Weight gradient of the 1x1 / 3x3 NHWC bf16 convolutions (stride 1 or 2) on CDNA4
+// matrix cores, for gfx950: a split-K GEMM over output pixels.
+//
+//   dw[co, kh, kw, ci] = sum_p dy[p, co] * x[n, oh*s + kh - pad, ow*s + kw - pad, ci]
+//   GEMM: M = Cout, N = Cin (one tap per tile), K = P = N*OH*OW output pixels
+//
+// Why: the weight gradients were the last convolution pass on MIOpen (5.4 ms of a 25 ms
+// ResNet-50 step plus 0.6 ms of its split-K zero-fills and casts, profiles/README.md).
+// Both operands carry the reduction index (the pixel) as their ROW and the GEMM index
+// (channel) contiguous, the "NT" layout: tiles are staged global->LDS unchanged
+// (16-byte global_load_lds, rows of BM or BN channels) and every MFMA operand is read
+// with the gfx950 transposing LDS read ds_read_b64_tr_b16, which hands each lane 4
+// pixels of one channel -- no register/ds_write transpose pass.
+//
+// LDS image: rows of 128 or 256 bytes (64 / 128 channels), 32-byte column groups
+// XOR-swizzled by the row (h(row) below) so the 8 rows one 32-lane half of a
+// transposing read touches (two 4-row blocks 8 rows apart) land on 8 distinct
+// 32-byte bank groups: conflict-free.  The swizzle is applied on the staging source
+// address (global_load_lds writes fixed LDS offsets) and on the read address.
+//
+// Split-K: P is 12.5 K .. 800 K pixels while M x N is at most 2048 x 512, so each
+// workgroup reduces a contiguous pixel range; partial f32 tiles go to a workspace in
+// the accumulator's native register order (coalesced 16-byte stores) and a second
+// kernel sums the splits, converts and scatters to [Cout][KS*KS][Cin] (deterministic).
+// Accumulating into an f32 destination (e.g. a flat f32 gradient slot) the splits add
+// their tiles with f32 atomics instead: no workspace, no second pass.  Workgroups of one
+// split are launched together (same pixel rows in L2) and remapped XCD-contiguously.
+//
+// Reference parity: the reference has no kernels of its own; it trains
+// tf.keras.applications ResNet-50 with TF's stock convolutions
+// (benchmarks/system/benchmark_kungfu.py:96).
+#include "common.hpp"
+#include "kernels.hpp"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace kfk {
+
+const void *zero_page();  // conv.hip
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kBK = 64;  // pixels per K-step
+
+struct WGeo {
+    int N, H, W, C, OH, OW, K;
+    int P, HW;
+    uint64_t m_hw, m_ow;  // floor(p / d) = (p * m) >> 40, exact for p * d < 2^40
+    int mtiles, ntiles, taps, tiles, splits, kps;
+};
+
+__device__ __forceinline__ int fdiv(int p, uint64_t m) {
+    return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 32-byte column-group swizzle of an LDS image row (ROW = 128 or 256 bytes).
+template <int ROW>
+__device__ __forceinline__ int hswz(int row) {
+    if constexpr (ROW == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+    else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t *p0, const uint8_t *p1) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// WM x WN waves (wave tile 64 co x 64 ci), STAGES-deep global_load_lds ring; S = stride.
+template <int KS, int S, int WM, int WN, int STAGES>
+__global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__restrict__ dy,
+                                                             const uint16_t *__restrict__ x,
+                                                             float *__restrict__ part, void *__restrict__ dw,
+                                                             const uint16_t *__restrict__ zero, WGeo g,
+                                                             int out_f32, int accumulate, int atomic_out) {
+    constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+    constexpr int PAD = (KS - 1) / 2;
+    constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per staged pixel row
+    constexpr int CPRA = ROWA / 16, CPRB = ROWB / 16;
+    constexpr int RPIA = 64 / CPRA, RPIB = 64 / CPRB;  // rows per 1 KB glds instruction
+    constexpr int A_BYTES = kBK * ROWA, B_BYTES = kBK * ROWB, STAGE = A_BYTES + B_BYTES;
+    constexpr int A_INST = kBK / RPIA / NW, B_INST = kBK / RPIB / NW;
+    constexpr int LOADS = A_INST + B_INST;
+    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * RPIA == kBK && B_INST * NW * RPIB == kBK, "split");
+    constexpr bool IDENT = KS == 1 && S == 1;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (orig >> 3);
+    const int split = wg / g.tiles, tile = wg - split * g.tiles;
+    const int mn = g.mtiles * g.ntiles;
+    const int tap = tile / mn, rem = tile - tap * mn;
+    const int mt = rem / g.ntiles, nt = rem - mt * g.ntiles;
+    const int kh = tap / KS, kw = tap - kh * KS;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int p_begin = split * g.kps * kBK;
+    int nsteps = (g.P - p_begin + kBK - 1) / kBK;
+    if (nsteps > g.kps) nsteps = g.kps;
+
+    // ---- staging descriptors: lane l of an instruction writes image bytes [16l, 16l+16)
+    int a_row[A_INST], a_col[A_INST];
+#pragma unroll
+    for (int j = 0; j < A_INST; ++j) {
+        const int r = (wave * A_INST + j) * RPIA + lane / CPRA;
+        const int pc = lane % CPRA;
+        const int lc = (((pc >> 1) ^ hswz<ROWA>(r)) << 1) | (pc & 1);
+        a_row[j] = r;
+        a_col[j] = m0 + lc * 8;
+    }
+    int b_row[B_INST], b_col[B_INST];
+#pragma unroll
+    for (int j = 0; j < B_INST; ++j) {
+        const int r = (wave * B_INST + j) * RPIB + lane / CPRB;
+        const int pc = lane % CPRB;
+        const int lc = (((pc >> 1) ^ hswz<ROWB>(r)) << 1) | (pc & 1);
+        b_row[j] = r;
+        b_col[j] = n0 + lc * 8;
+    }
+
+    auto stage = [&](int ks, int buf) {
+        const int p0 = p_begin + ks * kBK;
+        uint8_t *abase = lds + buf * STAGE;
+        uint8_t *bbase = abase + A_BYTES;
+#pragma unroll
+        for (int j = 0; j < A_INST; ++j) {
+            const int p = p0 + a_row[j];
+            const uint16_t *src = p < g.P ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
+            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < B_INST; ++j) {
+            const int p = p0 + b_row[j];
+            const uint16_t *src = zero;
+            if constexpr (IDENT) {
+                if (p < g.P) src = x + static_cast<uint32_t>(p * g.C + b_col[j]);
+            } else {
+                const int n = fdiv(p, g.m_hw);
+                const int r = p - n * g.HW;
+                const int oh = fdiv(r, g.m_ow);
+                const int ow = r - oh * g.OW;
+                const int ih = oh * S + kh - PAD, iw = ow * S + kw - PAD;
+                if (p < g.P && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                    static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
+                    src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
+            }
+            __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
+        }
+    };
+
+    // ---- fragment read addresses (transposing reads; see file comment)
+    // lane = 16 g + 4 q + p: block rows kb + q (kb = 32 s + 8 g [+4]), columns 16 c + 4 p.
+    const int wm = wave / WN, wn = wave % WN;
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int rowa0 = 8 * fg + fq;  // hswz is the same for rows rowa0 + {0, 4, 32, 36}
+    int aoff[4], boff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        aoff[i] = rowa0 * ROWA + 32 * ((wm * 4 + i) ^ hswz<ROWA>(rowa0)) + 8 * fp;
+        boff[i] = rowa0 * ROWB + 32 * ((wn * 4 + i) ^ hswz<ROWB>(rowa0)) + 8 * fp;
+    }
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p)
+        if (p < nsteps) stage(p, p);
+    int buf = 0;
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if (ks + STAGES - 1 <= nsteps) wait_vmcnt<LOADS * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t *abase = lds + buf * STAGE;
+        const uint8_t *bbase = abase + A_BYTES;
+        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af0[i] = tr_frag(abase + aoff[i], abase + aoff[i] + 4 * ROWA);
+            bf0[i] = tr_frag(bbase + boff[i], bbase + boff[i] + 4 * ROWB);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af1[i] = tr_frag(abase + aoff[i] + 32 * ROWA, abase + aoff[i] + 36 * ROWA);
+            bf1[i] = tr_frag(bbase + boff[i] + 32 * ROWB, bbase + boff[i] + 36 * ROWB);
+        }
+        mfma_block(af0, bf0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_block(af1, bf1);
+        buf = buf + 1 == STAGES ? 0 : buf + 1;
+    }
+    wait_vmcnt<0>();
+
+    // ---- epilogue.  C map (16x16): col (ci) = lane & 15, row (co) = (lane >> 4) * 4 + r.
+    if (atomic_out) {
+        // f32 destination, every split adds its tile in place (no workspace, no reduce pass)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                    const int ci = n0 + wn * 64 + j * 16 + (lane & 15);
+                    const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
+                    atomicAdd(static_cast<float *>(dw) + e, acc[i][j][r]);
+                }
+    } else if (g.splits == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+                    const int ci = n0 + wn * 64 + j * 16 + (lane & 15);
+                    const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
+                    float v = acc[i][j][r];
+                    if (out_f32) {
+                        float *o = static_cast<float *>(dw) + e;
+                        *o = accumulate ? *o + v : v;
+                    } else {
+                        uint16_t *o = static_cast<uint16_t *>(dw) + e;
+                        if (accumulate) v += bf16_to_f32(*o);
+                        *o = f32_to_bf16(v);
+                    }
+                }
+    } else {
+        f32x4 *dst = reinterpret_cast<f32x4 *>(part + static_cast<int64_t>(wg) * (BM * BN)) + tid;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * NT);
+    }
+}
+
+// Sum the split partials (workspace order of wgrad_kernel) and scatter to dw.
+// Block = 256 threads = OUT float4 outputs x SG split groups (SG = 256 / OUT, a power of
+// two <= splits): a few K outputs with hundreds of splits (the 56x56 layers) still keep
+// every CU's loads in flight; the SG partial sums meet in LDS.
+template <int WM, int WN>
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, void *__restrict__ dw,
+                                                           WGeo g, int out_f32, int accumulate, int sg_log2) {
+    constexpr int BM = 64 * WM, BN = 64 * WN, NT = 64 * WM * WN;
+    constexpr int TILE4 = BM * BN / 4;
+    __shared__ f32x4 red[256];
+    const int SG = 1 << sg_log2, OUT = 256 >> sg_log2;
+    const int t = threadIdx.x, o = t & (OUT - 1), sg = t >> (8 - sg_log2);
+    const int64_t total = static_cast<int64_t>(g.tiles) * TILE4;
+    const int64_t idx = static_cast<int64_t>(blockIdx.x) * OUT + o;
+    const int64_t stride_split = total;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (idx < total) {
+        const f32x4 *src = reinterpret_cast<const f32x4 *>(part) + idx;
+        int sp = sg;
+        for (; sp + 3 * SG < g.splits; sp += 4 * SG) {
+            const f32x4 a = __builtin_nontemporal_load(src + sp * stride_split);
+            const f32x4 b = __builtin_nontemporal_load(src + (sp + SG) * stride_split);
+            const f32x4 c = __builtin_nontemporal_load(src + (sp + 2 * SG) * stride_split);
+            const f32x4 d = __builtin_nontemporal_load(src + (sp + 3 * SG) * stride_split);
+            s += (a + b) + (c + d);
+        }
+        for (; sp < g.splits; sp += SG) s += __builtin_nontemporal_load(src + sp * stride_split);
+    }
+    red[t] = s;
+    __syncthreads();
+    if (sg == 0 && idx < total) {
+        for (int k = 1; k < SG; ++k) s += red[o + k * OUT];
+        const int tile = static_cast<int>(idx / TILE4);
+        const int rem = static_cast<int>(idx - static_cast<int64_t>(tile) * TILE4);
+        const int ij = rem / NT, tid = rem - ij * NT;
+        const int mn = g.mtiles * g.ntiles;
+        const int tap = tile / mn, r2 = tile - tap * mn;
+        const int mt = r2 / g.ntiles, nt = r2 - mt * g.ntiles;
+        const int lane = tid & 63, wave = tid >> 6;
+        const int wm = wave / WN, wn = wave % WN;
+        const int i = ij >> 2, j = ij & 3;
+        const int ci = nt * BN + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int co = mt * BM + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
+            float v = s[r];
+            if (out_f32) {
+                float *d = static_cast<float *>(dw) + e;
+                *d = accumulate ? *d + v : v;
+            } else {
+                uint16_t *d = static_cast<uint16_t *>(dw) + e;
+                if (accumulate) v += bf16_to_f32(*d);
+                *d = f32_to_bf16(v);
+            }
+        }
+    }
+}
+
+struct Tile {
+    int wm, wn;
+};
+// variant -> tile (co x ci): 0 128x128, 1 128x64, 2 64x128, 3 64x64, 4 256x128, 5 128x256
+constexpr Tile kTiles[] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}, {4, 2}, {2, 4}};
+constexpr int kNumVariants = 6;
+
+uint64_t magic40(int d) { return (uint64_t(1) << 40) / static_cast<uint64_t>(d) + 1; }
+
+WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const WgradPlan &plan) {
+    WGeo g;
+    const int pad = (ks - 1) / 2;
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
+    g.OH = (H + 2 * pad - ks) / stride + 1;
+    g.OW = (W + 2 * pad - ks) / stride + 1;
+    g.HW = g.OH * g.OW;
+    g.P = N * g.HW;
+    g.m_hw = magic40(g.HW);
+    g.m_ow = magic40(g.OW);
+    const Tile t = kTiles[plan.variant];
+    g.mtiles = Cout / (64 * t.wm);
+    g.ntiles = Cin / (64 * t.wn);
+    g.taps = ks * ks;
+    g.tiles = g.mtiles * g.ntiles * g.taps;
+    g.splits = plan.splits;
+    g.kps = plan.kps;
+    return g;
+}
+
+template <int KS, int S, int WM, int WN>
+void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, const WGeo &g, bool out_f32,
+              bool accumulate, bool atomic_out, hipStream_t s) {
+    // 3-deep global_load_lds ring (tools/bench_wgrad.py --sweep: 2 stages starve the 8-wave
+    // 256x128 tiles, 4 stages cost the 1-2 wave tiles their second/third workgroup per CU)
+    constexpr int STAGES = 3;
+    wgrad_kernel<KS, S, WM, WN, STAGES><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
+        dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out);
+    if (g.splits > 1 && !atomic_out) {
+        const int64_t total = static_cast<int64_t>(g.tiles) * (64 * WM) * (64 * WN) / 4;
+        int sgl = 0;  // split groups: enough blocks for the chip, at most 64 groups, <= splits
+        while (sgl < 6 && (2 << sgl) <= g.splits && (total << (sgl + 1)) <= int64_t(256) * 2048) ++sgl;
+        const int64_t grid = (total + (256 >> sgl) - 1) / (256 >> sgl);
+        wgrad_reduce_kernel<WM, WN><<<static_cast<int>(grid), 256, 0, s>>>(part, dw, g, out_f32, accumulate, sgl);
+    }
+}
+
+template <int KS, int S>
+void launch_ks(const uint16_t *dy, const uint16_t *x, void *dw, float *part, const WGeo &g, int variant,
+               bool out_f32, bool accumulate, bool atomic_out, hipStream_t s) {
+    switch (variant) {
+    case 0: launch_t<KS, S, 2, 2>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    case 1: launch_t<KS, S, 2, 1>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    case 2: launch_t<KS, S, 1, 2>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    case 3: launch_t<KS, S, 1, 1>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    case 4: launch_t<KS, S, 4, 2>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    default: launch_t<KS, S, 2, 4>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    }
+}
+
+}  // namespace
+
+int conv_wgrad_variants() { return kNumVariants; }
+
+bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride) {
+    return (ks == 1 || ks == 3) && (stride == 1 || stride == 2) && Cin % 64 == 0 && Cout % 64 == 0 && Cin >= 64 &&
+           Cout >= 64;
+}
+
+WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
+    WgradPlan pl;
+    const int64_t work = static_cast<int64_t>(Cin) * Cout * ks * ks;
+    if (variant < 0) {
+        // tools/bench_wgrad.py --sweep (profiles/README.md): 8-wave 256x128 tiles once the
+        // GEMM is big enough, else the largest 4/2/1-wave tile the channel counts allow
+        if (Cout % 256 == 0 && Cin % 128 == 0 && work >= 131072) variant = 4;
+        else if (Cout % 128 == 0 && Cin % 256 == 0 && work >= 131072) variant = 5;
+        else if (Cout % 128 == 0 && Cin % 128 == 0) variant = 0;
+        else if (Cout % 128 == 0) variant = 1;
+        else if (Cin % 128 == 0) variant = 2;
+        else variant = 3;
+    }
+    const Tile t = kTiles[variant];
+    if (Cout % (64 * t.wm) != 0 || Cin % (64 * t.wn) != 0) throw std::invalid_argument("conv_wgrad: tile/channel mismatch");
+    pl.variant = variant;
+    const int pad = (ks - 1) / 2;
+    const int OH = (H + 2 * pad - ks) / stride + 1, OW = (W + 2 * pad - ks) / stride + 1;
+    const int64_t P = static_cast<int64_t>(N) * OH * OW;
+    const int ksteps = static_cast<int>((P + kBK - 1) / kBK);
+    const int tiles = (Cout / (64 * t.wm)) * (Cin / (64 * t.wn)) * ks * ks;
+    if (splits < 0) {
+        // workgroups per launch: one per CU for the 4/8-wave tiles (2 for 3x3), more for the
+        // 1-2 wave tiles, so every CU keeps >= ~48 KB of loads in flight; >= 4 K-steps per split
+        const int nw = t.wm * t.wn;
+        int target = 256 * (nw >= 4 ? 1 : 2);
+        if (ks == 3) target *= nw == 1 ? 4 : 2;
+        splits = (target + tiles / 2) / tiles;
+        splits = std::max(1, std::min(splits, ksteps / 4));
+    }
+    splits = std::max(1, std::min(splits, ksteps));
+    pl.kps = (ksteps + splits - 1) / splits;
+    pl.splits = (ksteps + pl.kps - 1) / pl.kps;  // no empty split
+    pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * tiles * (64 * t.wm) * (64 * t.wn) : 0;
+    return pl;
+}
+
+void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W, int Cin,
+                       int Cout, int ks, int stride, const WgradPlan &plan, bool out_f32, bool accumulate,
+                       hipStream_t s) {
+    // split-K accumulating into an f32 destination: every split adds its tile with atomics
+    const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
+    if (!conv_wgrad_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: unsupported shape");
+    const WGeo g = make_geo(N, H, W, Cin, Cout, ks, stride, plan);
+    if (static_cast<int64_t>(g.P) * g.HW >= (int64_t(1) << 40) || g.P >= (1 << 23))
+        throw std::invalid_argument("conv_wgrad: too many pixels for the 40-bit division");
+    if (g.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad: split-K needs the workspace");
+    if (ks == 1) {
+        if (stride == 1) launch_ks<1, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else launch_ks<1, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+    } else {
+        if (stride == 1) launch_ks<3, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else launch_ks<3, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+    }
+}
+
+}  // namespace kfk

@@ -120,6 +120,24 @@ void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin,
 // wt[ci,kh,kw,co] = w[co,2-kh,2-kw,ci]: stride-1 data gradient = conv3x3(dy, wt).
 void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s);
 
+// Weight gradient of the KS x KS (pad (KS-1)/2, stride 1|2) NHWC convolution as a split-K
+// MFMA GEMM (conv_wgrad.hip): dw[co, kh, kw, ci] = sum_p dy[p, co] * x[pix(p, kh, kw), ci].
+// dw: bf16 (out_f32 = 0) or f32 (out_f32 = 1), [Cout][KS*KS][Cin]; accumulate: dw += result.
+// part: f32 workspace of conv_wgrad_workspace(...) floats (unused when that is 0).
+struct WgradPlan {
+    int variant = 0;  // tile choice
+    int splits = 1;   // K (pixel) splits
+    int kps = 0;      // K-steps per split
+    int64_t ws_floats = 0;
+};
+bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride);
+WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant = -1,
+                          int splits = -1);
+void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W, int Cin,
+                       int Cout, int ks, int stride, const WgradPlan &plan, bool out_f32, bool accumulate,
+                       hipStream_t s);
+int conv_wgrad_variants();
+
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
 struct BNShape {

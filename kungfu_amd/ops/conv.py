@@ -7,10 +7,12 @@
 * data gradient, stride 1: the same kernel on the flipped/transposed weights
   (``dx = conv3x3(dy, w')``, ``w'[ci,co,kh,kw] = w[co,ci,2-kh,2-kw]``);
   stride 2: MIOpen (``aten.convolution_backward``);
-* weight gradient: MIOpen.
+* weight gradient: the split-K MFMA kernel (csrc/kernels/conv_wgrad.hip, ``wgrad`` below,
+  also used by the fused bottleneck blocks) for 1x1 / 3x3, stride 1 / 2.
 
-Measured per ResNet-50 shape against MIOpen in ``tools/bench_conv3x3.py`` (profiles/README.md).
-Set ``KUNGFU_CONV3X3=0`` to route everything through MIOpen.
+Measured per ResNet-50 shape against MIOpen in ``tools/bench_conv3x3.py`` and
+``tools/bench_wgrad.py`` (profiles/README.md).  Set ``KUNGFU_CONV3X3=0`` to route the 3x3
+forward / data gradient through MIOpen, ``KUNGFU_WGRAD=0`` the weight gradients.
 """
 from __future__ import annotations
 
@@ -22,6 +24,32 @@ import torch.nn.functional as F
 from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_CONV3X3", "1") != "0"
+_WGRAD = os.environ.get("KUNGFU_WGRAD", "1") != "0"
+
+
+def set_wgrad_enabled(on: bool) -> bool:
+    """Turn the MFMA weight-gradient path on/off at run time; returns the previous setting."""
+    global _WGRAD
+    old, _WGRAD = _WGRAD, bool(on)
+    return old
+
+
+def _cl4(t: torch.Tensor) -> bool:
+    return t.dim() == 4 and t.dtype == torch.bfloat16 and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: int) -> torch.Tensor:
+    """Weight gradient of ``F.conv2d(x, w, stride=stride, padding=pad)`` (bf16, w's shape).
+
+    The MFMA split-K kernel for NHWC bf16 1x1 / 3x3 (pad (ks-1)/2) convolutions with
+    channel counts that are multiples of 64; MIOpen otherwise."""
+    ks = int(w.shape[2])
+    if (_WGRAD and x.is_cuda and _cl4(x) and _cl4(dy) and w.dim() == 4 and w.shape[3] == ks
+            and pad == (ks - 1) // 2 and hip_available()
+            and hip().conv_wgrad_supported(int(x.shape[1]), int(dy.shape[1]), ks, int(stride))):
+        return hip().conv_wgrad(dy, x, ks, int(stride))
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
 
 
 def set_enabled(on: bool) -> bool:
@@ -70,13 +98,11 @@ class _Conv3x3Fn(torch.autograd.Function):
         if need_dx and s == 1:
             dx = hip().conv3x3(dy, hip().conv3x3_flip_weight(w), 1)
             need_dx = False
-        if need_dx or need_dw:
-            gx, gw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
-                                                            [need_dx, need_dw, False])
-            if need_dx:
-                dx = gx
-            if need_dw:
-                dw = gw
+        if need_dw:
+            dw = wgrad(dy, x, w, s, 1)
+        if need_dx:
+            dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
         return dx, dw, None
 
 

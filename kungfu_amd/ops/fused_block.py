@@ -24,7 +24,7 @@ backward
   accumulates into the identity gradient produced by the BN3+add+ReLU backward
   (or into the downsample branch's data gradient) -- no elementwise add, no extra
   pass over the largest activation of the block;
-* weight gradients use MIOpen (``aten.convolution_backward`` weight-only);
+* weight gradients use the split-K MFMA kernel (``ops.conv.wgrad``, csrc/kernels/conv_wgrad.hip);
 * BN gamma/beta gradients go to the flat space's gradient sink when registered
   (parallel/mixed.py), conv weight gradients flow to the bf16 shadow views.
 
@@ -68,8 +68,9 @@ def _sums(bn, dev) -> torch.Tensor:
 
 
 def _wgrad(dy, x, w, stride, pad):
-    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
-                                               [False, True, False])[1]
+    from .conv import wgrad
+
+    return wgrad(dy, x, w, stride, pad)
 
 
 class _FlipCache:

@@ -290,6 +290,40 @@ def test_conv3x3_mfma_matches_torch(shape):
 
 
 @needs_gpu
+@pytest.mark.parametrize("shape", [(3, 64, 9, 11, 256, 1, 1), (2, 256, 14, 14, 64, 1, 1), (2, 128, 15, 13, 512, 1, 2),
+                                   (2, 64, 10, 12, 64, 3, 1), (3, 128, 9, 9, 256, 3, 2), (1, 512, 7, 7, 512, 3, 1),
+                                   (2, 192, 6, 5, 128, 3, 1)])
+def test_conv_wgrad_mfma_matches_torch(H, shape):
+    """Split-K MFMA weight gradient (every tile variant, several split counts, bf16 and
+    f32-accumulate outputs) vs the f32 torch weight gradient."""
+    N, C, Hh, Ww, K, ks, s = shape
+    pad = (ks - 1) // 2
+    torch.manual_seed(5)
+    x = torch.randn(N, C, Hh, Ww, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    OH, OW = (Hh + 2 * pad - ks) // s + 1, (Ww + 2 * pad - ks) // s + 1
+    dy = torch.randn(N, K, OH, OW, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, ks, ks), dy.float(), stride=s, padding=pad)
+    nrm = ref.norm()
+    for v in range(H.conv_wgrad_variants()):
+        try:
+            H.conv_wgrad_plan(N, Hh, Ww, C, K, ks, s, v, -1)
+        except Exception:
+            continue  # tile does not divide the channels
+        for sp in (1, 3, -1):
+            got = H.conv_wgrad(dy, x, ks, s, variant=v, splits=sp)
+            assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+            assert ((got.float() - ref).norm() / nrm).item() < 1e-2, (v, sp)
+    base = torch.randn(K, C, ks, ks, device="cuda").to(memory_format=torch.channels_last)
+    acc = base.clone()
+    H.conv_wgrad(dy, x, ks, s, out=acc, accumulate=True)
+    assert ((acc - base - ref).norm() / nrm).item() < 1e-4
+    from kungfu_amd.ops.conv import wgrad
+
+    w = torch.empty(K, C, ks, ks, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    assert ((wgrad(dy, x, w, s, pad).float() - ref).norm() / nrm).item() < 1e-2
+
+
+@needs_gpu
 def test_grad_accumulate_multi_tensor(H):
     """_hip.grad_accumulate (flat += bf16/f32 sources, batched tables) vs torch f32."""
     torch.manual_seed(3)
