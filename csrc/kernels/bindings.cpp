@@ -569,11 +569,19 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
 std::vector<at::Tensor> bn_pool_forward(at::Tensor x, at::Tensor weight, at::Tensor bias,
                                         c10::optional<at::Tensor> running_mean,
                                         c10::optional<at::Tensor> running_var, double momentum, double eps,
-                                        bool training, c10::optional<at::Tensor> num_batches) {
+                                        bool training, c10::optional<at::Tensor> num_batches,
+                                        c10::optional<at::Tensor> sums) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     const int H = static_cast<int>(x.size(2)), W = static_cast<int>(x.size(3));
     TORCH_CHECK(kfk::bn_pool_supported(sh, H, W), "bn_pool: unsupported shape");
+    double *sp = nullptr;
+    if (training && sums && sums->defined()) {
+        TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->numel() == 2 * C * kfk::kStatSlots &&
+                        sums->is_contiguous() && sums->device() == x.device(),
+                    "bn_pool: sums must be the conv epilogue's f64 [slots*2*C] workspace");
+        sp = sums->data_ptr<double>();
+    }
     auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
@@ -588,8 +596,85 @@ std::vector<at::Tensor> bn_pool_forward(at::Tensor x, at::Tensor weight, at::Ten
                                 arg.data_ptr<uint8_t>(), sh, H, W, training, b.rm, b.rv, static_cast<float>(momentum),
                                 static_cast<float>(eps), training ? partial.data_ptr<float>() : nullptr,
                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt,
-                                stream_of(x, 0));
+                                stream_of(x, 0), sp);
     return {yp, mean, invstd, coef, arg};
+}
+
+// ---- ResNet stem (stem.hip) ----
+// x [N, 3, H, W] channels_last bf16 -> [N, 4, H, W] channels_last (4th channel zero)
+at::Tensor stem_pad4(at::Tensor x) {
+    TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) && x.dim() == 4 &&
+                    x.size(1) == 3 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_pad4: x must be [N, 3, H, W] channels_last bf16/f32 on the GPU");
+    c10::DeviceGuard gd(x.device());
+    auto x4 = at::empty({x.size(0), 4, x.size(2), x.size(3)},
+                        x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+    const int64_t npix = x.size(0) * x.size(2) * x.size(3);
+    if (x.scalar_type() == at::kFloat)
+        kfk::launch_stem_pad4_f32(x.data_ptr<float>(), reinterpret_cast<uint16_t *>(x4.data_ptr()), npix,
+                                  stream_of(x, 0));
+    else
+        kfk::launch_stem_pad4(reinterpret_cast<const uint16_t *>(x.data_ptr()),
+                              reinterpret_cast<uint16_t *>(x4.data_ptr()), npix, stream_of(x, 0));
+    return x4;
+}
+
+// w [64, 3, 7, 7] channels_last bf16 -> packed [64, 224] (kh, kw<8, c<4), zero padded
+at::Tensor stem_pack_weight(at::Tensor w) {
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 &&
+                    w.size(2) == 7 && w.size(3) == 7 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_pack_weight: w must be [64, 3, 7, 7] channels_last bf16");
+    c10::DeviceGuard gd(w.device());
+    auto wp = at::empty({64, 224}, w.options());
+    kfk::launch_stem_pack_weight(reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                                 reinterpret_cast<uint16_t *>(wp.data_ptr()), stream_of(w, 0));
+    return wp;
+}
+
+// y = conv7x7s2p3(x, w) [N, 64, OH, OW] channels_last bf16; stats: BN sums workspace (f64 slots x 2 x 64)
+at::Tensor stem_forward(at::Tensor x4, at::Tensor wp, c10::optional<at::Tensor> stats) {
+    TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
+                    x4.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_forward: x4 must be [N, 4, H, W] channels_last bf16");
+    TORCH_CHECK(wp.scalar_type() == at::kBFloat16 && wp.numel() == 64 * 224 && wp.is_contiguous() &&
+                    wp.device() == x4.device(),
+                "stem_forward: wp must be the packed [64, 224] weights");
+    const int N = x4.size(0), H = x4.size(2), W = x4.size(3);
+    TORCH_CHECK(H >= 4 && W >= 4, "stem_forward: input too small");
+    double *sp = nullptr;
+    if (stats && stats->defined()) {
+        TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->numel() == 2 * 64 * kfk::kStatSlots &&
+                        stats->is_contiguous() && stats->device() == x4.device(),
+                    "stem_forward: stats must be a contiguous f64 [slots*2*64] tensor");
+        sp = stats->data_ptr<double>();
+    }
+    c10::DeviceGuard gd(x4.device());
+    auto y = at::empty({N, 64, kfk::stem_out(H), kfk::stem_out(W)},
+                       x4.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem_forward(reinterpret_cast<const uint16_t *>(x4.data_ptr()),
+                             reinterpret_cast<const uint16_t *>(wp.data_ptr()), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                             sp, N, H, W, stream_of(x4, 0));
+    return y;
+}
+
+// dw [64, 3, 7, 7] channels_last bf16 from dy [N, 64, OH, OW] and x4
+at::Tensor stem_wgrad(at::Tensor dy, at::Tensor x4, int64_t splits) {
+    TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
+                    x4.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_wgrad: x4 must be [N, 4, H, W] channels_last bf16");
+    const int N = x4.size(0), H = x4.size(2), W = x4.size(3);
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 64 &&
+                    dy.size(2) == kfk::stem_out(H) && dy.size(3) == kfk::stem_out(W) &&
+                    dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x4.device(),
+                "stem_wgrad: dy must be the [N, 64, OH, OW] channels_last bf16 output gradient");
+    c10::DeviceGuard gd(x4.device());
+    const int sp = splits > 0 ? static_cast<int>(splits) : kfk::stem_wgrad_splits(N, H, W);
+    auto part = at::empty({kfk::stem_wgrad_workspace(N, H, W, sp)}, x4.options().dtype(at::kFloat));
+    auto dw = at::empty({64, 3, 7, 7}, x4.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem_wgrad(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                           reinterpret_cast<const uint16_t *>(x4.data_ptr()), reinterpret_cast<uint16_t *>(dw.data_ptr()),
+                           part.data_ptr<float>(), N, H, W, sp, stream_of(x4, 0));
+    return dw;
 }
 
 // Returns (dx, dweight, dbias).
@@ -823,7 +908,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("bn_pool_forward", &bn_pool_forward,
           "stem BN+ReLU+MaxPool(3,2,1) forward -> (y_pool, mean, invstd, coef, argmax)", py::arg("x"),
           py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
-          py::arg("eps"), py::arg("training"), py::arg("num_batches") = py::none());
+          py::arg("eps"), py::arg("training"), py::arg("num_batches") = py::none(), py::arg("sums") = py::none());
+    m.def("stem_pad4", &stem_pad4, "[N,3,H,W] bf16/f32 -> [N,4,H,W] channels_last bf16 (zero 4th channel)");
+    m.def("stem_pack_weight", &stem_pack_weight, "[64,3,7,7] stem weights -> packed [64,224] for stem_forward");
+    m.def("stem_forward", &stem_forward, "7x7/2 pad-3 stem conv on MFMA with fused BN statistics",
+          py::arg("x4"), py::arg("wp"), py::arg("stats") = py::none());
+    m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient (split-K MFMA)", py::arg("dy"), py::arg("x4"),
+          py::arg("splits") = -1);
     m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)");
     m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
     m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");

@@ -753,9 +753,12 @@ bool bn_pool_supported(BNShape sh, int H, int W) {
 void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
                             BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
                             float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
-                            hipStream_t s) {
+                            hipStream_t s, double *sums) {
     const int C = sh.channels, cvec = C / 8;
-    if (training) {
+    if (training && sums) {
+        bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
+                                                         run_var, momentum, eps, coef, num_batches);
+    } else if (training) {
         launch_stats(x, sh, gamma, beta, run_mean, run_var, momentum, eps, partial, mean, invstd, coef, num_batches,
                      s);
     } else {

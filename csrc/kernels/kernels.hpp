@@ -138,6 +138,21 @@ void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *p
                        hipStream_t s);
 int conv_wgrad_variants();
 
+// ResNet stem: 7x7 stride-2 pad-3 convolution, 3 -> 64 channels, NHWC bf16 (stem.hip).
+// x4 = input padded to 4 channels; wp = weights packed [64][7 kh][8 kw][4 c] (zero padded).
+// stats (optional): kStatSlots x [2][64] f64 per-channel sum / sum of squares of the output.
+void launch_stem_pad4(const uint16_t *x, uint16_t *x4, int64_t npix, hipStream_t s);
+void launch_stem_pad4_f32(const float *x, uint16_t *x4, int64_t npix, hipStream_t s);  // + cast to bf16
+void launch_stem_pack_weight(const uint16_t *w, uint16_t *wp, hipStream_t s);
+int stem_out(int h);
+void launch_stem_forward(const uint16_t *x4, const uint16_t *wp, uint16_t *y, double *stats, int N, int H, int W,
+                         hipStream_t s);
+// dw [64][7][7][3] bf16; part: stem_wgrad_workspace(...) floats.
+int stem_wgrad_splits(int N, int H, int W);
+int64_t stem_wgrad_workspace(int N, int H, int W, int splits);
+void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
+                       int splits, hipStream_t s);
+
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
 struct BNShape {
@@ -171,7 +186,7 @@ bool bn_pool_supported(BNShape sh, int H, int W);
 void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
                             BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
                             float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
-                            hipStream_t s);
+                            hipStream_t s, double *sums = nullptr);
 void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,

@@ -1,0 +1,494 @@
+// ResNet stem convolution (7x7, stride 2, pad 3, 3 -> 64 channels, NHWC bf16) on CDNA4
+// matrix cores, for gfx950: forward with the following BN's batch statistics fused into the
+// epilogue, and the weight gradient.  (The stem input is the image: no data gradient.)
+//
+// Why: MIOpen ran this layer at ~80 TF/s (370 us forward + 354 us weight gradient + a 97 us
+// BN statistics pass per 256-image step, profiles/r12_*.md) because K = 3*7*7 = 147 fits no
+// library tiling.  Here the 3 input channels are padded to 4 (one 8-byte load per pixel,
+// ``stem_pad4``) and K is laid out (kh, kw, c) with kw padded to 8: one kh row of the
+// 7x7 window is 8 pixels x 4 channels = 32 bf16 = exactly one K-step of
+// v_mfma_f32_16x16x32_bf16, so the im2col is 7 K-steps of 8-byte pixel loads.  The padded
+// kw = 7 / c = 3 weights are zero (``stem_pack_weight``).
+//
+// Forward: 256-pixel x 64-channel tiles (4 waves, 64x64 wave tiles); a tile's whole
+// 7x8-pixel window is loaded into registers at once and staged into a double-buffered LDS
+// image (64-byte rows, 16-byte chunks XOR-swizzled by row so ds_read_b128 is conflict-free);
+// the packed weights sit in LDS (464-byte rows: conflict-free); the product is computed
+// transposed so the epilogue stores 4-channel bf16 quads straight from the accumulators and
+// reduces the per-channel sum / sum of squares with lane shuffles (f64 atomics into the BN's
+// slotted workspace, as conv.hip).
+// Weight gradient: split-K over pixels (64 pixels per K-step); operands read with the
+// transposing ds_read_b64_tr_b16 as in conv_wgrad.hip (dy image 128-byte rows, im2col
+// image 512-byte rows, 32-byte column groups XOR-swizzled), per-split f32 partial tiles
+// summed, unpacked to [64][7][7][3] and rounded by a second kernel.
+//
+// Reference parity: none (the reference trains tf.keras ResNet-50 with stock TF kernels,
+// benchmarks/system/benchmark_kungfu.py:96).
+#include "common.hpp"
+#include "kernels.hpp"
+
+#include <stdexcept>
+
+namespace kfk {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kKH = 7;           // window rows (one K-step each)
+constexpr int kKPad = 224;       // K = 7 kh x 8 kw x 4 c
+constexpr int kBRow = 464;       // LDS bytes per packed weight row (448 + 16)
+constexpr int kCout = 64;
+
+struct StemGeo {
+    int N, H, W, OH, OW, M;
+    uint64_t m_hw, m_ow;  // floor division magics (see conv_wgrad.hip)
+};
+
+__device__ __forceinline__ int fdiv(int p, uint64_t m) {
+    return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
+}
+
+__device__ __forceinline__ void unpack8(const uint4 &v, float (&f)[8]) {
+    const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        f[2 * k] = __uint_as_float(u[k] << 16);
+        f[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+    }
+}
+
+// x [P, 3] -> x4 [P, 4] (4th channel 0); two pixels per thread (12-byte aligned reads).
+__global__ void stem_pad4_kernel(const uint32_t *__restrict__ x, uint4 *__restrict__ x4, int64_t npairs,
+                                 const uint16_t *__restrict__ xtail, int64_t npix) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < npairs;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const uint32_t a = x[3 * i], b = x[3 * i + 1], c = x[3 * i + 2];
+        // a = (c0, c1) of p0, b = (c2 of p0, c0 of p1), c = (c1, c2) of p1
+        x4[i] = make_uint4(a, b & 0xffffu, (b >> 16) | (c << 16), c >> 16);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (npix & 1)) {  // odd pixel count: last pixel
+        const int64_t p = npix - 1;
+        uint16_t *o = reinterpret_cast<uint16_t *>(x4) + 4 * p;
+        o[0] = xtail[3 * p];
+        o[1] = xtail[3 * p + 1];
+        o[2] = xtail[3 * p + 2];
+        o[3] = 0;
+    }
+}
+
+// f32 input (the image before autocast): cast and pad in one pass, one pixel per thread.
+__global__ void stem_pad4_f32_kernel(const float *__restrict__ x, uint2 *__restrict__ x4, int64_t npix) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < npix;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const uint32_t c0 = f32_to_bf16(x[3 * i]), c1 = f32_to_bf16(x[3 * i + 1]), c2 = f32_to_bf16(x[3 * i + 2]);
+        x4[i] = make_uint2(c0 | (c1 << 16), c2);
+    }
+}
+
+// w [64][7][7][3] (channels_last [64, 3, 7, 7]) -> wp [64][7][8][4], zero padded.
+__global__ void stem_pack_weight_kernel(const uint16_t *__restrict__ w, uint16_t *__restrict__ wp) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < kCout * kKPad; i += gridDim.x * blockDim.x) {
+        const int co = i / kKPad, k = i - co * kKPad;
+        const int kh = k >> 5, kw = (k >> 2) & 7, c = k & 3;
+        wp[i] = (kw < 7 && c < 3) ? w[((co * 7 + kh) * 7 + kw) * 3 + c] : static_cast<uint16_t>(0);
+    }
+}
+
+// ---------------------------------------------------------------------------------- forward
+constexpr int kFwdBM = 256;
+constexpr int kAStage = kFwdBM * 64;  // 16 KB
+
+__device__ __forceinline__ int a_img_off(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// One 256-pixel x 64-channel tile per workgroup.  The MFMA computes the tile transposed
+// (A = weights: rows = output channels; B = im2col: columns = pixels), so each lane's
+// accumulator holds 4 consecutive channels of one pixel: stored as 8-byte bf16 quads
+// straight from registers (no LDS round trip; L2 merges the quads of a 128-byte pixel row).
+__global__ __launch_bounds__(256) void stem_fwd_kernel(const uint16_t *__restrict__ x4, const uint16_t *__restrict__ wp,
+                                                       uint16_t *__restrict__ y, double *__restrict__ stats,
+                                                       StemGeo g) {
+    constexpr int BM = kFwdBM, BN = kCout, NT = 256;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kAStage + kCout * kBRow];
+    uint8_t *bimg = lds + 2 * kAStage;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
+    const int mt = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + (orig >> 3);
+    const int m0 = mt * BM;
+
+    // packed weights -> LDS (once)
+    for (int q = tid; q < kCout * 28; q += NT) {
+        const int co = q / 28, c = q - co * 28;
+        *reinterpret_cast<uint4 *>(bimg + co * kBRow + c * 16) =
+            *reinterpret_cast<const uint4 *>(wp + co * kKPad + c * 8);
+    }
+
+    // A staging: thread -> window column kw = tid & 7, rows (tid >> 3) + 32 i
+    const int kw = tid & 7;
+    int off[8], woff[8];
+    uint32_t okm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = (tid >> 3) + 32 * i;
+        const int m = m0 + r;
+        woff[i] = a_img_off(r, kw >> 1) + 8 * (kw & 1);
+        off[i] = 0;
+        okm[i] = 0;
+        if (m < g.M) {
+            const int n = fdiv(m, g.m_hw);
+            const int rem = m - n * g.OH * g.OW;
+            const int oh = fdiv(rem, g.m_ow);
+            const int ow = rem - oh * g.OW;
+            const int ih0 = oh * 2 - 3, iw = ow * 2 - 3 + kw;
+            off[i] = ((n * g.H + ih0) * g.W + iw) * 4;
+            if (iw >= 0 && iw < g.W) {
+                uint32_t bits = 0;
+#pragma unroll
+                for (int kh = 0; kh < kKH; ++kh)
+                    if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H)) bits |= 1u << kh;
+                okm[i] = bits;
+            }
+        }
+    }
+    // all 7 window rows' loads issued up front: the K loop is 7 short steps
+    uint2 regs[kKH][8];
+#pragma unroll
+    for (int kh = 0; kh < kKH; ++kh)
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            regs[kh][i] = ((okm[i] >> kh) & 1u) ? *reinterpret_cast<const uint2 *>(x4 + (off[i] + kh * g.W * 4))
+                                               : make_uint2(0u, 0u);
+
+    f32x4 acc[4][4];  // [channel tile i][pixel tile j]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int kh = 0; kh < kKH; ++kh) {
+        uint8_t *abase = lds + (kh & 1) * kAStage;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *reinterpret_cast<uint2 *>(abase + woff[i]) = regs[kh][i];
+        __syncthreads();  // also orders this buffer's reuse: its previous readers passed the last barrier
+        bf16x8 wf[4], xf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = i * 16 + (lane & 15);
+            wf[i] = *reinterpret_cast<const bf16x8 *>(bimg + co * kBRow + 16 * (kh * 4 + (lane >> 4)));
+            const int m = wave * 64 + i * 16 + (lane & 15);
+            xf[i] = *reinterpret_cast<const bf16x8 *>(abase + a_img_off(m, lane >> 4));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[i], xf[j], acc[i][j], 0, 0, 0);
+    }
+
+    // ---- epilogue: lane holds channels 16 i + 4 (lane >> 4) + r of pixel wave*64 + 16 j + (lane & 15)
+    float s1[4][4], s2[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wave * 64 + j * 16 + (lane & 15);
+        if (m < g.M) {
+            uint16_t *dst = y + static_cast<int64_t>(m) * BN + (lane >> 4) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint16_t h[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    h[r] = f32_to_bf16(acc[i][j][r]);
+                    const float f = bf16_to_f32(h[r]);  // statistics of the stored (rounded) values
+                    s1[i][r] += f;
+                    s2[i][r] += f * f;
+                }
+                *reinterpret_cast<uint2 *>(dst + i * 16) =
+                    make_uint2(h[0] | (static_cast<uint32_t>(h[1]) << 16), h[2] | (static_cast<uint32_t>(h[3]) << 16));
+            }
+        }
+    }
+    if (stats) {
+        // sum over the 16 pixels of a lane group (lanes with equal lane >> 4), then over waves
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+                    s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+                }
+        __syncthreads();  // the A buffers are free: reuse as the [wave][2][64] reduction scratch
+        float *red = reinterpret_cast<float *>(lds);
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = i * 16 + (lane >> 4) * 4 + r;
+                    red[(wave * 2) * BN + co] = s1[i][r];
+                    red[(wave * 2 + 1) * BN + co] = s2[i][r];
+                }
+        }
+        __syncthreads();
+        if (tid < 2 * BN) {
+            const int which = tid / BN, co = tid % BN;
+            double t = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) t += red[(w * 2 + which) * BN + co];
+            atomicAdd(stats + (mt % kStatSlots) * 2 * BN + which * BN + co, t);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------- weight gradient
+constexpr int kBK = 64;               // pixels per K-step
+constexpr int kARow = 128;            // dy image: 64 channels
+constexpr int kIRow = 512;            // im2col image: 256 k (224 used)
+constexpr int kWStage = kBK * (kARow + kIRow);  // 40 KB
+
+template <int ROW>
+__device__ __forceinline__ int hswz(int row) {
+    if constexpr (ROW == 128) return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+    else return (row & 3) | (((row >> 3) & 1) << 2);  // 256- and 512-byte rows: 8 groups per bank row
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const uint8_t *p0, const uint8_t *p1) {
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p0));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4 *)(p1));
+    const s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// grid = splits; tile = 64 co x 256 k (wave w: k in [64w, 64w + 64); wave 3 uses k < 224 only)
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const uint16_t *__restrict__ dy,
+                                                         const uint16_t *__restrict__ x4, float *__restrict__ part,
+                                                         StemGeo g, int kps) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kWStage];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int split = blockIdx.x;
+    const int p_begin = split * kps * kBK;
+    int nsteps = (g.M - p_begin + kBK - 1) / kBK;
+    if (nsteps > kps) nsteps = kps;
+
+    // staging: dy rows (tid >> 2), 16-byte chunks 2 (tid & 3) + {0, 1};
+    //          im2col: pixel (tid >> 2), window slots q = (tid & 3) + 4 i (kh = q / 8, kw = q % 8)
+    const int spx = tid >> 2, ssub = tid & 3;
+    struct Regs {
+        uint4 d[2];
+        uint2 im[14];
+    };
+    auto gload = [&](Regs &R, int ks) {
+        const int p = p_begin + ks * kBK + spx;
+        const bool ok = p < g.M;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            R.d[u] = ok ? *reinterpret_cast<const uint4 *>(dy + static_cast<int64_t>(p) * kCout + (2 * ssub + u) * 8)
+                         : make_uint4(0u, 0u, 0u, 0u);
+        int n = 0, oh = 0, ow = 0;
+        if (ok) {
+            n = fdiv(p, g.m_hw);
+            const int rem = p - n * g.OH * g.OW;
+            oh = fdiv(rem, g.m_ow);
+            ow = rem - oh * g.OW;
+        }
+        const int ih0 = oh * 2 - 3, iw0 = ow * 2 - 3;
+        const int base = ((n * g.H + ih0) * g.W + iw0) * 4;
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
+            const bool in = ok && static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
+                            static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W);
+            R.im[i] = in ? *reinterpret_cast<const uint2 *>(x4 + (base + (kh * g.W + kw) * 4)) : make_uint2(0u, 0u);
+        }
+    };
+    auto swrite = [&](const Regs &R, int buf) {
+        uint8_t *ab = lds + buf * kWStage;
+        uint8_t *ib = ab + kBK * kARow;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = 2 * ssub + u;  // 16-byte chunk of the 128-byte row
+            const int grp = (c >> 1) ^ hswz<kARow>(spx);
+            *reinterpret_cast<uint4 *>(ab + spx * kARow + grp * 32 + (c & 1) * 16) = R.d[u];
+        }
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
+            const int byte = kh * 64 + kw * 8;  // k = kh*32 + kw*4 (+c) -> 2 bytes per k
+            const int grp = (byte >> 5) ^ hswz<kIRow>(spx);
+            *reinterpret_cast<uint2 *>(ib + spx * kIRow + grp * 32 + (byte & 31)) = R.im[i];
+        }
+    };
+
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int row0 = 8 * fg + fq;
+    int aoff[4], boff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        aoff[i] = row0 * kARow + 32 * (i ^ hswz<kARow>(row0)) + 8 * fp;
+        boff[i] = row0 * kIRow + 32 * ((wave * 4 + i) ^ hswz<kIRow>(row0)) + 8 * fp;
+    }
+    const int jmax = wave == 3 ? 2 : 4;
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int buf) {
+        const uint8_t *ab = lds + buf * kWStage;
+        const uint8_t *ib = ab + kBK * kARow;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 af[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                af[i] = tr_frag(ab + aoff[i] + 32 * s * kARow, ab + aoff[i] + (32 * s + 4) * kARow);
+                bfr[i] = tr_frag(ib + boff[i] + 32 * s * kIRow, ib + boff[i] + (32 * s + 4) * kIRow);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (j < jmax) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    Regs R;
+    if (nsteps > 0) {
+        gload(R, 0);
+        swrite(R, 0);
+    }
+    __syncthreads();
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if (ks + 1 < nsteps) gload(R, ks + 1);
+        compute(ks & 1);
+        if (ks + 1 < nsteps) swrite(R, (ks + 1) & 1);
+        __syncthreads();
+    }
+    // partial tile: part[split][co][k], k < 224
+    float *dst = part + static_cast<int64_t>(split) * kCout * kKPad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < jmax)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = i * 16 + (lane >> 4) * 4 + r;
+                    const int k = wave * 64 + j * 16 + (lane & 15);
+                    dst[co * kKPad + k] = acc[i][j][r];
+                }
+}
+
+// dw[co][kh][kw][c] (c < 3, kw < 7) = sum_s part[s][co][kh*32 + kw*4 + c]; block = 16 outputs x 16 split groups
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float *__restrict__ part, int splits,
+                                                                uint16_t *__restrict__ dw) {
+    __shared__ float red[256];
+    const int t = threadIdx.x, o = t & 15, sg = t >> 4;
+    const int e = blockIdx.x * 16 + o;  // output element (co, kh, kw, c) in dw order
+    constexpr int NOUT = kCout * 7 * 7 * 3;
+    float s = 0.f;
+    int k = 0, co = 0;
+    if (e < NOUT) {
+        co = e / 147;
+        const int r = e - co * 147, kh = r / 21, r2 = r - kh * 21, kw = r2 / 3, c = r2 - kw * 3;
+        k = kh * 32 + kw * 4 + c;
+        for (int sp = sg; sp < splits; sp += 16) s += part[(static_cast<int64_t>(sp) * kCout + co) * kKPad + k];
+    }
+    red[t] = s;
+    __syncthreads();
+    if (sg == 0 && e < NOUT) {
+        for (int q = 1; q < 16; ++q) s += red[o + 16 * q];
+        dw[e] = f32_to_bf16(s);
+    }
+}
+
+uint64_t magic40(int d) { return (uint64_t(1) << 40) / static_cast<uint64_t>(d) + 1; }
+
+StemGeo make_geo(int N, int H, int W) {
+    StemGeo g;
+    g.N = N, g.H = H, g.W = W;
+    g.OH = (H + 6 - 7) / 2 + 1;
+    g.OW = (W + 6 - 7) / 2 + 1;
+    g.M = N * g.OH * g.OW;
+    g.m_hw = magic40(g.OH * g.OW);
+    g.m_ow = magic40(g.OW);
+    return g;
+}
+
+void check_geo(const StemGeo &g) {
+    if (g.M <= 0 || static_cast<int64_t>(g.M) * g.OH * g.OW >= (int64_t(1) << 40) ||
+        static_cast<int64_t>(g.N) * g.H * g.W * 4 >= (int64_t(1) << 31))
+        throw std::invalid_argument("stem: shape out of range");
+}
+
+}  // namespace
+
+void launch_stem_pad4(const uint16_t *x, uint16_t *x4, int64_t npix, hipStream_t s) {
+    const int64_t npairs = npix / 2;
+    int64_t grid = (npairs + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    stem_pad4_kernel<<<static_cast<int>(grid), 256, 0, s>>>(reinterpret_cast<const uint32_t *>(x),
+                                                            reinterpret_cast<uint4 *>(x4), npairs, x, npix);
+}
+
+void launch_stem_pad4_f32(const float *x, uint16_t *x4, int64_t npix, hipStream_t s) {
+    int64_t grid = (npix + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    if (grid < 1) grid = 1;
+    stem_pad4_f32_kernel<<<static_cast<int>(grid), 256, 0, s>>>(x, reinterpret_cast<uint2 *>(x4), npix);
+}
+
+void launch_stem_pack_weight(const uint16_t *w, uint16_t *wp, hipStream_t s) {
+    stem_pack_weight_kernel<<<(kCout * kKPad + 255) / 256, 256, 0, s>>>(w, wp);
+}
+
+int stem_out(int h) { return (h + 6 - 7) / 2 + 1; }
+
+void launch_stem_forward(const uint16_t *x4, const uint16_t *wp, uint16_t *y, double *stats, int N, int H, int W,
+                         hipStream_t s) {
+    const StemGeo g = make_geo(N, H, W);
+    check_geo(g);
+    const int grid = (g.M + kFwdBM - 1) / kFwdBM;
+    stem_fwd_kernel<<<grid, 256, 0, s>>>(x4, wp, y, stats, g);
+}
+
+int64_t stem_wgrad_workspace(int N, int H, int W, int splits) {
+    (void)N, (void)H, (void)W;
+    return static_cast<int64_t>(splits) * kCout * kKPad;
+}
+
+int stem_wgrad_splits(int N, int H, int W) {
+    const StemGeo g = make_geo(N, H, W);
+    const int ksteps = (g.M + kBK - 1) / kBK;
+    int splits = 512;
+    if (splits > ksteps) splits = ksteps;
+    return splits < 1 ? 1 : splits;
+}
+
+void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
+                       int splits, hipStream_t s) {
+    const StemGeo g = make_geo(N, H, W);
+    check_geo(g);
+    const int ksteps = (g.M + kBK - 1) / kBK;
+    if (splits < 1) splits = 1;
+    if (splits > ksteps) splits = ksteps;
+    const int kps = (ksteps + splits - 1) / splits;
+    splits = (ksteps + kps - 1) / kps;  // no empty split
+    stem_wgrad_kernel<<<splits, 256, 0, s>>>(dy, x4, part, g, kps);
+    stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
+}
+
+}  // namespace kfk

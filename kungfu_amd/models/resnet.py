@@ -22,6 +22,8 @@ from typing import Callable, List, Optional, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops import stem as stem_ops
+
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
@@ -158,11 +160,18 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.conv1(x)
-        if self._fused:
-            x = self.bn1.forward_pool(x)  # BN+ReLU+MaxPool(3,2,1) in one HIP pass
+        if self._fused and stem_ops.eligible(self.conv1, x):
+            # MFMA stem conv with the BN batch statistics in its epilogue (ops/stem.py),
+            # then BN+ReLU+MaxPool(3,2,1) in one HIP pass without a statistics pass
+            from ..ops.fused_block import _sums
+            from ..parallel.mixed import shadow
+
+            sums = _sums(self.bn1, x.device) if self.training else None
+            x = self.bn1.forward_pool(stem_ops.stem_conv(x, shadow(self.conv1.weight), sums), sums=sums)
+        elif self._fused:
+            x = self.bn1.forward_pool(self.conv1(x))  # BN+ReLU+MaxPool(3,2,1) in one HIP pass
         else:
-            x = self.maxpool(self.bn1(x))
+            x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -79,9 +79,9 @@ class _BNActFn(torch.autograd.Function):
 
 class _BNActPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training, nbt):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training, nbt, sums):
         y, mean, invstd, coef, arg = hip().bn_pool_forward(x, weight, bias, running_mean, running_var, momentum, eps,
-                                                           training, nbt)
+                                                           training, nbt, sums)
         ctx.save_for_backward(x, mean, invstd, weight, coef, arg)
         ctx.training = training
         ctx.direct = _direct(weight, bias)
@@ -92,7 +92,7 @@ class _BNActPoolFn(torch.autograd.Function):
         x, mean, invstd, weight, coef, arg = ctx.saved_tensors
         dx, dw, db = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training)
         dw, db = _param_grads(ctx, dw, db)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 def bn_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
@@ -113,12 +113,17 @@ def bn_act(x, weight, bias, running_mean, running_var, training: bool, momentum:
 
 
 def bn_act_pool(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
-                num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """maxpool3x3s2p1(relu(bn(x))) -- one HIP forward kernel pass, one gather backward."""
+                num_batches_tracked: Optional[torch.Tensor] = None, sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """maxpool3x3s2p1(relu(bn(x))) -- one HIP forward kernel pass, one gather backward.
+
+    ``sums``: batch statistics already accumulated by the producing conv's epilogue
+    (``ops.stem``), consumed and re-zeroed -- no statistics pass."""
     if (_fusable(x, None) and weight is not None and momentum is not None and
             hip().bn_pool_supported(x.shape[1], x.shape[2], x.shape[3])):
         return _BNActPoolFn.apply(x, weight, bias, running_mean, running_var, momentum, eps, training,
-                                  num_batches_tracked if training else None)
+                                  num_batches_tracked if training else None, sums if training else None)
+    if sums is not None:
+        sums.zero_()  # not consumed by the fallback below
     y = bn_act(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=True,
                num_batches_tracked=num_batches_tracked)
     return F.max_pool2d(y, 3, 2, 1)
@@ -140,11 +145,12 @@ class BatchNormAct2d(nn.BatchNorm2d):
         a, nbt = self._args()
         return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt)
 
-    def forward_pool(self, x):
-        """relu(bn(x)) followed by MaxPool2d(3, stride 2, padding 1), fused."""
+    def forward_pool(self, x, sums: Optional[torch.Tensor] = None):
+        """relu(bn(x)) followed by MaxPool2d(3, stride 2, padding 1), fused (``sums``: batch
+        statistics from the producing conv's epilogue)."""
         assert self.relu
         a, nbt = self._args()
-        return bn_act_pool(x, *a, num_batches_tracked=nbt)
+        return bn_act_pool(x, *a, num_batches_tracked=nbt, sums=sums if a[4] else None)
 
 
 class BatchNormAddAct2d(BatchNormAct2d):

@@ -1,0 +1,74 @@
+"""ResNet stem convolution (7x7, stride 2, pad 3, 3 -> 64) on the hand-written MFMA kernels
+of ``csrc/kernels/stem.hip``.
+
+``stem_conv(x, w, stats)`` computes ``F.conv2d(x, w, stride=2, padding=3)`` for an NHWC
+image batch (f32 or bf16, channels_last) and bf16 weights, and -- when ``stats`` (the
+following BN's f64 slotted sums workspace, ``fused_block._sums``) is given -- accumulates
+the BN batch statistics in the conv epilogue, so ``bn_pool_forward(..., sums=stats)`` skips
+its statistics pass.  The image is cast to bf16 and padded to 4 channels in one pass; the
+weight gradient is the split-K MFMA kernel; the image gets no gradient.
+
+Set ``KUNGFU_STEM=0`` to use MIOpen.  No reference counterpart (the reference trains
+``tf.keras.applications`` ResNet-50, ``benchmarks/system/benchmark_kungfu.py:96``).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from .._lib import hip, hip_available
+
+_ENABLED = os.environ.get("KUNGFU_STEM", "1") != "0"
+
+
+def set_enabled(on: bool) -> bool:
+    global _ENABLED
+    old, _ENABLED = _ENABLED, bool(on)
+    return old
+
+
+def eligible(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (_ENABLED and x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and not x.requires_grad):
+        return False
+    if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    # the output is bf16: only where the conv would compute in bf16 anyway (bf16 input or autocast)
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda") and
+                                          torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if not (conv.in_channels == 3 and conv.out_channels == 64 and conv.kernel_size == (7, 7)
+            and conv.stride == (2, 2) and conv.padding == (3, 3) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.padding_mode == "zeros"):
+        return False
+    return x.shape[2] >= 4 and x.shape[3] >= 4 and hip_available()
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stats):
+        H = hip()
+        x4 = H.stem_pad4(x)
+        wb = w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16)
+        if not wb.is_contiguous(memory_format=torch.channels_last):
+            wb = wb.contiguous(memory_format=torch.channels_last)
+        y = H.stem_forward(x4, H.stem_pack_weight(wb), stats)
+        ctx.save_for_backward(x4)
+        ctx.wdtype = w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x4,) = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dw = hip().stem_wgrad(dy, x4) if ctx.needs_input_grad[1] else None
+        if dw is not None and dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+        return None, dw, None
+
+
+def stem_conv(x: torch.Tensor, w: torch.Tensor, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv7x7/2 pad 3 of an NHWC image (f32/bf16) -> bf16 [N, 64, OH, OW] channels_last."""
+    return _StemFn.apply(x, w, stats)

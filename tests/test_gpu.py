@@ -324,6 +324,40 @@ def test_conv_wgrad_mfma_matches_torch(H, shape):
 
 
 @needs_gpu
+@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 37, 45), (1, 16, 9)])
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
+def test_stem_conv_matches_torch(H, shape, xdtype):
+    """MFMA stem 7x7/2 conv (pad-4 + cast, fused BN statistics) and its split-K weight
+    gradient vs f32 torch."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.stem import stem_conv
+
+    N, Hh, Ww = shape
+    torch.manual_seed(6)
+    x = torch.randn(N, 3, Hh, Ww, device="cuda").to(xdtype).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device="cuda") * 0.1).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.bfloat16().float(), w.float(), stride=2, padding=3)
+    stats = torch.zeros(H.conv_stat_slots * 2 * 64, dtype=torch.float64, device="cuda")
+    wr = w.detach().requires_grad_()
+    y = stem_conv(x, wr, stats)
+    assert y.shape == ref.shape and y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last)
+    assert ((y.float() - ref).norm() / ref.norm()).item() < 1e-2
+    st = stats.view(H.conv_stat_slots, 2, 64).sum(0)
+    yf = y.float()
+    assert torch.allclose(st[0], yf.sum((0, 2, 3)).double(), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[1], (yf * yf).sum((0, 2, 3)).double(), rtol=1e-3, atol=1e-2)
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    dref = torch.nn.grad.conv2d_weight(x.bfloat16().float(), w.shape, dy.float(), stride=2, padding=3)
+    assert wr.grad.shape == w.shape
+    assert ((wr.grad.float() - dref).norm() / dref.norm()).item() < 1e-2
+    for sp in (1, 7):
+        dw = H.stem_wgrad(dy, H.stem_pad4(x), sp)
+        assert ((dw.float() - dref).norm() / dref.norm()).item() < 1e-2
+
+
+@needs_gpu
 def test_grad_accumulate_multi_tensor(H):
     """_hip.grad_accumulate (flat += bf16/f32 sources, batched tables) vs torch f32."""
     torch.manual_seed(3)
