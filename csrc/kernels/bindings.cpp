@@ -704,6 +704,44 @@ std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Ten
     return {dx, dw, db};
 }
 
+// Fused stem backward (stem.hip): (dw [64,3,7,7] channels_last bf16, dgamma, dbeta) from the
+// pooled gradient of BN+ReLU+MaxPool over the stem conv output y.
+std::vector<at::Tensor> stem_backward(at::Tensor dyp, at::Tensor arg, at::Tensor y, at::Tensor fcoef, at::Tensor mean,
+                                      at::Tensor invstd, at::Tensor weight, at::Tensor x4, bool training,
+                                      int64_t splits) {
+    TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
+                    x4.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_backward: x4 must be [N, 4, H, W] channels_last bf16");
+    const int N = x4.size(0), H = x4.size(2), W = x4.size(3);
+    const int OH = kfk::stem_out(H), OW = kfk::stem_out(W);
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
+                    y.size(2) == OH && y.size(3) == OW && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    y.device() == x4.device(),
+                "stem_backward: y must be the [N, 64, OH, OW] channels_last bf16 conv output");
+    if (!dyp.is_contiguous(at::MemoryFormat::ChannelsLast)) dyp = dyp.contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(dyp.scalar_type() == at::kBFloat16 && dyp.dim() == 4 && dyp.size(0) == N && dyp.size(1) == 64 &&
+                    dyp.size(2) == kfk::pool_out(OH) && dyp.size(3) == kfk::pool_out(OW) && dyp.device() == x4.device(),
+                "stem_backward: dyp must be the pooled [N, 64, PH, PW] gradient");
+    TORCH_CHECK(arg.scalar_type() == at::kByte && arg.numel() == dyp.numel() && arg.is_contiguous(),
+                "stem_backward: bad argmax");
+    TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() >= 128 && mean.numel() == 64 &&
+                    invstd.numel() == 64 && weight.numel() == 64 && weight.scalar_type() == at::kFloat,
+                "stem_backward: BN tensors must be f32 [64] (fcoef [128])");
+    c10::DeviceGuard gd(x4.device());
+    const int sp = splits > 0 ? static_cast<int>(splits) : 512;
+    auto fopt = x4.options().dtype(at::kFloat);
+    auto ws = at::empty({kfk::stem_bwd_workspace(sp)}, fopt);
+    auto dg = at::empty({64}, fopt), db = at::empty({64}, fopt);
+    auto dw = at::empty({64, 3, 7, 7}, x4.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem_backward(reinterpret_cast<const uint16_t *>(dyp.data_ptr()), arg.data_ptr<uint8_t>(),
+                              reinterpret_cast<const uint16_t *>(y.data_ptr()), fcoef.data_ptr<float>(),
+                              mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(),
+                              reinterpret_cast<const uint16_t *>(x4.data_ptr()), N, H, W, training, sp,
+                              ws.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(),
+                              reinterpret_cast<uint16_t *>(dw.data_ptr()), stream_of(x4, 0));
+    return {dw, dg, db};
+}
+
 // ---- device model store: HIP IPC export / import ------------------------------------
 // A dedicated hipMalloc allocation (not a caching-allocator sub-block) so the
 // IPC handle maps exactly this buffer; peers open it and pull over xGMI with
@@ -913,6 +951,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("stem_pack_weight", &stem_pack_weight, "[64,3,7,7] stem weights -> packed [64,224] for stem_forward");
     m.def("stem_forward", &stem_forward, "7x7/2 pad-3 stem conv on MFMA with fused BN statistics",
           py::arg("x4"), py::arg("wp"), py::arg("stats") = py::none());
+    m.def("stem_backward", &stem_backward,
+          "fused stem backward: pool-gradient gather + BN backward + conv weight gradient -> (dw, dgamma, dbeta)",
+          py::arg("dyp"), py::arg("arg"), py::arg("y"), py::arg("fcoef"), py::arg("mean"), py::arg("invstd"),
+          py::arg("weight"), py::arg("x4"), py::arg("training") = true, py::arg("splits") = -1);
     m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient (split-K MFMA)", py::arg("dy"), py::arg("x4"),
           py::arg("splits") = -1);
     m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)");

@@ -31,6 +31,8 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <stdexcept>
+
 namespace kfk {
 
 namespace {
@@ -379,53 +381,61 @@ struct PoolGrad {
     const uint4 *dyp;  // [N, OH, OW, C]
     const uint2 *arg;  // [N, OH, OW, C] bytes
     int H, W, OH, OW;
+    uint64_t m_hw, m_w;  // floor(p / d) = (p * m) >> 40 (exact for p * d < 2^40): no integer division
+    // Raw = the up to 4 covering windows' argmax bytes and gradients, loaded branch-free
+    // (invalid candidates re-read window 0 and carry kk = 0xff, which no argmax byte equals),
+    // so fetch() only issues loads and several rows' gathers stay in flight together; get()
+    // does the compare-and-add once the data is needed.
     struct Raw {
-        float g[8];
+        uint2 am[4];
+        uint4 d[4];
+        uint32_t kk;  // 4 packed candidate window offsets (0..8, or 0xff)
     };
     __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) g[k] = r.g[k];
-    }
-    template <int CVEC>
-    __device__ __forceinline__ Raw fetch(int64_t i, int64_t row, int cv) const {
-        Raw r;
-        load<CVEC>(i, row, cv, r.g);
-        return r;
+        for (int k = 0; k < 8; ++k) g[k] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint32_t kk = (r.kk >> (8 * c)) & 0xffu;
+            float d[8];
+            unpack8(r.d[c], d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t ak = ((k < 4 ? r.am[c].x : r.am[c].y) >> (8 * (k & 3))) & 0xffu;
+                g[k] += ak == kk ? d[k] : 0.f;
+            }
+        }
     }
     // rows < 2^31 (checked on the host): 32-bit index math only.
     template <int CVEC>
-    __device__ __forceinline__ void load(int64_t /*i*/, int64_t row64, int cv, float (&g)[8]) const {
+    __device__ __forceinline__ Raw fetch(int64_t /*i*/, int64_t row64, int cv) const {
         const uint32_t row = static_cast<uint32_t>(row64);
         const uint32_t hw = static_cast<uint32_t>(H) * static_cast<uint32_t>(W);
-        const uint32_t n = row / hw;
+        const uint32_t n = static_cast<uint32_t>((static_cast<uint64_t>(row) * m_hw) >> 40);
         const uint32_t rem = row - n * hw;
-        const int h = static_cast<int>(rem / static_cast<uint32_t>(W));
+        const int h = static_cast<int>((static_cast<uint64_t>(rem) * m_w) >> 40);
         const int w = static_cast<int>(rem) - h * W;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) g[k] = 0.f;
+        // windows oh with 2 oh - 1 <= h <= 2 oh + 1: h >> 1 always, (h + 1) >> 1 when h is odd
         const int oh_lo = h >> 1, oh_hi = (h + 1) >> 1;
         const int ow_lo = w >> 1, ow_hi = (w + 1) >> 1;
+        Raw r;
+        r.kk = 0;
+        const uint32_t base = (n * OH) * OW;
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            const int oh = a ? oh_hi : oh_lo;
-            if ((a && oh_hi == oh_lo) || oh >= OH) continue;
-            const int kh = h + 1 - 2 * oh;
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int ow = b ? ow_hi : ow_lo;
-                if ((b && ow_hi == ow_lo) || ow >= OW) continue;
-                const uint32_t kk = static_cast<uint32_t>(kh * 3 + (w + 1 - 2 * ow));
-                const uint32_t o = ((n * OH + oh) * OW + ow) * CVEC + cv;
-                const uint2 am = arg[o];
-                float d[8];
-                unpack8(dyp[o], d);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
-                    if (ak == kk) g[k] += d[k];
-                }
-            }
+        for (int c = 0; c < 4; ++c) {
+            const int oh = (c & 2) ? oh_hi : oh_lo, ow = (c & 1) ? ow_hi : ow_lo;
+            const bool ok = (!(c & 2) || oh_hi != oh_lo) && (!(c & 1) || ow_hi != ow_lo) && oh < OH && ow < OW;
+            const uint32_t kk = ok ? static_cast<uint32_t>((h + 1 - 2 * oh) * 3 + (w + 1 - 2 * ow)) : 0xffu;
+            const uint32_t o = ((base + (ok ? oh : oh_lo) * OW + (ok ? ow : ow_lo)) * CVEC) + cv;
+            r.am[c] = arg[o];
+            r.d[c] = dyp[o];
+            r.kk |= kk << (8 * c);
         }
+        return r;
+    }
+    template <int CVEC>
+    __device__ __forceinline__ void load(int64_t i, int64_t row, int cv, float (&g)[8]) const {
+        get(fetch<CVEC>(i, row, cv), g);
     }
 };
 
@@ -780,8 +790,12 @@ void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                              hipStream_t s) {
+    const uint64_t m_hw = (uint64_t(1) << 40) / (static_cast<uint64_t>(H) * W) + 1;
+    const uint64_t m_w = (uint64_t(1) << 40) / static_cast<uint64_t>(W) + 1;
+    if (static_cast<uint64_t>(sh.rows) * H * W >= (uint64_t(1) << 40))
+        throw std::invalid_argument("bn_pool_backward: too many rows for the 40-bit division");
     PoolGrad pg{reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint2 *>(arg), H, W, pool_out(H),
-                pool_out(W)};
+                pool_out(W), m_hw, m_w};
     launch_backward_impl(pg, x, fcoef, nullptr, mean, invstd, gamma, sh, RM_COEF, training, partial, dgamma, dbeta,
                          coef, dx, nullptr, s);
 }

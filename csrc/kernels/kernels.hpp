@@ -152,6 +152,15 @@ int stem_wgrad_splits(int N, int H, int W);
 int64_t stem_wgrad_workspace(int N, int H, int W, int splits);
 void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
                        int splits, hipStream_t s);
+// Fused stem backward: given the pooled gradient dyp + argmax of BN+ReLU+MaxPool over the conv
+// output y (fcoef = forward [scale; shift]), write dgamma, dbeta of the BN and the conv weight
+// gradient dw [64][7][7][3] bf16 -- the BN input gradient is never materialised.
+// ws: stem_bwd_workspace(splits) floats.
+int64_t stem_bwd_workspace(int splits);
+void launch_stem_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *y, const float *fcoef,
+                          const float *mean, const float *invstd, const float *gamma, const uint16_t *x4, int N, int H,
+                          int W, bool training, int splits, float *ws, float *dgamma, float *dbeta, uint16_t *dw,
+                          hipStream_t s);
 
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.

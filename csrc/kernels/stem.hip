@@ -414,6 +414,296 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float *__r
     }
 }
 
+// ------------------------------------------------- fused backward: pool + BN + weight gradient
+// The stem's forward is conv -> BN(batch stats) -> ReLU -> MaxPool(3,2,1), and the image needs
+// no gradient, so the BN input gradient dx = k1*dz + k2*y + k3 (dz = ReLU'-gated gradient
+// scattered back through the pool argmax, y = conv output, k = per-channel BN-backward
+// coefficients that depend on sum(dz) and sum(dz*y)) is only ever consumed by the weight
+// gradient.  By linearity
+//     dW[co][k] = k1[co] * S1[co][k] + k2[co] * S2[co][k] + k3[co] * S3[k],
+//     S1 = sum_p dz[p] (x) A[p],   S2 = sum_p y[p] (x) A[p],   S3 = sum_p A[p]   (A = im2col row)
+// so ONE pass over the pixels gathers dz, accumulates sum(dz), sum(dz*y) and the three MFMA
+// products (S3 via a constant ones-row A fragment), and a tiny finalize applies the BN
+// backward -- dx (411 MB at batch 256) is never written nor re-read, and the separate BN
+// reduce / apply passes disappear.
+constexpr int kPart1 = kCout * kKPad;                      // S1 or S2 floats
+constexpr int kPartStride = 2 * kPart1 + kKPad + 2 * kCout;  // S1 | S2 | S3 | sum dz | sum dz*y
+
+__global__ __launch_bounds__(256) void stem_bwd_kernel(const uint16_t *__restrict__ dyp,
+                                                       const uint8_t *__restrict__ arg,
+                                                       const uint16_t *__restrict__ y,
+                                                       const float *__restrict__ fcoef,
+                                                       const uint16_t *__restrict__ x4, float *__restrict__ part,
+                                                       StemGeo g, int PH, int PW, int kps) {
+    constexpr int kA2 = kBK * kARow;                      // second A image (y) after the first (dz)
+    constexpr int kStage = 2 * kA2 + kBK * kIRow;         // 48 KB
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int split = blockIdx.x;
+    const int p_begin = split * kps * kBK;
+    int nsteps = (g.M - p_begin + kBK - 1) / kBK;
+    if (nsteps > kps) nsteps = kps;
+
+    // staging: pixel spx = tid >> 2; channels 16 ssub + [0, 16) (two 8-channel vectors);
+    //          im2col window slots q = ssub + 4 i (kh = q / 8, kw = q % 8)
+    const int spx = tid >> 2, ssub = tid & 3;
+    float sc[2][8], sh[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sc[u][k] = fcoef[16 * ssub + 8 * u + k];
+            sh[u][k] = fcoef[kCout + 16 * ssub + 8 * u + k];
+        }
+    float sdz[2][8], sdzy[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sdz[u][k] = sdzy[u][k] = 0.f;
+
+    struct Regs {
+        uint4 dz[2], yv[2];
+        uint2 im[14];
+    };
+    auto gload = [&](Regs &R, int ks) {
+        const int p = p_begin + ks * kBK + spx;
+        const bool ok = p < g.M;
+        int n = 0, h = 0, w = 0;
+        if (ok) {
+            n = fdiv(p, g.m_hw);
+            const int rem = p - n * g.OH * g.OW;
+            h = fdiv(rem, g.m_ow);
+            w = rem - h * g.OW;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int cv = 2 * ssub + u;
+            float gz[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) gz[k] = 0.f;
+            uint4 yq = make_uint4(0u, 0u, 0u, 0u);
+            if (ok) {
+                yq = *reinterpret_cast<const uint4 *>(y + static_cast<int64_t>(p) * kCout + cv * 8);
+                // pool windows (oh, ow) with 2 oh - 1 <= h <= 2 oh + 1 (same for w): the gradient
+                // of window o reaches this pixel iff its argmax is this pixel's window offset
+                const int oh_lo = h >> 1, oh_hi = (h + 1) >> 1, ow_lo = w >> 1, ow_hi = (w + 1) >> 1;
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const int oh = a ? oh_hi : oh_lo;
+                    if ((a && oh_hi == oh_lo) || oh >= PH) continue;
+                    const int kh = h + 1 - 2 * oh;
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        const int ow = b ? ow_hi : ow_lo;
+                        if ((b && ow_hi == ow_lo) || ow >= PW) continue;
+                        const uint32_t kk = static_cast<uint32_t>(kh * 3 + (w + 1 - 2 * ow));
+                        const int64_t o = ((static_cast<int64_t>(n) * PH + oh) * PW + ow) * kCout + cv * 8;
+                        const uint2 am = *reinterpret_cast<const uint2 *>(arg + o);
+                        float d[8];
+                        unpack8(*reinterpret_cast<const uint4 *>(dyp + o), d);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
+                            if (ak == kk) gz[k] += d[k];
+                        }
+                    }
+                }
+            }
+            float yf[8];
+            unpack8(yq, yf);
+            uint32_t pk[4];
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+                const float z0 = (yf[k] * sc[u][k] + sh[u][k]) > 0.f ? gz[k] : 0.f;
+                const float z1 = (yf[k + 1] * sc[u][k + 1] + sh[u][k + 1]) > 0.f ? gz[k + 1] : 0.f;
+                sdz[u][k] += z0;
+                sdz[u][k + 1] += z1;
+                sdzy[u][k] += z0 * yf[k];
+                sdzy[u][k + 1] += z1 * yf[k + 1];
+                pk[k >> 1] = static_cast<uint32_t>(f32_to_bf16(z0)) | (static_cast<uint32_t>(f32_to_bf16(z1)) << 16);
+            }
+            R.dz[u] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            R.yv[u] = yq;
+        }
+        const int ih0 = h * 2 - 3, iw0 = w * 2 - 3;
+        const int base = ((n * g.H + ih0) * g.W + iw0) * 4;
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
+            const bool in = ok && static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
+                            static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W);
+            R.im[i] = in ? *reinterpret_cast<const uint2 *>(x4 + (base + (kh * g.W + kw) * 4)) : make_uint2(0u, 0u);
+        }
+    };
+    auto swrite = [&](const Regs &R, int buf) {
+        uint8_t *a1 = lds + buf * kStage;
+        uint8_t *a2 = a1 + kA2;
+        uint8_t *ib = a2 + kA2;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = 2 * ssub + u;  // 16-byte chunk of the 128-byte row
+            const int o = spx * kARow + ((c >> 1) ^ hswz<kARow>(spx)) * 32 + (c & 1) * 16;
+            *reinterpret_cast<uint4 *>(a1 + o) = R.dz[u];
+            *reinterpret_cast<uint4 *>(a2 + o) = R.yv[u];
+        }
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
+            const int byte = kh * 64 + kw * 8;
+            const int grp = (byte >> 5) ^ hswz<kIRow>(spx);
+            *reinterpret_cast<uint2 *>(ib + spx * kIRow + grp * 32 + (byte & 31)) = R.im[i];
+        }
+    };
+
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int row0 = 8 * fg + fq;
+    int aoff[4], boff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        aoff[i] = row0 * kARow + 32 * (i ^ hswz<kARow>(row0)) + 8 * fp;
+        boff[i] = row0 * kIRow + 32 * ((wave * 4 + i) ^ hswz<kIRow>(row0)) + 8 * fp;
+    }
+    const int jmax = wave == 3 ? 2 : 4;
+    // ones-row A fragment: row 0 of the 16x32 operand all ones -> S3 = column sums of B
+    bf16x8 ones;
+    {
+        const short one = (lane & 15) == 0 ? static_cast<short>(0x3f80) : static_cast<short>(0);
+        const s16x8 v = {one, one, one, one, one, one, one, one};
+        ones = __builtin_bit_cast(bf16x8, v);
+    }
+    f32x4 acc1[4][4], acc2[4][4], acc3[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        acc3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc1[i][j] = acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto compute = [&](int buf) {
+        const uint8_t *a1 = lds + buf * kStage;
+        const uint8_t *a2 = a1 + kA2;
+        const uint8_t *ib = a2 + kA2;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bf16x8 f1[4], f2[4], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                f1[i] = tr_frag(a1 + aoff[i] + 32 * s * kARow, a1 + aoff[i] + (32 * s + 4) * kARow);
+                f2[i] = tr_frag(a2 + aoff[i] + 32 * s * kARow, a2 + aoff[i] + (32 * s + 4) * kARow);
+                bfr[i] = tr_frag(ib + boff[i] + 32 * s * kIRow, ib + boff[i] + (32 * s + 4) * kIRow);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (j < jmax) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[i], bfr[j], acc1[i][j], 0, 0, 0);
+                        acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[i], bfr[j], acc2[i][j], 0, 0, 0);
+                    }
+                    acc3[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[j], acc3[j], 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    Regs R;
+    if (nsteps > 0) {
+        gload(R, 0);
+        swrite(R, 0);
+    }
+    __syncthreads();
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if (ks + 1 < nsteps) gload(R, ks + 1);
+        compute(ks & 1);
+        if (ks + 1 < nsteps) swrite(R, (ks + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- partials of this split: S1, S2 [co][k < 224], S3 [k], sum dz, sum dz*y [co]
+    float *dst = part + static_cast<int64_t>(split) * kPartStride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < jmax)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = i * 16 + (lane >> 4) * 4 + r;
+                    const int k = wave * 64 + j * 16 + (lane & 15);
+                    dst[co * kKPad + k] = acc1[i][j][r];
+                    dst[kPart1 + co * kKPad + k] = acc2[i][j][r];
+                }
+    if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < jmax) dst[2 * kPart1 + wave * 64 + j * 16 + lane] = acc3[j][0];
+    }
+    // per-channel sums: the 64 pixel-threads of each channel group meet in LDS
+    float *red = reinterpret_cast<float *>(lds);  // [64 spx][2][64 ch]; the loop's last barrier passed
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = 16 * ssub + 8 * u + k;
+            red[(spx * 2) * kCout + c] = sdz[u][k];
+            red[(spx * 2 + 1) * kCout + c] = sdzy[u][k];
+        }
+    __syncthreads();
+    if (tid < 2 * kCout) {
+        const int which = tid / kCout, c = tid % kCout;
+        float t = 0.f;
+        for (int q = 0; q < kBK; ++q) t += red[(q * 2 + which) * kCout + c];
+        dst[2 * kPart1 + kKPad + which * kCout + c] = t;
+    }
+}
+
+// tot[e] = sum over splits of part[split][e]; block = 16 elements x 16 split groups
+__global__ __launch_bounds__(256) void stem_bwd_fold_kernel(const float *__restrict__ part, int splits,
+                                                            float *__restrict__ tot) {
+    __shared__ float red[256];
+    const int t = threadIdx.x, o = t & 15, sg = t >> 4;
+    const int e = blockIdx.x * 16 + o;
+    float s = 0.f;
+    if (e < kPartStride)
+        for (int sp = sg; sp < splits; sp += 16) s += part[static_cast<int64_t>(sp) * kPartStride + e];
+    red[t] = s;
+    __syncthreads();
+    if (sg == 0 && e < kPartStride) {
+        for (int q = 1; q < 16; ++q) s += red[o + 16 * q];
+        tot[e] = s;
+    }
+}
+
+// BN backward coefficients per channel (as bn.hip's bn_bwd_finalize) and
+// dW[co][kh][kw][c] = k1 S1 + k2 S2 + k3 S3, rounded to bf16 in [64][7][7][3] order.
+__global__ __launch_bounds__(256) void stem_bwd_finalize_kernel(const float *__restrict__ tot,
+                                                                const float *__restrict__ mean,
+                                                                const float *__restrict__ invstd,
+                                                                const float *__restrict__ gamma, int64_t rows,
+                                                                int training, float *__restrict__ dgamma,
+                                                                float *__restrict__ dbeta, uint16_t *__restrict__ dw) {
+    const int co = blockIdx.x;
+    const double db = tot[2 * kPart1 + kKPad + co];
+    const double sxy = tot[2 * kPart1 + kKPad + kCout + co];
+    const double dg = static_cast<double>(invstd[co]) * (sxy - static_cast<double>(mean[co]) * db);
+    if (threadIdx.x == 0) {
+        dgamma[co] = static_cast<float>(dg);
+        dbeta[co] = static_cast<float>(db);
+    }
+    const float a = (gamma ? gamma[co] : 1.f) * invstd[co];
+    float k2 = 0.f, k3 = 0.f;
+    if (training) {
+        const float inv_m = 1.f / static_cast<float>(rows);
+        k2 = -a * static_cast<float>(dg) * invstd[co] * inv_m;
+        k3 = -a * static_cast<float>(db) * inv_m - k2 * mean[co];
+    }
+    for (int e = threadIdx.x; e < 147; e += blockDim.x) {
+        const int kh = e / 21, r2 = e - kh * 21, kw = r2 / 3, c = r2 - kw * 3;
+        const int k = kh * 32 + kw * 4 + c;
+        const float v = a * tot[co * kKPad + k] + k2 * tot[kPart1 + co * kKPad + k] + k3 * tot[2 * kPart1 + k];
+        dw[co * 147 + e] = f32_to_bf16(v);
+    }
+}
+
 uint64_t magic40(int d) { return (uint64_t(1) << 40) / static_cast<uint64_t>(d) + 1; }
 
 StemGeo make_geo(int N, int H, int W) {
@@ -489,6 +779,28 @@ void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, flo
     splits = (ksteps + kps - 1) / kps;  // no empty split
     stem_wgrad_kernel<<<splits, 256, 0, s>>>(dy, x4, part, g, kps);
     stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
+}
+
+
+int64_t stem_bwd_workspace(int splits) { return static_cast<int64_t>(splits + 1) * kPartStride; }
+
+void launch_stem_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *y, const float *fcoef,
+                          const float *mean, const float *invstd, const float *gamma, const uint16_t *x4, int N, int H,
+                          int W, bool training, int splits, float *ws, float *dgamma, float *dbeta, uint16_t *dw,
+                          hipStream_t s) {
+    const StemGeo g = make_geo(N, H, W);
+    check_geo(g);
+    const int PH = pool_out(g.OH), PW = pool_out(g.OW);
+    const int ksteps = (g.M + kBK - 1) / kBK;
+    if (splits < 1) splits = 1;
+    if (splits > ksteps) splits = ksteps;
+    const int kps = (ksteps + splits - 1) / splits;
+    splits = (ksteps + kps - 1) / kps;  // no empty split
+    float *tot = ws + static_cast<int64_t>(splits) * kPartStride;
+    stem_bwd_kernel<<<splits, 256, 0, s>>>(dyp, arg, y, fcoef, x4, ws, g, PH, PW, kps);
+    stem_bwd_fold_kernel<<<(kPartStride + 15) / 16, 256, 0, s>>>(ws, splits, tot);
+    stem_bwd_finalize_kernel<<<kCout, 256, 0, s>>>(tot, mean, invstd, gamma, g.M, training ? 1 : 0, dgamma, dbeta,
+                                                   dw);
 }
 
 }  // namespace kfk

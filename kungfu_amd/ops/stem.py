@@ -21,6 +21,9 @@ import torch
 from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_STEM", "1") != "0"
+# One-pass fused stem backward (``_StemBlockFn``); off by default until it beats the layered
+# BN-pool backward + weight-gradient kernels (tools/bench_stem.py).
+FUSED_BACKWARD = os.environ.get("KUNGFU_STEM_FUSED_BWD", "0") == "1"
 
 
 def set_enabled(on: bool) -> bool:
@@ -72,3 +75,46 @@ class _StemFn(torch.autograd.Function):
 def stem_conv(x: torch.Tensor, w: torch.Tensor, stats: Optional[torch.Tensor] = None) -> torch.Tensor:
     """conv7x7/2 pad 3 of an NHWC image (f32/bf16) -> bf16 [N, 64, OH, OW] channels_last."""
     return _StemFn.apply(x, w, stats)
+
+
+class _StemBlockFn(torch.autograd.Function):
+    """maxpool3x3s2p1(relu(bn(conv7x7s2p3(x)))) as ONE autograd node: the backward is the
+    fused stem kernel (pool-gradient gather + BN backward + conv weight gradient in one pass,
+    ``stem.hip: stem_bwd_kernel``) -- the BN input gradient is never materialised."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, running_mean, running_var, momentum, eps, training, nbt, sums):
+        from .fused_bn import _direct
+
+        H = hip()
+        x4 = H.stem_pad4(x)
+        wb = w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16)
+        if not wb.is_contiguous(memory_format=torch.channels_last):
+            wb = wb.contiguous(memory_format=torch.channels_last)
+        st = sums if training else None
+        y = H.stem_forward(x4, H.stem_pack_weight(wb), st)
+        yp, mean, invstd, coef, arg = H.bn_pool_forward(y, gamma, beta, running_mean, running_var, momentum, eps,
+                                                         training, nbt, st)
+        ctx.save_for_backward(x4, y, mean, invstd, gamma, coef, arg)
+        ctx.training = training
+        ctx.wdtype = w.dtype
+        ctx.direct = _direct(gamma, beta)
+        return yp
+
+    @staticmethod
+    def backward(ctx, dyp):
+        from .fused_bn import _param_grads
+
+        x4, y, mean, invstd, gamma, coef, arg = ctx.saved_tensors
+        dw, dg, db = hip().stem_backward(dyp, arg, y, coef, mean, invstd, gamma, x4, ctx.training)
+        dg, db = _param_grads(ctx, dg, db)
+        if dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+        return None, dw, dg, db, None, None, None, None, None, None, None
+
+
+def stem_block(x: torch.Tensor, w: torch.Tensor, bn, sums: Optional[torch.Tensor]) -> torch.Tensor:
+    """ResNet stem ``maxpool(relu(bn(conv(x))))`` on the fused kernels; ``bn`` is the fused
+    ``BatchNormAct2d`` (its parameters, running statistics and ``num_batches_tracked``)."""
+    (gamma, beta, rm, rv, use_batch, momentum, eps), nbt = bn._args()
+    return _StemBlockFn.apply(x, w, gamma, beta, rm, rv, momentum, eps, use_batch, nbt, sums)

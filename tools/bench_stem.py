@@ -50,3 +50,24 @@ for sp in (128, 256, 512, 1024, 2048):
     t["ours wgrad splits=%d" % sp] = timeit(lambda: H_.stem_wgrad(dy, x4, sp))
 for k, v in t.items():
     print("%-28s %8.1f us" % (k, v))
+
+# fused backward (pool gather + BN backward + weight gradient) vs the layered HIP path
+from kungfu_amd.ops.fused_bn import BatchNormAct2d  # noqa: E402
+
+bn = BatchNormAct2d(64).cuda()
+st = torch.zeros(H_.conv_stat_slots * 2 * 64, dtype=torch.float64, device="cuda")
+yc = H_.stem_forward(x4, wp, st)
+yp, mean, invstd, coef, arg = H_.bn_pool_forward(yc, bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.1, 1e-5,
+                                                 True, None, st)
+dyp = torch.randn_like(yp)
+t2 = {
+    "layered: bn_pool_backward": timeit(lambda: H_.bn_pool_backward(dyp, arg, yc, mean, invstd, bn.weight, coef, True)),
+    "layered: + stem_wgrad": timeit(lambda: H_.stem_wgrad(H_.bn_pool_backward(dyp, arg, yc, mean, invstd, bn.weight, coef,
+                                                                              True)[0], x4)),
+    "fused stem_backward": timeit(lambda: H_.stem_backward(dyp, arg, yc, coef, mean, invstd, bn.weight, x4, True)),
+}
+for sp in (256, 512, 1024, 2048):
+    t2["fused splits=%d" % sp] = timeit(lambda: H_.stem_backward(dyp, arg, yc, coef, mean, invstd, bn.weight, x4, True,
+                                                                 sp))
+for k, v in t2.items():
+    print("%-28s %8.1f us" % (k, v))
