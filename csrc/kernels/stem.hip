@@ -53,6 +53,15 @@ __device__ __forceinline__ int fdiv(int p, uint64_t m) {
     return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
 }
 
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// two f32 -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32 on gfx950
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+    const bf16x2 v = __builtin_convertvector(f32x2{a, b}, bf16x2);
+    return __builtin_bit_cast(uint32_t, v);
+}
+
 __device__ __forceinline__ void unpack8(const uint4 &v, float (&f)[8]) {
     const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
 #pragma unroll
@@ -247,6 +256,213 @@ __global__ __launch_bounds__(256) void stem_fwd_kernel(const uint16_t *__restric
 #pragma unroll
             for (int w = 0; w < 4; ++w) t += red[(w * 2 + which) * BN + co];
             atomicAdd(stats + (mt % kStatSlots) * 2 * BN + which * BN + co, t);
+        }
+    }
+}
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads()'s fence also waits for every
+// outstanding global load and store (vmcnt(0)), which would drain the input-row prefetch
+// queue and the output stores at every row.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// ------------------------------------------------------------- forward, row-based formulation
+// One output row (n, oh) = 112 pixels x 64 channels reads 7 input rows (ih = 2 oh - 3 + kh);
+// consecutive output rows share 5 of them.  Each workgroup walks a run of output rows keeping
+// the input rows in a 16-slot LDS ring (2 new rows per output row, prefetched into registers
+// during the previous row's MFMAs), so every input pixel is loaded once per workgroup instead
+// of ~12 times (the 7x7 / stride-2 window overlap) as in the per-pixel im2col staging above.
+// An input row sits in its slot with 3 zero pixels on the left: the 16-byte operand of
+// (output pixel ow, window columns kw, kw + 1) then starts at pixel 2 ow + kw, 16-byte
+// aligned for the even kw an MFMA fragment starts at.
+constexpr int kRowPad = 3;
+constexpr int kRowPx = 232;                 // 3 + 224 + 5 (covers 2 * 111 + 7 + 3)
+constexpr int kRowBytes = kRowPx * 8;
+constexpr int kRing = 16;
+
+__global__ __launch_bounds__(512) void stem_fwd_rows_kernel(const uint16_t *__restrict__ x4,
+                                                            const uint16_t *__restrict__ wp,
+                                                            uint16_t *__restrict__ y, double *__restrict__ stats,
+                                                            StemGeo g, int rows_per_wg) {
+    constexpr int BN = kCout;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kCout * kBRow + kRing * kRowBytes];
+    uint8_t *bimg = lds;
+    uint8_t *ring = lds + kCout * kBRow;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int R = g.N * g.OH;
+    const int r_begin = blockIdx.x * rows_per_wg;
+    const int r_end = r_begin + rows_per_wg < R ? r_begin + rows_per_wg : R;
+
+    for (int q = tid; q < kCout * 28; q += 512) {
+        const int co = q / 28, c = q - co * 28;
+        *reinterpret_cast<uint4 *>(bimg + co * kBRow + c * 16) =
+            *reinterpret_cast<const uint4 *>(wp + co * kKPad + c * 8);
+    }
+    // row loader: thread t < kRowPx owns padded pixel t of a row (8 bytes)
+    const int px = tid - kRowPad;
+    const bool pxok = tid < kRowPx && px >= 0 && px < g.W;
+    // Loads are unconditional (clamped to a valid pixel) and masked only when stored: a load
+    // inside a branch makes the compiler drain the whole memory counter (vmcnt(0)) at the join,
+    // which would serialise the prefetch queue below.
+    const int pxc = px < 0 ? 0 : (px >= g.W ? g.W - 1 : px);
+    auto row_value = [&](int n, int ih) -> uint2 {
+        const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih);
+        return *reinterpret_cast<const uint2 *>(x4 + ((static_cast<int64_t>(n) * g.H + ihc) * g.W + pxc) * 4);
+    };
+    auto row_store = [&](int ih, uint2 v) {
+        const bool ok = pxok && ih >= 0 && ih < g.H;
+        if (!ok) v = make_uint2(0u, 0u);
+        if (tid < kRowPx) *reinterpret_cast<uint2 *>(ring + ((ih + kRing) & (kRing - 1)) * kRowBytes + tid * 8) = v;
+    };
+
+    // stats: lane holds channels 16 i + 4 (lane >> 4) + r
+    float s1[4][4], s2[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+
+    // the packed weights as MFMA A fragments, resident in registers for the whole run; their
+    // LDS image is then reused as the per-row output staging tile
+    uint8_t *cimg = bimg;
+    static_assert(128 * (kCout * 2 + 16) <= kCout * kBRow, "output row tile fits the weight image");
+    lds_barrier();
+    bf16x8 wf[kKH][4];
+#pragma unroll
+    for (int kh = 0; kh < kKH; ++kh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            wf[kh][i] = *reinterpret_cast<const bf16x8 *>(bimg + (i * 16 + (lane & 15)) * kBRow +
+                                                          16 * (kh * 4 + (lane >> 4)));
+
+    int n = 0, oh = 0;
+    if (r_begin < r_end) {
+        n = r_begin / g.OH;
+        oh = r_begin - n * g.OH;
+    }
+    // input-row queue: the two new rows of output row oh + d are loaded at row oh + d - 3
+    // (three rows of MFMA work hide the load latency) and stored into the ring at row oh + d - 1
+    constexpr int kAhead = 3;
+    uint2 q0a = make_uint2(0u, 0u), q0b = q0a, q1a = q0a, q1b = q0a, q2a = q0a, q2b = q0a;
+    bool fresh = true;
+    for (int r = r_begin; r < r_end; ++r) {
+        if (fresh) {
+#pragma unroll
+            for (int kh = 0; kh < kKH; ++kh) row_store(2 * oh - 3 + kh, row_value(n, 2 * oh - 3 + kh));
+            // queue: rows of output rows oh + 1 .. oh + kAhead - 1 (same image)
+            q0a = row_value(n, 2 * oh + 4);
+            q0b = row_value(n, 2 * oh + 5);
+            q1a = row_value(n, 2 * oh + 6);
+            q1b = row_value(n, 2 * oh + 7);
+            lds_barrier();
+        }
+        const bool next_same = r + 1 < r_end && oh + 1 < g.OH;
+        // issue the loads for output row oh + kAhead
+        // (beyond the run / image these are clamped loads that are never stored)
+        q2a = row_value(n, 2 * (oh + kAhead) + 2);
+        q2b = row_value(n, 2 * (oh + kAhead) + 3);
+        // 8 waves: wave w owns output pixels [16 w, 16 w + 16) of the row, all 64 channels
+        f32x4 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int ow_t0 = wave * 16;
+        const bool live = ow_t0 < g.OW;
+        if (live) {
+            // all 7 im2col fragments of the row first (one LDS latency), then the 28 MFMAs
+            bf16x8 xf[kKH];
+            int owr = ow_t0 + (lane & 15);
+            owr = owr < g.OW ? owr : g.OW - 1;  // padding columns: any in-row data, never stored
+#pragma unroll
+            for (int kh = 0; kh < kKH; ++kh)
+                xf[kh] = *reinterpret_cast<const bf16x8 *>(ring + ((2 * oh - 3 + kh + kRing) & (kRing - 1)) * kRowBytes +
+                                                           16 * (owr + (lane >> 4)));
+#pragma unroll
+            for (int kh = 0; kh < kKH; ++kh)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh][i], xf[kh], acc[i], 0, 0, 0);
+        }
+        // lane holds channels 16 i + 4 (lane >> 4) + [0, 4) of pixel ow: 8-byte quads into an
+        // LDS [ow][64 ch] row image, then full 128-byte pixel rows out with 16-byte stores
+        // (scattered 8-byte global stores cost 2x the whole kernel)
+        constexpr int CROW = BN * 2 + 16;
+        {
+            const int ow = ow_t0 + (lane & 15);
+            if (ow < g.OW) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    // v_cvt_pk_bf16_f32 (RNE, two values per instruction); statistics of the stored values
+                    const uint32_t lo = pack_bf16x2(acc[i][0], acc[i][1]);
+                    const uint32_t hi = pack_bf16x2(acc[i][2], acc[i][3]);
+                    const float f0 = __uint_as_float(lo << 16), f1 = __uint_as_float(lo & 0xffff0000u);
+                    const float f2 = __uint_as_float(hi << 16), f3 = __uint_as_float(hi & 0xffff0000u);
+                    s1[i][0] += f0;
+                    s1[i][1] += f1;
+                    s1[i][2] += f2;
+                    s1[i][3] += f3;
+                    s2[i][0] += f0 * f0;
+                    s2[i][1] += f1 * f1;
+                    s2[i][2] += f2 * f2;
+                    s2[i][3] += f3 * f3;
+                    *reinterpret_cast<uint2 *>(cimg + ow * CROW + (i * 16 + (lane >> 4) * 4) * 2) = make_uint2(lo, hi);
+                }
+            }
+        }
+        lds_barrier();
+        {
+            uint4 *dst = reinterpret_cast<uint4 *>(y + (static_cast<int64_t>(n) * g.OH + oh) * g.OW * BN);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int v = tid + 512 * u;
+                if (v < g.OW * 8) dst[v] = *reinterpret_cast<const uint4 *>(cimg + (v >> 3) * CROW + (v & 7) * 16);
+            }
+        }
+        if (next_same) {  // rows 2 oh + 4, 2 oh + 5 (output row oh + 1): not in this row's window
+            row_store(2 * oh + 4, q0a);
+            row_store(2 * oh + 5, q0b);
+        }
+        q0a = q1a;
+        q0b = q1b;
+        q1a = q2a;
+        q1b = q2b;
+        lds_barrier();
+        fresh = !next_same;
+        if (++oh == g.OH) {
+            oh = 0;
+            ++n;
+        }
+    }
+    if (stats) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    s1[i][q] += __shfl_xor(s1[i][q], o, 64);
+                    s2[i][q] += __shfl_xor(s2[i][q], o, 64);
+                }
+        float *red = reinterpret_cast<float *>(ring);  // the last barrier passed: ring is free
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int co = i * 16 + (lane >> 4) * 4 + q;
+                    red[(wave * 2) * BN + co] = s1[i][q];
+                    red[(wave * 2 + 1) * BN + co] = s2[i][q];
+                }
+        }
+        lds_barrier();
+        if (tid < 2 * BN) {
+            const int which = tid / BN, co = tid % BN;
+            double t = 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) t += red[(w * 2 + which) * BN + co];
+            atomicAdd(stats + (blockIdx.x % kStatSlots) * 2 * BN + which * BN + co, t);
         }
     }
 }
@@ -751,6 +967,16 @@ void launch_stem_forward(const uint16_t *x4, const uint16_t *wp, uint16_t *y, do
                          hipStream_t s) {
     const StemGeo g = make_geo(N, H, W);
     check_geo(g);
+    if (g.W <= kRowPx - 8 && g.OW <= 128) {
+        // row-based kernel: one 8-wave workgroup per CU (2 waves / SIMD), each a run of output
+        // rows (a whole 112-row image at batch 256)
+        const int R = g.N * g.OH;
+        int grid = R < 256 ? R : 256;
+        const int rpw = (R + grid - 1) / grid;
+        grid = (R + rpw - 1) / rpw;
+        stem_fwd_rows_kernel<<<grid, 512, 0, s>>>(x4, wp, y, stats, g, rpw);
+        return;
+    }
     const int grid = (g.M + kFwdBM - 1) / kFwdBM;
     stem_fwd_kernel<<<grid, 256, 0, s>>>(x4, wp, y, stats, g);
 }
