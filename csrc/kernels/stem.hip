@@ -345,25 +345,28 @@ __global__ __launch_bounds__(512) void stem_fwd_rows_kernel(const uint16_t *__re
     }
     // input-row queue: the two new rows of output row oh + d are loaded at row oh + d - 3
     // (three rows of MFMA work hide the load latency) and stored into the ring at row oh + d - 1
-    constexpr int kAhead = 3;
-    uint2 q0a = make_uint2(0u, 0u), q0b = q0a, q1a = q0a, q1b = q0a, q2a = q0a, q2b = q0a;
+    // (slots rotate by renaming in a loop unrolled by 3: step(A, B, C), step(B, C, A), ...;
+    // copying a register that a load is still filling would make the compiler wait for it)
+    struct Q {
+        uint2 a, b;
+    };
     bool fresh = true;
-    for (int r = r_begin; r < r_end; ++r) {
+    auto step = [&](int r, Q &qa, Q &qb, Q &qc) {
         if (fresh) {
 #pragma unroll
             for (int kh = 0; kh < kKH; ++kh) row_store(2 * oh - 3 + kh, row_value(n, 2 * oh - 3 + kh));
-            // queue: rows of output rows oh + 1 .. oh + kAhead - 1 (same image)
-            q0a = row_value(n, 2 * oh + 4);
-            q0b = row_value(n, 2 * oh + 5);
-            q1a = row_value(n, 2 * oh + 6);
-            q1b = row_value(n, 2 * oh + 7);
+            // queue: rows of output rows oh + 1, oh + 2 (same image)
+            qa.a = row_value(n, 2 * oh + 4);
+            qa.b = row_value(n, 2 * oh + 5);
+            qb.a = row_value(n, 2 * oh + 6);
+            qb.b = row_value(n, 2 * oh + 7);
             lds_barrier();
         }
         const bool next_same = r + 1 < r_end && oh + 1 < g.OH;
-        // issue the loads for output row oh + kAhead
+        // issue the loads for output row oh + 3
         // (beyond the run / image these are clamped loads that are never stored)
-        q2a = row_value(n, 2 * (oh + kAhead) + 2);
-        q2b = row_value(n, 2 * (oh + kAhead) + 3);
+        qc.a = row_value(n, 2 * oh + 8);
+        qc.b = row_value(n, 2 * oh + 9);
         // 8 waves: wave w owns output pixels [16 w, 16 w + 16) of the row, all 64 channels
         f32x4 acc[4];
 #pragma unroll
@@ -421,19 +424,23 @@ __global__ __launch_bounds__(512) void stem_fwd_rows_kernel(const uint16_t *__re
             }
         }
         if (next_same) {  // rows 2 oh + 4, 2 oh + 5 (output row oh + 1): not in this row's window
-            row_store(2 * oh + 4, q0a);
-            row_store(2 * oh + 5, q0b);
+            row_store(2 * oh + 4, qa.a);
+            row_store(2 * oh + 5, qa.b);
         }
-        q0a = q1a;
-        q0b = q1b;
-        q1a = q2a;
-        q1b = q2b;
         lds_barrier();
         fresh = !next_same;
         if (++oh == g.OH) {
             oh = 0;
             ++n;
         }
+    };
+    Q q0, q1, q2;
+    for (int r = r_begin; r < r_end; r += 3) {
+        step(r, q0, q1, q2);
+        if (r + 1 >= r_end) break;
+        step(r + 1, q1, q2, q0);
+        if (r + 2 >= r_end) break;
+        step(r + 2, q2, q0, q1);
     }
     if (stats) {
 #pragma unroll
@@ -627,6 +634,174 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float *__r
     if (sg == 0 && e < NOUT) {
         for (int q = 1; q < 16; ++q) s += red[o + 16 * q];
         dw[e] = f32_to_bf16(s);
+    }
+}
+
+// ------------------------------------------------------- weight gradient, row-based formulation
+// dW[co][kh*32 + kw*4 + c] = sum over output rows (n, oh) and pixels ow of
+//     dy[n, oh, ow, co] * x4[n, 2 oh - 3 + kh, 2 ow - 3 + kw, c]
+// Per output row: GEMM M = 64 co, N = 32 per kh, K = 112 ow (padded to 128).  7 waves, wave =
+// kh.  A = dy^T read with ds_read_b64_tr_b16 from the dy row image ([ow][64 co], 128-byte rows,
+// rows 112..127 zero); B = the stride-2 window of input row 2 oh - 3 + kh, read with the same
+// transposing read straight from the input-row ring (lane (q, p) of a 16-lane group supplies
+// pixel 2 (ow0 + q) + kw0 + p: 4 channels = 8 bytes) -- no im2col image at all.
+constexpr int kDyRow = 128 * kARow;  // dy row image: 128 ow x 128 B
+
+__global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__restrict__ dy,
+                                                              const uint16_t *__restrict__ x4,
+                                                              float *__restrict__ part, StemGeo g, int rows_per_wg) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kRowBytes + 2 * kDyRow];
+    uint8_t *ring = lds;
+    uint8_t *dyimg = lds + kRing * kRowBytes;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = kh
+    const int R = g.N * g.OH;
+    const int r_begin = blockIdx.x * rows_per_wg;
+    const int r_end = r_begin + rows_per_wg < R ? r_begin + rows_per_wg : R;
+
+    // zero both dy images once (rows >= OW stay zero: the K padding)
+    for (int v = tid; v < 2 * kDyRow / 16; v += 448)
+        reinterpret_cast<uint4 *>(dyimg)[v] = make_uint4(0u, 0u, 0u, 0u);
+
+    // input-row loader (as the forward): thread t < kRowPx owns padded pixel t
+    const int px = tid - kRowPad;
+    const bool pxok = tid < kRowPx && px >= 0 && px < g.W;
+    const int pxc = px < 0 ? 0 : (px >= g.W ? g.W - 1 : px);
+    auto row_value = [&](int n, int ih) -> uint2 {
+        const int ihc = ih < 0 ? 0 : (ih >= g.H ? g.H - 1 : ih);
+        return *reinterpret_cast<const uint2 *>(x4 + ((static_cast<int64_t>(n) * g.H + ihc) * g.W + pxc) * 4);
+    };
+    auto row_store = [&](int ih, uint2 v) {
+        const bool ok = pxok && ih >= 0 && ih < g.H;
+        if (!ok) v = make_uint2(0u, 0u);
+        if (tid < kRowPx) *reinterpret_cast<uint2 *>(ring + ((ih + kRing) & (kRing - 1)) * kRowBytes + tid * 8) = v;
+    };
+    // dy row loader: chunk v = tid + 448 u (u = 0, 1) of the OW x 8 16-byte chunks
+    auto dy_load = [&](int r, uint4 (&d)[2]) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(dy + static_cast<int64_t>(r) * g.OW * kCout);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            int v = tid + 448 * u;
+            v = v < g.OW * 8 ? v : g.OW * 8 - 1;  // clamped (masked at the store)
+            d[u] = src[v];
+        }
+    };
+    auto dy_store = [&](int buf, const uint4 (&d)[2]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int v = tid + 448 * u;
+            if (v < g.OW * 8) {
+                const int ow = v >> 3, c = v & 7;
+                *reinterpret_cast<uint4 *>(dyimg + buf * kDyRow + ow * kARow + ((c >> 1) ^ hswz<kARow>(ow)) * 32 +
+                                           (c & 1) * 16) = d[u];
+            }
+        }
+    };
+
+    // fragment addressing (transposing reads): lane = 16 fg + 4 fq + fp
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int row0 = 8 * fg + fq;
+    int aoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] = row0 * kARow + 32 * (i ^ hswz<kARow>(row0)) + 8 * fp;
+
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int n = 0, oh = 0;
+    if (r_begin < r_end) {
+        n = r_begin / g.OH;
+        oh = r_begin - n * g.OH;
+    }
+    // Prefetch queue, 3 output rows deep: slot A holds output row r + 1's two new input rows and
+    // dy row (stored into the ring / the other dy image at the end of row r), B row r + 2, and
+    // row r + 3's loads are issued into C.  The loop is unrolled by 3 and rotates the slots by
+    // renaming (step(A, B, C), step(B, C, A), step(C, A, B)): copying a register that a load is
+    // still filling would make the compiler wait for that load.
+    struct Q {
+        uint2 a, b;
+        uint4 d[2];
+    };
+    auto rclamp = [&](int rr) { return rr < R ? rr : R - 1; };
+    bool fresh = true;
+    int buf = 0;
+    auto step = [&](int r, Q &qa, Q &qb, Q &qc) {
+        if (fresh) {
+            uint4 dcur[2];
+            dy_load(r, dcur);
+            dy_load(rclamp(r + 1), qa.d);
+            dy_load(rclamp(r + 2), qb.d);
+#pragma unroll
+            for (int kh = 0; kh < kKH; ++kh) row_store(2 * oh - 3 + kh, row_value(n, 2 * oh - 3 + kh));
+            qa.a = row_value(n, 2 * oh + 4);
+            qa.b = row_value(n, 2 * oh + 5);
+            qb.a = row_value(n, 2 * oh + 6);
+            qb.b = row_value(n, 2 * oh + 7);
+            dy_store(buf, dcur);
+            lds_barrier();
+        }
+        const bool next_same = r + 1 < r_end && oh + 1 < g.OH;
+        qc.a = row_value(n, 2 * oh + 8);  // the new input rows of output row oh + 3
+        qc.b = row_value(n, 2 * oh + 9);
+        dy_load(rclamp(r + 3), qc.d);
+
+        if (wave < kKH) {
+            const int kh = wave;
+            const uint8_t *rowp = ring + ((2 * oh - 3 + kh + kRing) & (kRing - 1)) * kRowBytes;
+            const uint8_t *ab = dyimg + buf * kDyRow;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {  // 32 output pixels per substep
+                bf16x8 af[4], bfr[2];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) af[i] = tr_frag(ab + aoff[i] + 32 * s * kARow, ab + aoff[i] + (32 * s + 4) * kARow);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    // rows q: ow = 32 s + 8 fg + fq (+4); cols 4 fp: kw = 4 j + fp, channels 0..3
+                    int ow0 = 32 * s + 8 * fg + fq, ow1 = ow0 + 4;
+                    ow0 = ow0 < g.OW ? ow0 : g.OW - 1;  // K padding: dy rows are zero there
+                    ow1 = ow1 < g.OW ? ow1 : g.OW - 1;
+                    bfr[j] = tr_frag(rowp + (2 * ow0 + 4 * j + fp) * 8, rowp + (2 * ow1 + 4 * j + fp) * 8);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            }
+        }
+        if (next_same) {  // rows of output row oh + 1 and its dy row, into the free slots / buffer
+            row_store(2 * oh + 4, qa.a);
+            row_store(2 * oh + 5, qa.b);
+            dy_store(buf ^ 1, qa.d);
+        }
+        lds_barrier();
+        buf ^= 1;
+        fresh = !next_same;
+        if (++oh == g.OH) {
+            oh = 0;
+            ++n;
+        }
+    };
+    Q q0, q1, q2;
+    for (int r = r_begin; r < r_end; r += 3) {
+        step(r, q0, q1, q2);
+        if (r + 1 >= r_end) break;
+        step(r + 1, q1, q2, q0);
+        if (r + 2 >= r_end) break;
+        step(r + 2, q2, q0, q1);
+    }
+    // partial tile of this workgroup: part[blockIdx][co][k < 224]
+    if (wave < kKH) {
+        float *dst = part + static_cast<int64_t>(blockIdx.x) * kCout * kKPad;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int co = i * 16 + (lane >> 4) * 4 + q;
+                    dst[co * kKPad + wave * 32 + j * 16 + (lane & 15)] = acc[i][j][q];
+                }
     }
 }
 
@@ -989,7 +1164,7 @@ int64_t stem_wgrad_workspace(int N, int H, int W, int splits) {
 int stem_wgrad_splits(int N, int H, int W) {
     const StemGeo g = make_geo(N, H, W);
     const int ksteps = (g.M + kBK - 1) / kBK;
-    int splits = 512;
+    int splits = 256;  // the row-based kernel: one workgroup per CU (tools/bench_stem.py)
     if (splits > ksteps) splits = ksteps;
     return splits < 1 ? 1 : splits;
 }
@@ -998,6 +1173,17 @@ void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, flo
                        int splits, hipStream_t s) {
     const StemGeo g = make_geo(N, H, W);
     check_geo(g);
+    if (g.W <= kRowPx - 8 && g.OW <= 128) {
+        // row-based kernel: splits = workgroups, each a run of output rows
+        const int R = g.N * g.OH;
+        if (splits < 1) splits = 1;
+        if (splits > R) splits = R;
+        const int rpw = (R + splits - 1) / splits;
+        splits = (R + rpw - 1) / rpw;
+        stem_wgrad_rows_kernel<<<splits, 448, 0, s>>>(dy, x4, part, g, rpw);
+        stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
+        return;
+    }
     const int ksteps = (g.M + kBK - 1) / kBK;
     if (splits < 1) splits = 1;
     if (splits > ksteps) splits = ksteps;
