@@ -23,6 +23,8 @@ CATEGORIES = [
     ("conv MFMA 1x1 (ours)", r"kfk::.*conv_kernel<1,"),
     ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,"),
     ("conv weight flip (ours)", r"kfk::.*conv_flip"),
+    ("conv MFMA wgrad (ours)", r"kfk::.*wgrad"),
+    ("stem conv MFMA (ours)", r"kfk::.*stem"),
     ("optimizer/flat (ours)", r"kfk::"),
     ("rccl", r"ncclDevKernel|oneRankReduce|rccl"),
     ("casts", r"bfloat16tofloat32_copy|bfloat16_copy|float_to|copy_kernel"),
@@ -33,6 +35,13 @@ CATEGORIES = [
     ("batchnorm (torch/MIOpen)", r"batch_norm|BatchNorm|MIOpenBatchNorm"),
     ("other elementwise", r"elementwise|reduce_kernel"),
 ]
+
+
+def short_name(name: str) -> str:
+    """Kernel name without namespaces noise and its argument list."""
+    nm = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+    nm = re.sub(r"\(.*", "", nm)
+    return nm[:110]
 
 
 def categorize(name: str) -> str:
@@ -83,7 +92,7 @@ def main():
             c = categorize(nm)
             cat_t[c] += d
             cat_n[c] += 1
-            short = re.sub(r"\(.*", "", nm)[:110]
+            short = short_name(nm)
             kern_t[short] += d
             kern_n[short] += 1
     ms = lambda ns: ns / n / 1e6
