@@ -30,6 +30,13 @@ sys.path.insert(0, ROOT)
 
 BASELINE_PER_GPU = 5507.0 / 16  # KungFu S-SGD ResNet-50, global batch 4096 on 16 x V100
 METRIC = "images/sec/GPU ResNet-50 SynchronousSGD at 1/2/4/8 MI355X; scaling efficiency"
+# The reference's other sync-scalability panels (global batch 4096 on 16 x V100):
+# (metric, per-GPU baseline img/s) for --model; the headline (default) is ResNet-50.
+MODEL_BASELINES = {
+    "resnet50": (METRIC, BASELINE_PER_GPU),
+    "vgg16": ("images/sec/GPU VGG16 SynchronousSGD at 1/2/4/8 MI355X", 3330.0 / 16),
+    "inception_v3": ("images/sec/GPU InceptionV3 SynchronousSGD at 1/2/4/8 MI355X", 7426.0 / 16),
+}
 
 
 def _setup_env():
@@ -130,8 +137,9 @@ def main():
     dt_t = torch.tensor([dt], dtype=torch.float64)
     dt_max = float(kf.ops.all_reduce(dt_t, op="max")[0]) if size > 1 else dt
     value = a.batch * size * a.steps / dt_max
+    metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
     res = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 2),
         "unit": "images/sec (aggregate over n_gpus)",
         "n_gpus": size,
@@ -140,7 +148,7 @@ def main():
         "ms_per_step": round(1000 * dt_max / a.steps, 3),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / (BASELINE_PER_GPU * size), 3),
+        "vs_baseline": round(value / (base_per_gpu * size), 3) if base_per_gpu else None,
         "dtype": "bf16",
         "data": "synthetic (random 224x224x3 images, random labels; random-init weights)",
         "config": {
@@ -154,7 +162,7 @@ def main():
             "fused_bn_hip": bool(fused_bn),
             "bf16_shadow_weights": bool(a.bf16_shadow),
             "per_gpu_img_s": round(value / size, 2),
-            "baseline_per_gpu_img_s": round(BASELINE_PER_GPU, 1),
+            "baseline_per_gpu_img_s": round(base_per_gpu, 1) if base_per_gpu else None,
             "warmup_s": round(warm_s, 1),
             "final_loss": round(float(loss.detach()), 4),
         },

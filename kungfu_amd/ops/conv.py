@@ -25,6 +25,7 @@ from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_CONV3X3", "1") != "0"
 _WGRAD = os.environ.get("KUNGFU_WGRAD", "1") != "0"
+_WGRAD_MAX_PIXELS = 1 << 23  # output pixels per conv_wgrad launch (csrc/kernels/conv_wgrad.hip)
 
 
 def set_wgrad_enabled(on: bool) -> bool:
@@ -47,7 +48,18 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: 
     if (_WGRAD and x.is_cuda and _cl4(x) and _cl4(dy) and w.dim() == 4 and w.shape[3] == ks
             and pad == (ks - 1) // 2 and hip_available()
             and hip().conv_wgrad_supported(int(x.shape[1]), int(dy.shape[1]), ks, int(stride))):
-        return hip().conv_wgrad(dy, x, ks, int(stride))
+        n = int(x.shape[0])
+        per_img = int(dy.shape[2]) * int(dy.shape[3])
+        if n * per_img < _WGRAD_MAX_PIXELS:
+            return hip().conv_wgrad(dy, x, ks, int(stride))
+        # the kernel's pixel index math holds < 2^23 output pixels per launch: sum over batch
+        # chunks into one f32 gradient (e.g. VGG-16's 224x224 layers at 256 images per GPU)
+        step = max(1, (_WGRAD_MAX_PIXELS - 1) // per_img)
+        acc = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(
+            memory_format=torch.channels_last)
+        for i in range(0, n, step):
+            hip().conv_wgrad(dy[i:i + step], x[i:i + step], ks, int(stride), out=acc, accumulate=True)
+        return acc.to(torch.bfloat16)
     return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
 

@@ -46,3 +46,19 @@ def test_trace_report_native_and_python():
     assert r.returncode == 0, r.stdout
     for name in ["optimizer::apply", "user::scope", "session::all_reduce"]:
         assert "[trace] " + name in r.stdout, r.stdout
+
+
+def test_bench_model_baselines():
+    """bench.py's per-model metric and per-GPU baseline (BASELINE.md sync panels at
+    global batch 4096 on 16 x V100): ResNet-50 is the headline and the default."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "kf_bench", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.MODEL_BASELINES["resnet50"] == (b.METRIC, 5507.0 / 16)
+    assert abs(b.MODEL_BASELINES["vgg16"][1] - 208.1) < 0.1
+    assert abs(b.MODEL_BASELINES["inception_v3"][1] - 464.1) < 0.1
+    assert all("SynchronousSGD" in m for m, _ in b.MODEL_BASELINES.values())

@@ -330,6 +330,25 @@ def test_conv_wgrad_mfma_matches_torch(H, shape):
 
 
 @needs_gpu
+def test_conv_wgrad_batch_chunks(H, monkeypatch):
+    """Weight gradients past the kernel's per-launch pixel limit (VGG-16's 224x224 layers at
+    256 images) are summed over batch chunks into one f32 gradient; the limit is lowered here
+    so the chunked path runs on a small shape (5 images, 2 per chunk)."""
+    import kungfu_amd.ops.conv as kconv
+
+    torch.manual_seed(6)
+    N, C, Hh, Ww, K = 5, 64, 20, 20, 128
+    x = torch.randn(N, C, Hh, Ww, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, Hh, Ww, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 3, 3), dy.float(), stride=1, padding=1)
+    w = torch.empty(K, C, 3, 3, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    monkeypatch.setattr(kconv, "_WGRAD_MAX_PIXELS", 2 * Hh * Ww + 1)
+    got = kconv.wgrad(dy, x, w, 1, 1)
+    assert got.dtype == torch.bfloat16 and got.shape == ref.shape
+    assert ((got.float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@needs_gpu
 @pytest.mark.parametrize("shape", [(2, 224, 224), (3, 37, 45), (1, 16, 9), (8, 64, 64)])
 @pytest.mark.parametrize("xdtype", [torch.float32, torch.bfloat16])
 def test_stem_conv_matches_torch(H, shape, xdtype):
