@@ -5,13 +5,29 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+# set by inception_v3(fused_bn=True) while the model is being built
+_FUSED_BN = [False]
+
+
 class BasicConv2d(nn.Module):
+    """conv -> BN -> ReLU.  With ``fused_bn`` the BN+ReLU is the HIP ``BatchNormAct2d``
+    (same parameters and state_dict keys), which runs its kernels for the channel counts
+    it supports (64, 128, ...) and the torch composition for the others (80, 192, ...)."""
+
     def __init__(self, cin, cout, **kw):
         super().__init__()
         self.conv = nn.Conv2d(cin, cout, bias=False, **kw)
-        self.bn = nn.BatchNorm2d(cout, eps=0.001)
+        self.fused = _FUSED_BN[0]
+        if self.fused:
+            from ..ops.fused_bn import BatchNormAct2d
+
+            self.bn = BatchNormAct2d(cout, relu=True, eps=0.001)
+        else:
+            self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
     def forward(self, x):
+        if self.fused:
+            return self.bn(self.conv(x))
         return F.relu(self.bn(self.conv(x)), inplace=True)
 
 
@@ -108,6 +124,9 @@ class InceptionV3(nn.Module):
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 
-def inception_v3(**kw):
-    kw.pop("fused_bn", None)
-    return InceptionV3(**kw)
+def inception_v3(fused_bn: bool = False, **kw):
+    _FUSED_BN[0] = bool(fused_bn)
+    try:
+        return InceptionV3(**kw)
+    finally:
+        _FUSED_BN[0] = False
