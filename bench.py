@@ -85,7 +85,7 @@ def main():
         from kungfu_amd.ops import fused_bn as fb
 
         fused_bn = 1 if fb.available() else 0
-    model = (get_model(a.model, fused_bn=bool(fused_bn)) if a.model.startswith("resnet") or a.model == "inception_v3"
+    model = (get_model(a.model, fused_bn=bool(fused_bn)) if a.model.startswith("resnet") or a.model in ("inception_v3", "vgg16")
              else get_model(a.model))
     model = model.to(dev).to(memory_format=torch.channels_last)
     base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)

@@ -391,6 +391,41 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c
     return dw;
 }
 
+static void check_bias_act(const at::Tensor &y, const char *name) {
+    TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
+                    y.is_contiguous(at::MemoryFormat::ChannelsLast) && kfk::bias_act_supported(y.size(1)),
+                name, " must be a 4-D channels_last bf16 GPU tensor with C/8 a power of two <= 256");
+}
+
+// y = relu(y + bias) in place (relu=false: y += bias); bias f32 [C]
+void bias_act_forward_(at::Tensor y, at::Tensor bias, bool relu) {
+    check_bias_act(y, "bias_act_forward_: y");
+    TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kFloat && bias.is_contiguous() &&
+                    bias.numel() == y.size(1) && bias.device() == y.device(),
+                "bias_act_forward_: bias must be a contiguous f32 [C] tensor on y's device");
+    c10::DeviceGuard gd(y.device());
+    const int64_t rows = y.numel() / y.size(1);
+    kfk::launch_bias_act_forward(reinterpret_cast<uint16_t *>(y.data_ptr()), bias.data_ptr<float>(), rows,
+                                 static_cast<int>(y.size(1)), relu, stream_of(y, 0));
+}
+
+// (dz, dbias): dz = dy * (y > 0) (relu; dz is dy itself without relu), dbias = sum dz over N, H, W (f32)
+std::vector<at::Tensor> bias_act_backward(at::Tensor dy, at::Tensor y, bool relu) {
+    check_bias_act(y, "bias_act_backward: y");
+    check_bias_act(dy, "bias_act_backward: dy");
+    TORCH_CHECK(dy.sizes() == y.sizes() && dy.device() == y.device(), "bias_act_backward: dy must match y");
+    c10::DeviceGuard gd(y.device());
+    const int C = static_cast<int>(y.size(1));
+    const int64_t rows = y.numel() / C;
+    at::Tensor dz = relu ? at::empty_like(dy, dy.options().memory_format(at::MemoryFormat::ChannelsLast)) : dy;
+    at::Tensor db = at::empty({C}, y.options().dtype(at::kFloat));
+    kfk::launch_bias_act_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                  reinterpret_cast<const uint16_t *>(y.data_ptr()),
+                                  reinterpret_cast<uint16_t *>(dz.data_ptr()), db.data_ptr<float>(), rows, C, relu,
+                                  stream_of(y, 0));
+    return {dz, db};
+}
+
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
@@ -918,6 +953,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
     m.def("conv_wgrad_supported", &kfk::conv_wgrad_supported);
+    m.def("bias_act_supported", &kfk::bias_act_supported);
+    m.def("bias_act_forward_", &bias_act_forward_, "y = relu(y + bias) in place (NHWC bf16, f32 bias)",
+          py::arg("y"), py::arg("bias"), py::arg("relu") = true);
+    m.def("bias_act_backward", &bias_act_backward, "(dy * (y > 0), its per-channel sum) in one pass",
+          py::arg("dy"), py::arg("y"), py::arg("relu") = true);
     m.def("conv_wgrad_variants", &kfk::conv_wgrad_variants);
     m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
         const auto p = kfk::conv_wgrad_plan(N, H, W, Cin, Cout, ks, stride, variant, splits);

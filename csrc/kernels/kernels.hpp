@@ -201,4 +201,11 @@ void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                              hipStream_t s);
 
+// Conv bias (+ ReLU) on NHWC bf16 [rows, C] (bias_act.hip): forward in place; backward
+// dz = dy * (y > 0) (relu) and dbias[c] = sum over rows (f32, zeroed first).
+bool bias_act_supported(int C);
+void launch_bias_act_forward(uint16_t *y, const float *bias, int64_t rows, int C, bool relu, hipStream_t s);
+void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, int64_t rows, int C,
+                              bool relu, hipStream_t s);
+
 }  // namespace kfk

@@ -6,13 +6,21 @@ CFG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512
 
 
 class VGG(nn.Module):
-    def __init__(self, cfg=CFG16, num_classes: int = 1000, batch_norm: bool = False):
+    def __init__(self, cfg=CFG16, num_classes: int = 1000, batch_norm: bool = False, fused: bool = False):
+        """``fused``: conv+bias+ReLU as one ``ops.conv.Conv2dReLU`` (fused bias/ReLU pass on the
+        MFMA path); an ``nn.Identity`` keeps the ReLU's slot so state_dict keys do not move."""
         super().__init__()
+        if fused and not batch_norm:
+            from ..ops.conv import Conv2dReLU
         layers, c = [], 3
         for v in cfg:
             if v == "M":
                 layers.append(nn.MaxPool2d(2, 2))
             else:
+                if fused and not batch_norm:
+                    layers += [Conv2dReLU(c, v, 3, padding=1), nn.Identity()]
+                    c = v
+                    continue
                 layers.append(nn.Conv2d(c, v, 3, padding=1))
                 if batch_norm:
                     layers.append(nn.BatchNorm2d(v))
@@ -29,6 +37,6 @@ class VGG(nn.Module):
         return self.classifier(torch.flatten(self.avgpool(self.features(x)), 1))
 
 
-def vgg16(**kw):
-    kw.pop("fused_bn", None)
-    return VGG(CFG16, **kw)
+def vgg16(fused_bn: bool = False, **kw):
+    """``fused_bn`` (the zoo-wide "use the HIP fusions" flag) selects the fused conv+bias+ReLU."""
+    return VGG(CFG16, fused=bool(fused_bn), **kw)

@@ -19,6 +19,7 @@ from __future__ import annotations
 import os
 
 import torch
+import torch.nn as nn
 import torch.nn.functional as F
 
 from .._lib import hip, hip_available
@@ -125,11 +126,51 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> torch.Tensor:
     return F.conv2d(x, w, stride=stride, padding=1)
 
 
-def conv2d(x, w, bias, stride, padding, dilation, groups):
-    """F.conv2d with the 3x3 MFMA fast path (bias handled outside the kernel)."""
+class _BiasActFn(torch.autograd.Function):
+    """y = relu(y + b) in place on a conv output (csrc/kernels/bias_act.hip); backward is one
+    pass producing dy * (y > 0) and its per-channel sum (the bias gradient)."""
+
+    @staticmethod
+    def forward(ctx, y, b, relu):
+        hip().bias_act_forward_(y, b, relu)
+        ctx.mark_dirty(y)
+        ctx.save_for_backward(y)
+        ctx.relu = relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        dz, db = hip().bias_act_backward(dy.contiguous(memory_format=torch.channels_last), y, ctx.relu)
+        return dz, db, None
+
+
+def conv2d(x, w, bias, stride, padding, dilation, groups, relu: bool = False):
+    """F.conv2d (+ ReLU) with the 3x3 MFMA fast path; there the bias (+ ReLU) is one in-place
+    HIP pass over the conv output (``_BiasActFn``) when the channel count allows."""
     if eligible(x, w, stride, padding, dilation, groups):
         y = _Conv3x3Fn.apply(x, w, int(stride if isinstance(stride, int) else stride[0]))
+        if bias is not None and hip().bias_act_supported(int(y.shape[1])):
+            return _BiasActFn.apply(y, bias.float().contiguous(), bool(relu))
         if bias is not None:
             y = y + bias.view(1, -1, 1, 1).to(y.dtype)
-        return y
-    return F.conv2d(x, w, bias, stride, padding, dilation, groups)
+        return F.relu(y) if relu else y
+    y = F.conv2d(x, w, bias, stride, padding, dilation, groups)
+    return F.relu(y) if relu else y
+
+
+class Conv2dReLU(nn.Conv2d):
+    """relu(conv2d(x) + bias) as one module (VGG's conv -> ReLU pairs): on the MFMA path the
+    bias and ReLU are fused into one pass.  Takes the bf16 shadow weights itself
+    (``kf_shadow_forward``: parallel/mixed.py registers its parameters, keeps this forward)."""
+
+    kf_shadow_forward = True
+
+    def forward(self, x):
+        from ..parallel.mixed import shadow
+
+        w = shadow(self.weight)
+        b = shadow(self.bias) if self.bias is not None else None
+        if self.padding_mode == "zeros" and x.dtype == torch.bfloat16:
+            return conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups, relu=True)
+        return F.relu(self._conv_forward(x, w, b))

@@ -139,7 +139,10 @@ def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> i
     from ..ops.fused_bn import BatchNormAct2d
 
     for m in model.modules():
-        if type(m).forward in (nn.Conv1d.forward, nn.Conv2d.forward, nn.Conv3d.forward):
+        if getattr(type(m), "kf_shadow_forward", False):  # takes shadow() in its own forward
+            if register(m.weight) and getattr(m, "bias", None) is not None:
+                register(m.bias)
+        elif type(m).forward in (nn.Conv1d.forward, nn.Conv2d.forward, nn.Conv3d.forward):
             if register(m.weight):
                 if m.bias is not None:
                     register(m.bias)
