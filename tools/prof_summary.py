@@ -24,6 +24,7 @@ CATEGORIES = [
     ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,"),
     ("conv weight flip (ours)", r"kfk::.*conv_flip"),
     ("conv MFMA wgrad (ours)", r"kfk::.*wgrad"),
+    ("conv bias+ReLU (ours)", r"kfk::.*bias_act"),
     ("stem conv MFMA (ours)", r"kfk::.*stem"),
     ("optimizer/flat (ours)", r"kfk::"),
     ("rccl", r"ncclDevKernel|oneRankReduce|rccl"),
