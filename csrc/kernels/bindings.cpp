@@ -426,6 +426,39 @@ std::vector<at::Tensor> bias_act_backward(at::Tensor dy, at::Tensor y, bool relu
     return {dz, db};
 }
 
+static void check_pool_in(const at::Tensor &x, const char *name) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0 && x.size(2) % 2 == 0 &&
+                    x.size(3) % 2 == 0,
+                name, " must be a 4-D channels_last bf16 GPU tensor with C % 8 == 0 and even H, W");
+}
+
+at::Tensor maxpool2x2_forward(at::Tensor x) {
+    check_pool_in(x, "maxpool2x2_forward: x");
+    c10::DeviceGuard gd(x.device());
+    auto y = at::empty({x.size(0), x.size(1), x.size(2) / 2, x.size(3) / 2},
+                       x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_maxpool2x2_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()),
+                                   reinterpret_cast<uint16_t *>(y.data_ptr()), x.size(0), static_cast<int>(x.size(2)),
+                                   static_cast<int>(x.size(3)), static_cast<int>(x.size(1)), stream_of(x, 0));
+    return y;
+}
+
+at::Tensor maxpool2x2_backward(at::Tensor x, at::Tensor dy) {
+    check_pool_in(x, "maxpool2x2_backward: x");
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == x.size(0) &&
+                    dy.size(1) == x.size(1) && dy.size(2) == x.size(2) / 2 && dy.size(3) == x.size(3) / 2 &&
+                    dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x.device(),
+                "maxpool2x2_backward: dy must be the channels_last bf16 pooled-output gradient");
+    c10::DeviceGuard gd(x.device());
+    auto dx = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_maxpool2x2_backward(reinterpret_cast<const uint16_t *>(x.data_ptr()),
+                                    reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                    reinterpret_cast<uint16_t *>(dx.data_ptr()), x.size(0), static_cast<int>(x.size(2)),
+                                    static_cast<int>(x.size(3)), static_cast<int>(x.size(1)), stream_of(x, 0));
+    return dx;
+}
+
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
@@ -954,6 +987,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
     m.def("conv_wgrad_supported", &kfk::conv_wgrad_supported);
     m.def("bias_act_supported", &kfk::bias_act_supported);
+    m.def("maxpool2x2_forward", &maxpool2x2_forward, "2x2/s2 max-pool, NHWC bf16 (no argmax tensor)");
+    m.def("maxpool2x2_backward", &maxpool2x2_backward, "2x2/s2 max-pool gradient (gather from x, dy)");
     m.def("bias_act_forward_", &bias_act_forward_, "y = relu(y + bias) in place (NHWC bf16, f32 bias)",
           py::arg("y"), py::arg("bias"), py::arg("relu") = true);
     m.def("bias_act_backward", &bias_act_backward, "(dy * (y > 0), its per-channel sum) in one pass",

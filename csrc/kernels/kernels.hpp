@@ -208,4 +208,10 @@ void launch_bias_act_forward(uint16_t *y, const float *bias, int64_t rows, int C
 void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, int64_t rows, int C,
                               bool relu, hipStream_t s);
 
+// 2x2 / stride-2 max-pool, NHWC bf16, C % 8 == 0, even H and W (pool.hip); backward
+// recomputes the window argmax from x and writes every dx element once.
+void launch_maxpool2x2_forward(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s);
+void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
+                                hipStream_t s);
+
 }  // namespace kfk

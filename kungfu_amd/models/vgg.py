@@ -15,6 +15,11 @@ class VGG(nn.Module):
         layers, c = [], 3
         for v in cfg:
             if v == "M":
+                if fused and not batch_norm:
+                    from ..ops.pool import MaxPool2x2
+
+                    layers.append(MaxPool2x2())
+                    continue
                 layers.append(nn.MaxPool2d(2, 2))
             else:
                 if fused and not batch_norm:

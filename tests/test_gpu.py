@@ -810,3 +810,26 @@ def test_vgg_fused_conv_relu_matches_stock():
         n += 1
     del kconv._BiasActFn.apply  # back to the inherited Function.apply
     assert n == 12 and len(calls) == 12
+
+
+@needs_gpu
+@pytest.mark.parametrize("shape", [(2, 64, 224, 224), (3, 512, 14, 14), (2, 8, 6, 10)])
+def test_maxpool2x2_matches_torch(H, shape):
+    """2x2/s2 max-pool forward and gradient (argmax recomputed from x, ties included: the
+    ReLU'd input has many all-zero windows) vs torch's max-pool on the same bf16 values."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.pool import max_pool2x2
+
+    torch.manual_seed(10)
+    x = torch.randn(*shape, device="cuda").clamp_min(0).bfloat16().to(memory_format=torch.channels_last)
+    dy = torch.randn(shape[0], shape[1], shape[2] // 2, shape[3] // 2, device="cuda").bfloat16().to(
+        memory_format=torch.channels_last)
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    yr.backward(dy.float())
+    xa = x.clone().requires_grad_(True)
+    ya = max_pool2x2(xa)
+    ya.backward(dy)
+    assert torch.equal(ya.float(), yr.detach())
+    assert torch.equal(xa.grad.float(), xr.grad)

@@ -25,6 +25,7 @@ CATEGORIES = [
     ("conv weight flip (ours)", r"kfk::.*conv_flip"),
     ("conv MFMA wgrad (ours)", r"kfk::.*wgrad"),
     ("conv bias+ReLU (ours)", r"kfk::.*bias_act"),
+    ("max-pool 2x2 (ours)", r"kfk::.*maxpool2"),
     ("stem conv MFMA (ours)", r"kfk::.*stem"),
     ("optimizer/flat (ours)", r"kfk::"),
     ("rccl", r"ncclDevKernel|oneRankReduce|rccl"),
