@@ -173,4 +173,10 @@ class Conv2dReLU(nn.Conv2d):
         b = shadow(self.bias) if self.bias is not None else None
         if self.padding_mode == "zeros" and x.dtype == torch.bfloat16:
             return conv2d(x, w, b, self.stride, self.padding, self.dilation, self.groups, relu=True)
+        if b is not None and x.is_cuda and hip_available() and hip().bias_act_supported(self.out_channels):
+            # e.g. the f32-image first layer under autocast: library conv, then the fused pass
+            y = self._conv_forward(x, w, None)
+            if y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=torch.channels_last):
+                return _BiasActFn.apply(y, b.float().contiguous(), True)
+            return F.relu(y + b.view(1, -1, 1, 1).to(y.dtype))
         return F.relu(self._conv_forward(x, w, b))

@@ -833,3 +833,27 @@ def test_maxpool2x2_matches_torch(H, shape):
     ya.backward(dy)
     assert torch.equal(ya.float(), yr.detach())
     assert torch.equal(xa.grad.float(), xr.grad)
+
+
+@needs_gpu
+def test_conv_relu_first_layer_autocast():
+    """Conv2dReLU on an f32 image under bf16 autocast (library conv, then the fused bias+ReLU
+    pass) vs the stock conv -> ReLU: output, input gradient and parameter gradients."""
+    import kungfu_amd.ops.conv as kconv
+
+    torch.manual_seed(11)
+    ref = torch.nn.Conv2d(3, 64, 3, padding=1).cuda().to(memory_format=torch.channels_last)
+    m = kconv.Conv2dReLU(3, 64, 3, padding=1).cuda().to(memory_format=torch.channels_last)
+    m.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 3, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+    gy = torch.randn(2, 64, 32, 32, device="cuda").to(memory_format=torch.channels_last)
+    outs = []
+    for mod, act in ((ref, True), (m, False)):
+        xx = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = mod(xx)
+            y = torch.relu(y) if act else y
+        y.float().backward(gy)
+        outs.append([y.detach().float(), xx.grad.float(), mod.weight.grad.float(), mod.bias.grad.float()])
+    for a, c in zip(*outs):
+        assert ((c - a).norm() / a.norm()).item() < 2e-2
