@@ -41,8 +41,19 @@ MODEL_BASELINES = {
 
 def _setup_env():
     # MIOpen tuning database shipped in-tree (find results for these shapes),
-    # so a fresh box skips the multi-minute exhaustive search.
+    # so a fresh box skips the multi-minute exhaustive search.  With several
+    # ranks on one node each gets its own copy (no lock contention on the
+    # sqlite caches when they compile / look up kernels at the same time).
     tdir = os.path.join(ROOT, "kungfu_amd", "tuning", "miopen")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and "MIOPEN_USER_DB_PATH" not in os.environ:
+        import shutil
+        import tempfile
+
+        dst = os.path.join(tempfile.gettempdir(), "kungfu_miopen_%s_%s" % (os.getuid(), os.environ.get("LOCAL_RANK", "0")))
+        if not os.path.isdir(dst):
+            shutil.copytree(tdir, dst)
+        tdir = dst
     os.environ.setdefault("MIOPEN_USER_DB_PATH", tdir)
     os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", tdir)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -55,7 +66,10 @@ def main():
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--batch", type=int, default=256, help="images per GPU")
     p.add_argument("--model", default="resnet50")
-    p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada", "local"])
+    p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada", "gns", "local"])
+    p.add_argument("--force-comm", type=int, default=1,
+                   help="1: S-SGD buckets go through the communicator even with one GPU (RCCL 1-rank all-reduce)")
+    p.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="gradient dtype on the wire")
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
     p.add_argument("--bucket-mb", type=float, default=None)
@@ -89,9 +103,15 @@ def main():
              else get_model(a.model))
     model = model.to(dev).to(memory_format=torch.channels_last)
     base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+    comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else None
     if a.optimizer == "ssgd":
         opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),
-                                                    bucket_mb=a.bucket_mb, overlap=bool(a.overlap))
+                                                    bucket_mb=a.bucket_mb, overlap=bool(a.overlap),
+                                                    force_comm=bool(a.force_comm), comm_dtype=comm_dtype)
+    elif a.optimizer == "gns":  # S-SGD + gradient-noise-scale monitor (K5 every step)
+        opt = kf.optimizers.MonitorGradientNoiseScaleOptimizer(base, device_batch_size=a.batch,
+                                                               named_parameters=model.named_parameters(),
+                                                               monitor_single=bool(a.force_comm))
     elif a.optimizer == "local":  # diagnostics only: fused flat SGD, no gradient exchange
         from kungfu_amd.optimizers.core import KungFuOptimizer
 
@@ -121,8 +141,11 @@ def main():
         return loss
 
     t_w0 = time.time()
-    for _ in range(a.warmup):
-        step()
+    first_loss = None
+    for i in range(a.warmup):
+        l0 = step()
+        if i == 0:
+            first_loss = float(l0.detach())
     torch.cuda.synchronize()
     warm_s = time.time() - t_w0
 
@@ -138,6 +161,8 @@ def main():
     dt_t = torch.tensor([dt], dtype=torch.float64)
     dt_max = float(kf.ops.all_reduce(dt_t, op="max")[0]) if size > 1 else dt
     value = a.batch * size * a.steps / dt_max
+    reducer = getattr(opt, "reducer", None)
+    comm_info = reducer.describe() if reducer is not None else {"comm_ranks": size}
     metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
     res = {
         "metric": metric,
@@ -165,7 +190,9 @@ def main():
             "per_gpu_img_s": round(value / size, 2),
             "baseline_per_gpu_img_s": round(base_per_gpu, 1) if base_per_gpu else None,
             "warmup_s": round(warm_s, 1),
+            "initial_loss": round(first_loss, 4) if first_loss is not None else None,
             "final_loss": round(float(loss.detach()), 4),
+            "comm": comm_info,
         },
     }
     if rank == 0:

@@ -128,6 +128,16 @@ void square(at::Tensor dst, at::Tensor src) {
     kfk::launch_square(dst.data_ptr<float>(), src.data_ptr(), src.numel(), dtype_code(src), stream_of(dst, 0));
 }
 
+void cast_copy(at::Tensor dst, at::Tensor src, double scale) {
+    check_gpu(dst, "dst");
+    check_gpu(src, "src");
+    const int sd = dtype_code(src), dd = dtype_code(dst);
+    TORCH_CHECK((sd == 9 || sd == 10) && (dd == 9 || dd == 10), "cast_copy: f32/bf16 only");
+    TORCH_CHECK(dst.numel() == src.numel() && dst.device() == src.device(), "cast_copy: size/device mismatch");
+    c10::DeviceGuard gd(dst.device());
+    kfk::launch_cast(dst.data_ptr(), src.data_ptr(), src.numel(), sd, dd, static_cast<float>(scale), stream_of(dst, 0));
+}
+
 at::Tensor sumsq2(at::Tensor a, c10::optional<at::Tensor> b) {
     check_gpu(a, "a");
     int dt = dtype_code(a);
@@ -967,6 +977,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("a"), py::arg("b"));
     m.def("scale_", &scale_, "x *= alpha");
     m.def("square", &square, "dst = src^2");
+    m.def("cast_copy", &cast_copy, "dst = scale * src with an f32 <-> bf16 cast");
     m.def("sumsq2", &sumsq2, "[sum(a^2), sum(b^2)] in one pass", py::arg("a"), py::arg("b") = py::none());
     m.def("variance", &variance, "sum |s2*inv - (s1*inv)^2|");
     m.def("gns_update", &gns_update, "device-side gradient-noise-scale EMA update");

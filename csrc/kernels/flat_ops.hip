@@ -327,6 +327,56 @@ __global__ __launch_bounds__(kBlock) void square_kernel(float *dst, const void *
     }
 }
 
+
+// ---------------------------------------------------------------- cast copy
+// dst = scale * src with a dtype change (f32 <-> bf16): the S-SGD engine's bf16
+// gradient wire format (bucket -> comm buffer before the all-reduce, back after).
+// 8 elements per lane: two float4 on the f32 side, one 16-byte bf16 vector.
+template <int SRC, int DST>
+__global__ __launch_bounds__(kBlock) void cast8_kernel(void *__restrict__ dst, const void *__restrict__ src, size_t n8,
+                                                       float scale) {
+    size_t stride = static_cast<size_t>(gridDim.x) * kBlock;
+    for (size_t i = static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x; i < n8; i += stride) {
+        float v[8];
+        if (SRC == DT_F32) {
+            const float4 *s = static_cast<const float4 *>(src) + 2 * i;
+            const float4 a = s[0], b = s[1];
+            v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w, v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+        } else {
+            const uint4 r = static_cast<const uint4 *>(src)[i];
+            const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[2 * k] = __uint_as_float(w[k] << 16);
+                v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] *= scale;
+        if (DST == DT_F32) {
+            float4 *d = static_cast<float4 *>(dst) + 2 * i;
+            d[0] = make_float4(v[0], v[1], v[2], v[3]);
+            d[1] = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+            uint4 o;
+            o.x = f32_to_bf16(v[0]) | (static_cast<uint32_t>(f32_to_bf16(v[1])) << 16);
+            o.y = f32_to_bf16(v[2]) | (static_cast<uint32_t>(f32_to_bf16(v[3])) << 16);
+            o.z = f32_to_bf16(v[4]) | (static_cast<uint32_t>(f32_to_bf16(v[5])) << 16);
+            o.w = f32_to_bf16(v[6]) | (static_cast<uint32_t>(f32_to_bf16(v[7])) << 16);
+            static_cast<uint4 *>(dst)[i] = o;
+        }
+    }
+}
+
+__global__ void cast_tail_kernel(void *dst, const void *src, size_t begin, size_t n, int sdt, int ddt, float scale) {
+    size_t i = begin + static_cast<size_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float v = sdt == DT_F32 ? static_cast<const float *>(src)[i] : bf16_to_f32(static_cast<const uint16_t *>(src)[i]);
+    v *= scale;
+    if (ddt == DT_F32) static_cast<float *>(dst)[i] = v;
+    else static_cast<uint16_t *>(dst)[i] = f32_to_bf16(v);
+}
+
 }  // namespace
 
 void launch_reduce(void *z, const void *x, const void *y, size_t n, int dtype, int op, hipStream_t s) {
@@ -420,6 +470,29 @@ void launch_square(float *dst, const void *src, size_t n, int dtype, hipStream_t
     if (n == 0) return;
     if (dtype == DT_BF16) square_kernel<true><<<grid_for(n), kBlock, 0, s>>>(dst, src, n);
     else square_kernel<false><<<grid_for(n), kBlock, 0, s>>>(dst, src, n);
+}
+
+void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, float scale, hipStream_t s) {
+    if (n == 0) return;
+    size_t n8 = 0;
+    if (aligned16(dst) && aligned16(src)) {
+        n8 = n / 8;
+        if (n8) {
+            if (src_dt == DT_F32 && dst_dt == DT_BF16)
+                cast8_kernel<DT_F32, DT_BF16><<<grid_for(n8), kBlock, 0, s>>>(dst, src, n8, scale);
+            else if (src_dt == DT_BF16 && dst_dt == DT_F32)
+                cast8_kernel<DT_BF16, DT_F32><<<grid_for(n8), kBlock, 0, s>>>(dst, src, n8, scale);
+            else if (src_dt == DT_F32)
+                cast8_kernel<DT_F32, DT_F32><<<grid_for(n8), kBlock, 0, s>>>(dst, src, n8, scale);
+            else
+                cast8_kernel<DT_BF16, DT_BF16><<<grid_for(n8), kBlock, 0, s>>>(dst, src, n8, scale);
+        }
+    }
+    size_t done = n8 * 8;
+    if (done < n) {
+        int g = static_cast<int>((n - done + kBlock - 1) / kBlock);
+        cast_tail_kernel<<<g, kBlock, 0, s>>>(dst, src, done, n, src_dt, dst_dt, scale);
+    }
 }
 
 }  // namespace kfk

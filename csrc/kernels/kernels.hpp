@@ -35,6 +35,8 @@ void launch_scale(void *x, size_t n, float alpha, int dtype, hipStream_t s);
 
 // K6 helper: dst = src^2 (f32 out, f32/bf16 in).
 void launch_square(float *dst, const void *src, size_t n, int dtype, hipStream_t s);
+// dst = scale * src, f32/bf16 -> f32/bf16 (bf16 gradient wire format)
+void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, float scale, hipStream_t s);
 
 // K5: out[0] = sum(a^2), out[1] = sum(b^2) in one pass (b may be null).
 // `partials` needs 2*kMaxGrid floats of scratch.

@@ -134,6 +134,8 @@ __global__ void fold1(const float *partials, int nparts, float *out) {
 __global__ void gns_update_kernel(const float *sumsq_small, const float *sumsq_big, float b_small, float b_big,
                                   float alpha, float *state) {
     float gs = *sumsq_small, gb = *sumsq_big;
+    // one peer (B == b): the estimator is undefined -- keep the state (count unchanged)
+    if (!(b_big > b_small)) return;
     float G = (b_big * gb - b_small * gs) / (b_big - b_small);
     float S = (gs - gb) / (1.f / b_small - 1.f / b_big);
     float cnt = state[3];

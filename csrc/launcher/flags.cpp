@@ -70,7 +70,8 @@ std::string Flags::usage() {
            "  -timeout DUR           kill the job after DUR (e.g. 30s, 5m)\n"
            "  -v[=bool]              stream worker output (true)\n"
            "  -q                     quiet launcher logs\n"
-           "  -allow-xgmi            keep all GPUs visible to every worker (alias -allow-nvlink)\n"
+           "  -allow-xgmi[=bool]     keep all GPUs visible to every worker (default; alias -allow-nvlink)\n"
+           "  -isolate-gpus          one visible GPU per worker (HIP_VISIBLE_DEVICES=<slot>)\n"
            "  -strategy NAME         STAR|MULTI_STAR|RING|CLIQUE|TREE|BINARY_TREE|BINARY_TREE_STAR|"
            "MULTI_BINARY_TREE_STAR|AUTO\n"
            "  -port N                runner port (38080)\n"
@@ -122,6 +123,7 @@ std::string Flags::parse(int argc, char **argv) {
             else if (name == "v") verbose = getb();
             else if (name == "nic") nic = get();
             else if (name == "allow-xgmi" || name == "allow-nvlink") allow_xgmi = getb();
+            else if (name == "isolate-gpus") allow_xgmi = !getb();
             else if (name == "strategy") {
                 auto s = get();
                 if (!parse_strategy(s, &strategy)) throw std::invalid_argument("invalid strategy " + s);

@@ -27,6 +27,9 @@ Proc Job::new_proc(const PeerID &peer, int gpu_id, int init_version, const Clust
     e["KUNGFU_ALLOW_XGMI"] = allow_xgmi ? "true" : "false";
     int idx = gpu_index(gpu_id);
     e["KUNGFU_HIP_VISIBLE_DEVICES"] = std::to_string(idx);
+    // ordinal of the slot among the devices this worker sees (all of the
+    // launcher's visible GPUs unless -isolate-gpus): what hipSetDevice takes
+    e["KUNGFU_HIP_DEVICE_ORDINAL"] = std::to_string(allow_xgmi ? gpu_id : 0);
     if (!allow_xgmi) {
         // One GPU per worker.  HIP honours HIP_VISIBLE_DEVICES; the CUDA name is
         // kept for frameworks that read it.

@@ -15,9 +15,12 @@
 //   xterm/log redirect         utils/iostream/{xterm,lazyfile}.go
 //   remote launch              utils/runner/remote/remote.go, cmd/kungfu-rrun, cmd/kungfu-distribute
 //
-// ROCm specifics: the per-worker GPU is exported as HIP_VISIBLE_DEVICES (and
-// KUNGFU_HIP_VISIBLE_DEVICES); -allow-xgmi (alias -allow-nvlink) keeps every
-// GPU visible so the worker selects its device by local rank.
+// ROCm specifics: the per-worker GPU slot is exported as KUNGFU_HIP_VISIBLE_DEVICES.
+// By default every GPU stays visible to every worker and the worker selects its
+// slot (hipSetDevice): RCCL's intra-node P2P/IPC transport over xGMI needs the
+// peers' devices to be visible, otherwise it falls back to a host-memory path.
+// -isolate-gpus (or -allow-xgmi=false) restores the reference's default of one
+// visible GPU per worker (HIP_VISIBLE_DEVICES=<slot>, job/job.go:31-98).
 #pragma once
 
 #include <kungfu/peer.hpp>
@@ -43,7 +46,7 @@ struct Flags {
     double timeout = 0;
     bool verbose = true;
     std::string nic;
-    bool allow_xgmi = false;
+    bool allow_xgmi = true;
     Strategy strategy = Strategy::BINARY_TREE_STAR;
     int port = kDefaultRunnerPort;
     int debug_port = 0;
@@ -110,7 +113,7 @@ struct Job {
     std::string prog;
     std::vector<std::string> args;
     std::string logdir;
-    bool allow_xgmi = false;
+    bool allow_xgmi = true;
 
     Proc new_proc(const PeerID &peer, int gpu_id, int init_version, const Cluster &cluster) const;
     std::vector<Proc> create_procs(const Cluster &cluster, uint32_t host) const;

@@ -26,13 +26,34 @@ def broadcast_parameters(state) -> None:
 broadcast_variables = broadcast_parameters
 
 
+def _scalar_holders(optimizer):
+    """Objects (the wrapper and the wrapped optimizer) exposing ``_kf_scalars`` /
+    ``_kf_load_scalars``: host-side state such as FusedSGD's first-step flag or
+    a monitor's step counter, which must match rank 0 after a (re)join."""
+    out = []
+    for o in (optimizer, getattr(optimizer, "inner", None)):
+        if o is not None and hasattr(o, "_kf_scalars") and all(o is not x for x in out):
+            out.append(o)
+    return out
+
+
 def broadcast_optimizer_state(optimizer) -> None:
-    """Broadcast optimizer state tensors (momentum, Adam moments, flat buffers)."""
+    """Broadcast optimizer state from rank 0: flat buffers (momentum, Adam moments
+    and step), per-parameter state tensors, and host-side scalars."""
     inner = getattr(optimizer, "inner", optimizer)
     flat_bufs = [getattr(inner, n, None) for n in ("momentum_buffer", "exp_avg", "exp_avg_sq", "_step_t")]
     for b in flat_bufs:
         if isinstance(b, torch.Tensor):
             ops.inplace_broadcast_(b)
+    holders = _scalar_holders(optimizer)
+    if holders:
+        vals = [list(map(float, h._kf_scalars())) for h in holders]
+        t = torch.tensor([v for vs in vals for v in vs], dtype=torch.float64)
+        ops.inplace_broadcast_(t)
+        k = 0
+        for h, vs in zip(holders, vals):
+            h._kf_load_scalars(t[k:k + len(vs)].tolist())
+            k += len(vs)
     for p, st in inner.state.items():
         for k in sorted(st.keys()):
             v = st[k]

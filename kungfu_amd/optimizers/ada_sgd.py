@@ -6,55 +6,45 @@ Parity: ``srcs/python/kungfu/tensorflow/optimizers/ada_sgd.py:12-83``
 (``tf.cond(global_step < change_step, sma, ssgd)`` + ``AdaSGDHook`` broadcasting
 all variables at ``change_step``).
 
-GPU: both phases share one flat parameter space; the S-SGD gradient reducer
-is registered from the start but disabled (``no_sync``) during the SMA phase,
-so the switch costs one broadcast and no re-allocation.
+Flat-space models (GPU, or CPU with ``flat=True``): both phases share one flat
+parameter space; the S-SGD gradient reducer is registered from the start but
+disabled during the SMA phase, so the switch costs one broadcast and no
+re-allocation.  Both the averager and the reducer re-bind to the current
+communicator after an elastic resize (see ``sma.ModelAverager`` and
+``ddp.GradReducer._bind``).
 """
 from __future__ import annotations
 
 import torch
 
 from .. import ops
-from .._lib import hip
-from ..parallel.comm import get_device_comm
 from ..parallel.ddp import GradReducer
 from .core import KungFuOptimizer
+from .sma import ModelAverager
 
 
 class _AdaptiveSGD(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, change_step: int = 1000, alpha: float = 0.1,
-                 fused: bool = True):
-        super().__init__(optimizer, named_parameters, fused=fused)
+                 fused: bool = True, flat=None):
+        super().__init__(optimizer, named_parameters, fused=fused, flat=flat)
         self.change_step = change_step
         self.alpha = alpha
         self.global_step = 0
         self.reducer = None
+        self.averager = None
         if self.space is not None:
-            self.comm = get_device_comm()
-            self._avg = torch.empty_like(self.space.flat_param)
+            self.averager = ModelAverager(self.space)
             self.reducer = GradReducer(self.space, op="avg")
             self.reducer._enabled = change_step <= 0
-            if change_step > 0:
-                self._launch_average()
 
     @property
     def phase(self) -> str:
         return "sma" if self.global_step < self.change_step else "ssgd"
 
-    def _launch_average(self):
-        comm = self.comm
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(comm.device))
-        comm.stream.wait_event(ev)
-        with torch.cuda.stream(comm.stream):
-            self._avg.copy_(self.space.flat_param, non_blocking=True)
-        comm.all_reduce(self._avg, op="avg")
-
     def _before_step(self):
         if self.phase == "sma":
-            if self.space is not None:
-                torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
-                hip().axpby(self.space.flat_param, self._avg, None, 1.0 - self.alpha, self.alpha)
+            if self.averager is not None:
+                self.averager.blend(self.alpha)
             else:
                 vs = [p for p in self.params if p.grad is not None]
                 avgs = [v.detach().clone() for v in vs]
@@ -72,18 +62,31 @@ class _AdaptiveSGD(KungFuOptimizer):
     def _after_step(self):
         self.global_step += 1
         if self.global_step == self.change_step:
-            # AdaSGDHook: broadcast every variable when switching to S-SGD
+            # AdaSGDHook: broadcast every global variable when switching to S-SGD -- in
+            # TF that includes the optimizer slots (momentum), so replicas continue
+            # identically
             if self.space is not None:
-                torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
+                from ..initializer import broadcast_optimizer_state
+
+                self.averager.wait()
                 ops.inplace_broadcast_(self.space.flat_param)
+                broadcast_optimizer_state(self)
                 self.reducer._enabled = True
             else:
                 for p in self.params:
                     ops.inplace_broadcast_(p.data)
-        elif self.phase == "sma" and self.space is not None:
-            self._launch_average()
+        elif self.phase == "sma" and self.averager is not None:
+            self.averager.launch()
+
+    def _kf_scalars(self):
+        return [self.global_step]
+
+    def _kf_load_scalars(self, vals):
+        self.global_step = int(vals[0])
+        if self.reducer is not None:
+            self.reducer._enabled = self.phase == "ssgd"
 
 
 def AdaptiveSGDOptimizer(optimizer, change_step: int, named_parameters=None, alpha: float = 0.1,
-                         fused: bool = True, name=None, use_locking=False, with_keras=False):
-    return _AdaptiveSGD(optimizer, named_parameters, change_step=change_step, alpha=alpha, fused=fused)
+                         fused: bool = True, name=None, use_locking=False, with_keras=False, flat=None):
+    return _AdaptiveSGD(optimizer, named_parameters, change_step=change_step, alpha=alpha, fused=fused, flat=flat)

@@ -75,6 +75,14 @@ class FusedSGD(torch.optim.Optimizer):
         self._first = False
         return loss
 
+    # host-side scalars that must match across replicas (broadcast_optimizer_state):
+    # a worker that joins a running job must not re-initialise the broadcast momentum
+    def _kf_scalars(self):
+        return [float(self._first)]
+
+    def _kf_load_scalars(self, vals):
+        self._first = bool(vals[0])
+
     def state_dict(self):
         sd = super().state_dict()
         sd["kungfu_flat"] = {"momentum_buffer": self.momentum_buffer, "first": self._first}
@@ -109,6 +117,19 @@ class FusedAdam(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = False):
         self.space.zero_grad()
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["kungfu_flat"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self._step_t}
+        return sd
+
+    def load_state_dict(self, sd):
+        flat = sd.pop("kungfu_flat", None)
+        super().load_state_dict(sd)
+        if flat is not None:
+            self.exp_avg.copy_(flat["exp_avg"])
+            self.exp_avg_sq.copy_(flat["exp_avg_sq"])
+            self._step_t.copy_(flat["step"])
 
     @torch.no_grad()
     def step(self, closure=None):

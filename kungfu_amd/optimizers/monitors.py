@@ -12,11 +12,17 @@ Parity:
   ``grad_variance.py:9-75``: all-reduce g^2 as well and report
   sum_tensors || E[g^2] - E[g]^2 ||_2.
 
-GPU design: the gradient all-reduce is the bucketed in-place engine; the
+Engine design: the gradient all-reduce is the bucketed in-place engine; the
 local |g|^2 is accumulated per bucket on the comm stream *before* that
 bucket's all-reduce (K5, one pass over the bucket), the global |g_avg|^2 after
 the last bucket, and the noise-scale EMA update runs on device (K5 epilogue):
 no extra gradient copy and no host sync on the training path.
+
+The peer count (B = b * np) is read from the current cluster at every
+monitored step, so the estimate stays right across elastic resizes.  With one
+peer the estimator is undefined (B == b); ``monitor_single=True`` still runs the
+K5 reductions every step (the bucket collectives are forced through the
+communicator) so they can be profiled, and the device EMA keeps its state.
 """
 from __future__ import annotations
 
@@ -25,21 +31,34 @@ from typing import Optional
 import torch
 
 from .. import ops, variables
-from .._lib import hip
-from .core import KungFuOptimizer
+from ..parallel.flat import sumsq
 from .sync_sgd import _SynchronousSGD
+
+
+def _gns_update_host(sq_small: float, sq_big: float, b: float, B: float, alpha: float, state: torch.Tensor):
+    """CPU twin of the device ``gns_update`` kernel (csrc/kernels/norms.hip)."""
+    if not B > b:
+        return
+    G = (B * sq_big - b * sq_small) / (B - b)
+    S = (sq_small - sq_big) / (1.0 / b - 1.0 / B)
+    cnt = float(state[3])
+    eg = G if cnt == 0 else alpha * float(state[0]) + (1 - alpha) * G
+    es = S if cnt == 0 else alpha * float(state[1]) + (1 - alpha) * S
+    state[0], state[1] = eg, es
+    state[2] = es / eg if eg != 0 else 0.0
+    state[3] = cnt + 1
 
 
 class _GradientNoiseScale(_SynchronousSGD):
     def __init__(self, optimizer, device_batch_size: int, named_parameters=None, monitor_interval: int = 1,
-                 alpha: float = 0.6, verbose: bool = False, fused: bool = True):
-        super().__init__(optimizer, named_parameters, op="avg", fused=fused)
+                 alpha: float = 0.6, verbose: bool = False, fused: bool = True, monitor_single: bool = False,
+                 flat=None):
+        super().__init__(optimizer, named_parameters, op="avg", fused=fused, force_comm=monitor_single, flat=flat)
         self.device_batch_size = float(device_batch_size)
-        self.np = ops.cluster_size()
-        self.global_batch_size = self.device_batch_size * self.np
         self.interval = max(1, int(monitor_interval))
         self.alpha = alpha
         self.verbose = verbose
+        self.monitor_single = monitor_single
         self.step_count = 0
         self._ema_g = ops.ExponentialMovingAverage(alpha)
         self._ema_s = ops.ExponentialMovingAverage(alpha)
@@ -51,23 +70,37 @@ class _GradientNoiseScale(_SynchronousSGD):
             self.reducer.pre_reduce = self._pre_reduce
             self.reducer.post_finish = self._post_finish
 
-    def _monitoring(self) -> bool:
-        return self.step_count % self.interval == 0 and self.np > 1
+    @property
+    def np(self) -> int:
+        return ops.cluster_size()
 
-    # GPU path -----------------------------------------------------------------
+    @property
+    def global_batch_size(self) -> float:
+        return self.device_batch_size * self.np
+
+    def _monitoring(self) -> bool:
+        return self.step_count % self.interval == 0 and (self.np > 1 or self.monitor_single)
+
+    # flat-space path ------------------------------------------------------------
     def _pre_reduce(self, bucket, g):
         if self._monitoring():
-            self._local_sq.add_(hip().sumsq2(g)[:1])
+            self._local_sq.add_(sumsq(g)[:1])
 
     def _post_finish(self):
         if not self._monitoring():
             return
-        big = hip().sumsq2(self.space.flat_grad)
-        hip().gns_update(self._local_sq, big[:1], self.device_batch_size, self.global_batch_size, self.alpha,
-                         self._state)
+        big = sumsq(self.space.flat_grad)
+        if self._state.is_cuda:
+            from .._lib import hip
+
+            hip().gns_update(self._local_sq, big[:1], self.device_batch_size, self.global_batch_size, self.alpha,
+                             self._state)
+        else:
+            _gns_update_host(float(self._local_sq), float(big[0]), self.device_batch_size, self.global_batch_size,
+                             self.alpha, self._state)
         self._local_sq.zero_()
 
-    # CPU path ------------------------------------------------------------------
+    # per-tensor CPU path ---------------------------------------------------------
     def sync_gradients(self):
         if self.space is not None or not self._monitoring():
             return super().sync_gradients()
@@ -93,31 +126,42 @@ class _GradientNoiseScale(_SynchronousSGD):
             return float(self._state[2].item()) if float(self._state[3].item()) > 0 else None
         return self._last
 
+    def _kf_scalars(self):
+        return [self.step_count]
+
+    def _kf_load_scalars(self, vals):
+        self.step_count = int(vals[0])
+
 
 def MonitorGradientNoiseScaleOptimizer(optimizer, device_batch_size: int, named_parameters=None,
                                        monitor_interval: int = 1, alpha: float = 0.6, verbose: bool = False,
-                                       fused: bool = True, name=None, use_locking=False):
+                                       fused: bool = True, name=None, use_locking=False, monitor_single: bool = False,
+                                       flat=None):
     return _GradientNoiseScale(optimizer, device_batch_size, named_parameters, monitor_interval=monitor_interval,
-                               alpha=alpha, verbose=verbose, fused=fused)
+                               alpha=alpha, verbose=verbose, fused=fused, monitor_single=monitor_single, flat=flat)
 
 
 class _GradVariance(_SynchronousSGD):
     def __init__(self, optimizer, named_parameters=None, monitor_interval: int = 1, verbose: bool = True,
-                 fused: bool = True):
-        super().__init__(optimizer, named_parameters, op="avg", fused=fused)
+                 fused: bool = True, flat=None):
+        super().__init__(optimizer, named_parameters, op="avg", fused=fused, flat=flat)
         self.interval = max(1, int(monitor_interval))
         self.verbose = verbose
         self.step_count = 0
         self.variance: Optional[float] = None
-        self.np = ops.cluster_size()
         if self.reducer is not None:
             dev = self.space.device
             self._sq = torch.zeros_like(self.space.flat_grad)
             offs = [o for o, _ in self.space.offsets] + [self.space.numel]
+            self._seg_host = offs
             self._seg = torch.tensor(offs, dtype=torch.int64, device=dev)
             self._var_t = torch.zeros((), dtype=torch.float32, device=dev)
             self.reducer.pre_reduce = self._pre_reduce
             self.reducer.post_finish = self._post_finish
+
+    @property
+    def np(self) -> int:
+        return ops.cluster_size()
 
     def _monitoring(self) -> bool:
         return self.step_count % self.interval == 0
@@ -125,12 +169,31 @@ class _GradVariance(_SynchronousSGD):
     def _pre_reduce(self, bucket, g):
         if self._monitoring():
             sq = self._sq[bucket.start:bucket.end]
-            hip().square(sq, g)
+            if sq.is_cuda:
+                from .._lib import hip
+
+                hip().square(sq, g)
+            else:
+                torch.mul(g, g, out=sq)
             self.reducer.comm.all_reduce(sq, op="avg")
 
     def _post_finish(self):
-        if self._monitoring():
+        if not self._monitoring():
+            return
+        if self.reducer.skip:  # one peer: E[g^2] = g^2 (the pre-reduce hook did not run)
+            if self._sq.is_cuda:
+                from .._lib import hip
+
+                hip().square(self._sq, self.space.flat_grad)
+            else:
+                torch.mul(self.space.flat_grad, self.space.flat_grad, out=self._sq)
+        if self._sq.is_cuda:
+            from .._lib import hip
+
             self._var_t = hip().seg_variance(self.space.flat_grad, self._sq, self._seg, 1.0)
+        else:
+            g, s, o = self.space.flat_grad, self._sq, self._seg_host
+            self._var_t = torch.tensor(sum(float((s[a:b] - g[a:b] * g[a:b]).norm()) for a, b in zip(o, o[1:])))
 
     def sync_gradients(self):
         if self.space is not None or not self._monitoring():
@@ -149,7 +212,15 @@ class _GradVariance(_SynchronousSGD):
                 print("Variance: %s" % self.variance, flush=True)
         self.step_count += 1
 
+    def _kf_scalars(self):
+        return [self.step_count]
+
+    def _kf_load_scalars(self, vals):
+        self.step_count = int(vals[0])
+
 
 def MonitorGradientVarianceOptimizer(optimizer, named_parameters=None, monitor_interval: int = 1,
-                                     verbose: bool = True, fused: bool = True, name=None, use_locking=False):
-    return _GradVariance(optimizer, named_parameters, monitor_interval=monitor_interval, verbose=verbose, fused=fused)
+                                     verbose: bool = True, fused: bool = True, name=None, use_locking=False,
+                                     flat=None):
+    return _GradVariance(optimizer, named_parameters, monitor_interval=monitor_interval, verbose=verbose, fused=fused,
+                         flat=flat)

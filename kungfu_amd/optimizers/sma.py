@@ -9,42 +9,82 @@ snapshotted into a comm buffer on the comm stream and all-reduced (op avg)
 there, so the model all-reduce overlaps the next iteration's forward and
 backward.  At ``step()`` the compute stream waits for it and one fused HIP
 kernel (K3 ``axpby``) blends the model, then the fused optimizer applies the
-local gradient.  CPU tensors use the host runtime's grouped all-reduce.
+local gradient.
+
+Elastic: the in-flight average is tagged with the (cluster version, comm
+epoch) it was issued under.  After a resize (or on the very first step, so a
+worker joining a running job issues no collective from its constructor) the
+stale average is discarded and a fresh one is computed from the current
+(just re-broadcast) parameters on the new communicator -- every member of the
+new cluster does this at the same point of its step.
+
+CPU models with a flat space run the same code over the host transport
+(:class:`~kungfu_amd.parallel.comm.HostComm`); models without one use the
+host runtime's grouped all-reduce per tensor.
 """
 from __future__ import annotations
 
 import torch
 
 from .. import ops
-from .._lib import hip
-from ..parallel.comm import get_device_comm
+from .._lib import runtime
+from ..parallel.comm import comm_epoch, get_device_comm
+from ..parallel.flat import axpby_
 from .core import KungFuOptimizer
 
 
-class _SynchronousAveraging(KungFuOptimizer):
-    def __init__(self, optimizer, named_parameters=None, alpha: float = 0.1, fused: bool = True):
-        super().__init__(optimizer, named_parameters, fused=fused)
-        self.alpha = alpha
-        self._avg = None
-        if self.space is not None:
-            self.comm = get_device_comm()
-            self._avg = torch.empty_like(self.space.flat_param)
-            self._launch_average()
+class ModelAverager:
+    """Asynchronous all-reduce (op avg) of a flat parameter buffer, re-bound after resizes.
+    Shared by SMA and AdaSGD."""
 
-    def _launch_average(self):
-        comm = self.comm
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(comm.device))
-        comm.stream.wait_event(ev)
-        with torch.cuda.stream(comm.stream):
+    def __init__(self, space):
+        self.space = space
+        self.comm = None
+        self.key = None  # (cluster version, comm epoch) of the pending average
+        self._avg = torch.empty_like(space.flat_param)
+
+    @staticmethod
+    def current_key():
+        return runtime.cluster_version(), comm_epoch()
+
+    def launch(self):
+        """Snapshot the parameters and start their average on the comm stream."""
+        if runtime.size() == 1:
+            self.key = self.current_key()
+            self.comm = None
+            return
+        self.comm = get_device_comm(device=self.space.device)
+        self.key = self.current_key()
+        self.comm.fence()
+        with self.comm.on_stream():
             self._avg.copy_(self.space.flat_param, non_blocking=True)
-        comm.all_reduce(self._avg, op="avg")
+        self.comm.all_reduce(self._avg, op="avg")
+
+    def blend(self, alpha: float):
+        """v <- (1 - alpha) v + alpha avg(v), using the pending average if it is
+        still valid for the current cluster, else a fresh one."""
+        if self.key != self.current_key():
+            self.launch()
+        if self.comm is None:  # one peer: the average is the model itself
+            return
+        self.comm.join()
+        axpby_(self.space.flat_param, self._avg, 1.0 - alpha, alpha)
+
+    def wait(self):
+        if self.comm is not None:
+            self.comm.join()
+
+
+class _SynchronousAveraging(KungFuOptimizer):
+    def __init__(self, optimizer, named_parameters=None, alpha: float = 0.1, fused: bool = True,
+                 flat=None):
+        super().__init__(optimizer, named_parameters, fused=fused, flat=flat)
+        self.alpha = alpha
+        self.averager = ModelAverager(self.space) if self.space is not None else None
 
     def _before_step(self):
-        if self.space is not None:
-            torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
-            # v <- (1 - a) v + a avg(v)
-            hip().axpby(self.space.flat_param, self._avg, None, 1.0 - self.alpha, self.alpha)
+        if self.averager is not None:
+            self.averager.blend(self.alpha)
             return
         vs = [p for p in self.params if p.grad is not None]
         avgs = [v.detach().clone() for v in vs]
@@ -54,13 +94,13 @@ class _SynchronousAveraging(KungFuOptimizer):
                 v.mul_(1.0 - self.alpha).add_(a, alpha=self.alpha)
 
     def _after_step(self):
-        if self.space is not None:
-            self._launch_average()
+        if self.averager is not None:
+            self.averager.launch()
 
 
 def SynchronousAveragingOptimizer(optimizer, named_parameters=None, alpha: float = 0.1, fused: bool = True,
-                                  name=None, use_locking=False, with_keras=False):
+                                  name=None, use_locking=False, with_keras=False, flat=None):
     """Wrap ``optimizer`` with synchronous model averaging (alpha = weight of
     the central model).  ``name``/``use_locking``/``with_keras`` are accepted
     for API parity with the reference and ignored."""
-    return _SynchronousAveraging(optimizer, named_parameters, alpha=alpha, fused=fused)
+    return _SynchronousAveraging(optimizer, named_parameters, alpha=alpha, fused=fused, flat=flat)

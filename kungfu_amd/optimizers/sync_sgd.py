@@ -30,15 +30,17 @@ from .core import KungFuOptimizer
 class _SynchronousSGD(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, op: str = "avg", fused: bool = True,
                  bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
-                 hierarchical: bool = False, monitor: bool = False, overlap: bool = True):
-        super().__init__(optimizer, named_parameters, fused=fused)
+                 hierarchical: bool = False, monitor: bool = False, overlap: bool = True,
+                 force_comm: bool = False, flat=None, first_bucket_mb: float = 1.0):
+        super().__init__(optimizer, named_parameters, fused=fused, flat=flat)
         self.op = op
         self.monitor = monitor
         self.hierarchical = hierarchical
         self.reducer: Optional[GradReducer] = None
         if self.space is not None and not hierarchical and overlap:
             self.reducer = GradReducer(self.space, op="avg" if op == "avg" else "sum", bucket_mb=bucket_mb,
-                                       comm_dtype=comm_dtype)
+                                       comm_dtype=comm_dtype, skip_single=not force_comm,
+                                       first_bucket_mb=first_bucket_mb)
 
     def _before_step(self):
         if self.reducer is not None:
@@ -71,14 +73,22 @@ class _SynchronousSGD(KungFuOptimizer):
 def SynchronousSGDOptimizer(optimizer, named_parameters=None, op: str = "avg", fused: bool = True,
                             bucket_mb: Optional[float] = None, comm_dtype: Optional[torch.dtype] = None,
                             hierarchical: bool = False, monitor: bool = False, overlap: bool = True,
-                            nccl=None, nccl_fusion=None, hierarchical_nccl=None):
+                            nccl=None, nccl_fusion=None, hierarchical_nccl=None, force_comm: bool = False,
+                            flat=None, first_bucket_mb: float = 1.0):
     """Wrap ``optimizer`` so that ``step()`` applies globally averaged gradients.
 
-    ``nccl``/``nccl_fusion``/``hierarchical_nccl`` are accepted for API parity
-    with the reference: on GPU the RCCL data plane is always used and fusion
-    is the flat bucketed buffer; ``hierarchical_nccl`` maps to ``hierarchical``.
+    * ``comm_dtype=torch.bfloat16``: bf16 gradients on the wire (half the bytes).
+    * ``force_comm=True``: issue the bucket collectives even with one peer
+      (exercises the RCCL data plane at N=1; by default a single peer skips them).
+    * ``flat=True``: use the flat-buffer bucket engine for CPU models too (over
+      the host transport); the default is flat on GPU, per-tensor on CPU.
+    * ``nccl``/``nccl_fusion`` are accepted for API parity with the reference and
+      have no effect (documented no-ops): on GPU the RCCL data plane is always
+      used and fusion is the flat bucketed buffer.  ``hierarchical_nccl`` maps
+      to ``hierarchical``.
     """
     if hierarchical_nccl:
         hierarchical = True
     return _SynchronousSGD(optimizer, named_parameters, op=op, fused=fused, bucket_mb=bucket_mb,
-                           comm_dtype=comm_dtype, hierarchical=hierarchical, monitor=monitor, overlap=overlap)
+                           comm_dtype=comm_dtype, hierarchical=hierarchical, monitor=monitor, overlap=overlap,
+                           force_comm=force_comm, flat=flat, first_bucket_mb=first_bucket_mb)

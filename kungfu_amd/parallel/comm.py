@@ -6,16 +6,31 @@ broadcasting ``ncclUniqueId`` over the KungFu host transport, re-created after
 an elastic resize (``ResetNcclHelper``, ``ops/gpu/scheduler.cpp:54-68``), and a
 local (per-host) communicator for the hierarchical path.
 
-MI355X design: collectives run on a dedicated high-priority HIP stream and are
-ordered against compute with events -- no ``hipStreamSynchronize`` on the hot
-path (the reference synchronises after every NCCL op).
+MI355X design: collectives run on a dedicated HIP stream and are ordered
+against compute with events -- no ``hipStreamSynchronize`` on the hot path
+(the reference synchronises after every NCCL op).
+
+Every communicator class exposes the same stream-ordering surface, which the
+training engines (``ddp.GradReducer``, SMA, AdaSGD, the monitors) use instead
+of touching HIP streams directly, so the same engine code also runs over the
+host transport (CPU tensors, or GPU ranks that share one device):
+
+* ``fence()``      -- the comm stream waits for work issued so far on compute;
+* ``on_stream()``  -- context manager: issue kernels on the comm stream;
+* ``join()``       -- the compute stream waits for everything on the comm stream.
+
+Communicators are cached per (scope, plane) and keyed by the cluster version:
+:func:`get_device_comm` rebuilds one lazily after an elastic resize, and
+:func:`comm_epoch` lets long-lived users (bucket reducers, optimizers) notice
+that they must re-bind (see ``GradReducer._bind``).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
-from typing import Optional
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -23,8 +38,8 @@ from .._lib import dtype_code, hip, op_code, runtime
 
 _U8 = 0
 _lock = threading.Lock()
-_global: Optional["DeviceComm"] = None
-_local: Optional["DeviceComm"] = None
+_comms: Dict[Tuple[str, str], object] = {}
+_epoch = [0]  # bumped by every reset/destroy: users re-bind when it changes
 
 
 def _bcast_bytes(data: bytes, name: str) -> bytes:
@@ -41,19 +56,41 @@ def _local_bcast_bytes(data: bytes, name: str) -> bytes:
     return buf.raw
 
 
-class DeviceComm:
+def _scope_rank_size(scope: str):
+    if scope == "global":
+        return runtime.rank(), runtime.size()
+    return runtime.local_rank(), runtime.local_size()
+
+
+class _StreamOrdered:
+    """fence / on_stream / join over ``self.stream`` (a torch.cuda.Stream, or None on CPU)."""
+
+    stream = None
+    device = None
+
+    def fence(self):
+        if self.stream is not None:
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+
+    def on_stream(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def join(self):
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+
+class DeviceComm(_StreamOrdered):
     """RCCL communicator + comm stream for the current cluster version."""
+
+    plane = "rccl"
 
     def __init__(self, scope: str = "global"):
         H = hip()
         self.scope = scope
         self.version = runtime.cluster_version()
-        if scope == "global":
-            self.rank, self.size = runtime.rank(), runtime.size()
-            leader = self.rank == 0
-        else:
-            self.rank, self.size = runtime.local_rank(), runtime.local_size()
-            leader = self.rank == 0
+        self.rank, self.size = _scope_rank_size(scope)
+        leader = self.rank == 0
         self.device = torch.cuda.current_device()
         uid = H.rccl_unique_id() if leader else bytes(128)
         name = "kungfu::rccl_uid::%s::v%d" % (scope, self.version)
@@ -137,80 +174,134 @@ class DeviceComm:
             self.comm = None
 
 
-class HostStagedComm:
-    """The DeviceComm interface over the host runtime (TCP/UDS graph collectives),
-    staging through pinned host memory.  Selected with ``KUNGFU_GPU_DATAPLANE=host``:
-    for ranks that share one GPU (RCCL refuses duplicate devices) and hosts
-    without a usable RCCL.  Every call synchronises its stream -- a functional
-    fallback, not a fast path.  Op names are sequence numbers, which match
-    across ranks because every rank issues the same collective sequence (the
-    ordered scheduler guarantees it for the bucket engine)."""
+class HostComm(_StreamOrdered):
+    """The DeviceComm interface over the host runtime (TCP/UDS graph collectives).
 
-    def __init__(self, scope: str = "global"):
+    * ``device="cpu"``: CPU tensors, no staging, no streams -- the engines
+      (bucketed S-SGD, SMA, AdaSGD, monitors) run unchanged on CPU peers, which
+      is how their multi-process / elastic behaviour is tested without GPUs.
+    * ``device`` a GPU (``KUNGFU_GPU_DATAPLANE=host``): staged through host
+      memory, for ranks that share one GPU (RCCL refuses duplicate devices) and
+      hosts without a usable RCCL.  Every call synchronises its stream -- a
+      functional fallback, not a fast path.
+
+    Op names are sequence numbers, which match across ranks because every rank
+    issues the same collective sequence (the ordered scheduler guarantees it
+    for the bucket engine)."""
+
+    plane = "host"
+
+    def __init__(self, scope: str = "global", device=None):
         self.scope = scope
         self.version = runtime.cluster_version()
-        if scope == "global":
-            self.rank, self.size = runtime.rank(), runtime.size()
-        else:
-            self.rank, self.size = runtime.local_rank(), runtime.local_size()
-        self.device = torch.cuda.current_device()
-        self.stream = torch.cuda.Stream(device=self.device)
+        self.rank, self.size = _scope_rank_size(scope)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        self.staged = device.type == "cuda"
+        self.device = torch.cuda.current_device() if self.staged else device
+        self.stream = torch.cuda.Stream(device=self.device) if self.staged else None
         self.comm = self  # "valid" marker for get_device_comm
         self._seq = 0
 
     def _name(self, kind):
         self._seq += 1
-        return "kf:staged:%s:%s:v%d:%d" % (self.scope, kind, self.version, self._seq)
+        return "kf:hostcomm:%s:%s:v%d:%d" % (self.scope, kind, self.version, self._seq)
 
-    def _run(self, inp, out, stream, fn):
+    def _run(self, inp, out, stream, fn, write=True):
+        """fn(h) on a contiguous host copy of ``inp``; the result lands in ``out``
+        (default ``inp``) when ``write``."""
+        dst = inp if out is None else out
+        if not self.staged:
+            h = inp if inp.is_contiguous() and dst is inp else inp.detach().contiguous().clone()
+            fn(h)
+            if write and h is not dst:
+                dst.copy_(h.view_as(dst))
+            return dst
         s = stream if stream is not None else self.stream
         if not isinstance(s, torch.cuda.Stream):
             s = torch.cuda.ExternalStream(int(s), device=self.device)
         with torch.cuda.stream(s):
             h = inp.detach().to("cpu").contiguous()  # synchronises s
             fn(h)
-            (inp if out is None else out).copy_(h.view_as(inp))
+            if write:
+                dst.copy_(h.view_as(dst))
             s.synchronize()
-        return inp if out is None else out
+        return dst
+
+    def _ar(self, h, op, nm):
+        red = op if op != "avg" else "sum"
+        args = (h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h))
+        if self.scope == "global":
+            runtime.all_reduce(*args, op_code(red), nm)
+        else:  # per-host: reduce to the local root, then broadcast back
+            runtime.local_reduce(*args, op_code(red), nm + ":r")
+            runtime.local_broadcast(*args, nm + ":b")
+        if op == "avg":
+            if h.is_floating_point():
+                h.div_(self.size)
+            else:
+                h.floor_divide_(self.size)
 
     def all_reduce(self, inp, out=None, op="sum", stream=None):
         nm = self._name("ar")
-        red = op if op != "avg" else "sum"
-
-        def f(h):
-            args = (h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h))
-            if self.scope == "global":
-                runtime.all_reduce(*args, op_code(red), nm)
-            else:  # per-host: reduce to the local root, then broadcast back
-                runtime.local_reduce(*args, op_code(red), nm + ":r")
-                runtime.local_broadcast(*args, nm + ":b")
-            if op == "avg":
-                h.div_(self.size)
-
-        return self._run(inp, out, stream, f)
+        return self._run(inp, out, stream, lambda h: self._ar(h, op, nm))
 
     def graph_all_reduce(self, t, op="sum", pairs=None, stream=None):
         # the host runtime executes the session's strategy graphs itself
         return self.all_reduce(t, t, op=op, stream=stream)
 
     def broadcast(self, t, root: int = 0, stream=None):
-        if root != 0:
-            raise NotImplementedError("host-staged broadcast supports root 0")
         nm = self._name("bc")
-        fn = runtime.broadcast if self.scope == "global" else runtime.local_broadcast
-        return self._run(t, None, stream, lambda h: fn(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), nm))
+        if root == 0:
+            fn = runtime.broadcast if self.scope == "global" else runtime.local_broadcast
+            return self._run(t, None, stream,
+                             lambda h: fn(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), nm))
+
+        # any other root: a sum in which every non-root contributes zeros (exact: x + 0 == x)
+        def f(h):
+            if self.rank != root:
+                h.zero_()
+            self._ar(h, "sum", nm)
+
+        return self._run(t, None, stream, f)
 
     def reduce(self, inp, out=None, op="sum", root=0, stream=None):
-        return self.all_reduce(inp, out, op, stream)
+        """Result on ``root`` only; the other ranks' ``out`` is left untouched (RCCL semantics)."""
+        nm = self._name("rd")
+        red = op if op != "avg" else "sum"
+        if root == 0:
+            fn = runtime.reduce if self.scope == "global" else runtime.local_reduce
+
+            def f(h):
+                fn(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), op_code(red), nm)
+                if op == "avg" and self.rank == 0:
+                    h.div_(self.size)
+        else:
+            def f(h):
+                self._ar(h, op, nm)
+
+        if self.rank == root:
+            return self._run(inp, out, stream, f)
+        # non-roots take part in the collective but keep their buffers
+        self._run(inp, inp.detach().clone() if out is None else out.detach().clone(), stream, f, write=False)
+        return inp if out is None else out
 
     def all_gather(self, inp, out, stream=None):
         nm = self._name("ag")
-        s = stream if stream is not None else self.stream
-        with torch.cuda.stream(s if isinstance(s, torch.cuda.Stream) else torch.cuda.ExternalStream(int(s))):
+
+        def run():
             h = inp.detach().to("cpu").contiguous()
             ho = torch.empty((self.size,) + tuple(h.shape), dtype=h.dtype)
             runtime.all_gather(h.data_ptr(), ho.data_ptr(), h.numel(), dtype_code(h), nm)
             out.copy_(ho.view_as(out))
+
+        if not self.staged:
+            run()
+            return out
+        s = stream if stream is not None else self.stream
+        with torch.cuda.stream(s if isinstance(s, torch.cuda.Stream) else torch.cuda.ExternalStream(int(s))):
+            run()
         return out
 
     def reduce_scatter(self, inp, out, op="sum", stream=None):
@@ -230,40 +321,55 @@ class HostStagedComm:
         self.comm = None
 
 
+# Kept for callers of the round-1 name.
+HostStagedComm = HostComm
+
+
 def _use_host_staging() -> bool:
     return os.environ.get("KUNGFU_GPU_DATAPLANE", "rccl") == "host"
 
 
-def get_device_comm(scope: str = "global"):
-    """Current communicator; rebuilt when the cluster version changed (resize)."""
-    global _global, _local
+def comm_epoch() -> int:
+    """Changes whenever the communicators are reset (elastic resize) -- users
+    that cached a communicator compare it with the value they bound at."""
+    return _epoch[0]
+
+
+def get_device_comm(scope: str = "global", device=None):
+    """Current communicator for ``scope`` ("global" or "local"); rebuilt when the
+    cluster version changed (resize).  ``device`` selects the plane: a CPU
+    device gives the host-transport :class:`HostComm`, otherwise RCCL (or the
+    host-staged fallback under ``KUNGFU_GPU_DATAPLANE=host``)."""
     from ..python import _ensure
 
     _ensure()
+    cpu = device is not None and torch.device(device).type == "cpu"
+    kind = "cpu" if cpu else ("staged" if _use_host_staging() else "rccl")
     with _lock:
         ver = runtime.cluster_version()
-        cur = _global if scope == "global" else _local
+        cur = _comms.get((scope, kind))
         if cur is None or cur.version != ver or cur.comm is None:
             if cur is not None:
                 cur.destroy()
-            cur = HostStagedComm(scope) if _use_host_staging() else DeviceComm(scope)
-            if scope == "global":
-                _global = cur
+            if kind == "cpu":
+                cur = HostComm(scope, device="cpu")
+            elif kind == "staged":
+                cur = HostComm(scope)
             else:
-                _local = cur
+                cur = DeviceComm(scope)
+            _comms[(scope, kind)] = cur
         return cur
 
 
 def destroy_device_comm():
-    global _global, _local
     with _lock:
-        for c in (_global, _local):
-            if c is not None:
-                try:
-                    c.destroy()
-                except Exception:
-                    pass
-        _global = _local = None
+        for c in _comms.values():
+            try:
+                c.destroy()
+            except Exception:
+                pass
+        _comms.clear()
+        _epoch[0] += 1
 
 
 def reset_device_comm():

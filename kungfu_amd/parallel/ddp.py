@@ -2,29 +2,47 @@
 
 Parity: the reference's gradient synchronisation for S-SGD --
 ``srcs/python/kungfu/tensorflow/optimizers/sync_sgd.py:78-109`` (per-tensor or
-fused NCCL all-reduce, then divide by np) and the NCCL order scheduler
+fused NCCL all-reduce, then divide by np), the NCCL order scheduler
 (``srcs/cpp/src/nccl/scheduler.cpp:9-131``: identical collective order on
-every rank, learned from rank 0's arrival order).
+every rank, learned from rank 0's arrival order) and the NCCL re-initialisation
+after a resize (``srcs/cpp/src/tensorflow/ops/gpu/scheduler.cpp:54-68``).
 
 MI355X design:
 * gradients are views of one flat buffer (:class:`FlatParamSpace`); buckets
   are contiguous slices of it, in backward order, so each bucket is one
   in-place RCCL all-reduce -- no pack/unpack.
 * a post-accumulate-grad hook counts ready grads per bucket; when a bucket is
-  complete it is launched on the high-priority comm stream after an event on
-  the compute stream, overlapping with the rest of backward.
+  complete it is launched on the comm stream (normal priority, see
+  ``comm.py``) after an event on the compute stream, overlapping with the rest
+  of backward.
 * buckets are launched in one fixed order on every rank (a ready bucket waits
-  for its predecessors): index order first, then -- from the first step whose
-  bucket completions are known -- rank 0's observed completion order,
+  for its predecessors): index order first, then -- from the second step after
+  (re)binding to a communicator -- rank 0's observed completion order,
   broadcast once (the reference scheduler's auto-order), decided by the native
   ``kungfu::OrderedScheduler`` (csrc/runtime/scheduler.cpp).
 * an autograd end-of-backward callback launches any bucket whose params got
   no gradient (unused params keep zeros) and makes the compute stream wait
   for the comm stream, so ``loss.backward()`` returns with the reduced
   gradients correctly ordered before the optimizer kernels -- no host sync.
+* the communicator is bound lazily, at the first gradient of a backward, and
+  re-bound whenever the cluster changed (elastic resize): the peer count
+  (``skip``), the scheduler and its learned order are rebuilt for the new
+  membership.  Nothing collective happens in the constructor, so a worker
+  that joins a running job constructs its optimizer without blocking on
+  peers that are still inside their own step.
+* a gradient that arrives after its bucket was launched (a parameter used
+  more times than during the step the engine learned from) is an error, as in
+  ``torch.nn.parallel.DistributedDataParallel``: the autograd engine has
+  already accumulated it into the slice RCCL is reducing, so the step cannot
+  be repaired consistently on every rank.  Parameters used several times per
+  step are fine (their accumulation count is learned on the first step);
+  models whose use count changes between steps need ``overlap=False``.
 * bucket sizing: the first bucket is small (starts communication early), the
   rest default to 32 MiB: few, large collectives suit RCCL rings over the
   point-to-point xGMI links; tunable via ``KUNGFU_BUCKET_MB``.
+* ``comm_dtype=torch.bfloat16`` halves the bytes on the wire: the bucket is
+  cast into a persistent bf16 comm buffer on the comm stream (HIP kernel),
+  reduced there, and cast back (f32 accumulation stays in the flat buffer).
 """
 from __future__ import annotations
 
@@ -35,7 +53,7 @@ from typing import List, Optional
 import torch
 
 from ..utils.trace import traced
-from .comm import get_device_comm
+from .comm import comm_epoch, get_device_comm
 from .flat import FlatParamSpace
 
 
@@ -50,23 +68,33 @@ class Bucket:
         self.staged_off: List[int] = []
 
 
+class LateGradientError(RuntimeError):
+    pass
+
+
 class GradReducer:
     def __init__(self, space: FlatParamSpace, op: str = "avg", bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
                  skip_single: bool = True):
         # skip_single: with one peer the average of the gradients IS the local
         # gradient, so no collective is issued (the engine's hooks still run).
+        # skip_single=False sends every bucket through the communicator even
+        # with one peer (exercises the RCCL path / stream ordering at N=1).
         self.space = space
         self.op = op
+        self.skip_single = skip_single
         cap_mb = float(os.environ.get("KUNGFU_BUCKET_MB", bucket_mb if bucket_mb is not None else 32.0))
         esz = space.flat_grad.element_size()
-        self.comm = get_device_comm()
-        self.comm_dtype = comm_dtype
+        if comm_dtype is not None and comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("comm_dtype must be float32 or bfloat16")
+        self.comm_dtype = comm_dtype if comm_dtype != space.flat_grad.dtype else None
+        if self.comm_dtype is not None and space.device.type != "cuda":
+            self.comm_dtype = None  # host transport: f32 on the wire
+        self._cbuf: Optional[torch.Tensor] = None
         # KUNGFU_GPU_ALLREDUCE=graph: buckets follow the session's KungFu strategy graphs
         # (set_tree / set_strategy / adaptation) as device send/recv rounds instead of RCCL's
         # own all-reduce algorithm
         self.graph = os.environ.get("KUNGFU_GPU_ALLREDUCE", "rccl") == "graph"
-        self.skip = skip_single and self.comm.size == 1
         self.buckets: List[Bucket] = []
         cap = max(1, int(first_bucket_mb * (1 << 20) / esz))
         start = None
@@ -97,17 +125,17 @@ class GradReducer:
         # every bucket at the end of backward; later steps overlap.
         self._expected: Optional[List[int]] = None
         self._fires = [0] * len(space.params)
-        # Collective order (identical on every rank): bucket index order until
-        # the auto-order step, then rank 0's observed completion order --
-        # kungfu::OrderedScheduler in the C++ runtime.
-        from .._lib import runtime
-
-        self.sched = runtime.OrderedScheduler(len(self.buckets))
+        # Communicator binding (lazy; see _bind).
+        self.comm = None
+        self.skip = True
+        self.sched = None
+        self._bound = None  # (cluster version, comm epoch) bound at
+        self._steps_bound = 0  # completed backward passes since the last (re)bind
         self._ordered = False
+        self.rebinds = 0
         self._armed = False
         self._enabled = True
         self._hooks = []
-        self._warned = False
         # Optional callbacks (used by the monitoring optimizers):
         #   pre_reduce(bucket, local_grad_view)  on the comm stream, before the all-reduce
         #   post_finish()                        on the compute stream, after all buckets
@@ -118,7 +146,50 @@ class GradReducer:
         # direct gradients (parallel/mixed.py) are delivered to put()
         self._prev_sink = getattr(space, "sink", None)
         space.sink = self
-        self._reset()
+        self._reset_buckets()
+
+    # ------------------------------------------------------------ binding
+    def _bind(self):
+        """(Re)bind to the current cluster: called at the start of every backward.
+        Cheap when nothing changed (two integer reads)."""
+        from .._lib import runtime
+
+        key = (runtime.cluster_version(), comm_epoch())
+        if key == self._bound:
+            return
+        size = runtime.size()
+        self.skip = self.skip_single and size == 1
+        self.comm = None if self.skip else get_device_comm(device=self.space.device)
+        # The learned collective order belongs to the old membership: start again
+        # from index order; the new rank 0's arrival order is adopted after one step.
+        self.sched = runtime.OrderedScheduler(len(self.buckets))
+        self._ordered = False
+        self._steps_bound = 0
+        if self._bound is not None:
+            self.rebinds += 1
+        self._bound = key
+
+    @property
+    def bytes_per_step(self) -> int:
+        """Bytes each rank hands to the collective per step (0 when skipped)."""
+        if self.skip:
+            return 0
+        esz = torch.empty((), dtype=self.comm_dtype or self.space.flat_grad.dtype).element_size()
+        return self.space.numel * esz
+
+    def describe(self) -> dict:
+        from .._lib import runtime
+
+        return {
+            "buckets": len(self.buckets),
+            "bucket_mb": round(max(b.end - b.start for b in self.buckets) * self.space.flat_grad.element_size()
+                               / (1 << 20), 2),
+            "comm_ranks": (self.comm.size if self.comm is not None else runtime.size()),
+            "comm_plane": ("skip" if self.skip else getattr(self.comm, "plane", "?")),
+            "comm_dtype": str(self.comm_dtype or self.space.flat_grad.dtype).replace("torch.", ""),
+            "comm_bytes_per_step": self.bytes_per_step,
+            "overlap": True,
+        }
 
     # ------------------------------------------------------------------ hooks
     def _make_hook(self, i: int):
@@ -142,7 +213,9 @@ class GradReducer:
         buffer by one multi-tensor kernel when its bucket launches."""
         b = self.param_bucket[i]
         o, n = self.space.offsets[i]
-        if (not self._enabled or b.launched or g.dtype not in (torch.bfloat16, torch.float32)
+        if self._enabled and b.launched:
+            self._late(i)
+        if (not self._enabled or g.dtype not in (torch.bfloat16, torch.float32)
                 or g.stride() != self.space.strides[i] or not g.is_cuda):
             with torch.no_grad():
                 self.space.grad_view(i).add_(g)
@@ -152,20 +225,26 @@ class GradReducer:
         if self._enabled:
             self._mark(i)
 
+    def _late(self, i: int):
+        if self.skip:  # no collective in flight: the late gradient simply accumulates
+            return
+        raise LateGradientError(
+            "kungfu_amd: parameter %r received a gradient after its bucket's all-reduce was launched "
+            "(it was used more often in this backward than in the step the engine learned from). Use "
+            "SynchronousSGDOptimizer(..., overlap=False) for models whose parameter use changes between "
+            "steps." % self.space.names[i])
+
     def _mark(self, i: int):
         if not self._armed:
             self._armed = True
+            self._bind()
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
         self._fires[i] += 1
         if self._expected is None:
             return
         b = self.param_bucket[i]
         if b.launched:
-            if not self._warned:
-                self._warned = True
-                print("[kungfu_amd] warning: parameter %s received a gradient after its bucket was "
-                      "reduced (dynamic graph); overlap disabled" % self.space.names[i])
-            self._expected = None
+            self._late(i)
             return
         b.pending -= 1
         if b.pending == 0:
@@ -187,19 +266,22 @@ class GradReducer:
         if self.skip:
             return
         comm = self.comm
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(comm.device))
-        comm.stream.wait_event(ev)
+        comm.fence()
         g = self.space.flat_grad[b.start:b.end]
         if self.pre_reduce is not None:
-            with torch.cuda.stream(comm.stream):
+            with comm.on_stream():
                 self.pre_reduce(b, g)
-        if self.comm_dtype is not None and self.comm_dtype != g.dtype:
-            with torch.cuda.stream(comm.stream):
-                c = g.to(self.comm_dtype)
-                self._reduce(comm, c)
-                g.copy_(c)
-                c.record_stream(comm.stream)
+        if self.comm_dtype is not None:
+            from .._lib import hip
+
+            if self._cbuf is None:
+                self._cbuf = torch.empty(self.space.numel, dtype=self.comm_dtype, device=self.space.device)
+            c = self._cbuf[b.start:b.end]
+            with comm.on_stream():
+                hip().cast_copy(c, g, 1.0)
+            self._reduce(comm, c)
+            with comm.on_stream():
+                hip().cast_copy(g, c, 1.0)
         else:
             self._reduce(comm, g)
 
@@ -209,7 +291,7 @@ class GradReducer:
             return
         comm.graph_all_reduce(g, op="sum")
         if self.op == "avg":
-            with torch.cuda.stream(comm.stream):
+            with comm.on_stream():
                 g.mul_(1.0 / comm.size)
 
     def _finish(self):
@@ -217,24 +299,29 @@ class GradReducer:
             if not self.buckets[j].launched:
                 self._launch(self.buckets[j])
         if not self.skip:
-            torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
-        if self._expected is not None and not self._ordered and not self.skip:
-            # first step with known bucket completion: every rank adopts rank 0's
-            # arrival order for its collectives from now on (native auto-order)
-            self.sched.auto_order()
-            self._ordered = True
-        if self._expected is None and not self._warned:
+            self.comm.join()
+            if self._steps_bound == 1 and not self._ordered:
+                # second step on this communicator: every rank adopts rank 0's
+                # arrival order for its collectives from now on (native auto-order).
+                # The step count since binding is the same on every rank (old
+                # members and workers that just joined), so all of them take
+                # part in this broadcast.
+                self.sched.auto_order()
+                self._ordered = True
+        if self._expected is None:
             self._expected = list(self._fires)
-        self._reset()
+        self._steps_bound += 1
+        self._reset_buckets()
         if self.post_finish is not None:
             self.post_finish()
 
-    def _reset(self):
+    def _reset_buckets(self):
         for b in self.buckets:
             b.pending = sum(self._expected[i] for i in b.params) if self._expected is not None else 1
             b.launched = False
         self._fires = [0] * len(self.space.params)
-        self.sched.reset()
+        if self.sched is not None:
+            self.sched.reset()
         self._armed = False
 
     # ------------------------------------------------------------------ API
@@ -246,11 +333,13 @@ class GradReducer:
 
     def reduce_all_now(self):
         """Reduce every bucket immediately (for grads computed without hooks)."""
-        self._reset()
+        self._bind()
+        self._reset_buckets()
         for j in self.sched.flush():
             self._launch(self.buckets[j])
         if not self.skip:
-            torch.cuda.current_stream(self.comm.device).wait_stream(self.comm.stream)
+            self.comm.join()
+        self._reset_buckets()
 
     @contextlib.contextmanager
     def no_sync(self):

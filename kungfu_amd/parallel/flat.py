@@ -153,3 +153,25 @@ class FlatParamSpace:
 
     def state_slices(self):
         return list(zip(self.params, self.offsets))
+
+
+def axpby_(y: torch.Tensor, x: torch.Tensor, a: float, b: float) -> torch.Tensor:
+    """y <- a*y + b*x: one fused HIP kernel (K3/K4) on GPU, torch ops on CPU."""
+    if y.is_cuda:
+        from .._lib import hip
+
+        hip().axpby(y, x, None, a, b)
+    else:
+        y.mul_(a).add_(x, alpha=b)
+    return y
+
+
+def sumsq(t: torch.Tensor, other: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[sum(t^2), sum(other^2)] (f32, on t's device): one-pass K5 kernel on GPU."""
+    if t.is_cuda:
+        from .._lib import hip
+
+        return hip().sumsq2(t, other)
+    a = t.double().square().sum()
+    b = other.double().square().sum() if other is not None else torch.zeros((), dtype=torch.float64)
+    return torch.stack([a, b]).float()

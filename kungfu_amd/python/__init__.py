@@ -194,16 +194,19 @@ def print_strategy_stats() -> None:
 def get_hip_index() -> int:
     """GPU index for this worker (parity: ``_get_cuda_index``).
 
-    Under ``kungfu-run`` the worker sees exactly its GPU (HIP_VISIBLE_DEVICES),
-    so the index is 0 unless ``-allow-xgmi`` kept all GPUs visible; under
-    torchrun it is LOCAL_RANK.  ``KUNGFU_FORCE_DEVICE`` overrides (tests that
-    co-locate several peers on one GPU).
+    Under ``kungfu-run`` every GPU stays visible by default and the worker's
+    slot from the launcher's GPU pool is ``KUNGFU_HIP_DEVICE_ORDINAL`` (so RCCL
+    can use P2P/IPC over xGMI); with ``-isolate-gpus`` the worker sees exactly
+    its GPU (``HIP_VISIBLE_DEVICES``) and the index is 0.  Under torchrun it is
+    ``LOCAL_RANK``.  ``KUNGFU_FORCE_DEVICE`` overrides (tests that co-locate
+    several peers on one GPU).
     """
     if "KUNGFU_FORCE_DEVICE" in os.environ:
         return int(os.environ["KUNGFU_FORCE_DEVICE"])
     if "KUNGFU_SELF_SPEC" in os.environ:
-        if os.environ.get("KUNGFU_ALLOW_XGMI", "false") == "true":
-            return current_local_rank()
+        if os.environ.get("KUNGFU_ALLOW_XGMI", "true") == "true":
+            slot = os.environ.get("KUNGFU_HIP_DEVICE_ORDINAL")
+            return int(slot) if slot not in (None, "") else current_local_rank()
         return 0
     return int(os.environ.get("LOCAL_RANK", "0"))
 

@@ -1,0 +1,142 @@
+"""GPU tests of the S-SGD engine's data plane: the RCCL path exercised
+with one rank (``force_comm``), bf16 gradients on the wire, and elastic resize of the
+GPU optimizers (2 ranks sharing the GPU over the host-staged plane)."""
+import re
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import free_port_block, kungfu_run, worker
+
+pytestmark = pytest.mark.gpu
+needs_gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+
+
+@pytest.fixture(scope="module")
+def H():
+    from kungfu_amd._lib import hip
+
+    return hip()
+
+
+@needs_gpu
+@pytest.mark.parametrize("n", [1, 7, 4096, (1 << 20) + 5])
+def test_cast_copy_kernel(H, n):
+    x = torch.randn(n, device="cuda") * 3
+    b = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    H.cast_copy(b, x, 0.5)
+    assert torch.equal(b, (x * 0.5).bfloat16())
+    y = torch.empty(n, device="cuda")
+    H.cast_copy(y, b, 2.0)
+    assert torch.equal(y, b.float() * 2.0)
+
+
+def _mlp_run(force_comm, comm_dtype=None, steps=3):
+    import kungfu_amd as kf
+
+    kf.init()
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 10)).cuda()
+    opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9),
+                                                force_comm=force_comm, comm_dtype=comm_dtype)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    grads = []
+    for _ in range(steps):
+        x = torch.randn(32, 64, device="cuda", generator=g)
+        y = torch.randint(0, 10, (32,), device="cuda", generator=g)
+        opt.zero_grad()
+        F.cross_entropy(m(x), y).backward()
+        grads.append(opt.space.flat_grad.clone())
+        opt.step()
+    torch.cuda.synchronize()
+    return opt, grads
+
+
+@needs_gpu
+def test_force_comm_rccl_one_rank_matches_skip():
+    """Every bucket through the comm stream + events + a 1-rank RCCL all-reduce (avg):
+    bit-identical to the skip path, and the reducer reports the RCCL plane."""
+    o_skip, g_skip = _mlp_run(False)
+    o_rccl, g_rccl = _mlp_run(True)
+    d = o_rccl.reducer.describe()
+    assert d["comm_plane"] == "rccl" and d["comm_ranks"] == 1 and d["comm_bytes_per_step"] > 0, d
+    assert o_skip.reducer.describe()["comm_plane"] == "skip"
+    for a, b in zip(g_skip, g_rccl):
+        assert torch.equal(a, b)
+    assert torch.equal(o_skip.space.flat_param, o_rccl.space.flat_param)
+
+
+@needs_gpu
+def test_bf16_gradient_comm_within_rounding():
+    """bf16 on the wire: the averaged gradient equals the f32 one rounded to bf16."""
+    _, g32 = _mlp_run(True, steps=1)
+    o16, g16 = _mlp_run(True, comm_dtype=torch.bfloat16, steps=1)
+    assert o16.reducer.describe()["comm_dtype"] == "bfloat16"
+    assert torch.equal(g16[0], g32[0].bfloat16().float())
+
+
+@needs_gpu
+def test_gns_single_peer_keeps_state(H):
+    """B == b (one peer): the device GNS update leaves its state untouched (no inf/NaN)."""
+    st = torch.zeros(4, device="cuda")
+    one = torch.ones(1, device="cuda")
+    H.gns_update(one, one, 32.0, 32.0, 0.6, st)
+    assert torch.equal(st, torch.zeros(4, device="cuda"))
+
+
+@needs_gpu
+def test_gns_monitor_single_gpu_runs_kernels():
+    """monitor_single: the K5 reductions run every step with one GPU (forced comm path)."""
+    import kungfu_amd as kf
+
+    kf.init()
+    torch.manual_seed(0)
+    m = torch.nn.Linear(128, 8).cuda()
+    opt = kf.optimizers.MonitorGradientNoiseScaleOptimizer(torch.optim.SGD(m.parameters(), lr=0.1),
+                                                           device_batch_size=16, monitor_single=True)
+    seen = []
+    orig = opt.reducer.post_finish
+
+    def capture():
+        seen.append(opt._local_sq.clone())  # |g_local|^2 accumulated by the per-bucket K5 pass
+        orig()
+
+    opt.reducer.post_finish = capture
+    x = torch.randn(16, 128, device="cuda")
+    opt.zero_grad()
+    m(x).square().mean().backward()
+    local = seen[0]
+    ref = opt.space.flat_grad.double().square().sum()
+    assert abs(local.item() / ref.item() - 1) < 1e-5
+    opt.step()
+    assert opt.noise_scale is None  # undefined with one peer
+
+
+@needs_gpu
+def test_elastic_resnet18_gns_two_ranks_one_gpu():
+    """kungfu-run -w with 2 ranks sharing the GPU (host-staged plane), ResNet-18 with the
+    gradient-noise-scale monitor through 1 -> 2 -> 1 peers: after every step all replicas
+    hold bit-identical flat parameters and the monitor reports a finite noise scale while
+    two peers train (VERDICT r1 'Next round' #1)."""
+    base = free_port_block(16)
+    cfg = base + 15
+    r = kungfu_run(1, [worker("elastic_train.py"), "--schedule", "1:3,2:3,1:3", "--max-step", "9",
+                       "--optimizer", "gns", "--device", "cuda", "--model", "resnet18", "--global-batch", "16"],
+                   timeout=400, port_base=base,
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"},
+                   extra=["-w", "-builtin-config-port", str(cfg), "-config-server",
+                          "http://127.0.0.1:%d/config" % cfg, "-H", "127.0.0.1:4"])
+    assert r.returncode == 0, r.stdout[-5000:]
+    steps = re.findall(r"STEP (\d+) np=(\d+) rank=(\d+) loss=(\S+) h=(\w+)(?: gns=(\S+))?", r.stdout)
+    by = {}
+    for st, np_, rk, loss, h, gns in steps:
+        by.setdefault(int(st), []).append((int(np_), h, gns, float(loss)))
+    assert sorted(by) == list(range(9)), r.stdout[-3000:]
+    for st, rows in by.items():
+        assert len(rows) == rows[0][0], (st, rows)
+        assert len({h for _, h, _, _ in rows}) == 1, (st, rows)
+        assert all(l == l for *_, l in rows)
+    gns = [float(g) for rows in by.values() for n, _, g, _ in rows if n == 2 and g not in ("", "None")]
+    assert gns and all(g == g and abs(g) < 1e12 for g in gns), r.stdout[-3000:]
+    assert "ELASTIC_TRAIN_DONE rank=0 np=1 step=9 v=2" in r.stdout
