@@ -83,7 +83,7 @@ def main():
     names = {}
     for s, e, n, q in ks:
         if lo <= s < hi and comm_re.search(n):
-            k = re.sub(r"\(.*", "", n)[:90]
+            k = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", "").replace("void ", "", 1))[:90]
             names[k] = names.get(k, 0) + (e - s)
     for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:8]:
         print("| `%s` | %.3f ms/step |" % (k, v / a.steps / 1e6))
