@@ -8,8 +8,14 @@
 #   kungfu_amd/lib/libkungfu_amd.so       C++ runtime + extern "C" ABI
 #   kungfu_amd/_kungfu$(PYEXT)            pybind11 binding of the runtime
 #   kungfu_amd/_hip$(PYEXT)               HIP/CDNA4 kernels + RCCL controller (torch extension)
-#   bin/kungfu-run, bin/kungfu-config-server, bin/kungfu-rrun, bin/kungfu-distribute, bin/kungfu-test-util
+#   bin/kungfu-run, bin/kungfu-config-server, bin/kungfu-rrun, bin/kungfu-distribute, bin/kungfu-test-util,
+#   bin/kungfu-bad-worker
 
+# ./configure writes config.mk (build toggles); defaults: trace scopes compiled in,
+# HIP kernels + RCCL built, native tests built on demand.
+-include config.mk
+KUNGFU_ENABLE_TRACE ?= 1
+KUNGFU_ENABLE_HIP   ?= 1
 PYTHON     ?= python3
 CXX        ?= g++
 HIPCC      ?= /opt/rocm/bin/hipcc
@@ -21,6 +27,9 @@ PYEXT      := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_
 TORCH_DIR  := $(shell $(PYTHON) -c "import os,torch;print(os.path.dirname(torch.__file__))" 2>/dev/null)
 
 CXXFLAGS   := -std=c++17 -O3 -fPIC -Wall -Wextra -Wno-unused-parameter -Icsrc/include -mavx2 -mf16c -pthread $(EXTRA_CXXFLAGS)
+ifeq ($(KUNGFU_ENABLE_TRACE),0)
+CXXFLAGS   += -DKUNGFU_DISABLE_TRACE
+endif
 LDFLAGS    := -pthread -ldl $(EXTRA_LDFLAGS)
 
 RT_SRCS    := base plan log monitor transport session http peer capi model_avg scheduler
@@ -30,7 +39,8 @@ PY_MOD     := kungfu_amd/_kungfu$(PYEXT)
 
 LAUNCH_SRCS := runner job configserver_main flags
 LAUNCH_OBJS := $(patsubst %,$(BUILD)/launcher/%.o,$(LAUNCH_SRCS))
-BINS       := bin/kungfu-run bin/kungfu-config-server bin/kungfu-rrun bin/kungfu-distribute bin/kungfu-test-util
+BINS       := bin/kungfu-run bin/kungfu-config-server bin/kungfu-rrun bin/kungfu-distribute bin/kungfu-test-util \
+              bin/kungfu-bad-worker
 
 HIP_SRCS   := $(wildcard csrc/kernels/*.hip)
 HIP_OBJS   := $(patsubst csrc/kernels/%.hip,$(BUILD)/hip/%.o,$(HIP_SRCS))
@@ -43,7 +53,11 @@ TORCH_LIBS := -L$(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip
               -Wl,-rpath,$(TORCH_DIR)/lib
 
 .PHONY: all runtime hip launcher clean
+ifeq ($(KUNGFU_ENABLE_HIP),0)
+all: runtime launcher   # host-only build: no hipcc, no RCCL (CPU / gloo-style training)
+else
 all: runtime launcher hip
+endif
 runtime: $(RT_LIB) $(PY_MOD)
 launcher: $(BINS)
 hip: $(HIP_MOD)
@@ -87,6 +101,10 @@ bin/kungfu-test-util: $(BUILD)/launcher/test_util.o $(RT_OBJS)
 	@mkdir -p bin
 	$(CXX) -o $@ $^ $(LDFLAGS)
 
+bin/kungfu-bad-worker: $(BUILD)/launcher/bad_worker.o $(RT_OBJS)
+	@mkdir -p bin
+	$(CXX) -o $@ $^ $(LDFLAGS)
+
 $(BUILD)/hip/%.o: csrc/kernels/%.hip $(wildcard csrc/kernels/*.hpp)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -102,6 +120,9 @@ clean:
 	rm -rf $(BUILD) $(RT_LIB) $(PY_MOD) $(HIP_MOD) $(BINS)
 
 # ---- native tests (host only; sanitizer builds for race / memory checks) ----
+ifeq ($(KUNGFU_BUILD_TESTS),1)
+all: build/native_test build/native_test_asan build/native_test_tsan
+endif
 NT_SRCS := tests/native/test_runtime.cpp $(patsubst %,csrc/runtime/%.cpp,$(RT_SRCS))
 .PHONY: native-test native-test-asan native-test-tsan
 build/native_test: $(NT_SRCS) $(wildcard csrc/include/kungfu/*.hpp)

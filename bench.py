@@ -11,8 +11,14 @@ compute with f32 master weights, channels_last, SGD momentum 0.9 + wd 1e-4 via
 ``kungfu_amd.optimizers.SynchronousSGDOptimizer`` (bucketed RCCL all-reduce
 overlapped with backward, fused HIP SGD step), one process per GPU.
 
+BERT-base (BASELINE.json config 5): ``--model bert_base --optimizer gns`` trains the
+110 M-parameter encoder on synthetic 128-token pre-training batches (MLM on 20
+masked positions + NSP, AdamW) through S-SGD with the gradient-noise-scale
+monitor and reports sequences/s (and tokens/s in ``config``).
+
 Usage:
     python bench.py [--gpus 1] [--steps 20] [--warmup 5]
+    python bench.py --model bert_base --optimizer gns
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 Rank 0 prints ONE JSON line.
@@ -36,6 +42,8 @@ MODEL_BASELINES = {
     "resnet50": (METRIC, BASELINE_PER_GPU),
     "vgg16": ("images/sec/GPU VGG16 SynchronousSGD at 1/2/4/8 MI355X", 3330.0 / 16),
     "inception_v3": ("images/sec/GPU InceptionV3 SynchronousSGD at 1/2/4/8 MI355X", 7426.0 / 16),
+    # BASELINE.json config 5; the reference publishes no BERT number
+    "bert_base": ("sequences/sec/GPU BERT-base (seq 128) SynchronousSGD + gradient-noise-scale monitor", None),
 }
 
 
@@ -64,8 +72,10 @@ def main():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=8)
-    p.add_argument("--batch", type=int, default=256, help="images per GPU")
+    p.add_argument("--batch", type=int, default=None, help="images (sequences) per GPU: 256 (BERT: 128)")
     p.add_argument("--model", default="resnet50")
+    p.add_argument("--seq-len", type=int, default=128, help="BERT sequence length")
+    p.add_argument("--adam", type=int, default=-1, help="1: AdamW inner optimizer (default for BERT), 0: SGD momentum")
     p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada", "gns", "local"])
     p.add_argument("--force-comm", type=int, default=1,
                    help="1: S-SGD buckets go through the communicator even with one GPU (RCCL 1-rank all-reduce)")
@@ -78,6 +88,11 @@ def main():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--json-out", default=None)
     a = p.parse_args()
+    bert = a.model.startswith("bert")
+    if a.batch is None:
+        a.batch = 128 if bert else 256
+    if a.adam < 0:
+        a.adam = 1 if bert else 0
     _setup_env()
 
     import torch
@@ -101,8 +116,15 @@ def main():
         fused_bn = 1 if fb.available() else 0
     model = (get_model(a.model, fused_bn=bool(fused_bn)) if a.model.startswith("resnet") or a.model in ("inception_v3", "vgg16")
              else get_model(a.model))
-    model = model.to(dev).to(memory_format=torch.channels_last)
-    base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+    model = model.to(dev)
+    if not bert:
+        model = model.to(memory_format=torch.channels_last)
+    if a.adam:
+        base = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
+        opt_desc = "AdamW lr=1e-4 wd=0.01"
+    else:
+        base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
+        opt_desc = "SGD momentum=0.9 wd=1e-4"
     comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else None
     if a.optimizer == "ssgd":
         opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),
@@ -128,14 +150,24 @@ def main():
 
         enable_bf16_shadow(model, opt)
 
-    x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (a.batch,), device=dev)
+    if bert:
+        from kungfu_amd.models.bert import pretraining_loss, synthetic_pretraining_batch
+
+        data = synthetic_pretraining_batch(a.batch, a.seq_len, device=dev)
+
+        def compute_loss():
+            return pretraining_loss(model, data)
+    else:
+        x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (a.batch,), device=dev)
+
+        def compute_loss():
+            return F.cross_entropy(model(x).float(), y)
 
     def step():
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            out = model(x)
-        loss = F.cross_entropy(out.float(), y)
+            loss = compute_loss()
         loss.backward()
         opt.step()
         return loss
@@ -164,10 +196,11 @@ def main():
     reducer = getattr(opt, "reducer", None)
     comm_info = reducer.describe() if reducer is not None else {"comm_ranks": size}
     metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
+    unit = "sequences/sec (aggregate over n_gpus)" if bert else "images/sec (aggregate over n_gpus)"
     res = {
         "metric": metric,
         "value": round(value, 2),
-        "unit": "images/sec (aggregate over n_gpus)",
+        "unit": unit,
         "n_gpus": size,
         "steps": a.steps,
         "warmup": a.warmup,
@@ -176,18 +209,22 @@ def main():
         "scaling": "weak",
         "vs_baseline": round(value / (base_per_gpu * size), 3) if base_per_gpu else None,
         "dtype": "bf16",
-        "data": "synthetic (random 224x224x3 images, random labels; random-init weights)",
+        "data": ("synthetic (random token ids, 20 masked positions per sequence, random MLM/NSP labels; "
+                 "random-init weights)" if bert else
+                 "synthetic (random 224x224x3 images, random labels; random-init weights)"),
         "config": {
             "model": a.model,
             "global_batch": a.batch * size,
             "per_gpu_batch": a.batch,
-            "seq_len": None,
-            "image_size": 224,
+            "seq_len": a.seq_len if bert else None,
+            "image_size": None if bert else 224,
             "parallelism": "dp%d" % size,
-            "optimizer": "%s(SGD momentum=0.9 wd=1e-4)" % a.optimizer,
+            "optimizer": "%s(%s)" % (a.optimizer, opt_desc),
             "fused_bn_hip": bool(fused_bn),
             "bf16_shadow_weights": bool(a.bf16_shadow),
             "per_gpu_img_s": round(value / size, 2),
+            "tokens_per_s": round(value * a.seq_len, 1) if bert else None,
+            "gradient_noise_scale": (opt.noise_scale if a.optimizer == "gns" else None),
             "baseline_per_gpu_img_s": round(base_per_gpu, 1) if base_per_gpu else None,
             "warmup_s": round(warm_s, 1),
             "initial_loss": round(first_loss, 4) if first_loss is not None else None,

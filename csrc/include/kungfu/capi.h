@@ -51,6 +51,10 @@ int kungfu_local_reduce(const void *send, void *recv, size_t count, int dtype, i
 int kungfu_local_broadcast(const void *send, void *recv, size_t count, int dtype, const char *name);
 int kungfu_gather(const void *send, size_t count, int dtype, void *recv, const char *name);
 int kungfu_all_gather(const void *send, size_t count, int dtype, void *recv, const char *name);
+/* gather to rank 0 -> rank 0 runs transform(gathered [np x count], out, arg) -> broadcast out_bytes of out */
+typedef void (*kungfu_transform_t)(const void *gathered, void *out, void *arg);
+int kungfu_all_gather_transform(const void *send, size_t count, int dtype, void *out, size_t out_bytes,
+                                kungfu_transform_t transform, void *arg, const char *name);
 
 int kungfu_save(const char *name, const void *data, size_t len);
 int kungfu_save_version(const char *version, const char *name, const void *data, size_t len);

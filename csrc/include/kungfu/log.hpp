@@ -71,6 +71,13 @@ void trace_record(const std::string &name, double seconds);
 
 #define KF_TRACE_CAT2(a, b) a##b
 #define KF_TRACE_CAT(a, b) KF_TRACE_CAT2(a, b)
+// Compile-time switch (./configure --disable-trace => -DKUNGFU_DISABLE_TRACE): scopes
+// compile to nothing, like the reference's stdtracer-less build (utils/trace.hpp:1-16).
+// Otherwise they are runtime-gated by KUNGFU_CONFIG_ENABLE_TRACE.
+#ifdef KUNGFU_DISABLE_TRACE
+#define KF_TRACE_SCOPE(name) ((void)0)
+#else
 #define KF_TRACE_SCOPE(name) ::kungfu::TraceScope KF_TRACE_CAT(_kf_trace_, __LINE__)(name)
+#endif
 
 }  // namespace kungfu

@@ -23,6 +23,8 @@
 namespace kungfu {
 
 uint32_t parse_ipv4(const std::string &s);  // throws on error
+// dotted IPv4, or a host / DNS name resolved to its first IPv4 address (throws on error)
+uint32_t resolve_ipv4(const std::string &host);
 std::string format_ipv4(uint32_t ip);
 
 struct PeerID {

@@ -98,6 +98,13 @@ class Session {
     void local_broadcast(const Workspace &w);
     void gather(const Workspace &w);      // recv has count*np on root
     void all_gather(const Workspace &w);  // recv has count*np everywhere
+    // Gather every peer's `send` (count x dtype) to rank 0, let rank 0 compute
+    // `out_bytes` of output from the gathered [np x count] buffer with `f`, and
+    // broadcast that output to every peer (parity: kungfu::Peer::AllGatherTransform,
+    // srcs/cpp/src/session.cpp:162-181; used for topology-from-latencies flows).
+    void all_gather_transform(const void *send, size_t count, DType dtype, void *out, size_t out_bytes,
+                              const std::function<void(const void *gathered, void *out)> &f,
+                              const std::string &name);
 
     // Adaptation
     bool set_global_strategy(const StrategyList &sl);  // barrier+consensus+swap+barrier
@@ -112,6 +119,16 @@ class Session {
     void calc_stats();
 
     std::vector<double> peer_latencies();
+
+    // Named point-to-point transfers on the collective channel: the host-staged
+    // backend of the device graph plane runs plan_graph_all_reduce rounds with them.
+    void send_to(int rank, const std::string &name, const void *data, size_t len);
+    void recv_from(int rank, const std::string &name, void *buf, size_t len);
+    // Device planes (RCCL graph all-reduce timed with HIP events) report monitored
+    // collectives here, so calc_stats / check_interference see GPU traffic too
+    // (adaptiveStrategies.go:61-121, monitoring.go:15-35).  Times are seconds on
+    // any clock that is consistent within one stats window.
+    void record_strategy_stat(double begin, double end, uint64_t bytes);
 
   private:
     void run_graphs(const Workspace &w, const std::vector<const Graph *> &graphs);

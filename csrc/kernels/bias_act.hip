@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_fwd_kernel(uint4 *__restrict_
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             f[k] += b[k];
-            if (RELU) f[k] = f[k] > 0.f ? f[k] : 0.f;
+            if (RELU) f[k] = !(f[k] <= 0.f) ? f[k] : 0.f;  // NaN stays NaN (torch.relu)
         }
         y[i] = pack8v(f);
     }

@@ -59,8 +59,9 @@ __global__ __launch_bounds__(kBlock) void maxpool2_fwd_kernel(const uint4 *__res
 #pragma unroll
             for (int p = 1; p < 4; ++p) {
                 const uint32_t w = bits_of(v[p], k);
-                if (lo16(w) > ml) ml = lo16(w), bl = w & 0xffffu;
-                if (hi16(w) > mh) mh = hi16(w), bh = w >> 16;
+                // NaN propagates like torch's max-pool: a NaN always takes the window
+                if (lo16(w) > ml || isnan(lo16(w))) ml = lo16(w), bl = w & 0xffffu;
+                if (hi16(w) > mh || isnan(hi16(w))) mh = hi16(w), bh = w >> 16;
             }
             out[k] = bl | (bh << 16);
         }
@@ -88,8 +89,8 @@ __global__ __launch_bounds__(kBlock) void maxpool2_bwd_kernel(const uint4 *__res
 #pragma unroll
             for (int p = 1; p < 4; ++p) {
                 const uint32_t w = bits_of(v[p], k);
-                if (lo16(w) > ml) ml = lo16(w), pl = p;
-                if (hi16(w) > mh) mh = hi16(w), ph = p;
+                if (lo16(w) > ml || isnan(lo16(w))) ml = lo16(w), pl = p;
+                if (hi16(w) > mh || isnan(hi16(w))) mh = hi16(w), ph = p;
             }
             const uint32_t gw = bits_of(gv, k);
 #pragma unroll

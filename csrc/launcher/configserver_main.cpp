@@ -37,7 +37,7 @@ int kungfu_run_main(int argc, char **argv) {
     }
     uint32_t self_ip;
     try {
-        self_ip = infer_self_ipv4(f.self, f.nic);
+        self_ip = infer_self_ipv4(f.self, f.nic, f.hosts);
     } catch (const std::exception &e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

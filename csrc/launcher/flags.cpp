@@ -219,8 +219,31 @@ ContainerInfo parse_modelarts_env() {
     return info;
 }
 
+std::vector<uint32_t> local_ipv4s() {
+    std::vector<uint32_t> out;
+    ifaddrs *ifa = nullptr;
+    if (getifaddrs(&ifa) != 0) return out;
+    for (auto *p = ifa; p; p = p->ifa_next)
+        if (p->ifa_addr && p->ifa_addr->sa_family == AF_INET)
+            out.push_back(ntohl(reinterpret_cast<sockaddr_in *>(p->ifa_addr)->sin_addr.s_addr));
+    freeifaddrs(ifa);
+    return out;
+}
+
+uint32_t infer_self_ipv4(const std::string &self, const std::string &nic, const HostList &hosts) {
+    if (self.empty() && nic.empty()) {
+        // no hint: the local address that appears in the host list (so `-H node1:8,node2:8`
+        // works unchanged on every node), else loopback
+        auto mine = local_ipv4s();
+        for (auto &h : hosts)
+            for (uint32_t ip : mine)
+                if (h.ipv4 == ip) return ip;
+    }
+    return infer_self_ipv4(self, nic);
+}
+
 uint32_t infer_self_ipv4(const std::string &self, const std::string &nic) {
-    if (!self.empty()) return parse_ipv4(self);
+    if (!self.empty()) return resolve_ipv4(self);
     if (!nic.empty()) {
         ifaddrs *ifa = nullptr;
         if (getifaddrs(&ifa) != 0) throw std::runtime_error("getifaddrs failed");

@@ -71,6 +71,9 @@ struct Flags {
 };
 
 uint32_t infer_self_ipv4(const std::string &self, const std::string &nic);
+// ... and, with neither hint, the local IPv4 that appears in the host list
+uint32_t infer_self_ipv4(const std::string &self, const std::string &nic, const HostList &hosts);
+std::vector<uint32_t> local_ipv4s();
 
 // Platform peer discovery (ModelArts DLS_* / BATCH_CUSTOM<i>_HOSTS env).
 struct ContainerInfo {

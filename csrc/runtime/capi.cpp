@@ -189,6 +189,13 @@ int kungfu_all_gather(const void *send, size_t count, int dtype, void *recv, con
     KF_CAPI_TRY(require_session()->all_gather(ws(send, recv, count, dtype, 0, name)))
 }
 
+int kungfu_all_gather_transform(const void *send, size_t count, int dtype, void *out, size_t out_bytes,
+                                kungfu_transform_t transform, void *arg, const char *name) {
+    KF_CAPI_TRY(require_session()->all_gather_transform(
+        send, count, static_cast<DType>(dtype), out, out_bytes,
+        [&](const void *g, void *o) { transform(g, o, arg); }, name))
+}
+
 int kungfu_save(const char *name, const void *data, size_t len) { KF_CAPI_TRY(require_peer().save(name, data, len)) }
 
 int kungfu_save_version(const char *version, const char *name, const void *data, size_t len) {

@@ -1,6 +1,9 @@
 // Planning layer implementation.  See plan.hpp for the parity map.
 #include <kungfu/plan.hpp>
 
+#include <netdb.h>
+#include <netinet/in.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <map>
@@ -55,6 +58,22 @@ uint32_t parse_ipv4(const std::string &s) {
         if (v > 255) throw std::invalid_argument("invalid IPv4: " + s);
         ip = (ip << 8) | static_cast<uint32_t>(v);
     }
+    return ip;
+}
+
+uint32_t resolve_ipv4(const std::string &host) {
+    try {
+        return parse_ipv4(host);
+    } catch (const std::invalid_argument &) {
+    }
+    // hostname / DNS name (parity: runner/discovery.go resolution of -H entries)
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_INET;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res)
+        throw std::invalid_argument("cannot resolve host: " + host);
+    uint32_t ip = ntohl(reinterpret_cast<sockaddr_in *>(res->ai_addr)->sin_addr.s_addr);
+    freeaddrinfo(res);
     return ip;
 }
 
@@ -201,7 +220,7 @@ HostSpec HostSpec::parse(const std::string &s) {
     auto parts = split(s, ':');
     if (parts.empty() || parts.size() > 3) throw std::invalid_argument("invalid host spec: " + s);
     HostSpec h;
-    h.ipv4 = parse_ipv4(parts[0]);
+    h.ipv4 = resolve_ipv4(parts[0]);
     h.slots = parts.size() >= 2 ? std::stoi(parts[1]) : 1;
     h.public_addr = parts.size() == 3 ? parts[2] : parts[0];
     if (h.slots < 0) throw std::invalid_argument("invalid slots: " + s);

@@ -327,6 +327,35 @@ PYBIND11_MODULE(_kungfu, m) {
         py::gil_scoped_release r;
         return s->set_global_strategy(sl);
     });
+    m.def("all_gather_transform", [](uintptr_t send, size_t count, int dt, uintptr_t out, size_t out_bytes,
+                                     py::function f, const std::string &name) {
+        auto s = require_session();
+        const size_t esz = dtype_size(static_cast<DType>(dt));
+        const int np = s->size();
+        py::gil_scoped_release r;
+        s->all_gather_transform(reinterpret_cast<const void *>(send), count, static_cast<DType>(dt),
+                                reinterpret_cast<void *>(out), out_bytes,
+                                [&](const void *g, void *o) {
+                                    py::gil_scoped_acquire a;
+                                    // f(gathered_ptr, gathered_bytes, out_ptr, out_bytes) on rank 0
+                                    f(reinterpret_cast<uintptr_t>(g), count * esz * np, reinterpret_cast<uintptr_t>(o),
+                                      out_bytes);
+                                },
+                                name);
+    }, "gather to rank 0, transform there with f(gathered_ptr, nbytes, out_ptr, out_bytes), broadcast out");
+    m.def("send_to", [](int rank, const std::string &name, uintptr_t data, size_t nbytes) {
+        auto s = require_session();
+        py::gil_scoped_release r;
+        s->send_to(rank, name, reinterpret_cast<const void *>(data), nbytes);
+    }, "named point-to-point send on the collective channel");
+    m.def("recv_from", [](int rank, const std::string &name, uintptr_t buf, size_t nbytes) {
+        auto s = require_session();
+        py::gil_scoped_release r;
+        s->recv_from(rank, name, reinterpret_cast<void *>(buf), nbytes);
+    }, "named point-to-point receive (exact size)");
+    m.def("record_strategy_stat", [](double begin, double end, uint64_t bytes) {
+        require_session()->record_strategy_stat(begin, end, bytes);
+    }, "account a monitored collective of a device plane to the current global strategy");
     m.def("calc_stats", [] { require_session()->calc_stats(); });
     m.def("log_stats", [] { require_session()->log_stats(); });
     m.def("strategy_throughputs", [] { return require_session()->strategy_throughputs(); });

@@ -463,6 +463,39 @@ bool Session::check_interference() {
     return total > size() / 2;
 }
 
+void Session::all_gather_transform(const void *send, size_t count, DType dtype, void *out, size_t out_bytes,
+                                   const std::function<void(const void *, void *)> &f, const std::string &name) {
+    const size_t esz = dtype_size(dtype);
+    std::vector<char> gathered(rank_ == 0 ? count * esz * size() : 0);
+    gather(Workspace{send, gathered.data(), count, dtype, ReduceOp::SUM, name + ":gather"});
+    if (rank_ == 0) f(gathered.data(), out);
+    broadcast(Workspace{out, out, out_bytes, DType::U8, ReduceOp::SUM, name + ":bcast"});
+}
+
+void Session::send_to(int rank, const std::string &name, const void *data, size_t len) {
+    if (rank < 0 || rank >= size() || rank == rank_) throw std::invalid_argument("send_to: bad rank");
+    router_->client().send(peers_[rank], ConnType::COLLECTIVE, name, data, len, kNoFlag);
+}
+
+void Session::recv_from(int rank, const std::string &name, void *buf, size_t len) {
+    if (rank < 0 || rank >= size() || rank == rank_) throw std::invalid_argument("recv_from: bad rank");
+    std::vector<char> b = router_->collective().recv(peers_[rank], name);
+    if (b.size() != len) throw std::runtime_error("kungfu: size mismatch in " + name);
+    if (len) std::memcpy(buf, b.data(), len);
+    BufferPool::get().put(std::move(b));
+}
+
+void Session::record_strategy_stat(double begin, double end, uint64_t bytes) {
+    std::vector<std::shared_ptr<StrategyStat>> sts;
+    {
+        std::lock_guard<std::mutex> lk(strat_mu_);
+        for (auto &p : global_) sts.push_back(p.stat);
+    }
+    if (sts.empty()) return;
+    // every strategy of the list carried an equal share of the chunks
+    for (auto &st : sts) st->update(begin, end, bytes / sts.size());
+}
+
 std::vector<double> Session::peer_latencies() {
     std::vector<double> out(peers_.size(), 0.0);
     std::vector<std::function<void()>> fs;

@@ -53,18 +53,45 @@ class BertForPreTraining(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
-    def forward(self, ids, types=None):
+    def forward(self, ids, types=None, mlm_positions=None):
+        """Returns (MLM logits, NSP logits).  With ``mlm_positions`` ([B, P] token indices,
+        the masked positions: 20 per 128-token sequence in BERT pre-training) only those
+        positions go through the MLM head -- the vocabulary projection is the largest GEMM
+        of the model, and pre-training never needs it for unmasked tokens."""
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
         types = torch.zeros_like(ids) if types is None else types
         x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ(types))
         for layer in self.layers:
             x = layer(x)
-        h = self.mlm_ln(F.gelu(self.mlm_dense(x)))
-        mlm = h @ self.tok.weight.t() + self.mlm_bias  # tied output embedding
+        hs = x
+        if mlm_positions is not None:
+            hs = torch.gather(x, 1, mlm_positions.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
+        h = self.mlm_ln(F.gelu(self.mlm_dense(hs)))
+        mlm = F.linear(h, self.tok.weight, self.mlm_bias)  # tied output embedding
         return mlm, self.nsp(x[:, 0])
 
 
 def bert_base(**kw):
     kw.pop("fused_bn", None)
     return BertForPreTraining(**kw)
+
+
+def synthetic_pretraining_batch(batch: int, seq_len: int = 128, vocab: int = 30522, max_predictions: int = 20,
+                                device=None, generator=None):
+    """Random BERT pre-training batch of the real shapes: token ids, segment ids, masked
+    positions (distinct per sequence) with their labels, and next-sentence labels."""
+    kw = dict(device=device, generator=generator)
+    ids = torch.randint(0, vocab, (batch, seq_len), **kw)
+    types = (torch.arange(seq_len, device=device) >= seq_len // 2).long().expand(batch, -1).contiguous()
+    pos = torch.rand(batch, seq_len, **kw).argsort(dim=1)[:, :max_predictions].sort(dim=1).values
+    mlm_labels = torch.randint(0, vocab, (batch, max_predictions), **kw)
+    nsp_labels = torch.randint(0, 2, (batch,), **kw)
+    return ids, types, pos, mlm_labels, nsp_labels
+
+
+def pretraining_loss(model, batch):
+    ids, types, pos, mlm_labels, nsp_labels = batch
+    mlm, nsp = model(ids, types, pos)
+    return (F.cross_entropy(mlm.float().reshape(-1, mlm.shape[-1]), mlm_labels.reshape(-1))
+            + F.cross_entropy(nsp.float(), nsp_labels))

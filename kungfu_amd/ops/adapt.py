@@ -92,6 +92,9 @@ def set_strategy(name: str) -> bool:
 
 def calc_stats() -> None:
     _ensure()
+    from ..parallel.comm import flush_strategy_stats
+
+    flush_strategy_stats()  # monitored device collectives (HIP-event timed) first
     runtime.calc_stats()
 
 

@@ -258,21 +258,17 @@ def monitored_all_reduce_(x: torch.Tensor, tree: Optional[Sequence[int]] = None,
     plane run the same graphs on the device: grouped send/recv rounds over xGMI + the K1
     reduce kernel (``DeviceComm.graph_all_reduce``)."""
     _ensure()
-    if x.is_cuda and not _gpu_host_staging():
+    if x.is_cuda:
+        # device graph plane (RCCL rounds, or the host-staged rounds under
+        # KUNGFU_GPU_DATAPLANE=host), timed into the strategy statistics
         c = x if x.is_contiguous() else x.contiguous()
         pairs = [(list(tree), list(tree))] if tree else None
-        _dev_comm().graph_all_reduce(c, op=op, pairs=pairs, stream=_cs())
+        _dev_comm().graph_all_reduce(c, op=op, pairs=pairs, stream=_cs(), monitored=True)
         if c is not x:
             x.copy_(c)
         return x
-
-    def run(h):
-        runtime.monitored_all_reduce(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), op_code(op),
-                                     name or _auto_name("mallreduce"), list(tree or []))
-
-    if x.is_cuda:
-        return _staged(x, run)
-    run(x)
+    runtime.monitored_all_reduce(x.data_ptr(), x.data_ptr(), x.numel(), dtype_code(x), op_code(op),
+                                 name or _auto_name("mallreduce"), list(tree or []))
     return x
 
 

@@ -128,7 +128,12 @@ def conv3x3(x: torch.Tensor, w: torch.Tensor, stride: int = 1) -> torch.Tensor:
 
 class _BiasActFn(torch.autograd.Function):
     """y = relu(y + b) in place on a conv output (csrc/kernels/bias_act.hip); backward is one
-    pass producing dy * (y > 0) and its per-channel sum (the bias gradient)."""
+    pass producing dy * (y > 0) and its per-channel sum (the bias gradient).
+
+    Determinism: the per-channel bias-gradient sum is accumulated with f32 atomics across
+    workgroups, so it is NOT bitwise reproducible between runs (differences at the f32
+    rounding level, like MIOpen's split-K paths); the gated data gradient is exact.  The
+    ReLU keeps NaN (``!(v <= 0)``), as ``torch.relu`` does."""
 
     @staticmethod
     def forward(ctx, y, b, relu):

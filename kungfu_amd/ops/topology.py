@@ -8,13 +8,13 @@ KungfuRoundRobin).  The MST itself is native (Prim, C++).
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+import ctypes
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
 from .._lib import runtime
 from ..python import _ensure
-from .collective import all_gather
 
 
 def peer_info() -> Tuple[int, int]:
@@ -42,11 +42,36 @@ def mst_father(weights: torch.Tensor, root: int = 0) -> List[int]:
     return list(runtime.minimum_spanning_tree(w.reshape(-1).tolist(), w.shape[0], root))
 
 
+def all_gather_transform(x: torch.Tensor, out_like: torch.Tensor, fn, name: Optional[str] = None) -> torch.Tensor:
+    """Native AllGatherTransform (srcs/cpp/src/session.cpp:162-181): every peer's ``x`` is
+    gathered to rank 0, ``fn(gathered [np, *x.shape]) -> tensor shaped like out_like`` runs
+    there only, and its result is broadcast to every peer."""
+    _ensure()
+    from .._lib import dtype_code
+    from .collective import _auto_name
+
+    h = x.detach().cpu().contiguous()
+    out = torch.zeros_like(out_like, device="cpu").contiguous()
+    np_ = runtime.size()
+
+    def run(gptr, gbytes, optr, obytes):
+        g = torch.frombuffer(bytearray((ctypes.c_char * gbytes).from_address(gptr)), dtype=h.dtype)
+        res = fn(g.view((np_,) + tuple(h.shape))).to(out.dtype).contiguous().view(-1)
+        ctypes.memmove(optr, res.data_ptr(), min(obytes, res.numel() * res.element_size()))
+
+    runtime.all_gather_transform(h.data_ptr(), h.numel(), dtype_code(h), out.data_ptr(),
+                                 out.numel() * out.element_size(), run, name or _auto_name("agt"))
+    return out
+
+
 def global_minimum_spanning_tree(self_weights: torch.Tensor) -> torch.Tensor:
-    """Every peer contributes its row of weights (e.g. latencies to every
-    peer); rows are all-gathered and every peer computes the same MST."""
-    w = all_gather(self_weights.detach().float().cpu())
-    return minimum_spanning_tree(w)
+    """Every peer contributes its row of weights (e.g. latencies to every peer); rank 0
+    computes the MST of the gathered matrix and broadcasts the edges (one native
+    AllGatherTransform instead of every peer computing it, as in the reference)."""
+    n = runtime.size() if runtime.initialized() else 1
+    w = self_weights.detach().float()
+    return all_gather_transform(w, torch.zeros(max(n - 1, 0), 2, dtype=torch.int32),
+                                lambda g: minimum_spanning_tree(g).reshape(-1, 2))
 
 
 def get_neighbour_mask(edges: torch.Tensor, cluster_size: int = None, self_rank: int = None) -> torch.Tensor:

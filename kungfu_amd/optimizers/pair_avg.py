@@ -6,19 +6,24 @@ step pick a random peer != self, *pull* its (fused) model from its store,
 store; a save + barrier at step 0; no global synchronisation afterwards.
 
 MI355X design:
-* the model store is device resident: two dedicated HIP allocations per peer
-  (double buffer), exported with HIP IPC at start-up (handles exchanged once
-  through the host runtime's all-gather).  A pull is a one-sided device copy
-  from the peer's buffer over xGMI -- the owner does not participate -- then
-  one fused K4 kernel averages into the flat parameter buffer.
-* the owner publishes its model by a D2D copy into the buffer not currently
-  advertised, and advertises ``(buffer, version)`` in its host store one step
-  later (when that copy has certainly completed); readers fetch the 16-byte
-  record over the host P2P channel first.  A reader can only see a torn
-  buffer if its pull spans more than one full owner iteration (the reference
-  has an unguarded race on its blob instead).
+* the model store is device resident: three dedicated HIP allocations per peer
+  (a ring), exported with HIP IPC at start-up (handles exchanged once through
+  the host runtime's all-gather).  A pull is a one-sided device copy from the
+  peer's buffer over xGMI -- the owner does not participate -- then one fused
+  K4 kernel averages into the flat parameter buffer.
+* publication protocol (torn-read free, unlike the reference's unguarded blob,
+  SURVEY §5.2): the owner snapshots version k into ring slot k % 3 at the end
+  of step k, and ADVERTISES ``(slot, k)`` in its host store at the start of
+  step k+1, after host-waiting on that copy's event -- an advertised slot is
+  always complete.  Slot k % 3 is next written by snapshot k+3, which is issued
+  only after version k+2 has been advertised.  A reader therefore (1) fetches
+  the 16-byte record, (2) copies the slot and waits for its own copy, (3)
+  fetches the record again: if the advertised version advanced by 2 or more
+  the copy may overlap a rewrite and is dropped (``dropped`` counts them), else
+  it is an exact snapshot of version k.
 * peers on other hosts (no IPC) are pulled through the host P2P store
-  (device -> host snapshot on the owner, TCP pull on the reader).
+  (device -> host snapshot on the owner, TCP pull on the reader), which copies
+  under the store's lock.
 CPU tensors use the host P2P store for everything.
 """
 from __future__ import annotations
@@ -38,13 +43,15 @@ _REC = "kf:pair:rec"
 
 
 class DeviceModelStore:
+    SLOTS = 3
+
     def __init__(self, numel: int, device: torch.device, name: str):
         H = hip()
         self.numel = numel
         self.name = name
         self.device = device
         self.rank, self.size = runtime.rank(), runtime.size()
-        self.bufs = [H.ipc_alloc(numel, device.index), H.ipc_alloc(numel, device.index)]
+        self.bufs = [H.ipc_alloc(numel, device.index) for _ in range(self.SLOTS)]
         hs = b"".join(H.ipc_handle(b) for b in self.bufs)
         mine = torch.frombuffer(bytearray(hs), dtype=torch.uint8).clone()
         allh = ops.all_gather(mine, name="kf:pair:handles:" + name)
@@ -59,22 +66,25 @@ class DeviceModelStore:
             self.local[r] = same_host
             if same_host:
                 raw = bytes(allh[r].tolist())
-                self.peer_bufs[r] = [H.ipc_open(raw[i * 64:(i + 1) * 64], numel, device.index) for i in range(2)]
+                self.peer_bufs[r] = [H.ipc_open(raw[i * 64:(i + 1) * 64], numel, device.index)
+                                     for i in range(self.SLOTS)]
         self.cross_host = not all(self.local.values()) if self.local else False
-        self.version = 0
-        self.write_idx = 0
+        self.version = 0  # last advertised version
+        self._next = 0  # version of the next snapshot
         self._pending: Optional[torch.cuda.Event] = None
-        self._pending_idx = 0
+        self._pending_ver = 0
         self._host_copy = None
+        self.dropped = 0
+        self.last_pulled = None  # (peer, version) of the last accepted pull
 
     def publish(self, flat: torch.Tensor):
-        """Snapshot ``flat`` into the non-advertised buffer (stream-ordered)."""
-        idx = self.write_idx
-        self.bufs[idx].copy_(flat, non_blocking=True)
+        """Snapshot ``flat`` into ring slot version % 3 (stream-ordered)."""
+        self._next += 1
+        ver = self._next
+        self.bufs[ver % self.SLOTS].copy_(flat, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        self._pending, self._pending_idx = ev, idx
-        self.write_idx ^= 1
+        self._pending, self._pending_ver = ev, ver
         if self.cross_host:
             self._host_copy = flat.detach().to("cpu", non_blocking=False)
 
@@ -82,25 +92,41 @@ class DeviceModelStore:
         if self._pending is None:
             return
         self._pending.synchronize()  # issued one iteration ago: normally already complete
-        self.version += 1
-        rec = torch.tensor([self._pending_idx, self.version], dtype=torch.int64)
+        self.version = self._pending_ver
+        rec = torch.tensor([self.version % self.SLOTS, self.version], dtype=torch.int64)
         runtime.save(_REC + self.name, rec.data_ptr(), 16)
         if self._host_copy is not None:
             runtime.save("kf:pair:model:" + self.name, self._host_copy.data_ptr(), self.numel * 4)
         self._pending = None
 
-    @traced("pair::pull")
-    def pull(self, target: int, out: torch.Tensor) -> bool:
+    def _record(self, target: int):
         rec = torch.zeros(2, dtype=torch.int64)
         if not runtime.request(target, "", _REC + self.name, rec.data_ptr(), 16):
+            return None
+        return int(rec[0]), int(rec[1])
+
+    @traced("pair::pull")
+    def pull(self, target: int, out: torch.Tensor) -> bool:
+        rec = self._record(target)
+        if rec is None:
             return False
+        slot, ver = rec
         if self.local.get(target, False):
-            out.copy_(self.peer_bufs[target][int(rec[0])], non_blocking=True)
+            out.copy_(self.peer_bufs[target][slot], non_blocking=True)
+            done = torch.cuda.Event()
+            done.record()
+            done.synchronize()
+            after = self._record(target)
+            if after is None or after[1] - ver >= self.SLOTS - 1:
+                self.dropped += 1  # the owner may have started rewriting this slot
+                return False
+            self.last_pulled = (target, ver)
             return True
         h = torch.empty(self.numel, dtype=torch.float32)
         if not runtime.request(target, "", "kf:pair:model:" + self.name, h.data_ptr(), self.numel * 4):
             return False
         out.copy_(h)
+        self.last_pulled = (target, ver)
         return True
 
 

@@ -62,6 +62,62 @@ def _scope_rank_size(scope: str):
     return runtime.local_rank(), runtime.local_size()
 
 
+def _graph_plan(owner, pairs, rank: int, count: int):
+    """(rounds, scratch elems) of a graph all-reduce, cached per (pairs, count) on ``owner``."""
+    if pairs is None:
+        pairs = runtime.global_strategy_pairs()
+    key = (tuple((tuple(a), tuple(b)) for a, b in pairs), count)
+    cache = owner.__dict__.setdefault("_graph_plans", {})
+    plan = cache.get(key)
+    if plan is None:
+        if len(cache) > 64:
+            cache.clear()
+        plan = runtime.plan_graph_all_reduce([(list(a), list(b)) for a, b in key[0]], rank, count)
+        cache[key] = plan
+    return plan
+
+
+class _DeviceStats:
+    """Strategy statistics for device-plane graph all-reduces (parity: the monitored
+    all-reduce of ``srcs/go/kungfu/session/monitoring.go:15-35`` feeding
+    ``adaptiveStrategies.go:61-121``): each monitored collective is bracketed by two HIP
+    events on its stream; completed pairs are converted to (begin, end) seconds on the
+    device timeline (relative to one base event) and accounted to the session's current
+    global strategy, so ``calc_stats`` / ``check_interference`` / ``set_tree`` adaptation
+    works for GPU training.  No host sync on the hot path: events are only queried, and
+    drained by :func:`flush_strategy_stats` (called by ``calc_stats``)."""
+
+    def _stat_begin(self, stream):
+        if getattr(self, "_stat_base", None) is None:
+            self._stat_base = torch.cuda.Event(enable_timing=True)
+            self._stat_base.record(stream)
+            self._stat_pending = []
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        return ev
+
+    def _stat_end(self, start, stream, nbytes: int):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        self._stat_pending.append((start, ev, nbytes))
+        self.flush_stats(block=False)
+
+    def flush_stats(self, block: bool = True):
+        pend = getattr(self, "_stat_pending", None)
+        if not pend:
+            return
+        keep = []
+        for st, en, nb in pend:
+            if not block and not en.query():
+                keep.append((st, en, nb))
+                continue
+            en.synchronize()
+            b = self._stat_base.elapsed_time(st) / 1e3
+            e = self._stat_base.elapsed_time(en) / 1e3
+            runtime.record_strategy_stat(b, e, int(nb))
+        self._stat_pending = keep
+
+
 class _StreamOrdered:
     """fence / on_stream / join over ``self.stream`` (a torch.cuda.Stream, or None on CPU)."""
 
@@ -80,7 +136,7 @@ class _StreamOrdered:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
 
 
-class DeviceComm(_StreamOrdered):
+class DeviceComm(_StreamOrdered, _DeviceStats):
     """RCCL communicator + comm stream for the current cluster version."""
 
     plane = "rccl"
@@ -140,28 +196,24 @@ class DeviceComm(_StreamOrdered):
     def group_end(self):
         hip().rccl_group_end()
 
-    def graph_all_reduce(self, t: torch.Tensor, op="sum", pairs=None, stream=None):
+    def graph_all_reduce(self, t: torch.Tensor, op="sum", pairs=None, stream=None, monitored: bool = False):
         """In-place all-reduce along KungFu strategy graphs (default: the session's current
         global strategy, which ``set_tree`` / ``set_strategy`` / adaptation swap) as grouped
-        RCCL send/recv rounds + the K1 reduce kernel (see ``plan_graph_all_reduce``)."""
+        RCCL send/recv rounds + the K1 reduce kernel (see ``plan_graph_all_reduce``).
+        ``monitored``: account its bytes and device time to the strategy statistics."""
         if self.size == 1:
             return t
-        if pairs is None:
-            pairs = runtime.global_strategy_pairs()
-        key = (tuple((tuple(a), tuple(b)) for a, b in pairs), t.numel())
-        cache = self.__dict__.setdefault("_graph_plans", {})
-        plan = cache.get(key)
-        if plan is None:
-            if len(cache) > 64:
-                cache.clear()
-            plan = runtime.plan_graph_all_reduce([(list(a), list(b)) for a, b in key[0]], self.rank, t.numel())
-            cache[key] = plan
-        rounds, nscratch = plan
+        rounds, nscratch = _graph_plan(self, pairs, self.rank, t.numel())
         scratch = torch.empty(max(int(nscratch), 1), dtype=t.dtype, device=t.device)
         s = stream if stream is not None else self.stream
-        if hasattr(s, "cuda_stream") and s != torch.cuda.current_stream(t.device):
+        if not hasattr(s, "cuda_stream"):
+            s = torch.cuda.ExternalStream(int(s), device=self.device)
+        if s != torch.cuda.current_stream(t.device):
             scratch.record_stream(s)
-        self.comm.graph_run(t, scratch, rounds, op_code(op), self._s(stream))
+        st = self._stat_begin(s) if monitored else None
+        self.comm.graph_run(t, scratch, rounds, op_code(op), s.cuda_stream)
+        if monitored:
+            self._stat_end(st, s, t.numel() * t.element_size())
         return t
 
     def destroy(self):
@@ -247,9 +299,61 @@ class HostComm(_StreamOrdered):
         nm = self._name("ar")
         return self._run(inp, out, stream, lambda h: self._ar(h, op, nm))
 
-    def graph_all_reduce(self, t, op="sum", pairs=None, stream=None):
-        # the host runtime executes the session's strategy graphs itself
-        return self.all_reduce(t, t, op=op, stream=stream)
+    def graph_all_reduce(self, t, op="sum", pairs=None, stream=None, monitored: bool = False):
+        """CPU tensors: the host runtime executes the strategy graphs itself (monitored:
+        native strategy statistics).  Staged GPU tensors: the device graph plane's round
+        plan (``plan_graph_all_reduce``, the same one RCCL executes) with host transfers
+        (``send_to`` / ``recv_from``) and the device K1 reduce kernel -- so the plan and
+        the kernel are testable with ranks that share one GPU."""
+        if not self.staged:
+            nm = self._name("gar")
+            red = op if op != "avg" else "sum"
+            c = t if t.is_contiguous() else t.contiguous()
+            if monitored or pairs is not None:
+                tree = list(pairs[0][0]) if pairs is not None and len(pairs) == 1 and pairs[0][0] == pairs[0][1] else []
+                runtime.monitored_all_reduce(c.data_ptr(), c.data_ptr(), c.numel(), dtype_code(c), op_code(red), nm,
+                                             tree)
+            else:
+                runtime.all_reduce(c.data_ptr(), c.data_ptr(), c.numel(), dtype_code(c), op_code(red), nm)
+            if op == "avg":
+                c.div_(self.size)
+            if c is not t:
+                t.copy_(c)
+            return t
+        if self.size == 1:
+            return t
+        import time
+
+        from .._lib import hip
+
+        rounds, nscratch = _graph_plan(self, pairs, self.rank, t.numel())
+        nm = self._name("graph")
+        s = stream if stream is not None else self.stream
+        if not isinstance(s, torch.cuda.Stream):
+            s = torch.cuda.ExternalStream(int(s), device=self.device)
+        esz = t.element_size()
+        t0 = time.time()
+        with torch.cuda.stream(s):
+            flat = t.view(-1)
+            scratch = torch.empty(max(int(nscratch), 1), dtype=t.dtype, device=t.device)
+            for ri, rnd in enumerate(rounds):
+                s.synchronize()  # the previous round's reduces are complete before sending
+                for recv, peer, off, ln, sc in rnd:
+                    if not recv and ln:
+                        h = flat[off:off + ln].to("cpu")
+                        runtime.send_to(peer, "%s:r%d:%d" % (nm, ri, off), h.data_ptr(), ln * esz)
+                for recv, peer, off, ln, sc in rnd:
+                    if recv and ln:
+                        h = torch.empty(ln, dtype=t.dtype)
+                        runtime.recv_from(peer, "%s:r%d:%d" % (nm, ri, off), h.data_ptr(), ln * esz)
+                        dst = scratch[sc:sc + ln] if sc >= 0 else flat[off:off + ln]
+                        dst.copy_(h)
+                        if sc >= 0:  # K1: reduce the received chunk into place on the device
+                            hip().reduce(flat[off:off + ln], flat[off:off + ln], dst, op_code(op))
+            s.synchronize()
+        if monitored:
+            runtime.record_strategy_stat(t0, time.time(), t.numel() * esz)
+        return t
 
     def broadcast(self, t, root: int = 0, stream=None):
         nm = self._name("bc")
@@ -327,6 +431,17 @@ HostStagedComm = HostComm
 
 def _use_host_staging() -> bool:
     return os.environ.get("KUNGFU_GPU_DATAPLANE", "rccl") == "host"
+
+
+def flush_strategy_stats() -> None:
+    """Account every completed monitored device collective to the strategy statistics
+    (waits for the pending ones).  Called by ``calc_stats``."""
+    with _lock:
+        comms = list(_comms.values())
+    for c in comms:
+        f = getattr(c, "flush_stats", None)
+        if f is not None:
+            f(block=True)
 
 
 def comm_epoch() -> int:

@@ -39,7 +39,10 @@ MI355X design:
   models whose use count changes between steps need ``overlap=False``.
 * bucket sizing: the first bucket is small (starts communication early), the
   rest default to 32 MiB: few, large collectives suit RCCL rings over the
-  point-to-point xGMI links; tunable via ``KUNGFU_BUCKET_MB``.
+  point-to-point xGMI links; tunable via ``KUNGFU_BUCKET_MB``.  The last
+  ``tail_bucket_mb`` (4 MiB, ``KUNGFU_TAIL_BUCKET_MB``) of the buffer -- the first
+  layers, whose gradients arrive last -- is bucketed separately so the
+  collective that cannot overlap with backward is small.
 * ``comm_dtype=torch.bfloat16`` halves the bytes on the wire: the bucket is
   cast into a persistent bf16 comm buffer on the comm stream (HIP kernel),
   reduced there, and cast back (f32 accumulation stays in the flat buffer).
@@ -75,6 +78,7 @@ class LateGradientError(RuntimeError):
 class GradReducer:
     def __init__(self, space: FlatParamSpace, op: str = "avg", bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
+                 tail_bucket_mb: float = 4.0,
                  skip_single: bool = True):
         # skip_single: with one peer the average of the gradients IS the local
         # gradient, so no collective is issued (the engine's hooks still run).
@@ -97,6 +101,12 @@ class GradReducer:
         self.graph = os.environ.get("KUNGFU_GPU_ALLREDUCE", "rccl") == "graph"
         self.buckets: List[Bucket] = []
         cap = max(1, int(first_bucket_mb * (1 << 20) / esz))
+        # The last bucket is launched only when backward has produced its final
+        # gradient, so its whole all-reduce is exposed: the tail of the buffer (the
+        # model's first layers) gets buckets of at most tail_mb.
+        tail_mb = float(os.environ.get("KUNGFU_TAIL_BUCKET_MB", tail_bucket_mb))
+        tail_cap = max(1, int(tail_mb * (1 << 20) / esz))
+        tail_start = space.numel - tail_cap
         start = None
         cur: List[int] = []
         last_end = 0
@@ -105,7 +115,10 @@ class GradReducer:
                 start = o
             cur.append(i)
             end = o + n
-            if (end - start) >= cap:
+            nxt = space.offsets[i + 1][0] if i + 1 < len(space.offsets) else None
+            # close before the next param crosses into the tail region (keeps the tail separate)
+            enter_tail = nxt is not None and start < tail_start <= nxt + space.offsets[i + 1][1] and end <= tail_start
+            if (end - start) >= cap or (enter_tail and end - start > 0) or (start >= tail_start and end - start >= tail_cap):
                 self.buckets.append(Bucket(len(self.buckets), start, end, cur))
                 cap = max(1, int(cap_mb * (1 << 20) / esz))
                 start, cur = None, []
@@ -289,7 +302,7 @@ class GradReducer:
         if not self.graph:
             comm.all_reduce(g, op=self.op)
             return
-        comm.graph_all_reduce(g, op="sum")
+        comm.graph_all_reduce(g, op="sum", monitored=True)
         if self.op == "avg":
             with comm.on_stream():
                 g.mul_(1.0 / comm.size)

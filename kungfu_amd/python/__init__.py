@@ -177,6 +177,9 @@ def check_interference() -> bool:
 
 def calc_stats() -> None:
     _ensure()
+    from ..parallel.comm import flush_strategy_stats
+
+    flush_strategy_stats()
     runtime.calc_stats()
 
 

@@ -49,7 +49,9 @@ def free_port_block(n: int = 16) -> int:
             return base
 
 
-def kungfu_run(np_, script_args, strategy=None, timeout=120, extra=None, env=None, port_base=None):
+def kungfu_run(np_, script_args, strategy=None, timeout=120, extra=None, env=None, port_base=None, raw=False):
+    """Run ``python script_args...`` (or the program ``script_args[0]`` itself when ``raw``)
+    under kungfu-run on 127.0.0.1."""
     base = port_base or free_port_block(np_ + 2)
     cmd = [os.path.join(ROOT, "bin", "kungfu-run"), "-q", "-np", str(np_), "-H", "127.0.0.1:%d" % max(np_, 1),
            "-port-range", "%d-%d" % (base + 1, base + 1 + max(np_, 1) + 4), "-port", str(base)]
@@ -57,7 +59,7 @@ def kungfu_run(np_, script_args, strategy=None, timeout=120, extra=None, env=Non
         cmd += ["-strategy", strategy]
     if extra:
         cmd += extra
-    cmd += [sys.executable] + list(script_args)
+    cmd += ([] if raw else [sys.executable]) + list(script_args)
     e = dict(os.environ)
     e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
     if env:

@@ -23,3 +23,15 @@ def test_model_averaging_ops(np_):
     r = kungfu_run(np_, [worker("model_avg.py")], timeout=180)
     assert r.returncode == 0, r.stdout[-4000:]
     assert r.stdout.count("MODEL_AVG_OK") == np_, r.stdout[-4000:]
+
+
+def test_p2p_send_recv_and_device_stats():
+    r = kungfu_run(2, [worker("p2p_stats.py")], timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert r.stdout.count("P2P_STATS_OK") == 2
+
+
+def test_all_gather_transform_mst():
+    r = kungfu_run(3, [worker("agt.py")], timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert r.stdout.count("AGT_OK") == 3

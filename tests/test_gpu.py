@@ -559,6 +559,16 @@ def test_pair_averaging_ipc_two_procs_one_gpu():
 
 
 @needs_gpu
+def test_pair_averaging_skewed_peers_no_torn_reads():
+    """One peer sleeps between steps while the other rewrites its snapshot ring flat out:
+    every accepted pull is a complete snapshot (uniform model invariant)."""
+    r = kungfu_run(2, [worker("pair_stress.py")], timeout=300, extra=["-allow-xgmi"],
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"})
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("PAIR_STRESS_OK") == 2, r.stdout[-4000:]
+
+
+@needs_gpu
 def test_smoke_entry():
     r = subprocess.run([sys.executable, "-c", "import __graft_entry__ as g; g.smoke()"], cwd=ROOT,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
@@ -699,6 +709,16 @@ def test_device_graph_allreduce_two_ranks():
                    env={"KUNGFU_FORCE_DEVICE": "0"})
     if "GRAPH_GPU_SKIP" in r.stdout:
         pytest.skip("RCCL refuses 2 ranks on one GPU: " + r.stdout[-300:])
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("GRAPH_GPU_OK") == 2, r.stdout[-4000:]
+
+
+@needs_gpu
+def test_device_graph_allreduce_two_ranks_host_staged():
+    """The device graph plane's round plans + device K1 reduce with 2 ranks on one GPU
+    (host transfers), every strategy, graph-mode S-SGD, and device strategy statistics."""
+    r = kungfu_run(2, [worker("graph_gpu.py")], timeout=300,
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"})
     assert r.returncode == 0, r.stdout[-4000:]
     assert r.stdout.count("GRAPH_GPU_OK") == 2, r.stdout[-4000:]
 
@@ -857,3 +877,28 @@ def test_conv_relu_first_layer_autocast():
         outs.append([y.detach().float(), xx.grad.float(), mod.weight.grad.float(), mod.bias.grad.float()])
     for a, c in zip(*outs):
         assert ((c - a).norm() / a.norm()).item() < 2e-2
+
+
+@needs_gpu
+def test_relu_and_maxpool_propagate_nan(H):
+    """the fused ReLU and the 2x2 max-pool keep a NaN (torch.relu / max_pool2d do),
+    so a diverging loss surfaces on the fused VGG path too."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.pool import max_pool2x2
+
+    y = torch.randn(2, 64, 4, 6, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    y[0, 3, 1, 2] = float("nan")
+    y[1, 10, 0, 0] = float("nan")
+    b = torch.zeros(64, device="cuda")
+    z = y.clone()
+    H.bias_act_forward_(z, b, True)
+    assert torch.isnan(z[0, 3, 1, 2]) and torch.isnan(z[1, 10, 0, 0])
+    assert torch.equal(torch.isnan(z), torch.isnan(torch.relu(y)))
+    x = torch.randn(2, 64, 8, 8, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    x[0, 5, 3, 3] = float("nan")  # bottom-right of its window: a strict '>' would drop it
+    x[1, 7, 0, 1] = float("nan")
+    ref = F.max_pool2d(x.float(), 2, 2)
+    got = max_pool2x2(x)
+    assert torch.equal(torch.isnan(got.float()), torch.isnan(ref))
+    assert torch.equal(torch.nan_to_num(got.float(), nan=7.0), torch.nan_to_num(ref, nan=7.0))

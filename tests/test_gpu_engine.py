@@ -140,3 +140,101 @@ def test_elastic_resnet18_gns_two_ranks_one_gpu():
     gns = [float(g) for rows in by.values() for n, _, g, _ in rows if n == 2 and g not in ("", "None")]
     assert gns and all(g == g and abs(g) < 1e12 for g in gns), r.stdout[-3000:]
     assert "ELASTIC_TRAIN_DONE rank=0 np=1 step=9 v=2" in r.stdout
+
+
+@needs_gpu
+def test_gns_on_bert_gradients_matches_fp64(H):
+    """K5 on real BERT-base gradients: |g_small|^2 (half batch) and |g_big|^2 (full batch)
+    from the one-pass sumsq kernel, then the device EMA update, against float64 torch and
+    the reference formulas (grad_noise_scale.py:56-88)."""
+    from kungfu_amd.models.bert import bert_base, pretraining_loss, synthetic_pretraining_batch
+
+    torch.manual_seed(0)
+    m = bert_base(layers=2).cuda()
+    data = synthetic_pretraining_batch(8, 128, device="cuda")
+
+    def flat_grad(b):
+        m.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = pretraining_loss(m, b)
+        loss.backward()
+        return torch.cat([p.grad.reshape(-1) for p in m.parameters() if p.grad is not None]).float()
+
+    half = tuple(t[:4] for t in data)
+    g_small, g_big = flat_grad(half), flat_grad(data)
+    s = H.sumsq2(g_small, g_big)
+    ref = [g_small.double().square().sum().item(), g_big.double().square().sum().item()]
+    for got, want in zip(s.tolist(), ref):
+        assert abs(got / want - 1) < 1e-5, (got, want)
+    st = torch.zeros(4, device="cuda")
+    H.gns_update(s[:1], s[1:2], 4.0, 8.0, 0.6, st)
+    G = (8 * ref[1] - 4 * ref[0]) / (8 - 4)
+    S = (ref[0] - ref[1]) / (1 / 4 - 1 / 8)
+    assert abs(st[0].item() / G - 1) < 1e-4 and abs(st[1].item() / S - 1) < 1e-4
+    assert abs(st[2].item() - S / G) <= 1e-4 * abs(S / G)
+
+
+@needs_gpu
+def test_bench_bert_gns_json():
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+
+    r = subprocess.run([sys.executable, "bench.py", "--model", "bert_base", "--optimizer", "gns", "--steps", "2",
+                        "--warmup", "2", "--batch", "8"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["unit"].startswith("sequences/sec") and d["value"] > 0 and d["config"]["seq_len"] == 128
+    assert d["config"]["comm"]["comm_plane"] == "rccl"
+
+
+def _resnet50_trajectory(engine: bool, steps=10, batch=64, lr=0.1):
+    """Loss trajectory of ResNet-50 at 224x224 (batch 64, SGD lr 0.1 momentum 0.9 wd 1e-4,
+    bf16 autocast): the bench's fused engine (HIP BN / MFMA convs / bf16 shadow weights /
+    bucketed S-SGD / fused SGD) or the stock modules with torch.optim.SGD."""
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet50
+
+    kf.init()
+    torch.manual_seed(1234)
+    model = resnet50(fused_bn=engine).cuda().to(memory_format=torch.channels_last)
+    base = torch.optim.SGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    if engine:
+        from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+        opt = kf.optimizers.SynchronousSGDOptimizer(base)
+        enable_bf16_shadow(model, opt)
+    else:
+        opt = base
+    g = torch.Generator(device="cuda").manual_seed(99)
+    x = torch.randn(batch, 3, 224, 224, device="cuda", generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (batch,), device="cuda", generator=g)
+    out = []
+    for _ in range(steps):
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(model(x).float(), y)
+        loss.backward()
+        opt.step()
+        out.append(loss.item())
+    return out
+
+
+@needs_gpu
+def test_resnet50_full_size_engine_matches_stock():
+    """Full-size numerics of the bench path: 224x224, batch 64, lr 0.1,
+    10 steps on one fixed batch.  The fused engine's loss trajectory must stay within the
+    spread of two stock runs (MIOpen's split-K kernels are not bitwise deterministic) plus
+    the bf16-rounding band, and both must memorise the batch the same way."""
+    a = _resnet50_trajectory(False)
+    b = _resnet50_trajectory(False)
+    e = _resnet50_trajectory(True)
+    print("stock", a, "\nstock", b, "\nengine", e)
+    assert abs(e[0] - a[0]) < 0.02 * a[0], (a, e)  # same initial model and data
+    for i, (x0, x1, xe) in enumerate(zip(a, b, e)):
+        spread = abs(x0 - x1)
+        assert abs(xe - x0) <= max(3 * spread, 0.15 * abs(x0) + 0.1), (i, a, b, e)
+    assert e[-1] < e[0] and a[-1] < a[0]

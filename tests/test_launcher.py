@@ -213,3 +213,43 @@ def test_monitoring_http_metrics(tmp_path):
     r = kungfu_run(2, [s], timeout=120, env={"KUNGFU_CONFIG_ENABLE_MONITORING": "true"})
     assert r.returncode == 0, r.stdout[-3000:]
     assert r.stdout.count("MONITOR_OK") == 2, r.stdout[-3000:]
+
+
+def test_bad_worker_cancels_job():
+    """Fault injection (parity: tests/go/cmd/kungfu-bad-worker): rank 0 of the native
+    bad worker exits 1 after 3 all-reduce steps; the peers block in the next collective
+    and kungfu-run cancels them (any failure cancels all)."""
+    from conftest import ROOT
+
+    r = kungfu_run(3, [os.path.join(ROOT, "bin", "kungfu-bad-worker"), "-error-after", "3"], timeout=60, raw=True)
+    assert r.returncode != 0, r.stdout[-3000:]
+    assert "rank 0 fails at step 3" in r.stdout
+    assert r.stdout.count("step 2 ok") == 3  # every worker completed the collectives before the failure
+    assert "exited with error" in r.stdout
+
+
+def test_retry_on_stderr_prefix(tmp_path):
+    """The runner restarts a worker whose first stderr line starts with
+    KUNGFU_CONFIG_RETRY_STDERR_PREFIX (parity: the ld.so-bug hack,
+    srcs/go/utils/runner/local/hack.go:14-35, injected like kungfu-bench-allreduce
+    -rand-nccl-failure)."""
+    marker = tmp_path / "attempts"
+    s = _script(tmp_path, """
+        import os, sys
+        m = %r
+        n = int(open(m).read()) if os.path.exists(m) else 0
+        open(m, "w").write(str(n + 1))
+        if n < 2:
+            sys.stderr.write("Inconsistency detected by ld.so: injected failure\\n")
+            sys.stderr.flush()
+            sys.exit(1)
+        print("RETRY_WORKER_OK attempt=%%d" %% (n + 1), flush=True)
+    """ % str(marker))
+    r = kungfu_run(1, [s], timeout=60, env={"KUNGFU_CONFIG_RETRY_STDERR_PREFIX": "Inconsistency detected by ld.so"})
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "RETRY_WORKER_OK attempt=3" in r.stdout
+    assert r.stdout.count("restarting") == 2
+    # without the prefix configured the same failure is fatal
+    marker.unlink()
+    r = kungfu_run(1, [s], timeout=60)
+    assert r.returncode != 0

@@ -192,3 +192,29 @@ def test_graph_round_plan_shapes():
         _simulate([(f, f)], m, 37, rng)
     with pytest.raises(Exception):
         K.plan_graph_all_reduce([([1, 0], [1, 0])], 0, 10)  # cycle
+
+
+def test_host_list_resolves_hostnames():
+    """-H entries may be host / DNS names (parity: runner/discovery.go); the public
+    address keeps the name, the worker list gets the resolved IPv4."""
+    pl = K.gen_peer_list("localhost:2", 2, "10000-11000")
+    assert pl == "127.0.0.1:10000,127.0.0.1:10001"
+    with pytest.raises(Exception):
+        K.gen_peer_list("no-such-host.invalid:2", 2, "10000-11000")
+
+
+def test_kungfu_run_with_hostname_host_list(tmp_path):
+    import os
+    import subprocess
+    import sys
+
+    from conftest import ROOT, free_port_block
+
+    s = tmp_path / "w.py"
+    s.write_text("import os; print('HOSTNAME_OK', os.environ['KUNGFU_SELF_SPEC'])\n")
+    base = free_port_block(6)
+    r = subprocess.run([os.path.join(ROOT, "bin", "kungfu-run"), "-q", "-np", "2", "-H", "localhost:2",
+                        "-port-range", "%d-%d" % (base + 1, base + 5), "-port", str(base), sys.executable, str(s)],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.count("HOSTNAME_OK 127.0.0.1:") == 2

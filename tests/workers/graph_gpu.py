@@ -1,7 +1,9 @@
-"""Worker: device graph all-reduce (KungFu strategy graphs as grouped RCCL send/recv rounds
-+ the K1 reduce kernel) for every strategy and a set_tree forest, plus the bucketed S-SGD
-reducer in graph mode.  Needs a working multi-rank RCCL communicator; when ranks share one
-GPU and RCCL refuses it, prints GRAPH_GPU_SKIP."""
+"""Worker: device graph all-reduce (KungFu strategy graphs as round plans + the K1 reduce
+kernel) for every strategy and a set_tree forest, plus the bucketed S-SGD reducer in graph
+mode, plus device strategy statistics (monitored all-reduce -> calc_stats ->
+check_interference).  The transfers are grouped RCCL send/recv rounds, or -- with
+KUNGFU_GPU_DATAPLANE=host, for ranks sharing one GPU -- the same rounds over the host
+transport.  When RCCL refuses ranks that share a GPU, prints GRAPH_GPU_SKIP."""
 import os
 
 import torch
@@ -53,5 +55,15 @@ torch.cuda.synchronize()
 w = opt.space.flat_param.double().sum().reshape(1)
 ws = kf.ops.all_gather(w.cpu())
 assert torch.all(ws == ws[0]), ws
-print("GRAPH_GPU_OK rank=%d np=%d" % (r, n), flush=True)
+# device strategy statistics: one active strategy (a tree), monitored device all-reduces
+assert kf.ops.set_tree([0] * n)
+for _ in range(4):
+    x = torch.ones(1 << 18, device=dev)
+    kf.ops.monitored_all_reduce_(x)
+    assert float(x[0]) == n
+kf.ops.calc_stats()
+tp = runtime.strategy_throughputs()
+assert len(tp) == 1 and tp[0] > 0, tp
+assert kf.ops.check_interference() is False  # first call sets the reference window
+print("GRAPH_GPU_OK rank=%d np=%d throughput=%.1fMiB/s" % (r, n, tp[0] / (1 << 20)), flush=True)
 kf.finalize()
