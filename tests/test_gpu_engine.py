@@ -225,16 +225,30 @@ def _resnet50_trajectory(engine: bool, steps=10, batch=64, lr=0.1):
 
 @needs_gpu
 def test_resnet50_full_size_engine_matches_stock():
-    """Full-size numerics of the bench path: 224x224, batch 64, lr 0.1,
-    10 steps on one fixed batch.  The fused engine's loss trajectory must stay within the
-    spread of two stock runs (MIOpen's split-K kernels are not bitwise deterministic) plus
-    the bf16-rounding band, and both must memorise the batch the same way."""
+    """Full-size numerics of the bench path: 224x224, batch 64, SGD momentum
+    0.9, 10 steps on one fixed batch, fused engine vs two stock runs from the same seed.
+
+    lr 0.1 (the bench's): the STOCK model itself climbs from 7.16 to ~10-11 by step 4 and
+    then oscillates chaotically (two stock runs measured 16.97 vs 9.75 at step 7, MIOpen's
+    split-K kernels not being bitwise deterministic) -- no warm-up at that LR from random
+    init.  This is why the bench's final_loss sits above ln(1000).  The engine must follow the
+    stock trajectory through the deterministic phase and stay within the stock spread after.
+    lr 0.01: both memorise the batch (7.16 -> 4.19) and agree within 2 % at every step.
+    Measured on MI355X (r2): lr 0.1 stock 7.16/5.03/6.54/8.58/10.53/11.28, engine
+    7.17/5.04/6.63/8.82/10.61/10.79; lr 0.01 stock .../4.79/4.40/4.19, engine .../4.80/4.42/4.19."""
     a = _resnet50_trajectory(False)
     b = _resnet50_trajectory(False)
     e = _resnet50_trajectory(True)
-    print("stock", a, "\nstock", b, "\nengine", e)
-    assert abs(e[0] - a[0]) < 0.02 * a[0], (a, e)  # same initial model and data
+    print("lr0.1 stock", a, "\nlr0.1 stock", b, "\nlr0.1 engine", e)
+    assert abs(e[0] - a[0]) < 0.01 * a[0], (a, e)  # same initial model and data
     for i, (x0, x1, xe) in enumerate(zip(a, b, e)):
         spread = abs(x0 - x1)
-        assert abs(xe - x0) <= max(3 * spread, 0.15 * abs(x0) + 0.1), (i, a, b, e)
-    assert e[-1] < e[0] and a[-1] < a[0]
+        tol = 0.05 * abs(x0) + 0.05 if i < 6 else max(3 * spread, 0.25 * abs(x0))
+        assert abs(xe - x0) <= max(3 * spread, tol), (i, a, b, e)
+    a = _resnet50_trajectory(False, lr=0.01)
+    e = _resnet50_trajectory(True, lr=0.01)
+    print("lr0.01 stock", a, "\nlr0.01 engine", e)
+    for t in (a, e):  # memorising the batch: a steady decrease, then a plateau near 4.19
+        assert all(y < x for x, y in zip(t[:7], t[1:7])) and t[-1] < 0.65 * t[0], t
+    for x0, xe in zip(a, e):  # measured within 0.5 % at every step
+        assert abs(xe - x0) <= 0.02 * x0, (a, e)
