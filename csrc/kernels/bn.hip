@@ -59,6 +59,15 @@ struct Chunking {
     int nchunks;
 };
 
+// Threads per block for a row of CVEC 16-byte vectors: the largest multiple of CVEC that
+// fits 256 (all 256 when CVEC divides it).  Every grid stride is then a multiple of CVEC, so
+// a lane's channel group stays fixed -- for any C % 8 == 0 (Inception's 80, 96, 160, 192,
+// 320, 384, 448 channels included), not only powers of two.
+template <int CVEC>
+constexpr int bn_threads() {
+    return (kBlock / CVEC) * CVEC;
+}
+
 constexpr int kMaxChunks = 512;
 constexpr int kFoldCh = 8;                    // channels per fold block
 constexpr int kFoldLanes = kBlock / kFoldCh;  // chunk lanes per channel (32)
@@ -129,7 +138,7 @@ __device__ __forceinline__ void reduce_to_partials(float (&acc)[NV][8], float *l
         for (int k = 0; k < 8; ++k) dst[k] = acc[v][k];
     }
     __syncthreads();
-    for (int c = tid; c < C; c += kBlock) {
+    for (int c = tid; c < C; c += bn_threads<CVEC>()) {
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             float s = 0.f;
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
                                                           const float *__restrict__ coef, uint4 *__restrict__ y,
                                                           uint8_t *__restrict__ mask, int64_t nvec) {
     constexpr int C = CVEC * 8;
-    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
     float sc[8], sh[8];
 #pragma unroll
@@ -278,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
         sc[k] = coef[cv * 8 + k];
         sh[k] = coef[C + cv * 8 + k];
     }
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;  // multiple of CVEC
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();  // multiple of CVEC
     for (int64_t i = tid; i < nvec; i += stride) {
         float f[8];
         unpack8(x[i], f);
@@ -311,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__re
                                                                uint2 *__restrict__ arg, int H, int W, int OH, int OW,
                                                                int64_t nout_vec) {
     constexpr int C = CVEC * 8;
-    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
     float sc[8], sh[8];
 #pragma unroll
@@ -319,7 +328,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__re
         sc[k] = coef[cv * 8 + k];
         sh[k] = coef[C + cv * 8 + k];
     }
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();
     for (int64_t i = tid; i < nout_vec; i += stride) {
         const int64_t p = i / CVEC;
         const int ow = static_cast<int>(p % OW);
@@ -594,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
                                                               const float *__restrict__ coef, uint4 *__restrict__ dx,
                                                               uint4 *__restrict__ dres, int64_t nvec) {
     constexpr int C = CVEC * 8;
-    const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
     float k1[8], k2[8], k3[8], sc[8], sh[8];
 #pragma unroll
@@ -604,7 +613,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
         k3[k] = coef[2 * C + cv * 8 + k];
     }
     load_fwd_coef<CVEC, RM>(fcoef, cv, sc, sh);
-    const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();
     for (int64_t i = tid; i < nvec; i += stride) {
         float g[8], xv[8];
         grad.get(grad.template fetch<CVEC>(i, i / CVEC, cv), g);
@@ -621,6 +630,15 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
 template <typename F>
 void dispatch_cvec(int cvec, F &&f) {
     switch (cvec) {
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 6: f(std::integral_constant<int, 6>()); break;
+    case 10: f(std::integral_constant<int, 10>()); break;
+    case 12: f(std::integral_constant<int, 12>()); break;
+    case 20: f(std::integral_constant<int, 20>()); break;
+    case 24: f(std::integral_constant<int, 24>()); break;
+    case 40: f(std::integral_constant<int, 40>()); break;
+    case 48: f(std::integral_constant<int, 48>()); break;
+    case 56: f(std::integral_constant<int, 56>()); break;
     case 8: f(std::integral_constant<int, 8>()); break;
     case 16: f(std::integral_constant<int, 16>()); break;
     case 32: f(std::integral_constant<int, 32>()); break;
@@ -631,11 +649,12 @@ void dispatch_cvec(int cvec, F &&f) {
     }
 }
 
-int apply_grid(int64_t nvec) {
-    int64_t g = (nvec + kBlock - 1) / kBlock;
+// blocks of bn_threads<CVEC>() threads (a multiple of CVEC, so any grid keeps cv fixed)
+int apply_grid(int64_t nvec, int cvec) {
+    const int nt = (kBlock / cvec) * cvec;
+    int64_t g = (nvec + nt - 1) / nt;
     if (g > kMaxGrid) g = kMaxGrid;
     if (g < 1) g = 1;
-    // kBlock is a multiple of every supported CVEC, so any grid keeps cv fixed
     return static_cast<int>(g);
 }
 
@@ -646,7 +665,7 @@ void launch_stats(const uint16_t *x, BNShape sh, const float *gamma, const float
     Chunking ch = chunking(sh);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
-        bn_stats_kernel<CV><<<ch.nchunks, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), sh.rows,
+        bn_stats_kernel<CV><<<ch.nchunks, bn_threads<CV>(), 0, s>>>(reinterpret_cast<const uint4 *>(x), sh.rows,
                                                           ch.rows_per_chunk, partial);
     });
     bn_stats_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, beta,
@@ -672,7 +691,7 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
         auto go = [&](auto rmc) {
             constexpr int RM = decltype(rmc)::value;
             bn_bwd_reduce_kernel<CV, RM, G>
-                <<<ch.nchunks, kBlock, 0, s>>>(grad, xx, fcoef, mask, sh.rows, ch.rows_per_chunk, partial);
+                <<<ch.nchunks, bn_threads<CV>(), 0, s>>>(grad, xx, fcoef, mask, sh.rows, ch.rows_per_chunk, partial);
         };
         if (rm == RM_COEF) go(std::integral_constant<int, RM_COEF>());
         else if (rm == RM_BITS) go(std::integral_constant<int, RM_BITS>());
@@ -681,14 +700,14 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
     bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
                                                                    invstd, dgamma, dbeta, coef, training);
     }
-    const int g = apply_grid(nvec);
+    const int g = apply_grid(nvec, cvec);
     uint4 *o = reinterpret_cast<uint4 *>(dx), *r = reinterpret_cast<uint4 *>(dres);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
         auto go = [&](auto rmc, auto drc) {
             constexpr int RM = decltype(rmc)::value;
             constexpr bool DR = decltype(drc)::value;
-            bn_bwd_apply_kernel<CV, RM, DR, G><<<g, kBlock, 0, s>>>(grad, xx, fcoef, mask, coef, o, r, nvec);
+            bn_bwd_apply_kernel<CV, RM, DR, G><<<g, bn_threads<CV>(), 0, s>>>(grad, xx, fcoef, mask, coef, o, r, nvec);
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -709,8 +728,13 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
 
 bool bn_supported_channels(int C) {
     if (C % 8) return false;
-    int cv = C / 8;
-    return cv >= 8 && cv <= 256 && (cv & (cv - 1)) == 0;
+    switch (C / 8) {
+    case 4: case 6: case 8: case 10: case 12: case 16: case 20: case 24: case 32: case 40: case 48: case 56:
+    case 64: case 128: case 256:
+        return true;
+    default:
+        return false;
+    }
 }
 
 int bn_num_chunks(BNShape sh) { return chunking(sh).nchunks; }
@@ -730,18 +754,19 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
     } else {
         bn_eval_coef<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, run_mean, run_var, eps, mean, invstd, coef);
     }
-    const int g = apply_grid(nvec);
+    const int g = apply_grid(nvec, cvec);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
+        constexpr int NT = bn_threads<CV>();
         const uint4 *xv = reinterpret_cast<const uint4 *>(x);
         const uint4 *rv = reinterpret_cast<const uint4 *>(res);
         uint4 *yv = reinterpret_cast<uint4 *>(y);
         if (res) {
-            if (relu) bn_apply_kernel<CV, true, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
-            else bn_apply_kernel<CV, true, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            if (relu) bn_apply_kernel<CV, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            else bn_apply_kernel<CV, true, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
         } else {
-            if (relu) bn_apply_kernel<CV, false, true><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
-            else bn_apply_kernel<CV, false, false><<<g, kBlock, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            if (relu) bn_apply_kernel<CV, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            else bn_apply_kernel<CV, false, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
         }
     });
 }
@@ -777,10 +802,10 @@ void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *
     const int OH = pool_out(H), OW = pool_out(W);
     const int64_t N = sh.rows / (static_cast<int64_t>(H) * W);
     const int64_t nout = N * OH * OW * cvec;
-    const int g = apply_grid(nout);
+    const int g = apply_grid(nout, cvec);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
-        bn_pool_apply_kernel<CV><<<g, kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), coef,
+        bn_pool_apply_kernel<CV><<<g, bn_threads<CV>(), 0, s>>>(reinterpret_cast<const uint4 *>(x), coef,
                                                       reinterpret_cast<uint4 *>(yp), reinterpret_cast<uint2 *>(arg), H,
                                                       W, OH, OW, nout);
     });

@@ -71,13 +71,15 @@ __device__ __forceinline__ void wait_vmcnt() {
 //   kEpiBwdCoef / kEpiBwdBits  the output is the gradient of a BN(+ReLU) output whose input
 //                 is ea.bx: sum(dz) and sum(dz * x) with dz = grad * relu' from the forward
 //                 coefficients ea.fcoef (recomputed) or from the 1-bit mask ea.bmask.
-template <int KS, int WM, int WN, int STAGES, int EPI>
+template <int KS, int WM, int WN, int STAGES, int EPI, int TM = 4, int TN = 4>
 __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__restrict__ x,
                                                             const uint16_t *__restrict__ w,
                                                             uint16_t *__restrict__ y,
                                                             const uint16_t *__restrict__ zero, Geo g,
                                                             EpiArgs ea) {
-    constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+    // wave tile (16*TM) x (16*TN): TM x TN accumulators of one 16x16x32 MFMA each
+    constexpr int WTM = 16 * TM, WTN = 16 * TN;
+    constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
     constexpr int TAPS = KS * KS, PAD = (KS - 1) / 2;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
     constexpr int STAGE = A_BYTES + B_BYTES;
@@ -85,7 +87,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int B_INST = BN / 8 / NW;
     constexpr int LOADS = A_INST + B_INST;
     static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
+    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
+    constexpr int GROUPS = NT / VPR;
+    constexpr int EPI_BYTES = BM * CROW + (STATS ? 2 * GROUPS * BN * 4 : 0);
+    constexpr int LDS_BYTES = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
@@ -155,17 +164,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     };
 
     const int wm = wave / WN, wn = wave % WN;
-    f32x4 acc[4][4];
+    f32x4 acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+    auto mfma_block = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     };
 
@@ -185,18 +194,26 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         const uint8_t *bbase = abase + A_BYTES;
         // all 16 fragments of the K-step issued up front (substep 1 lands while
         // substep 0's MFMAs run)
-        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+        bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ra = wm * 64 + i * 16 + (lane & 15), rb = wn * 64 + i * 16 + (lane & 15);
+        for (int i = 0; i < TM; ++i) {
+            const int ra = wm * WTM + i * 16 + (lane & 15);
             af0[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, lane >> 4));
-            bf0[i] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, lane >> 4));
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int ra = wm * 64 + i * 16 + (lane & 15), rb = wn * 64 + i * 16 + (lane & 15);
+        for (int j = 0; j < TN; ++j) {
+            const int rb = wn * WTN + j * 16 + (lane & 15);
+            bf0[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, lane >> 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int ra = wm * WTM + i * 16 + (lane & 15);
             af1[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, 4 + (lane >> 4)));
-            bf1[i] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, 4 + (lane >> 4)));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int rb = wn * WTN + j * 16 + (lane & 15);
+            bf1[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, 4 + (lane >> 4)));
         }
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
@@ -215,24 +232,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 
     // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
     // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r.
-    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row
-    static_assert(BM * CROW <= STAGES * STAGE, "C tile fits the staging LDS");
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-                const int col = wn * 64 + j * 16 + (lane & 15);
+                const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+                const int col = wn * WTN + j * 16 + (lane & 15);
                 *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(acc[i][j][r]);
             }
     __syncthreads();
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
     // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
-    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     static_assert(NT % VPR == 0, "fixed channel group per thread");
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
     const int cv = tid % VPR;
     float s1[8], s2[8], sc[8], sh[8];
 #pragma unroll
@@ -298,9 +311,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     }
     if constexpr (STATS) {
         // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
-        constexpr int GROUPS = NT / VPR;
         float *red = reinterpret_cast<float *>(lds + BM * CROW);
-        static_assert(BM * CROW + 2 * GROUPS * BN * 4 <= STAGES * STAGE, "stats scratch fits");
         __syncthreads();
         const int grp = tid / VPR;
 #pragma unroll
@@ -385,11 +396,13 @@ const void *zero_page() {
     return p;
 }
 
-template <int KS, int WM, int WN, int ST, int EPI>
+template <int KS, int WM, int WN, int ST, int EPI, int TM = 4, int TN = 4>
 void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
-    g.mtiles = (g.M + 64 * WM - 1) / (64 * WM);
-    g.ntiles = g.K / (64 * WN);
-    conv_kernel<KS, WM, WN, ST, EPI><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
+    if (g.K % BN) throw std::invalid_argument("conv: Cout not a multiple of the tile");
+    g.mtiles = (g.M + BM - 1) / BM;
+    g.ntiles = g.K / BN;
+    conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
         x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
 }
 
@@ -420,7 +433,9 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     // default per shape class (tools/bench_conv3x3.py, tools/bench_conv.py): 3x3 -> 256x128 /
     // 8 waves / 3 stages when Cout allows; 1x1 (1-16 K-steps) -> 128x128 / 4 waves / 2 stages
     // (two blocks per CU keep more HBM traffic in flight); Cout = 64 -> 256x64 / 4 waves
-    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : 1) : 2;
+    // 3x3 without a fused epilogue and Cout % 256 == 0 (VGG's compute-bound layers): 256x256 /
+    // 8 waves of 64x128 (tools/bench_vgg_conv.py: 1.15-1.17 PF/s vs 1.06-1.12 for 256x128).
+    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : (epi == 0 && g.K % 256 == 0 ? 7 : 1)) : 2;
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
             [[fallthrough]];
@@ -430,12 +445,21 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     case 3: launch_variant<KS, 4, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 256x64 3st
     case 4: launch_variant<KS, 8, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 512x64
     case 5: launch_variant<KS, 2, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 128x64
-    default: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
-             launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                        // 128x64 3st
+    case 6: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
+            launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 128x64 3st
+    // larger wave tiles (tuning candidates for the compute-bound 3x3 shapes)
+    case 7: if (epi || g.K % 256) throw std::invalid_argument("conv variant 7: epi 0, Cout % 256");    // 256x256, 8w, 64x128
+            launch_epi<KS, 4, 2, 2, 0, 4, 8>(x, w, y, g, ea, s); break;
+    case 8: if (epi || g.K % 256) throw std::invalid_argument("conv variant 8: epi 0, Cout % 256");    // 256x256, 8w, 128x64
+            launch_epi<KS, 2, 4, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
+    case 9: if (epi || g.K % 128) throw std::invalid_argument("conv variant 9: epi 0, Cout % 128");    // 256x128, 4w, 128x64
+            launch_epi<KS, 2, 2, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
+    default: if (epi || g.K % 128) throw std::invalid_argument("conv variant 10: epi 0, Cout % 128");  // 128x128, 2w, 64x128 3st
+            launch_epi<KS, 2, 1, 3, 0, 4, 8>(x, w, y, g, ea, s); break;
     }
 }
 
-int conv3x3_variants() { return 7; }
+int conv3x3_variants() { return 11; }
 
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
                  int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant) {

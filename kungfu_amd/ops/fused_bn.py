@@ -6,9 +6,9 @@
 
 Both subclass ``nn.BatchNorm2d`` (same parameters, buffers and state_dict
 keys).  The HIP path runs for bf16, 4-D, channels_last inputs on GPU with a
-supported channel count (C/8 a power of two in [8, 256], i.e. C in
-{64, 128, ..., 2048}); anything else uses the PyTorch composition, so results
-are the same model either way.
+supported channel count (C % 8 == 0 with C/8 in {4, 6, 8, 10, 12, 16, 20, 24, 32,
+40, 48, 56, 64, 128, 256}: every ResNet and Inception-v3 BN, 32 to 2048 channels);
+anything else uses the PyTorch composition, so results are the same model either way.
 
 What is saved for backward is chosen to minimise HBM traffic: x (already kept
 alive as the producing conv's output), the per-channel forward coefficients

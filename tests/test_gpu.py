@@ -133,7 +133,11 @@ def test_pack_unpack(H):
 
 
 @needs_gpu
-@pytest.mark.parametrize("shape", [(4, 64, 16, 16), (8, 256, 14, 14), (2, 2048, 7, 7), (3, 128, 5, 9)])
+@pytest.mark.parametrize("shape", [(4, 64, 16, 16), (8, 256, 14, 14), (2, 2048, 7, 7), (3, 128, 5, 9),
+                                   # Inception-v3 channel counts (C/8 not a power of two)
+                                   (4, 80, 17, 17), (4, 192, 9, 9), (2, 448, 8, 8), (3, 32, 13, 11),
+                                   (2, 48, 10, 10), (2, 96, 7, 9), (2, 160, 6, 6), (2, 320, 5, 5),
+                                   (2, 384, 5, 7)])
 @pytest.mark.parametrize("relu,with_res", [(True, False), (True, True), (False, False)])
 def test_fused_bn(shape, relu, with_res):
     import torch.nn.functional as F
@@ -750,9 +754,9 @@ def test_inception_fused_bn_matches_torch_bn():
     for n, i0, o0 in acts:
         with torch.autocast("cuda", dtype=torch.bfloat16):
             o1 = fmods[n](i0)
-        n_fused += int(o0.shape[1] in (64, 128))
+        n_fused += int(o0.shape[1] % 8 == 0)
         assert ((o1.float() - o0.float()).norm() / o0.float().norm()).item() < 1e-2, n
-    assert n_fused >= 15
+    assert n_fused >= 90  # every BN of the net (C % 8 == 0) takes the HIP kernels
     # backward of one fused layer (32 -> 64, 3x3) on the same input and upstream gradient
     r, f = ref.stem[2], fmods["stem.2"]
     xi = torch.randn(4, 32, 40, 40, device="cuda").to(memory_format=torch.channels_last)
