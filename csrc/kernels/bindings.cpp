@@ -469,6 +469,53 @@ at::Tensor maxpool2x2_backward(at::Tensor x, at::Tensor dy) {
     return dx;
 }
 
+static void check_pool3_in(const at::Tensor &x, const char *name) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0 && x.size(2) >= 3 &&
+                    x.size(3) >= 3,
+                name, " must be a 4-D channels_last bf16 GPU tensor with C % 8 == 0 and H, W >= 3");
+}
+
+std::tuple<at::Tensor, at::Tensor> maxpool3s2_forward(at::Tensor x, int64_t pad) {
+    check_pool3_in(x, "maxpool3x3s2_forward: x");
+    TORCH_CHECK(pad == 0 || pad == 1, "maxpool3x3s2: pad 0 or 1");
+    c10::DeviceGuard gd(x.device());
+    const int H = x.size(2), W = x.size(3);
+    const int OH = kfk::maxpool3s2_out(H, pad), OW = kfk::maxpool3s2_out(W, pad);
+    auto y = at::empty({x.size(0), x.size(1), OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    auto arg = at::empty({x.size(0), OH, OW, x.size(1)}, x.options().dtype(at::kByte));
+    kfk::launch_maxpool3s2_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()),
+                                   reinterpret_cast<uint16_t *>(y.data_ptr()), arg.data_ptr<uint8_t>(), x.size(0), H, W,
+                                   static_cast<int>(x.size(1)), static_cast<int>(pad), stream_of(x, 0));
+    return {y, arg};
+}
+
+at::Tensor maxpool3s2_backward(at::Tensor dy, at::Tensor arg, int64_t H, int64_t W, int64_t pad) {
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                    dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(1) % 8 == 0,
+                "maxpool3x3s2_backward: dy must be channels_last bf16 with C % 8 == 0");
+    TORCH_CHECK(dy.size(2) == kfk::maxpool3s2_out(H, pad) && dy.size(3) == kfk::maxpool3s2_out(W, pad) &&
+                    arg.scalar_type() == at::kByte && arg.numel() == dy.numel() && arg.device() == dy.device(),
+                "maxpool3x3s2_backward: shape mismatch");
+    c10::DeviceGuard gd(dy.device());
+    auto dx = at::empty({dy.size(0), dy.size(1), H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_maxpool3s2_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
+                                    reinterpret_cast<uint16_t *>(dx.data_ptr()), dy.size(0), static_cast<int>(H),
+                                    static_cast<int>(W), static_cast<int>(dy.size(1)), static_cast<int>(pad),
+                                    stream_of(dy, 0));
+    return dx;
+}
+
+at::Tensor avgpool3s1(at::Tensor x) {
+    check_pool3_in(x, "avgpool3x3s1: x");
+    c10::DeviceGuard gd(x.device());
+    auto y = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_avgpool3s1(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                           x.size(0), static_cast<int>(x.size(2)), static_cast<int>(x.size(3)),
+                           static_cast<int>(x.size(1)), stream_of(x, 0));
+    return y;
+}
+
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
@@ -1000,6 +1047,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("bias_act_supported", &kfk::bias_act_supported);
     m.def("maxpool2x2_forward", &maxpool2x2_forward, "2x2/s2 max-pool, NHWC bf16 (no argmax tensor)");
     m.def("maxpool2x2_backward", &maxpool2x2_backward, "2x2/s2 max-pool gradient (gather from x, dy)");
+    m.def("maxpool3s2_forward", &maxpool3s2_forward, "3x3/s2 max-pool (pad 0/1), NHWC bf16 -> (y, argmax bytes)");
+    m.def("maxpool3s2_backward", &maxpool3s2_backward, "3x3/s2 max-pool gradient (gather via the argmax bytes)");
+    m.def("avgpool3s1", &avgpool3s1, "3x3/s1/p1 average pool, count_include_pad (also its own gradient on dy)");
     m.def("bias_act_forward_", &bias_act_forward_, "y = relu(y + bias) in place (NHWC bf16, f32 bias)",
           py::arg("y"), py::arg("bias"), py::arg("relu") = true);
     m.def("bias_act_backward", &bias_act_backward, "(dy * (y > 0), its per-channel sum) in one pass",

@@ -213,6 +213,14 @@ void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *d
 // 2x2 / stride-2 max-pool, NHWC bf16, C % 8 == 0, even H and W (pool.hip); backward
 // recomputes the window argmax from x and writes every dx element once.
 void launch_maxpool2x2_forward(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s);
+// 3x3 / stride-2 / pad (0 or 1) max-pool with a byte argmax per element, gather backward;
+// 3x3 / stride-1 / pad-1 average pool (count_include_pad; its gradient is the same stencil)
+int maxpool3s2_out(int h, int pad);
+void launch_maxpool3s2_forward(const uint16_t *x, uint16_t *y, uint8_t *arg, int64_t N, int H, int W, int C, int pad,
+                               hipStream_t s);
+void launch_maxpool3s2_backward(const uint16_t *dy, const uint8_t *arg, uint16_t *dx, int64_t N, int H, int W, int C,
+                                int pad, hipStream_t s);
+void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s);
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
                                 hipStream_t s);
 

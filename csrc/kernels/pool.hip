@@ -102,6 +102,151 @@ __global__ __launch_bounds__(kBlock) void maxpool2_bwd_kernel(const uint4 *__res
     }
 }
 
+
+// ---------------------------------------------------------------- 3x3 pools (Inception-v3)
+//
+// max 3x3 / stride 2 / pad P (P = 0: Inception's reduction pools): the windows overlap, so
+// the forward also writes the window argmax (0..8) as one byte per element (8 bytes per
+// 16-byte output vector, 1/2 of y -- vs torch's int64 per element, 8x of y) and the backward
+// is a gather over the <= 2x2 windows covering each input pixel (no zero-fill, no atomics,
+// every dx element written once).  NaN takes the window, as in torch.
+//
+// avg 3x3 / stride 1 / pad 1, count_include_pad (the Inception pool branches): a 9-tap
+// stencil with divisor 9; its gradient is the same stencil applied to dy.
+struct Pool3Geo {
+    int H, W, OH, OW, CV, P;
+    int64_t nout;  // N * OH * OW * CV
+};
+
+__global__ __launch_bounds__(kBlock) void maxpool3s2_fwd_kernel(const uint4 *__restrict__ x, uint4 *__restrict__ y,
+                                                                uint2 *__restrict__ arg, Pool3Geo g) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < g.nout;
+         i += static_cast<int64_t>(gridDim.x) * kBlock) {
+        const int cv = static_cast<int>(i % g.CV);
+        int64_t t = i / g.CV;
+        const int ow = static_cast<int>(t % g.OW);
+        t /= g.OW;
+        const int oh = static_cast<int>(t % g.OH);
+        const int64_t n = t / g.OH;
+        float best[8];
+        uint32_t a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            best[k] = -INFINITY;
+            a[k] = 0;
+        }
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+            const int h = 2 * oh - g.P + kh;
+            if (h < 0 || h >= g.H) continue;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int w = 2 * ow - g.P + kw;
+                if (w < 0 || w >= g.W) continue;
+                const uint4 v = x[((n * g.H + h) * g.W + w) * g.CV + cv];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float f = (k & 1) ? hi16(bits_of(v, k >> 1)) : lo16(bits_of(v, k >> 1));
+                    if (f > best[k] || isnan(f)) {  // torch: a later NaN takes over
+                        best[k] = f;
+                        a[k] = kh * 3 + kw;
+                    }
+                }
+            }
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = static_cast<uint32_t>(f32_to_bf16(best[2 * k])) |
+                   (static_cast<uint32_t>(f32_to_bf16(best[2 * k + 1])) << 16);
+        y[i] = make_uint4(o[0], o[1], o[2], o[3]);
+        arg[i] = make_uint2(a[0] | (a[1] << 8) | (a[2] << 16) | (a[3] << 24),
+                            a[4] | (a[5] << 8) | (a[6] << 16) | (a[7] << 24));
+    }
+}
+
+// one lane per input vector: gather dy of every window (oh, ow) that contains (h, w) and
+// whose argmax byte points at it.  nin = N * H * W * CV.
+__global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const uint4 *__restrict__ dy,
+                                                                const uint2 *__restrict__ arg, uint4 *__restrict__ dx,
+                                                                Pool3Geo g, int64_t nin) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < nin;
+         i += static_cast<int64_t>(gridDim.x) * kBlock) {
+        const int cv = static_cast<int>(i % g.CV);
+        int64_t t = i / g.CV;
+        const int w = static_cast<int>(t % g.W);
+        t /= g.W;
+        const int h = static_cast<int>(t % g.H);
+        const int64_t n = t / g.H;
+        // windows with 2*oh - P <= h <= 2*oh - P + 2
+        const int hp = h + g.P, wp = w + g.P;
+        int oh0 = (hp - 2 + 1) / 2, oh1 = hp / 2, ow0 = (wp - 2 + 1) / 2, ow1 = wp / 2;
+        if (hp - 2 < 0) oh0 = 0;
+        if (wp - 2 < 0) ow0 = 0;
+        if (oh1 > g.OH - 1) oh1 = g.OH - 1;
+        if (ow1 > g.OW - 1) ow1 = g.OW - 1;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        for (int oh = oh0; oh <= oh1; ++oh)
+            for (int ow = ow0; ow <= ow1; ++ow) {
+                const int64_t o = ((n * g.OH + oh) * g.OW + ow) * g.CV + cv;
+                const uint2 am = arg[o];
+                const uint4 d = dy[o];
+                const uint32_t me = static_cast<uint32_t>((hp - 2 * oh) * 3 + (wp - 2 * ow));
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
+                    const float f = (k & 1) ? hi16(bits_of(d, k >> 1)) : lo16(bits_of(d, k >> 1));
+                    acc[k] += ak == me ? f : 0.f;
+                }
+            }
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k])) | (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1])) << 16);
+        dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// y = (1/9) * sum of the 3x3 window (zero padding, count_include_pad), same H x W
+__global__ __launch_bounds__(kBlock) void avgpool3s1_kernel(const uint4 *__restrict__ x, uint4 *__restrict__ y, int H,
+                                                            int W, int CV, int64_t n) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * kBlock) {
+        const int cv = static_cast<int>(i % CV);
+        int64_t t = i / CV;
+        const int w = static_cast<int>(t % W);
+        t /= W;
+        const int h = static_cast<int>(t % H);
+        const int64_t nn = t / H;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+        for (int dh = -1; dh <= 1; ++dh) {
+            const int hh = h + dh;
+            if (hh < 0 || hh >= H) continue;
+#pragma unroll
+            for (int dw = -1; dw <= 1; ++dw) {
+                const int ww = w + dw;
+                if (ww < 0 || ww >= W) continue;
+                const uint4 v = x[((nn * H + hh) * W + ww) * CV + cv];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    acc[k] += (k & 1) ? hi16(bits_of(v, k >> 1)) : lo16(bits_of(v, k >> 1));
+            }
+        }
+        constexpr float inv9 = 1.f / 9.f;
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k] * inv9)) |
+                   (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1] * inv9)) << 16);
+        y[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 PoolGeo pool_geo(int64_t N, int H, int W, int C) {
     if (C % 8 || H % 2 || W % 2) throw std::invalid_argument("maxpool2x2: needs C % 8 == 0 and even H, W");
     PoolGeo g;
@@ -132,6 +277,41 @@ void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t 
     maxpool2_bwd_kernel<<<pool_grid(g.nout), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x),
                                                               reinterpret_cast<const uint4 *>(dy),
                                                               reinterpret_cast<uint4 *>(dx), g);
+}
+
+int maxpool3s2_out(int h, int pad) { return (h + 2 * pad - 3) / 2 + 1; }
+
+void launch_maxpool3s2_forward(const uint16_t *x, uint16_t *y, uint8_t *arg, int64_t N, int H, int W, int C, int pad,
+                               hipStream_t s) {
+    if (C % 8) throw std::invalid_argument("maxpool3x3s2: needs C % 8 == 0");
+    Pool3Geo g;
+    g.H = H, g.W = W, g.P = pad, g.CV = C / 8, g.OH = maxpool3s2_out(H, pad), g.OW = maxpool3s2_out(W, pad);
+    g.nout = N * g.OH * g.OW * g.CV;
+    if (g.nout <= 0) return;
+    maxpool3s2_fwd_kernel<<<pool_grid(g.nout), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x),
+                                                                reinterpret_cast<uint4 *>(y),
+                                                                reinterpret_cast<uint2 *>(arg), g);
+}
+
+void launch_maxpool3s2_backward(const uint16_t *dy, const uint8_t *arg, uint16_t *dx, int64_t N, int H, int W, int C,
+                                int pad, hipStream_t s) {
+    if (C % 8) throw std::invalid_argument("maxpool3x3s2: needs C % 8 == 0");
+    Pool3Geo g;
+    g.H = H, g.W = W, g.P = pad, g.CV = C / 8, g.OH = maxpool3s2_out(H, pad), g.OW = maxpool3s2_out(W, pad);
+    g.nout = N * g.OH * g.OW * g.CV;
+    const int64_t nin = N * H * W * g.CV;
+    if (nin <= 0) return;
+    maxpool3s2_bwd_kernel<<<pool_grid(nin), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(dy),
+                                                             reinterpret_cast<const uint2 *>(arg),
+                                                             reinterpret_cast<uint4 *>(dx), g, nin);
+}
+
+void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s) {
+    if (C % 8) throw std::invalid_argument("avgpool3x3s1: needs C % 8 == 0");
+    const int64_t n = N * H * W * (C / 8);
+    if (n <= 0) return;
+    avgpool3s1_kernel<<<pool_grid(n), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), reinterpret_cast<uint4 *>(y),
+                                                       H, W, C / 8, n);
 }
 
 }  // namespace kfk

@@ -32,10 +32,33 @@ class BasicConv2d(nn.Module):
     def forward(self, x):
         y = self.conv(x)
         if self.pool_after_conv:
-            y = F.avg_pool2d(y, 3, 1, 1)
+            if self.fused:  # HIP 3x3/s1/p1 stencil (forward and backward)
+                from ..ops.pool import avg_pool3x3s1
+
+                y = avg_pool3x3s1(y)
+            else:
+                y = F.avg_pool2d(y, 3, 1, 1)
         if self.fused:
             return self.bn(y)
         return F.relu(self.bn(y), inplace=True)
+
+
+def _pool_module():
+    """The stem's MaxPool2d(3, 2): HIP kernels (byte argmax, gather backward) in the fused model."""
+    if _FUSED_BN[0]:
+        from ..ops.pool import MaxPool3x3s2
+
+        return MaxPool3x3s2()
+    return nn.MaxPool2d(3, 2)
+
+
+def _max_pool3s2(x, fused: bool):
+    """F.max_pool2d(x, 3, 2); in the fused model on the HIP kernels when the input qualifies."""
+    if not fused:
+        return F.max_pool2d(x, 3, 2)
+    from ..ops.pool import max_pool3x3s2
+
+    return max_pool3x3s2(x)
 
 
 def _branch_pool(cin, cout):
@@ -60,12 +83,13 @@ class InceptionA(nn.Module):
 class InceptionB(nn.Module):
     def __init__(self, cin):
         super().__init__()
+        self.fused = _FUSED_BN[0]
         self.b3 = BasicConv2d(cin, 384, kernel_size=3, stride=2)
         self.bd = nn.Sequential(BasicConv2d(cin, 64, kernel_size=1), BasicConv2d(64, 96, kernel_size=3, padding=1),
                                 BasicConv2d(96, 96, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.bd(x), F.max_pool2d(x, 3, 2)], 1)
+        return torch.cat([self.b3(x), self.bd(x), _max_pool3s2(x, self.fused)], 1)
 
 
 class InceptionC(nn.Module):
@@ -89,6 +113,7 @@ class InceptionC(nn.Module):
 class InceptionD(nn.Module):
     def __init__(self, cin):
         super().__init__()
+        self.fused = _FUSED_BN[0]
         self.b3 = nn.Sequential(BasicConv2d(cin, 192, kernel_size=1), BasicConv2d(192, 320, kernel_size=3, stride=2))
         self.b7 = nn.Sequential(BasicConv2d(cin, 192, kernel_size=1),
                                 BasicConv2d(192, 192, kernel_size=(1, 7), padding=(0, 3)),
@@ -96,7 +121,7 @@ class InceptionD(nn.Module):
                                 BasicConv2d(192, 192, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.b7(x), F.max_pool2d(x, 3, 2)], 1)
+        return torch.cat([self.b3(x), self.b7(x), _max_pool3s2(x, self.fused)], 1)
 
 
 class InceptionE(nn.Module):
@@ -122,10 +147,11 @@ class InceptionE(nn.Module):
 class InceptionV3(nn.Module):
     def __init__(self, num_classes: int = 1000):
         super().__init__()
+        pool = _pool_module
         self.stem = nn.Sequential(
             BasicConv2d(3, 32, kernel_size=3, stride=2), BasicConv2d(32, 32, kernel_size=3),
-            BasicConv2d(32, 64, kernel_size=3, padding=1), nn.MaxPool2d(3, 2),
-            BasicConv2d(64, 80, kernel_size=1), BasicConv2d(80, 192, kernel_size=3), nn.MaxPool2d(3, 2))
+            BasicConv2d(32, 64, kernel_size=3, padding=1), pool(),
+            BasicConv2d(64, 80, kernel_size=1), BasicConv2d(80, 192, kernel_size=3), pool())
         self.blocks = nn.Sequential(
             InceptionA(192, 32), InceptionA(256, 64), InceptionA(288, 64), InceptionB(288),
             InceptionC(768, 128), InceptionC(768, 160), InceptionC(768, 160), InceptionC(768, 192),

@@ -1,4 +1,7 @@
-"""2x2 / stride-2 max-pool on the HIP kernels of csrc/kernels/pool.hip (VGG-16's pools).
+"""Pooling on the HIP kernels of csrc/kernels/pool.hip: VGG-16's 2x2/s2 max-pool, and
+Inception-v3's 3x3/s2 max-pool and 3x3/s1/p1 average pool (see the section below).
+
+2x2 / stride-2 max-pool:
 
 The windows do not overlap, so no argmax tensor is written: the backward re-reads the window
 from x (kept alive as the pool's input anyway) and gathers, writing every dx element once.
@@ -47,3 +50,66 @@ class MaxPool2x2(nn.MaxPool2d):
 
     def forward(self, x):
         return max_pool2x2(x)
+
+
+# ---------------------------------------------------------------- 3x3 pools (Inception-v3)
+
+def _eligible3(x: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.shape[2] >= 3 and x.shape[3] >= 3
+            and x.is_contiguous(memory_format=torch.channels_last) and hip_available())
+
+
+class _MaxPool3s2Fn(torch.autograd.Function):
+    """3x3/s2 max-pool: the forward also writes a byte argmax per element (1/2 of y, vs
+    torch's int64 per element); the backward gathers through it (pool.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, pad):
+        y, arg = hip().maxpool3s2_forward(x, pad)
+        ctx.save_for_backward(arg)
+        ctx.hw = (x.shape[2], x.shape[3], pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        H, W, pad = ctx.hw
+        return hip().maxpool3s2_backward(dy.contiguous(memory_format=torch.channels_last), arg, H, W, pad), None
+
+
+def max_pool3x3s2(x: torch.Tensor, padding: int = 0) -> torch.Tensor:
+    """``F.max_pool2d(x, 3, 2, padding)`` (padding 0 or 1)."""
+    if padding in (0, 1) and _eligible3(x):
+        return _MaxPool3s2Fn.apply(x, padding)
+    return F.max_pool2d(x, 3, 2, padding)
+
+
+class _AvgPool3s1Fn(torch.autograd.Function):
+    """3x3/s1/p1 average pool with count_include_pad: the gradient is the same 9-tap
+    stencil applied to dy, so forward and backward are one kernel."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return hip().avgpool3s1(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return hip().avgpool3s1(dy.contiguous(memory_format=torch.channels_last))
+
+
+def avg_pool3x3s1(x: torch.Tensor) -> torch.Tensor:
+    """``F.avg_pool2d(x, 3, 1, 1)`` (count_include_pad=True, torch's default)."""
+    if _eligible3(x):
+        return _AvgPool3s1Fn.apply(x)
+    return F.avg_pool2d(x, 3, 1, 1)
+
+
+class MaxPool3x3s2(nn.MaxPool2d):
+    """``nn.MaxPool2d(3, 2)`` on the HIP kernels when eligible."""
+
+    def __init__(self, padding: int = 0):
+        super().__init__(3, 2, padding)
+
+    def forward(self, x):
+        return max_pool3x3s2(x, self.padding)

@@ -906,3 +906,48 @@ def test_relu_and_maxpool_propagate_nan(H):
     got = max_pool2x2(x)
     assert torch.equal(torch.isnan(got.float()), torch.isnan(ref))
     assert torch.equal(torch.nan_to_num(got.float(), nan=7.0), torch.nan_to_num(ref, nan=7.0))
+
+
+@needs_gpu
+@pytest.mark.parametrize("shape,pad", [((2, 64, 147, 147), 0), ((2, 192, 71, 71), 0), ((3, 288, 35, 35), 0),
+                                       ((2, 40, 9, 10), 0), ((2, 16, 12, 11), 1)])
+def test_maxpool3x3s2_matches_torch(shape, pad):
+    """3x3/s2 max-pool (byte argmax + gather backward) vs torch's max-pool on the same bf16
+    values: identical outputs and gradients (ties: first maximum, like torch)."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.pool import max_pool3x3s2
+
+    torch.manual_seed(12)
+    x = torch.randn(*shape, device="cuda").clamp_min(0).bfloat16().to(memory_format=torch.channels_last)
+    xr = x.float().cpu().contiguous().requires_grad_(True)  # CPU NCHW reference
+    yr = F.max_pool2d(xr, 3, 2, pad)
+    dy = torch.randn_like(yr).bfloat16().cuda().to(memory_format=torch.channels_last)
+    yr.backward(dy.float().cpu())
+    xa = x.clone().requires_grad_(True)
+    ya = max_pool3x3s2(xa, pad)
+    ya.backward(dy)
+    assert torch.equal(ya.float().cpu(), yr.detach())
+    assert ((xa.grad.float().cpu() - xr.grad).abs().max() <= 2e-2 * xr.grad.abs().max()).item()
+
+
+@needs_gpu
+@pytest.mark.parametrize("shape", [(2, 32, 35, 35), (2, 192, 17, 17), (3, 320, 8, 8), (2, 8, 3, 5)])
+def test_avgpool3x3s1_matches_torch(shape):
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.pool import avg_pool3x3s1
+
+    torch.manual_seed(13)
+    x = torch.randn(*shape, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    dy = torch.randn(*shape, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    # reference in float64 on the CPU (NCHW): on this ROCm build the GPU NHWC avg_pool2d
+    # BACKWARD returns the gradient shifted by the padding (tools/dbg_avgpool.py: its dx(0,0)
+    # equals the true dx(1,1)), so torch-on-GPU cannot be the reference for the gradient
+    xr = x.double().cpu().contiguous().requires_grad_(True)
+    yr = F.avg_pool2d(xr, 3, 1, 1)
+    yr.backward(dy.double().cpu().contiguous())
+    xa = x.clone().requires_grad_(True)
+    ya = avg_pool3x3s1(xa)
+    ya.backward(dy)
+    assert _rel(ya.cpu(), yr) < 1e-2 and _rel(xa.grad.cpu(), xr.grad) < 1e-2
