@@ -422,6 +422,10 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
         int target = 256 * (nw >= 4 ? 1 : 2);
         if (ks == 3) target *= nw == 1 ? 4 : 2;
         splits = (target + tiles / 2) / tiles;
+        // large-pixel 3x3 shapes (VGG-16's 56..224 layers, batch 256): ~100 K-steps per split
+        // and up to 512 splits (tools/bench_vgg_wgrad.py: 112x112 128->128 313 -> 477 TF/s,
+        // 56x56 128->256 587 -> 761 TF/s; 28x28 and smaller keep the default)
+        if (ks == 3 && P >= 800000) splits = std::max(splits, std::min(512, ksteps / 96));
         splits = std::max(1, std::min(splits, ksteps / 4));
     }
     splits = std::max(1, std::min(splits, ksteps));

@@ -1,0 +1,51 @@
+"""ResNet-50 1x1 convolution shapes (batch 256, NHWC bf16) on every tile variant of the MFMA
+conv kernel, with the fused BN-statistics epilogue the bottleneck uses: time, achieved HBM
+bandwidth (input + output bytes) and TF/s.  Picks the memory-bound shapes' best tile."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kungfu_amd._lib import hip  # noqa: E402
+
+H_ = hip()
+# (H, Cin, Cout, stride)
+SHAPES = [(56, 64, 64, 1), (56, 64, 256, 1), (56, 256, 64, 1), (56, 256, 128, 1), (28, 128, 512, 1),
+          (28, 512, 128, 1), (14, 256, 1024, 1), (14, 1024, 256, 1), (7, 512, 2048, 1), (7, 2048, 512, 1)]
+
+
+def cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def timeit(f, n=20):
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+N = int(os.environ.get("BATCH", "256"))
+for Hh, C, K, s in SHAPES:
+    x = cl(torch.randn(N, C, Hh, Hh, device="cuda")).bfloat16()
+    w = cl(torch.randn(K, C, 1, 1, device="cuda") * 0.05).bfloat16()
+    st = torch.zeros(H_.conv_stat_slots * 2 * K, dtype=torch.float64, device="cuda")
+    M = N * (Hh // s) * (Hh // s)
+    nbytes = 2.0 * (N * Hh * Hh * C + M * K)
+    flop = 2.0 * M * K * C
+    res = []
+    for v in range(7):
+        for epi, tag in ((st, "st"), (None, "")):
+            try:
+                us = timeit(lambda: H_.conv(x, w, s, epi, None, v))
+            except Exception:  # noqa: BLE001
+                continue
+            res.append("v%d%s:%.0fus/%.1fTB/s" % (v, tag, us, nbytes / us / 1e6))
+    print("H=%2d %4d->%4d  %6.0fMB %5.1fGF  %s" % (Hh, C, K, nbytes / 1e6, flop / 1e9, " ".join(res)), flush=True)
