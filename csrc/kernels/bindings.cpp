@@ -516,6 +516,58 @@ at::Tensor avgpool3s1(at::Tensor x) {
     return y;
 }
 
+// y, s, mean, rstd = layernorm(x [+ r]) over the last dim (bf16 rows, f32 affine)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_forward(at::Tensor x, c10::optional<at::Tensor> r,
+                                                                             at::Tensor gamma, at::Tensor beta,
+                                                                             double eps) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
+                "layernorm: x must be a contiguous bf16 GPU tensor");
+    const int D = static_cast<int>(x.size(-1));
+    TORCH_CHECK(kfk::layernorm_supported(D), "layernorm: unsupported row length ", D);
+    TORCH_CHECK(gamma.scalar_type() == at::kFloat && beta.scalar_type() == at::kFloat && gamma.numel() == D &&
+                    beta.numel() == D && gamma.is_contiguous() && beta.is_contiguous(),
+                "layernorm: f32 gamma/beta of length D");
+    const uint16_t *rp = nullptr;
+    if (r && r->defined()) {
+        TORCH_CHECK(r->scalar_type() == at::kBFloat16 && r->is_contiguous() && r->sizes() == x.sizes(),
+                    "layernorm: residual must match x");
+        rp = reinterpret_cast<const uint16_t *>(r->data_ptr());
+    }
+    c10::DeviceGuard gd(x.device());
+    const int64_t rows = x.numel() / D;
+    auto y = at::empty_like(x);
+    auto sv = rp ? at::empty_like(x) : x;
+    auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+    auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+    kfk::launch_layernorm_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, gamma.data_ptr<float>(),
+                                  beta.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                                  rp ? reinterpret_cast<uint16_t *>(sv.data_ptr()) : nullptr, mean.data_ptr<float>(),
+                                  rstd.data_ptr<float>(), rows, D, static_cast<float>(eps), stream_of(x, 0));
+    return {y, sv, mean, rstd};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy, at::Tensor s, at::Tensor gamma,
+                                                                  at::Tensor mean, at::Tensor rstd) {
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && s.sizes() == dy.sizes() &&
+                    s.scalar_type() == at::kBFloat16 && s.is_contiguous(),
+                "layernorm_backward: contiguous bf16 dy and s of equal shape");
+    const int D = static_cast<int>(dy.size(-1));
+    TORCH_CHECK(kfk::layernorm_supported(D) && gamma.numel() == D, "layernorm_backward: bad D");
+    c10::DeviceGuard gd(dy.device());
+    const int64_t rows = dy.numel() / D;
+    TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_backward: stats size");
+    auto ds = at::empty_like(dy);
+    auto partial = at::empty({kfk::layernorm_bwd_blocks(rows), 2, D}, dy.options().dtype(at::kFloat));
+    auto dgamma = at::empty({D}, dy.options().dtype(at::kFloat));
+    auto dbeta = at::empty({D}, dy.options().dtype(at::kFloat));
+    kfk::launch_layernorm_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                   reinterpret_cast<const uint16_t *>(s.data_ptr()), gamma.data_ptr<float>(),
+                                   mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                   reinterpret_cast<uint16_t *>(ds.data_ptr()), partial.data_ptr<float>(),
+                                   dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, stream_of(dy, 0));
+    return {ds, dgamma, dbeta};
+}
+
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
     TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
@@ -1049,6 +1101,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("maxpool2x2_backward", &maxpool2x2_backward, "2x2/s2 max-pool gradient (gather from x, dy)");
     m.def("maxpool3s2_forward", &maxpool3s2_forward, "3x3/s2 max-pool (pad 0/1), NHWC bf16 -> (y, argmax bytes)");
     m.def("maxpool3s2_backward", &maxpool3s2_backward, "3x3/s2 max-pool gradient (gather via the argmax bytes)");
+    m.def("layernorm_supported", &kfk::layernorm_supported);
+    m.def("layernorm_forward", &layernorm_forward, "fused residual-add + LayerNorm (bf16 rows) -> (y, s, mean, rstd)",
+          py::arg("x"), py::arg("r"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
+    m.def("layernorm_backward", &layernorm_backward, "LayerNorm backward -> (ds, dgamma, dbeta)");
     m.def("avgpool3s1", &avgpool3s1, "3x3/s1/p1 average pool, count_include_pad (also its own gradient on dy)");
     m.def("bias_act_forward_", &bias_act_forward_, "y = relu(y + bias) in place (NHWC bf16, f32 bias)",
           py::arg("y"), py::arg("bias"), py::arg("relu") = true);

@@ -221,6 +221,17 @@ void launch_maxpool3s2_forward(const uint16_t *x, uint16_t *y, uint8_t *arg, int
 void launch_maxpool3s2_backward(const uint16_t *dy, const uint8_t *arg, uint16_t *dx, int64_t N, int H, int W, int C,
                                 int pad, hipStream_t s);
 void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s);
+
+// Fused residual-add + LayerNorm over rows of D (layernorm.hip): bf16 x, r (optional), y, s
+// (= x + r, saved for backward), f32 gamma/beta/mean/rstd; backward -> ds (bf16) and
+// dgamma/dbeta (f32) through [blocks][2][D] f32 partials.
+bool layernorm_supported(int D);
+int layernorm_bwd_blocks(int64_t rows);
+void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
+                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st);
+void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
+                               const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
+                               int64_t rows, int D, hipStream_t st);
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
                                 hipStream_t s);
 

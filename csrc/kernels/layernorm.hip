@@ -1,0 +1,250 @@
+// Fused residual-add + LayerNorm for transformer blocks (BERT-base, D = 768), bf16 in/out,
+// f32 statistics, for gfx950.
+//
+//   forward   s = x + r (optional r);  y = (s - mean) * rstd * gamma + beta      (bf16 y, s)
+//   backward  g = dy * gamma;  ds = rstd * (g - mean(g) - xhat * mean(g * xhat))
+//             dgamma = sum_rows dy * xhat,  dbeta = sum_rows dy                    (f32)
+//
+// Why: under bf16 autocast torch runs LayerNorm in f32 (an f32 output the next GEMM casts
+// back to bf16), the residual add in f32, and the backward as three kernels (input
+// gradient, per-block gamma/beta partials, their reduction): ~5 ms of a 30 ms BERT-base
+// step (profiles/r2b_bert_base_gns.md).  Here the residual stream stays bf16 and each
+// direction is one pass over the activations plus a tiny column reduction.
+//
+// Layout: rows of D contiguous elements (D % 256 == 0, D <= 4096).  One wave64 per row;
+// lane l owns the 4-element groups l, l + 64, l + 128, ... (8-byte accesses, coalesced
+// across the wave), so each lane's columns are FIXED: the backward accumulates its
+// dgamma/dbeta columns in registers across all the rows its wave visits (grid-stride),
+// then one block reduction writes [blocks][2][D] f32 partials for a column-sum kernel.
+#include "common.hpp"
+#include "kernels.hpp"
+
+#include <stdexcept>
+
+namespace kfk {
+
+namespace {
+
+constexpr int kLnWaves = 4;  // waves (rows in flight) per block
+
+__device__ __forceinline__ void unpack4(const uint2 &v, float (&f)[4]) {
+    f[0] = __uint_as_float(v.x << 16);
+    f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16);
+    f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint2 pack4(const float (&f)[4]) {
+    return make_uint2(static_cast<uint32_t>(f32_to_bf16(f[0])) | (static_cast<uint32_t>(f32_to_bf16(f[1])) << 16),
+                      static_cast<uint32_t>(f32_to_bf16(f[2])) | (static_cast<uint32_t>(f32_to_bf16(f[3])) << 16));
+}
+
+template <int G>  // G = D / 256 four-element groups per lane
+__global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const uint2 *__restrict__ x,
+                                                               const uint2 *__restrict__ r,
+                                                               const float *__restrict__ gamma,
+                                                               const float *__restrict__ beta, uint2 *__restrict__ y,
+                                                               uint2 *__restrict__ s_out, float *__restrict__ mean,
+                                                               float *__restrict__ rstd, int64_t rows, float eps) {
+    constexpr int D = 256 * G;
+    const int lane = threadIdx.x & 63;
+    float gm[G][4], bt[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            gm[j][k] = gamma[(j * 64 + lane) * 4 + k];
+            bt[j][k] = beta[(j * 64 + lane) * 4 + k];
+        }
+    const int64_t wstride = static_cast<int64_t>(gridDim.x) * kLnWaves;
+    for (int64_t row = static_cast<int64_t>(blockIdx.x) * kLnWaves + (threadIdx.x >> 6); row < rows; row += wstride) {
+        const int64_t base = row * (D / 4);
+        float v[G][4];
+        float sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            unpack4(x[base + j * 64 + lane], v[j]);
+            if (r) {
+                float t[4];
+                unpack4(r[base + j * 64 + lane], t);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[j][k] += t[k];
+            }
+            // the residual stream is bf16: normalise exactly the values that are stored
+            uint2 sv = pack4(v[j]);
+            if (s_out) s_out[base + j * 64 + lane] = sv;
+            unpack4(sv, v[j]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sum += v[j][k];
+        }
+        const float mu = wave_sum(sum) * (1.f / D);
+        float var = 0.f;
+#pragma unroll
+        for (int j = 0; j < G; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float d = v[j][k] - mu;
+                var += d * d;
+            }
+        const float rs = rsqrtf(wave_sum(var) * (1.f / D) + eps);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            float o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = (v[j][k] - mu) * rs * gm[j][k] + bt[j][k];
+            y[base + j * 64 + lane] = pack4(o);
+        }
+        if (lane == 0) {
+            mean[row] = mu;
+            rstd[row] = rs;
+        }
+    }
+}
+
+template <int G>
+__global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__restrict__ dy,
+                                                               const uint2 *__restrict__ s,
+                                                               const float *__restrict__ gamma,
+                                                               const float *__restrict__ mean,
+                                                               const float *__restrict__ rstd, uint2 *__restrict__ ds,
+                                                               float *__restrict__ partial, int64_t rows) {
+    constexpr int D = 256 * G;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float gm[G][4], dg[G][4], db[G][4];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            gm[j][k] = gamma[(j * 64 + lane) * 4 + k];
+            dg[j][k] = db[j][k] = 0.f;
+        }
+    const int64_t wstride = static_cast<int64_t>(gridDim.x) * kLnWaves;
+    for (int64_t row = static_cast<int64_t>(blockIdx.x) * kLnWaves + wave; row < rows; row += wstride) {
+        const int64_t base = row * (D / 4);
+        const float mu = mean[row], rs = rstd[row];
+        float xh[G][4], g[G][4];
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            float d[4], xv[4];
+            unpack4(dy[base + j * 64 + lane], d);
+            unpack4(s[base + j * 64 + lane], xv);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                xh[j][k] = (xv[k] - mu) * rs;
+                g[j][k] = d[k] * gm[j][k];
+                a1 += g[j][k];
+                a2 += g[j][k] * xh[j][k];
+                dg[j][k] += d[k] * xh[j][k];
+                db[j][k] += d[k];
+            }
+        }
+        const float m1 = wave_sum(a1) * (1.f / D), m2 = wave_sum(a2) * (1.f / D);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            float o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
+            ds[base + j * 64 + lane] = pack4(o);
+        }
+    }
+    // block reduction of the per-lane column sums -> partial[block][2][D]
+    __shared__ float red[kLnWaves][2][D];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            red[wave][0][(j * 64 + lane) * 4 + k] = dg[j][k];
+            red[wave][1][(j * 64 + lane) * 4 + k] = db[j][k];
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += 64 * kLnWaves) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kLnWaves; ++w) t += (&red[w][0][0])[c];
+        partial[static_cast<int64_t>(blockIdx.x) * 2 * D + c] = t;
+    }
+}
+
+// out[c] = sum_b partial[b][c] for c < 2D.  Block = 64 consecutive columns x 16 row groups
+// (coalesced 256-byte row segments, 16 independent f64 chains per column), then an LDS
+// reduction over the groups.
+constexpr int kColGroups = 16;
+__global__ __launch_bounds__(64 * kColGroups) void ln_colsum_kernel(const float *__restrict__ partial, int nblocks,
+                                                                    int cols, float *__restrict__ dgamma,
+                                                                    float *__restrict__ dbeta, int D) {
+    __shared__ double red[kColGroups][64];
+    const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + lane;
+    double t = 0;
+    if (c < cols) {
+#pragma unroll 8
+        for (int b = grp; b < nblocks; b += kColGroups) t += partial[static_cast<int64_t>(b) * cols + c];
+    }
+    red[grp][lane] = t;
+    __syncthreads();
+    if (grp == 0 && c < cols) {
+        double u = 0;
+#pragma unroll
+        for (int g = 0; g < kColGroups; ++g) u += red[g][lane];
+        if (c < D) dgamma[c] = static_cast<float>(u);
+        else dbeta[c - D] = static_cast<float>(u);
+    }
+}
+
+template <typename F>
+void dispatch_g(int D, F &&f) {
+    switch (D / 256) {
+    case 1: f(std::integral_constant<int, 1>()); break;
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 6: f(std::integral_constant<int, 6>()); break;
+    case 8: f(std::integral_constant<int, 8>()); break;
+    case 12: f(std::integral_constant<int, 12>()); break;
+    case 16: f(std::integral_constant<int, 16>()); break;
+    default: throw std::invalid_argument("layernorm: D must be 256 x {1,2,3,4,6,8,12,16}");
+    }
+}
+
+}  // namespace
+
+bool layernorm_supported(int D) {
+    const int g = D / 256;
+    return D % 256 == 0 && (g == 1 || g == 2 || g == 3 || g == 4 || g == 6 || g == 8 || g == 12 || g == 16);
+}
+
+int layernorm_bwd_blocks(int64_t rows) {
+    int64_t b = (rows + kLnWaves * 8 - 1) / (kLnWaves * 8);  // >= 8 rows per wave
+    if (b > 1024) b = 1024;
+    return static_cast<int>(b < 1 ? 1 : b);
+}
+
+void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
+                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st) {
+    if (rows <= 0) return;
+    int64_t blocks = (rows + kLnWaves - 1) / kLnWaves;
+    if (blocks > 8192) blocks = 8192;
+    dispatch_g(D, [&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        ln_fwd_kernel<G><<<static_cast<int>(blocks), 64 * kLnWaves, 0, st>>>(
+            reinterpret_cast<const uint2 *>(x), reinterpret_cast<const uint2 *>(r), gamma, beta,
+            reinterpret_cast<uint2 *>(y), reinterpret_cast<uint2 *>(s), mean, rstd, rows, eps);
+    });
+}
+
+void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
+                               const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
+                               int64_t rows, int D, hipStream_t st) {
+    if (rows <= 0) return;
+    const int blocks = layernorm_bwd_blocks(rows);
+    dispatch_g(D, [&](auto gc) {
+        constexpr int G = decltype(gc)::value;
+        ln_bwd_kernel<G><<<blocks, 64 * kLnWaves, 0, st>>>(reinterpret_cast<const uint2 *>(dy),
+                                                            reinterpret_cast<const uint2 *>(s), gamma, mean, rstd,
+                                                            reinterpret_cast<uint2 *>(ds), partial, rows);
+    });
+    ln_colsum_kernel<<<(2 * D + 63) / 64, 64 * kColGroups, 0, st>>>(partial, blocks, 2 * D, dgamma, dbeta, D);
+}
+
+}  // namespace kfk

@@ -12,13 +12,17 @@ import torch.nn.functional as F
 class BertLayer(nn.Module):
     def __init__(self, d=768, heads=12, ffn=3072, dropout=0.1):
         super().__init__()
+        from ..ops.layernorm import AddLayerNorm
+
         self.heads = heads
         self.qkv = nn.Linear(d, 3 * d)
         self.out = nn.Linear(d, d)
-        self.ln1 = nn.LayerNorm(d, eps=1e-12)
+        # fused residual-add + LayerNorm (HIP, bf16 residual stream) -- torch.nn.LayerNorm
+        # parameters and state_dict keys, torch composition off the GPU fast path
+        self.ln1 = AddLayerNorm(d, eps=1e-12)
         self.fc1 = nn.Linear(d, ffn)
         self.fc2 = nn.Linear(ffn, d)
-        self.ln2 = nn.LayerNorm(d, eps=1e-12)
+        self.ln2 = AddLayerNorm(d, eps=1e-12)
         self.dropout = dropout
 
     def forward(self, x, mask=None):
@@ -27,9 +31,9 @@ class BertLayer(nn.Module):
         a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
                                            dropout_p=self.dropout if self.training else 0.0)
         a = a.transpose(1, 2).reshape(B, S, D)
-        x = self.ln1(x + F.dropout(self.out(a), self.dropout, self.training))
+        x = self.ln1(x, F.dropout(self.out(a), self.dropout, self.training))
         h = self.fc2(F.gelu(self.fc1(x)))
-        return self.ln2(x + F.dropout(h, self.dropout, self.training))
+        return self.ln2(x, F.dropout(h, self.dropout, self.training))
 
 
 class BertForPreTraining(nn.Module):
@@ -62,6 +66,8 @@ class BertForPreTraining(nn.Module):
         pos = torch.arange(S, device=ids.device)
         types = torch.zeros_like(ids) if types is None else types
         x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ(types))
+        if torch.is_autocast_enabled(x.device.type) and x.is_cuda:
+            x = x.to(torch.get_autocast_dtype(x.device.type))  # bf16 residual stream from here on
         for layer in self.layers:
             x = layer(x)
         hs = x

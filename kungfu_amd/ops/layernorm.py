@@ -1,0 +1,58 @@
+"""Fused residual-add + LayerNorm on the HIP kernels of csrc/kernels/layernorm.hip.
+
+``AddLayerNorm(D)`` is an ``nn.LayerNorm`` (same parameters and state_dict keys) whose
+``forward(x, residual=None)`` computes ``layer_norm(x + residual)``.  For bf16 GPU inputs
+(the transformer residual stream under bf16 autocast) it runs one HIP pass each way and
+keeps the stream in bf16; torch's autocast LayerNorm instead produces f32 (which the next
+GEMM casts back to bf16) and its backward is three kernels.  Anything else (CPU, f32,
+unsupported D) uses the torch composition.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._lib import hip, hip_available
+
+
+class _AddLayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, eps):
+        y, s, mean, rstd = hip().layernorm_forward(x, r, gamma, beta, eps)
+        ctx.save_for_backward(s, gamma, mean, rstd)
+        ctx.has_r = r is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, gamma, mean, rstd = ctx.saved_tensors
+        ds, dg, db = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd)
+        # d(x + r)/dx = d(x + r)/dr = 1: both inputs receive ds
+        return ds, (ds if ctx.has_r else None), dg, db, None
+
+
+def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and hip_available()):
+        return False
+    if r is not None and (r.dtype != torch.bfloat16 or r.shape != x.shape or not r.is_contiguous()):
+        return False
+    return w is not None and w.dtype == torch.float32 and hip().layernorm_supported(int(x.shape[-1]))
+
+
+def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, bias: torch.Tensor,
+                   eps: float = 1e-5) -> torch.Tensor:
+    """``F.layer_norm(x + residual, (D,), weight, bias, eps)``."""
+    if _eligible(x, residual, weight):
+        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps))
+    s = x if residual is None else x + residual
+    return F.layer_norm(s, s.shape[-1:], weight, bias, eps)
+
+
+class AddLayerNorm(nn.LayerNorm):
+    def forward(self, x, residual=None):
+        if residual is not None and residual.dtype != x.dtype and x.is_cuda:
+            residual = residual.to(x.dtype)  # e.g. an f32 dropout output beside a bf16 stream
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps)

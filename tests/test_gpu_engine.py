@@ -252,3 +252,37 @@ def test_resnet50_full_size_engine_matches_stock():
         assert all(y < x for x, y in zip(t[:7], t[1:7])) and t[-1] < 0.65 * t[0], t
     for x0, xe in zip(a, e):  # measured within 0.5 % at every step
         assert abs(xe - x0) <= 0.02 * x0, (a, e)
+
+
+@needs_gpu
+@pytest.mark.parametrize("D,rows,res", [(768, 4096, True), (768, 333, False), (1024, 1000, True), (256, 7, True)])
+def test_add_layernorm_matches_fp32(D, rows, res):
+    """Fused residual-add + LayerNorm (bf16 stream) vs the float32 torch composition:
+    output, both input gradients, dgamma, dbeta."""
+    from kungfu_amd.ops.layernorm import add_layer_norm
+
+    torch.manual_seed(21)
+    x = (torch.randn(rows, D, device="cuda") * 2 + 0.3).bfloat16()
+    r = torch.randn(rows, D, device="cuda").bfloat16() if res else None
+    w = torch.rand(D, device="cuda") + 0.5
+    b = torch.randn(D, device="cuda") * 0.1
+    dy = torch.randn(rows, D, device="cuda").bfloat16()
+    xr = x.float().requires_grad_(True)
+    rr = r.float().requires_grad_(True) if res else None
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr + rr if res else xr, (D,), wr, br, 1e-12)
+    yr.backward(dy.float())
+    xa = x.clone().requires_grad_(True)
+    ra = r.clone().requires_grad_(True) if res else None
+    wa, ba = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ya = add_layer_norm(xa, ra, wa, ba, 1e-12)
+    assert ya.dtype == torch.bfloat16
+    ya.backward(dy)
+
+    def rel(a, b_):
+        return ((a.float() - b_.float()).norm() / b_.float().norm()).item()
+
+    assert rel(ya, yr) < 1e-2
+    assert rel(xa.grad, xr.grad) < 2e-2 and rel(wa.grad, wr.grad) < 1e-2 and rel(ba.grad, br.grad) < 1e-3
+    if res:
+        assert torch.equal(xa.grad, ra.grad) and rel(ra.grad, rr.grad) < 2e-2
