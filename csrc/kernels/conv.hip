@@ -25,6 +25,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace kfk {
@@ -71,7 +72,11 @@ __device__ __forceinline__ void wait_vmcnt() {
 //   kEpiBwdCoef / kEpiBwdBits  the output is the gradient of a BN(+ReLU) output whose input
 //                 is ea.bx: sum(dz) and sum(dz * x) with dz = grad * relu' from the forward
 //                 coefficients ea.fcoef (recomputed) or from the 1-bit mask ea.bmask.
-template <int KS, int WM, int WN, int STAGES, int EPI, int TM = 4, int TN = 4>
+// PERSIST: the grid is smaller than the tile count; each block keeps ONE n-tile and walks
+// m-tiles mt0, mt0 + mstride, ... -- its per-channel statistics accumulate in registers
+// across all of them and reach the f64 slots with ONE set of atomics per block (instead of
+// one per tile: 3.2 M f64 atomics for a 56x56 64->256 conv at batch 256).
+template <int KS, int WM, int WN, int STAGES, int EPI, int TM = 4, int TN = 4, bool PERSIST = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__restrict__ x,
                                                             const uint16_t *__restrict__ w,
                                                             uint16_t *__restrict__ y,
@@ -102,8 +107,25 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     const int nwg = gridDim.x, orig = blockIdx.x;
     const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
     const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-    const int mt = wg / g.ntiles, nt = wg - mt * g.ntiles;
-    const int m0 = mt * BM, n0 = nt * BN;
+    const int mt_first = wg / g.ntiles, nt = wg - mt_first * g.ntiles;
+    const int n0 = nt * BN;
+    const int mstride = PERSIST ? nwg / g.ntiles : g.mtiles;  // nwg % ntiles == 0 when persistent
+    const int cv = tid % (BN / 8);  // the epilogue's fixed 8-channel group of this thread
+    float s1[8], s2[8], sc[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+    if constexpr ((EPI & kEpiBwdCoef) != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sc[k] = ea.fcoef[n0 + cv * 8 + k];
+            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
+        }
+    }
+    int mt_last = mt_first;
+    for (int mt = mt_first; mt < g.mtiles; mt += mstride) {
+    mt_last = mt;
+    const int m0 = mt * BM;
+    if (mt != mt_first) __syncthreads();  // every thread is done with the previous tile's LDS
 
     // ---- per-lane staging descriptors (fixed for the whole K loop)
     // lane l of a glds instruction writes image bytes [l*16, l*16+16) of its
@@ -246,17 +268,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
     // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
     static_assert(NT % VPR == 0, "fixed channel group per thread");
-    const int cv = tid % VPR;
-    float s1[8], s2[8], sc[8], sh[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-    if constexpr ((EPI & kEpiBwdCoef) != 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[k] = ea.fcoef[n0 + cv * 8 + k];
-            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
-        }
-    }
     for (int v = tid; v < BM * VPR; v += NT) {
         const int row = v / VPR;
         const int m = m0 + row;
@@ -309,6 +320,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             }
         }
     }
+    }  // m-tile loop
     if constexpr (STATS) {
         // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
         float *red = reinterpret_cast<float *>(lds + BM * CROW);
@@ -327,7 +339,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 t1 += red[p * BN + col];
                 t2 += red[(GROUPS + p) * BN + col];
             }
-            double *sl = ea.stats + (mt % kStatSlots) * 2 * g.K;  // spread atomics over slots
+            double *sl = ea.stats + ((mt_last + wg) % kStatSlots) * 2 * g.K;  // spread atomics over slots
             atomicAdd(sl + n0 + col, t1);
             atomicAdd(sl + g.K + n0 + col, t2);
         }
@@ -402,6 +414,21 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     if (g.K % BN) throw std::invalid_argument("conv: Cout not a multiple of the tile");
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = g.K / BN;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
+    if constexpr (STATS) {
+        // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
+        // statistics flush per block instead of per tile
+        static const int cap = [] {
+            const char *v = std::getenv("KUNGFU_CONV_PERSIST_BLOCKS");
+            return v ? std::atoi(v) : 1024;
+        }();
+        const int per_n = cap / g.ntiles;
+        if (cap > 0 && per_n >= 1 && g.mtiles > 2 * per_n) {
+            conv_kernel<KS, WM, WN, ST, EPI, TM, TN, true><<<per_n * g.ntiles, 64 * WM * WN, 0, s>>>(
+                x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
+            return;
+        }
+    }
     conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
         x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
 }

@@ -951,3 +951,34 @@ def test_avgpool3x3s1_matches_torch(shape):
     ya = avg_pool3x3s1(xa)
     ya.backward(dy)
     assert _rel(ya.cpu(), yr) < 1e-2 and _rel(xa.grad.cpu(), xr.grad) < 1e-2
+
+
+@needs_gpu
+@pytest.mark.parametrize("H,C,K,stride,ks", [(56, 64, 256, 1, 1), (28, 128, 512, 1, 1), (28, 64, 128, 1, 3),
+                                            (56, 256, 512, 2, 1)])
+def test_conv_persistent_stats_epilogue(H, C, K, stride, ks):
+    """Large-M convolutions take the persistent-block path of the statistics epilogue (one
+    atomic flush per block, stats accumulated across m-tiles): output vs torch, and the
+    per-channel sum / sum of squares vs float64 sums of that output."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(14)
+    N = 64
+    x = torch.randn(N, C, H, H, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, ks, ks, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+    st = torch.zeros(H_slots() * 2 * K, dtype=torch.float64, device="cuda")
+    from kungfu_amd._lib import hip
+
+    y = hip().conv(x, w, stride, st, None, -1)
+    ref = F.conv2d(x.float(), w.float(), stride=stride, padding=(ks - 1) // 2)
+    assert _rel(y, ref) < 1e-2
+    sums = st.view(-1, 2, K).sum(0)
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, K)
+    torch.testing.assert_close(sums[0], yd.sum(0), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(sums[1], (yd * yd).sum(0), rtol=1e-6, atol=1e-3)
+
+
+def H_slots():
+    from kungfu_amd._lib import hip
+
+    return hip().conv_stat_slots
