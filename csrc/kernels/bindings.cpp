@@ -1111,6 +1111,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("bias_act_backward", &bias_act_backward, "(dy * (y > 0), its per-channel sum) in one pass",
           py::arg("dy"), py::arg("y"), py::arg("relu") = true);
     m.def("conv_wgrad_variants", &kfk::conv_wgrad_variants);
+    m.def("conv_wgrad_max_pixels", &kfk::conv_wgrad_max_pixels, py::arg("N"), py::arg("H"), py::arg("W"),
+          py::arg("Cin"), py::arg("Cout"), py::arg("ks"), py::arg("stride"));
     m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
         const auto p = kfk::conv_wgrad_plan(N, H, W, Cin, Cout, ks, stride, variant, splits);
         return py::make_tuple(p.variant, p.splits, p.kps, p.ws_floats);

@@ -267,6 +267,208 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Row-image 3x3 / stride-1 weight gradient for narrow channel tiles (64 co x 64 ci per tap).
+//
+// wgrad_kernel runs one workgroup per TAP: every tap re-stages its own copy of dy and of the
+// shifted input, and a 64x64 tile is one wave whose 16 LDS-DMA pieces per K-step cost more
+// issue time than its 32 MFMAs (VGG-16 64->64 at 224x224: 247 TF/s; ResNet-50 layer1: 238).
+// Here ONE workgroup of 9 waves (wave = tap) shares each K-step's staging:
+//   * a K-step is a segment of 64 output pixels: 64 consecutive pixels of one output row
+//     (OW >= 64) or R = 64 / OW whole rows (OW < 64);
+//   * dy is staged as 64 pixel rows (A operand, as in wgrad_kernel), the input as an image of
+//     the (R + 2) input rows x (L + 2) pixels around the segment, zero-padded at the borders;
+//   * tap (kh, kw)'s B operand is that image read at row offset kh * (L + 2) + kw: the
+//     transposing reads (ds_read_b64_tr_b16) take per-lane row addresses, so the im2col shift
+//     is only an address offset -- every input pixel is staged once per segment.
+// 33-35 LDS-DMA pieces per K-step are spread over the 9 waves (4 each) against 32 MFMAs per
+// wave.  Partial tiles use wgrad_kernel's workspace order (reduced by wgrad_reduce_kernel).
+struct RGeo {
+    int N, H, W, C, K;
+    int L, R, spr, gpi, nseg;  // segment: L pixels per row, R rows; segments per row / per image
+    int XW, xrows, xpieces;    // input image: XW = L + 2 pixels per row, xrows rows, 1 KB pieces
+    int mtiles, ntiles, tiles, splits, kps;
+};
+
+template <int STAGES>
+__global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restrict__ dy,
+                                                         const uint16_t *__restrict__ x,
+                                                         float *__restrict__ part, void *__restrict__ dw,
+                                                         const uint16_t *__restrict__ zero, RGeo g, int out_f32,
+                                                         int accumulate, int atomic_out) {
+    constexpr int ROW = 128;            // 64 channels
+    constexpr int MAXP = 4;             // pieces per wave per K-step (9 * 4 >= 8 + 25)
+    constexpr int STAGE = (8 + 25 + 1) * 1024;  // dy 8 KB | input image <= 25 KB | dummy 1 KB
+    constexpr int DUMMY = (8 + 25) * 1024;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // = tap
+    const int kh = wave / 3, kw = wave - 3 * (wave / 3);
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, rr8 = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (orig >> 3);
+    const int mn = g.mtiles * g.ntiles;
+    const int split = wg / mn, ctile = wg - split * mn;
+    const int mt = ctile / g.ntiles, nt = ctile - mt * g.ntiles;
+    const int m0 = mt * 64, n0 = nt * 64;
+    const int seg0 = split * g.kps;
+    int nsteps = g.nseg - seg0;
+    if (nsteps > g.kps) nsteps = g.kps;
+
+    // ---- staging descriptors: wave issues pieces wave + 9u; piece < 8: dy, else input image
+    const int total = 8 + g.xpieces;
+    int p_kind[MAXP], p_r[MAXP], p_c[MAXP], p_col[MAXP];  // kind 0 dy, 1 x, 2 dummy
+#pragma unroll
+    for (int u = 0; u < MAXP; ++u) {
+        const int pq = wave + 9 * u;
+        const int pc = lane & 7;
+        if (pq < 8) {
+            const int t = pq * 8 + (lane >> 3);  // dy slot
+            p_kind[u] = 0;
+            p_r[u] = t / g.L;
+            p_c[u] = t - p_r[u] * g.L;
+            if (p_r[u] >= g.R) p_r[u] = 1 << 20;  // slot past the segment: invalid
+            p_col[u] = m0 + ((((pc >> 1) ^ hswz<ROW>(t)) << 1) | (pc & 1)) * 8;
+        } else if (pq < total) {
+            const int t = (pq - 8) * 8 + (lane >> 3);  // image row
+            p_kind[u] = 1;
+            p_r[u] = t / g.XW;
+            p_c[u] = t - p_r[u] * g.XW;
+            if (t >= g.xrows) p_r[u] = 1 << 20;
+            p_col[u] = n0 + ((((pc >> 1) ^ hswz<ROW>(t)) << 1) | (pc & 1)) * 8;
+        } else {
+            p_kind[u] = 2;
+            p_r[u] = p_c[u] = p_col[u] = 0;
+        }
+    }
+    const int segs_img = g.gpi * g.spr;
+    auto stage = [&](int ks, int buf) {
+        const int seg = seg0 + ks;
+        const int n = seg / segs_img, rem = seg - n * segs_img;
+        const int grp = rem / g.spr, sidx = rem - grp * g.spr;
+        const int oh0 = grp * g.R, ow0 = sidx * 64;
+        uint8_t *base = lds + buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            const int pq = wave + 9 * u;
+            const uint16_t *src = zero;
+            uint8_t *dst = base + DUMMY;
+            if (p_kind[u] == 0) {
+                const int oh = oh0 + p_r[u], ow = ow0 + p_c[u];
+                if (oh < g.H && ow < g.W) src = dy + static_cast<uint32_t>(((n * g.H + oh) * g.W + ow) * g.K + p_col[u]);
+                dst = base + pq * 1024;
+            } else if (p_kind[u] == 1) {
+                const int ih = oh0 + p_r[u] - 1, iw = ow0 + p_c[u] - 1;
+                if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                    static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
+                    src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + p_col[u]);
+                dst = base + pq * 1024;
+            }
+            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        }
+    };
+
+    // ---- fragment addresses.  lane = 16 fg + 4 fq + fp; K-slots j = 8 fg + fq + {0, 4, 32, 36}.
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int rowa0 = 8 * fg + fq;
+    int aoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] = rowa0 * ROW + 32 * (i ^ hswz<ROW>(rowa0)) + 8 * fp;
+    int boff[4][4];  // [sub-read][ci block]
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int j = rowa0 + (s & 1) * 4 + (s >> 1) * 32;
+        const int r = j / g.L, c = j - r * g.L;
+        const int jrow = r < g.R ? r * g.XW + c : 0;  // slots past the segment read a staged row (dy is 0)
+        const int trow = jrow + kh * g.XW + kw;
+        const int h = hswz<ROW>(trow);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) boff[s][i] = 8192 + trow * ROW + 32 * (i ^ h) + 8 * fp;
+    }
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p)
+        if (p < nsteps) stage(p, p);
+    int buf = 0;
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if (ks + STAGES - 1 <= nsteps) wait_vmcnt<MAXP * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t *base = lds + buf * STAGE;
+        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af0[i] = tr_frag(base + aoff[i], base + aoff[i] + 4 * ROW);
+            bf0[i] = tr_frag(base + boff[0][i], base + boff[1][i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            af1[i] = tr_frag(base + aoff[i] + 32 * ROW, base + aoff[i] + 36 * ROW);
+            bf1[i] = tr_frag(base + boff[2][i], base + boff[3][i]);
+        }
+        mfma_block(af0, bf0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_block(af1, bf1);
+        buf = buf + 1 == STAGES ? 0 : buf + 1;
+    }
+    wait_vmcnt<0>();
+
+    // ---- epilogue (wgrad_kernel's three forms; tile = this wave's tap)
+    const int tap = wave, taps = 9;
+    if (atomic_out || g.splits == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = m0 + i * 16 + (lane >> 4) * 4 + r;
+                    const int ci = n0 + j * 16 + (lane & 15);
+                    const int64_t e = (static_cast<int64_t>(co) * taps + tap) * g.C + ci;
+                    float v = acc[i][j][r];
+                    if (atomic_out) {
+                        atomicAdd(static_cast<float *>(dw) + e, v);
+                    } else if (out_f32) {
+                        float *o = static_cast<float *>(dw) + e;
+                        *o = accumulate ? *o + v : v;
+                    } else {
+                        uint16_t *o = static_cast<uint16_t *>(dw) + e;
+                        if (accumulate) v += bf16_to_f32(*o);
+                        *o = f32_to_bf16(v);
+                    }
+                }
+    } else {
+        const int tile = tap * mn + mt * g.ntiles + nt;
+        f32x4 *dst = reinterpret_cast<f32x4 *>(part + (static_cast<int64_t>(split) * g.tiles + tile) * 4096) + lane;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * 64);
+    }
+}
+
 // Sum the split partials (workspace order of wgrad_kernel) and scatter to dw.
 // Block = 256 threads = OUT float4 outputs x SG split groups (SG = 256 / OUT, a power of
 // two <= splits): a few K outputs with hundreds of splits (the 56x56 layers) still keep
@@ -331,11 +533,46 @@ struct Tile {
 };
 // variant -> tile (co x ci): 0 128x128, 1 128x64, 2 64x128, 3 64x64, 4 256x128, 5 128x256
 constexpr Tile kTiles[] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}, {4, 2}, {2, 4}};
-constexpr int kNumVariants = 6;
+constexpr int kNumVariants = 7;  // + 6: wgrad_rows_kernel (3x3 / stride 1, 9 taps per workgroup)
+constexpr int kRowsVariant = 6;
+
+bool rows_supported(int Cin, int Cout, int ks, int stride) {
+    return ks == 3 && stride == 1 && Cin % 64 == 0 && Cout % 64 == 0;
+}
+// default for the narrow channel counts (tools/bench_wgrad.py): wide tiles keep the tap-tiled kernel
+bool rows_default(int Cin, int Cout, int ks, int stride) {
+    return rows_supported(Cin, Cout, ks, stride) && Cin <= 128 && Cout <= 128;
+}
+
+RGeo rows_segments(int N, int H, int W, int Cin, int Cout) {
+    RGeo g{};
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
+    if (W >= 64) {
+        g.L = 64, g.R = 1, g.spr = (W + 63) / 64, g.gpi = H;
+    } else {
+        g.L = W, g.R = 64 / W, g.spr = 1, g.gpi = (H + g.R - 1) / g.R;
+    }
+    g.nseg = N * g.gpi * g.spr;
+    g.XW = g.L + 2;
+    g.xrows = (g.R + 2) * g.XW;
+    g.xpieces = (g.xrows + 7) / 8;
+    g.mtiles = Cout / 64, g.ntiles = Cin / 64;
+    g.tiles = g.mtiles * g.ntiles * 9;
+    return g;
+}
+
+RGeo make_rgeo(int N, int H, int W, int Cin, int Cout, const WgradPlan &plan) {
+    RGeo g = rows_segments(N, H, W, Cin, Cout);
+    if (g.xpieces > 25) throw std::invalid_argument("conv_wgrad rows: input image exceeds the stage");
+    g.splits = plan.splits;
+    g.kps = plan.kps;
+    return g;
+}
 
 uint64_t magic40(int d) { return (uint64_t(1) << 40) / static_cast<uint64_t>(d) + 1; }
 
 WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const WgradPlan &plan) {
+    // (tap-tiled variants 0-5 only)
     WGeo g;
     const int pad = (ks - 1) / 2;
     g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
@@ -389,6 +626,13 @@ void launch_ks(const uint16_t *dy, const uint16_t *x, void *dw, float *part, con
 
 int conv_wgrad_variants() { return kNumVariants; }
 
+int64_t conv_wgrad_max_pixels(int N, int H, int W, int Cin, int Cout, int ks, int stride) {
+    // the tap-tiled kernel's 40-bit magic division holds < 2^23 output pixels; the row-image
+    // kernel only needs 32-bit element offsets (checked by the caller)
+    const WgradPlan pl = conv_wgrad_plan(N, H, W, Cin, Cout, ks, stride, -1, -1);
+    return pl.variant == kRowsVariant ? (int64_t(1) << 31) : (int64_t(1) << 23);
+}
+
 bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride) {
     return (ks == 1 || ks == 3) && (stride == 1 || stride == 2) && Cin % 64 == 0 && Cout % 64 == 0 && Cin >= 64 &&
            Cout >= 64;
@@ -397,6 +641,19 @@ bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride) {
 WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
     WgradPlan pl;
     const int64_t work = static_cast<int64_t>(Cin) * Cout * ks * ks;
+    if (variant < 0 && rows_default(Cin, Cout, ks, stride)) variant = kRowsVariant;
+    if (variant == kRowsVariant) {
+        if (!rows_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: rows variant needs 3x3/s1");
+        pl.variant = variant;
+        const RGeo rg = rows_segments(N, H, W, Cin, Cout);
+        const int ct = rg.mtiles * rg.ntiles;
+        if (splits < 0) splits = std::max(1, (512 + ct / 2) / ct);  // 2 workgroups of 9 waves per CU
+        splits = std::max(1, std::min(splits, std::max(1, rg.nseg / 4)));
+        pl.kps = (rg.nseg + splits - 1) / splits;
+        pl.splits = (rg.nseg + pl.kps - 1) / pl.kps;
+        pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * ct * 9 * 4096 : 0;
+        return pl;
+    }
     if (variant < 0) {
         // tools/bench_wgrad.py --sweep (profiles/README.md): 8-wave 256x128 tiles once the
         // GEMM is big enough, else the largest 4/2/1-wave tile the channel counts allow
@@ -441,6 +698,23 @@ void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *p
     // split-K accumulating into an f32 destination: every split adds its tile with atomics
     const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
     if (!conv_wgrad_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: unsupported shape");
+    if (plan.variant == kRowsVariant) {
+        if (!rows_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: rows variant needs 3x3/s1");
+        const RGeo rg = make_rgeo(N, H, W, Cin, Cout, plan);
+        wgrad_rows_kernel<2><<<rg.mtiles * rg.ntiles * rg.splits, 576, 0, s>>>(
+            dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), rg, out_f32, accumulate, atomic_out);
+        if (rg.splits > 1 && !atomic_out) {
+            WGeo g{};
+            g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = 9, g.tiles = rg.tiles;
+            g.splits = rg.splits;
+            const int64_t tot = static_cast<int64_t>(g.tiles) * 1024;
+            int sgl = 0;
+            while (sgl < 6 && (2 << sgl) <= g.splits && (tot << (sgl + 1)) <= int64_t(256) * 2048) ++sgl;
+            const int64_t grid = (tot + (256 >> sgl) - 1) / (256 >> sgl);
+            wgrad_reduce_kernel<1, 1><<<static_cast<int>(grid), 256, 0, s>>>(part, dw, g, out_f32, accumulate, sgl);
+        }
+        return;
+    }
     const WGeo g = make_geo(N, H, W, Cin, Cout, ks, stride, plan);
     if (static_cast<int64_t>(g.P) * g.HW >= (int64_t(1) << 40) || g.P >= (1 << 23))
         throw std::invalid_argument("conv_wgrad: too many pixels for the 40-bit division");

@@ -133,6 +133,8 @@ struct WgradPlan {
     int64_t ws_floats = 0;
 };
 bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride);
+// output pixels (N*OH*OW) one launch of the default plan handles
+int64_t conv_wgrad_max_pixels(int N, int H, int W, int Cin, int Cout, int ks, int stride);
 WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant = -1,
                           int splits = -1);
 void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W, int Cin,

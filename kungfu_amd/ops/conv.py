@@ -26,7 +26,7 @@ from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_CONV3X3", "1") != "0"
 _WGRAD = os.environ.get("KUNGFU_WGRAD", "1") != "0"
-_WGRAD_MAX_PIXELS = 1 << 23  # output pixels per conv_wgrad launch (csrc/kernels/conv_wgrad.hip)
+_WGRAD_MAX_PIXELS = 1 << 31  # test hook; the kernels' own cap: hip().conv_wgrad_max_pixels
 
 
 def set_wgrad_enabled(on: bool) -> bool:
@@ -51,11 +51,13 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: 
             and hip().conv_wgrad_supported(int(x.shape[1]), int(dy.shape[1]), ks, int(stride))):
         n = int(x.shape[0])
         per_img = int(dy.shape[2]) * int(dy.shape[3])
-        if n * per_img < _WGRAD_MAX_PIXELS:
+        cap = min(_WGRAD_MAX_PIXELS, hip().conv_wgrad_max_pixels(n, int(x.shape[2]), int(x.shape[3]), int(x.shape[1]),
+                                                                 int(dy.shape[1]), ks, int(stride)))
+        if n * per_img < cap:
             return hip().conv_wgrad(dy, x, ks, int(stride))
-        # the kernel's pixel index math holds < 2^23 output pixels per launch: sum over batch
-        # chunks into one f32 gradient (e.g. VGG-16's 224x224 layers at 256 images per GPU)
-        step = max(1, (_WGRAD_MAX_PIXELS - 1) // per_img)
+        # the tap-tiled kernel's pixel index math holds < 2^23 output pixels per launch: sum over
+        # batch chunks into one f32 gradient (the row-image 3x3 kernel has no such cap)
+        step = max(1, (cap - 1) // per_img)
         acc = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(
             memory_format=torch.channels_last)
         for i in range(0, n, step):

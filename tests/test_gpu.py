@@ -302,7 +302,8 @@ def test_conv3x3_mfma_matches_torch(shape):
 @needs_gpu
 @pytest.mark.parametrize("shape", [(3, 64, 9, 11, 256, 1, 1), (2, 256, 14, 14, 64, 1, 1), (2, 128, 15, 13, 512, 1, 2),
                                    (2, 64, 10, 12, 64, 3, 1), (3, 128, 9, 9, 256, 3, 2), (1, 512, 7, 7, 512, 3, 1),
-                                   (2, 192, 6, 5, 128, 3, 1)])
+                                   (2, 192, 6, 5, 128, 3, 1), (1, 64, 4, 130, 128, 3, 1), (2, 128, 5, 64, 64, 3, 1),
+                                   (3, 64, 9, 28, 64, 3, 1)])
 def test_conv_wgrad_mfma_matches_torch(H, shape):
     """Split-K MFMA weight gradient (every tile variant, several split counts, bf16 and
     f32-accumulate outputs) vs the f32 torch weight gradient."""

@@ -33,6 +33,8 @@ def timeit(f, n=20):
 
 
 N = int(os.environ.get("BATCH", "256"))
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,5,6").split(",")]
+MODES = os.environ.get("MODES", "st,").split(",")
 for Hh, C, K, s in SHAPES:
     x = cl(torch.randn(N, C, Hh, Hh, device="cuda")).bfloat16()
     w = cl(torch.randn(K, C, 1, 1, device="cuda") * 0.05).bfloat16()
@@ -41,11 +43,20 @@ for Hh, C, K, s in SHAPES:
     nbytes = 2.0 * (N * Hh * Hh * C + M * K)
     flop = 2.0 * M * K * C
     res = []
-    for v in range(7):
-        for epi, tag in ((st, "st"), (None, "")):
+    OH = Hh // s
+    out = cl(torch.randn(N, K, OH, OH, device="cuda")).bfloat16()
+    bx = torch.empty_like(out)
+    mask = torch.zeros(out.numel() // 8, dtype=torch.uint8, device="cuda")
+    modes = {"st": (lambda v: H_.conv(x, w, s, st, None, v), 0),
+             "": (lambda v: H_.conv(x, w, s, None, None, v), 0),
+             # dgrad-style: accumulate into `out` + BN-backward sums over bx and the ReLU mask
+             "ab": (lambda v: H_.conv(x, w, s, st, out, v, bn_x=bx, bn_mask=mask), 4.0 * M * K)}
+    for v in VARIANTS:
+        for tag in MODES:
+            f, extra = modes[tag]
             try:
-                us = timeit(lambda: H_.conv(x, w, s, epi, None, v))
+                us = timeit(lambda: f(v))
             except Exception:  # noqa: BLE001
                 continue
-            res.append("v%d%s:%.0fus/%.1fTB/s" % (v, tag, us, nbytes / us / 1e6))
+            res.append("v%d%s:%.0fus/%.1fTB/s" % (v, tag, us, (nbytes + extra) / us / 1e6))
     print("H=%2d %4d->%4d  %6.0fMB %5.1fGF  %s" % (Hh, C, K, nbytes / 1e6, flop / 1e9, " ".join(res)), flush=True)
