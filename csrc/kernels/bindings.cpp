@@ -287,7 +287,8 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 // [scale; shift]) gives the ReLU gate.
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
-                c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask) {
+                c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
+                c10::optional<at::Tensor> bias, bool gate) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -326,7 +327,24 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
     ea.stats = sp;
     int epi = accum ? kfk::kEpiAccum : 0;
     const bool bwd = bn_x && bn_x->defined();
-    if (bwd) {
+    if (bias && bias->defined()) {
+        // relu(conv + bias): VGG's conv + bias + ReLU as the conv epilogue
+        TORCH_CHECK(!accum && !sp && !bwd && !gate, "conv: bias epilogue excludes out/stats/bn_x/gate");
+        TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == K && bias->is_contiguous() &&
+                        bias->device() == x.device(),
+                    "conv: bias must be a contiguous bf16 [Cout] tensor on x's device");
+        ea.bias = reinterpret_cast<const uint16_t *>(bias->data_ptr());
+        epi = kfk::kEpiBiasRelu;
+    } else if (gate) {
+        // gradient of a ReLU output bn_x: y = conv * (bn_x > 0); stats[slot][0] += sum(y)
+        TORCH_CHECK(!accum && sp && bwd && !(bn_mask && bn_mask->defined()) && !(bn_fcoef && bn_fcoef->defined()),
+                    "conv: gate needs stats and bn_x (the ReLU output), no out/bn_mask/bn_fcoef");
+        TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->sizes() == y.sizes() &&
+                        bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) && bn_x->device() == x.device(),
+                    "conv: bn_x must be the ReLU output (bf16 channels_last, the output's shape)");
+        ea.bx = reinterpret_cast<const uint16_t *>(bn_x->data_ptr());
+        epi = kfk::kEpiGate;
+    } else if (bwd) {
         TORCH_CHECK(sp, "conv: BN-backward statistics need the stats workspace");
         TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->sizes() == y.sizes() &&
                         bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) && bn_x->device() == x.device(),
@@ -454,8 +472,15 @@ at::Tensor maxpool2x2_forward(at::Tensor x) {
     return y;
 }
 
-at::Tensor maxpool2x2_backward(at::Tensor x, at::Tensor dy) {
+at::Tensor maxpool2x2_backward(at::Tensor x, at::Tensor dy, c10::optional<at::Tensor> gate_stats) {
     check_pool_in(x, "maxpool2x2_backward: x");
+    double *gs = nullptr;
+    if (gate_stats && gate_stats->defined()) {
+        TORCH_CHECK(gate_stats->is_cuda() && gate_stats->scalar_type() == at::kDouble && gate_stats->is_contiguous() &&
+                        gate_stats->numel() == 2 * x.size(1) * kfk::kStatSlots && gate_stats->device() == x.device(),
+                    "maxpool2x2_backward: gate_stats must be a contiguous f64 [slots * 2 * C] tensor");
+        gs = gate_stats->data_ptr<double>();
+    }
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == x.size(0) &&
                     dy.size(1) == x.size(1) && dy.size(2) == x.size(2) / 2 && dy.size(3) == x.size(3) / 2 &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.device() == x.device(),
@@ -465,7 +490,7 @@ at::Tensor maxpool2x2_backward(at::Tensor x, at::Tensor dy) {
     kfk::launch_maxpool2x2_backward(reinterpret_cast<const uint16_t *>(x.data_ptr()),
                                     reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                                     reinterpret_cast<uint16_t *>(dx.data_ptr()), x.size(0), static_cast<int>(x.size(2)),
-                                    static_cast<int>(x.size(3)), static_cast<int>(x.size(1)), stream_of(x, 0));
+                                    static_cast<int>(x.size(3)), static_cast<int>(x.size(1)), stream_of(x, 0), gs);
     return dx;
 }
 
@@ -1091,14 +1116,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv", &conv, "1x1/3x3 NHWC bf16 convolution (MFMA implicit GEMM) with fused BN-statistics and "
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
-          py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none());
+          py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
+          py::arg("gate") = false);
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
     m.def("conv_wgrad_supported", &kfk::conv_wgrad_supported);
     m.def("bias_act_supported", &kfk::bias_act_supported);
     m.def("maxpool2x2_forward", &maxpool2x2_forward, "2x2/s2 max-pool, NHWC bf16 (no argmax tensor)");
-    m.def("maxpool2x2_backward", &maxpool2x2_backward, "2x2/s2 max-pool gradient (gather from x, dy)");
+    m.def("maxpool2x2_backward", &maxpool2x2_backward, "2x2/s2 max-pool gradient (gather from x, dy); gate_stats: "
+          "x is a ReLU output, also gate by x > 0 and sum the result per channel", py::arg("x"), py::arg("dy"),
+          py::arg("gate_stats") = py::none());
     m.def("maxpool3s2_forward", &maxpool3s2_forward, "3x3/s2 max-pool (pad 0/1), NHWC bf16 -> (y, argmax bytes)");
     m.def("maxpool3s2_backward", &maxpool3s2_backward, "3x3/s2 max-pool gradient (gather via the argmax bytes)");
     m.def("layernorm_supported", &kfk::layernorm_supported);

@@ -93,10 +93,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int LOADS = A_INST + B_INST;
     static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
     constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
+    constexpr bool GATE = (EPI & kEpiGate) != 0;
+    constexpr int NSUM = GATE ? 1 : 2;  // the gate needs sum(y) only
     constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     constexpr int GROUPS = NT / VPR;
-    constexpr int EPI_BYTES = BM * CROW + (STATS ? 2 * GROUPS * BN * 4 : 0);
+    constexpr int EPI_BYTES = BM * CROW + (STATS ? NSUM * GROUPS * BN * 4 : 0);
     constexpr int LDS_BYTES = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
@@ -254,6 +256,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 
     // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
     // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r.
+    float bcol[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        bcol[j] = 0.f;
+        if constexpr ((EPI & kEpiBiasRelu) != 0) bcol[j] = bf16_to_f32(ea.bias[n0 + wn * WTN + j * 16 + (lane & 15)]);
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -262,7 +270,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             for (int r = 0; r < 4; ++r) {
                 const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
                 const int col = wn * WTN + j * 16 + (lane & 15);
-                *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(acc[i][j][r]);
+                float v = acc[i][j][r];
+                if constexpr ((EPI & kEpiBiasRelu) != 0) {
+                    v += bcol[j];
+                    v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
+                }
+                *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(v);
             }
     __syncthreads();
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
@@ -290,11 +303,26 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 }
                 val = make_uint4(o[0], o[1], o[2], o[3]);
             }
+            if constexpr (GATE) {
+                // gradient of a ReLU output: keep y where bx > 0 (NaN passes), sum the kept values
+                const uint4 bv = *reinterpret_cast<const uint4 *>(ea.bx + e);
+                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bv);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&val);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
+                                          (!(__uint_as_float(bw[k] & 0xffff0000u) <= 0.f) ? 0xffff0000u : 0u);
+                    vw[k] &= keep;
+                }
+            }
             *dst = val;
             if constexpr (STATS) {
                 float f[8];
                 unpack_bf16x8(val, f);
-                if constexpr ((EPI & kEpiFwdStats) != 0) {
+                if constexpr (GATE) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s1[k] += f[k];
+                } else if constexpr ((EPI & kEpiFwdStats) != 0) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         s1[k] += f[k];
@@ -329,7 +357,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             red[grp * BN + cv * 8 + k] = s1[k];
-            red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
+            if constexpr (NSUM == 2) red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
         }
         __syncthreads();
         for (int col = tid; col < BN; col += NT) {
@@ -337,11 +365,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll 4
             for (int p = 0; p < GROUPS; ++p) {
                 t1 += red[p * BN + col];
-                t2 += red[(GROUPS + p) * BN + col];
+                if constexpr (NSUM == 2) t2 += red[(GROUPS + p) * BN + col];
             }
             double *sl = ea.stats + ((mt_last + wg) % kStatSlots) * 2 * g.K;  // spread atomics over slots
             atomicAdd(sl + n0 + col, t1);
-            atomicAdd(sl + g.K + n0 + col, t2);
+            if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
         }
     }
 }
@@ -414,7 +442,7 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     if (g.K % BN) throw std::invalid_argument("conv: Cout not a multiple of the tile");
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = g.K / BN;
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits)) != 0;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
     if constexpr (STATS) {
         // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
         // statistics flush per block instead of per tile
@@ -449,6 +477,8 @@ void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
         case kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiBwdBits>(x, w, y, g, ea, s); break;
         case kEpiAccum | kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdBits>(x, w, y, g, ea, s); break;
         case kEpiAccum | kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdCoef>(x, w, y, g, ea, s); break;
+        case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu>(x, w, y, g, ea, s); break;
+        case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate>(x, w, y, g, ea, s); break;
         default: throw std::invalid_argument("conv: unsupported epilogue combination");
         }
     }
@@ -462,7 +492,8 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     // (two blocks per CU keep more HBM traffic in flight); Cout = 64 -> 256x64 / 4 waves
     // 3x3 without a fused epilogue and Cout % 256 == 0 (VGG's compute-bound layers): 256x256 /
     // 8 waves of 64x128 (tools/bench_vgg_conv.py: 1.15-1.17 PF/s vs 1.06-1.12 for 256x128).
-    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : (epi == 0 && g.K % 256 == 0 ? 7 : 1)) : 2;
+    const bool big_ok = epi == 0 || epi == kEpiBiasRelu || epi == kEpiGate;  // epilogues of the 256x256 tile
+    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : (big_ok && g.K % 256 == 0 ? 7 : 1)) : 2;
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
             [[fallthrough]];
@@ -475,8 +506,11 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     case 6: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
             launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 128x64 3st
     // larger wave tiles (tuning candidates for the compute-bound 3x3 shapes)
-    case 7: if (epi || g.K % 256) throw std::invalid_argument("conv variant 7: epi 0, Cout % 256");    // 256x256, 8w, 64x128
-            launch_epi<KS, 4, 2, 2, 0, 4, 8>(x, w, y, g, ea, s); break;
+    case 7: if (!big_ok || g.K % 256) throw std::invalid_argument("conv variant 7: epi 0/bias-relu/gate, Cout % 256");
+            if (epi == kEpiBiasRelu) launch_epi<KS, 4, 2, 2, kEpiBiasRelu, 4, 8>(x, w, y, g, ea, s);  // 256x256, 8w, 64x128
+            else if (epi == kEpiGate) launch_epi<KS, 4, 2, 2, kEpiGate, 4, 8>(x, w, y, g, ea, s);
+            else launch_epi<KS, 4, 2, 2, 0, 4, 8>(x, w, y, g, ea, s);
+            break;
     case 8: if (epi || g.K % 256) throw std::invalid_argument("conv variant 8: epi 0, Cout % 256");    // 256x256, 8w, 128x64
             launch_epi<KS, 2, 4, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
     case 9: if (epi || g.K % 128) throw std::invalid_argument("conv variant 9: epi 0, Cout % 128");    // 256x128, 4w, 128x64

@@ -98,8 +98,12 @@ int conv3x3_variants();
 // keeping atomic contention per address low); bn_forward(sums=...) folds the slots.
 constexpr int kStatSlots = 16;
 bool conv_supported(int Cin, int Cout, int ks, int stride);
-enum ConvEpi : int { kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8 };
+// kEpiBiasRelu: y = relu(conv + bias) (bf16 bias, VGG's conv+bias+ReLU in the conv's epilogue);
+// kEpiGate: the output is the gradient of a ReLU output ea.bx: y = conv * (bx > 0) (NaN in bx
+// passes, like torch.relu's backward) and stats[slot][0][c] += sum(y) (that layer's bias gradient).
+enum ConvEpi : int { kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32 };
 struct EpiArgs {
+    const uint16_t *bias = nullptr;  // kEpiBiasRelu: bf16 [K]
     double *stats = nullptr;         // kStatSlots x [2][K] f64 (zeroed; consumed + re-zeroed by the BN)
     const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output
     const float *fcoef = nullptr;    // bwd coef: forward [scale(K); shift(K)]
@@ -234,7 +238,9 @@ void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float 
 void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
                                const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
                                int64_t rows, int D, hipStream_t st);
+// gate_stats != nullptr: x is a ReLU output, dx = that ReLU's input gradient (window max > 0 only)
+// and the per-channel sums of dx go to gate_stats[slot][0][C] (kStatSlots x 2 x C f64, zeroed)
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
-                                hipStream_t s);
+                                hipStream_t s, double *gate_stats = nullptr);
 
 }  // namespace kfk

@@ -69,9 +69,15 @@ __global__ __launch_bounds__(kBlock) void maxpool2_fwd_kernel(const uint4 *__res
     }
 }
 
+// GATE: x is a ReLU output and dx goes on as that ReLU's input gradient: the window maximum
+// passes dy only where it is > 0 (NaN passes, like torch.relu's backward), and the per-channel
+// sums of dx (the preceding conv's bias gradient) go to the f64 slots stats[slot][0][C].
+// The grid stride is a multiple of CV (kBlock % CV == 0), so a thread keeps one channel group.
+template <bool GATE>
 __global__ __launch_bounds__(kBlock) void maxpool2_bwd_kernel(const uint4 *__restrict__ x,
                                                               const uint4 *__restrict__ dy, uint4 *__restrict__ dx,
-                                                              PoolGeo g) {
+                                                              PoolGeo g, double *__restrict__ stats) {
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int64_t rowv = static_cast<int64_t>(g.W) * g.CV;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < g.nout;
          i += static_cast<int64_t>(gridDim.x) * kBlock) {
@@ -92,13 +98,32 @@ __global__ __launch_bounds__(kBlock) void maxpool2_bwd_kernel(const uint4 *__res
                 if (lo16(w) > ml || isnan(lo16(w))) ml = lo16(w), pl = p;
                 if (hi16(w) > mh || isnan(hi16(w))) mh = hi16(w), ph = p;
             }
-            const uint32_t gw = bits_of(gv, k);
+            uint32_t gw = bits_of(gv, k);
+            if constexpr (GATE) {
+                if (ml <= 0.f) gw &= 0xffff0000u;
+                if (mh <= 0.f) gw &= 0xffffu;
+                csum[2 * k] += lo16(gw);
+                csum[2 * k + 1] += hi16(gw);
+            }
 #pragma unroll
             for (int p = 0; p < 4; ++p)
                 o[p][k] = (p == pl ? (gw & 0xffffu) : 0u) | (p == ph ? (gw & 0xffff0000u) : 0u);
         }
 #pragma unroll
         for (int p = 0; p < 4; ++p) dx[off[p]] = make_uint4(o[p][0], o[p][1], o[p][2], o[p][3]);
+    }
+    if constexpr (GATE) {
+        __shared__ float red[kBlock][9];  // padded: the CV threads of a channel group are spread
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) red[t][k] = csum[k];
+        __syncthreads();
+        for (int c = t; c < g.CV * 8; c += kBlock) {
+            const int cvi = c >> 3, k = c & 7;  // fold channel 8 cvi + k
+            double a = 0;
+            for (int u = cvi; u < kBlock; u += g.CV) a += red[u][k];
+            atomicAdd(stats + (blockIdx.x % kStatSlots) * 2 * (g.CV * 8) + c, a);
+        }
     }
 }
 
@@ -271,12 +296,19 @@ void launch_maxpool2x2_forward(const uint16_t *x, uint16_t *y, int64_t N, int H,
 }
 
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
-                                hipStream_t s) {
+                                hipStream_t s, double *gate_stats) {
     const PoolGeo g = pool_geo(N, H, W, C);
     if (g.nout == 0) return;
-    maxpool2_bwd_kernel<<<pool_grid(g.nout), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x),
-                                                              reinterpret_cast<const uint4 *>(dy),
-                                                              reinterpret_cast<uint4 *>(dx), g);
+    if (gate_stats) {
+        if (kBlock % g.CV != 0) throw std::invalid_argument("maxpool2x2 gate: C/8 must divide 256");
+        maxpool2_bwd_kernel<true><<<pool_grid(g.nout), kBlock, 0, s>>>(
+            reinterpret_cast<const uint4 *>(x), reinterpret_cast<const uint4 *>(dy), reinterpret_cast<uint4 *>(dx), g,
+            gate_stats);
+        return;
+    }
+    maxpool2_bwd_kernel<false><<<pool_grid(g.nout), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x),
+                                                                     reinterpret_cast<const uint4 *>(dy),
+                                                                     reinterpret_cast<uint4 *>(dx), g, nullptr);
 }
 
 int maxpool3s2_out(int h, int pad) { return (h + 2 * pad - 3) / 2 + 1; }

@@ -31,7 +31,14 @@ class VGG(nn.Module):
                     layers.append(nn.BatchNorm2d(v))
                 layers.append(nn.ReLU(inplace=True))
                 c = v
-        self.features = nn.Sequential(*layers)
+        if fused and not batch_norm:
+            # the whole conv/bias/ReLU/pool stack as one autograd node (bias + ReLU inside the
+            # conv and pool kernels, ops/vgg_fused.py); same modules, same state_dict keys
+            from ..ops.vgg_fused import FusedVGGFeatures
+
+            self.features = FusedVGGFeatures(*layers)
+        else:
+            self.features = nn.Sequential(*layers)
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
         self.classifier = nn.Sequential(
             nn.Linear(512 * 7 * 7, 4096), nn.ReLU(True), nn.Dropout(),

@@ -983,3 +983,88 @@ def H_slots():
     from kungfu_amd._lib import hip
 
     return hip().conv_stat_slots
+
+
+@needs_gpu
+@pytest.mark.parametrize("N,Hh,C,K", [(3, 12, 64, 64), (2, 10, 64, 128), (2, 9, 128, 256), (1, 8, 256, 512)])
+def test_conv_bias_relu_and_gate_epilogues(H, N, Hh, C, K):
+    """conv epilogues of the fused VGG stack: relu(conv + bias) vs f32 torch; the ReLU-gated
+    data gradient (conv * (y_prev > 0)) bit-exact vs the plain kernel output masked, and its
+    per-channel sums (the bias gradient) vs f64 sums."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(31)
+    cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
+    x = cl(torch.randn(N, C, Hh, Hh, device="cuda")).bfloat16()
+    w = cl(torch.randn(K, C, 3, 3, device="cuda") * 0.05).bfloat16()
+    b = (torch.randn(K, device="cuda") * 0.5).bfloat16()
+    y = H.conv(x, w, 1, bias=b)
+    ref = F.relu(F.conv2d(x.float(), w.float(), padding=1) + b.float().view(1, -1, 1, 1))
+    assert _rel(y, ref) < 1e-2
+    assert (y.float() >= 0).all()
+    yprev = cl(F.relu(torch.randn(N, K, Hh, Hh, device="cuda"))).bfloat16()
+    st = torch.zeros(H.conv_stat_slots * 2 * K, dtype=torch.float64, device="cuda")
+    dz = H.conv(x, w, 1, st, None, -1, bn_x=yprev, gate=True)
+    plain = H.conv(x, w, 1)
+    exp = torch.where(yprev > 0, plain, torch.zeros_like(plain))
+    torch.testing.assert_close(dz.float(), exp.float(), rtol=0, atol=0)
+    sums = st.view(-1, 2, K)[:, 0].sum(0)
+    torch.testing.assert_close(sums, exp.double().sum((0, 2, 3)), rtol=1e-6, atol=1e-3)
+
+
+@needs_gpu
+@pytest.mark.parametrize("C", [64, 128, 512])
+def test_maxpool2x2_gate_backward(H, C):
+    """2x2 max-pool backward with the ReLU gate of its input and the per-channel gradient sums
+    (VGG's conv -> ReLU -> pool): bit-exact vs the plain gather masked by x > 0."""
+    torch.manual_seed(32)
+    cl = lambda t: t.contiguous(memory_format=torch.channels_last)  # noqa: E731
+    x = cl(torch.relu(torch.randn(3, C, 10, 12, device="cuda"))).bfloat16()
+    x[:, :, :4] = 0  # whole windows of zeros: the ReLU gate closes
+    dy = cl(torch.randn(3, C, 5, 6, device="cuda")).bfloat16()
+    st = torch.zeros(H.conv_stat_slots * 2 * C, dtype=torch.float64, device="cuda")
+    dx = H.maxpool2x2_backward(x, dy, gate_stats=st)
+    plain = H.maxpool2x2_backward(x, dy)
+    exp = torch.where(x > 0, plain, torch.zeros_like(plain))
+    torch.testing.assert_close(dx.float(), exp.float(), rtol=0, atol=0)
+    torch.testing.assert_close(st.view(-1, 2, C)[:, 0].sum(0), exp.double().sum((0, 2, 3)), rtol=1e-6, atol=1e-3)
+
+
+@needs_gpu
+def test_vgg16_fused_stack_matches_layered():
+    """VGG-16 with its feature stack as one fused autograd node (bias/ReLU in the conv and pool
+    kernels) vs the same modules run layer by layer (Conv2dReLU + MaxPool2x2), both under bf16
+    autocast, each measured against an f32 run of the same weights: at random init the early
+    layers' gradients are tiny and carry ~5-45 % bf16 noise on EITHER path (the layered path
+    differs that much from itself between runs), so the fused path must be as close to f32 as
+    the layered one, not bit-equal to it."""
+    from kungfu_amd.models.vgg import vgg16
+    from kungfu_amd.ops.vgg_fused import FusedVGGFeatures
+
+    torch.manual_seed(33)
+    m = vgg16(fused_bn=True).cuda().to(memory_format=torch.channels_last).eval()  # no dropout masks
+    x = torch.randn(4, 3, 64, 64, device="cuda").to(memory_format=torch.channels_last)
+    tgt = torch.randint(0, 1000, (4,), device="cuda")
+
+    def run(fused, amp=True):
+        m.zero_grad(set_to_none=True)
+        orig = FusedVGGFeatures.forward
+        if not fused:
+            FusedVGGFeatures.forward = torch.nn.Sequential.forward
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                out = m(x)
+                loss = torch.nn.functional.cross_entropy(out.float(), tgt)
+            loss.backward()
+        finally:
+            FusedVGGFeatures.forward = orig
+        return out.float().detach(), {k: p.grad.detach().float().clone() for k, p in m.named_parameters()}
+
+    o1, g1 = run(True)
+    o0, g0 = run(False)
+    of, gf = run(False, amp=False)
+    rel = lambda a, b: ((a - b).norm() / (b.norm() + 1e-12)).item()  # noqa: E731
+    assert rel(o1, of) < 1.5 * rel(o0, of) + 1e-3
+    for k in gf:
+        e1, e0 = rel(g1[k], gf[k]), rel(g0[k], gf[k])
+        assert e1 < 1.5 * e0 + 0.02, (k, e1, e0)
