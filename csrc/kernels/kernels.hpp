@@ -119,6 +119,7 @@ struct FlipTable {
     uint16_t *dst[kMax];
     int cout[kMax], cin[kMax], taps[kMax];
     int64_t start[kMax + 1];
+    int tstart[kMax + 1];  // 64x64 transpose tiles (filled by launch_conv_flip_multi)
 };
 void launch_conv_flip_multi(const FlipTable &tab, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,KS-1-kh,KS-1-kw,ci]: stride-1 data gradient = conv(dy, wt).

@@ -300,7 +300,10 @@ class GradReducer:
 
     def _reduce(self, comm, g):
         if not self.graph:
-            comm.all_reduce(g, op=self.op)
+            # one rank: the average IS the sum, and RCCL's in-place one-rank sum is free while
+            # its one-rank average is a scaled copy of the bucket (oneRankReduce<PreMulSum>:
+            # 1.4 ms/step of HBM traffic for VGG-16's 528 MB of gradients)
+            comm.all_reduce(g, op=self.op if comm.size > 1 or self.op != "avg" else "sum")
             return
         comm.graph_all_reduce(g, op="sum", monitored=True)
         if self.op == "avg":

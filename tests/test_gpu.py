@@ -1068,3 +1068,18 @@ def test_vgg16_fused_stack_matches_layered():
     for k in gf:
         e1, e0 = rel(g1[k], gf[k]), rel(g0[k], gf[k])
         assert e1 < 1.5 * e0 + 0.02, (k, e1, e0)
+
+
+@needs_gpu
+def test_conv_flip_weights_multi_matches_single(H):
+    """Multi-tensor weight flip (tiled transpose, one launch for many layers, incl. channel
+    counts that are not multiples of the 64x64 tile) == w.flip(2, 3).transpose(0, 1)."""
+    torch.manual_seed(34)
+    shapes = [(64, 64, 3), (256, 64, 1), (64, 256, 1), (512, 128, 3), (96, 40, 3), (8, 200, 1)]
+    srcs = [torch.randn(co, ci, k, k, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+            for co, ci, k in shapes]
+    dsts = [torch.empty(ci, co, k, k, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+            for co, ci, k in shapes]
+    H.conv_flip_weights(srcs, dsts)
+    for w, d in zip(srcs, dsts):
+        torch.testing.assert_close(d, w.flip(2, 3).transpose(0, 1), rtol=0, atol=0)
