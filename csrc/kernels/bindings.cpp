@@ -288,7 +288,7 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
                 c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
-                c10::optional<at::Tensor> bias, bool gate) {
+                c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -367,6 +367,14 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
         epi |= kfk::kEpiFwdStats;
     }
     TORCH_CHECK(!(epi & kfk::kEpiFwdStats) || !(epi & kfk::kEpiAccum), "conv: stats + accumulate unsupported");
+    if (acc_mask && acc_mask->defined()) {
+        // out = out * acc_mask + conv (out: a raw ReLU-output gradient, acc_mask: that ReLU's bits)
+        TORCH_CHECK(accum && acc_mask->scalar_type() == at::kByte && acc_mask->numel() == y.numel() / 8 &&
+                        acc_mask->device() == x.device() && !(epi & kfk::kEpiBwdCoef),
+                    "conv: acc_mask needs out and one byte per 8 output elements");
+        ea.amask = acc_mask->data_ptr<uint8_t>();
+        epi |= kfk::kEpiAccMask;
+    }
     kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
                      reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), ea, epi,
                      stream_of(x, 0), static_cast<int>(variant));
@@ -1117,7 +1125,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
-          py::arg("gate") = false);
+          py::arg("gate") = false, py::arg("acc_mask") = py::none());
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);

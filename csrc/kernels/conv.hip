@@ -289,7 +289,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             uint4 *dst = reinterpret_cast<uint4 *>(y + e);
             uint4 val = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
             if constexpr ((EPI & kEpiAccum) != 0) {
-                const uint4 old = *dst;
+                uint4 old = *dst;
+                if constexpr ((EPI & kEpiAccMask) != 0) {
+                    const uint32_t mb = ea.amask[e >> 3];  // 8 channels from an 8-aligned e
+                    uint32_t *ow = reinterpret_cast<uint32_t *>(&old);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        ow[k] &= (((mb >> (2 * k)) & 1u) ? 0xffffu : 0u) | (((mb >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
+                }
                 const uint32_t *a = reinterpret_cast<const uint32_t *>(&val);
                 const uint32_t *b = reinterpret_cast<const uint32_t *>(&old);
                 uint32_t o[4];
@@ -503,6 +510,10 @@ void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
         case kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiBwdBits>(x, w, y, g, ea, s); break;
         case kEpiAccum | kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdBits>(x, w, y, g, ea, s); break;
         case kEpiAccum | kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdCoef>(x, w, y, g, ea, s); break;
+        case kEpiAccum | kEpiAccMask: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiAccMask>(x, w, y, g, ea, s); break;
+        case kEpiAccum | kEpiAccMask | kEpiBwdBits:
+            launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiAccMask | kEpiBwdBits>(x, w, y, g, ea, s);
+            break;
         case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu>(x, w, y, g, ea, s); break;
         case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate>(x, w, y, g, ea, s); break;
         default: throw std::invalid_argument("conv: unsupported epilogue combination");

@@ -101,8 +101,15 @@ bool conv_supported(int Cin, int Cout, int ks, int stride);
 // kEpiBiasRelu: y = relu(conv + bias) (bf16 bias, VGG's conv+bias+ReLU in the conv's epilogue);
 // kEpiGate: the output is the gradient of a ReLU output ea.bx: y = conv * (bx > 0) (NaN in bx
 // passes, like torch.relu's backward) and stats[slot][0][c] += sum(y) (that layer's bias gradient).
-enum ConvEpi : int { kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32 };
+// kEpiAccMask (with kEpiAccum): y = old * amask + conv -- the residual gradient dz = dout * relu'
+// formed from the raw output gradient and the 1-bit ReLU mask on the fly, so the BN3+add+ReLU
+// backward need not write dz (ResNet identity blocks).
+enum ConvEpi : int {
+    kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
+    kEpiAccMask = 64
+};
 struct EpiArgs {
+    const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
     const uint16_t *bias = nullptr;  // kEpiBiasRelu: bf16 [K]
     double *stats = nullptr;         // kStatSlots x [2][K] f64 (zeroed; consumed + re-zeroed by the BN)
     const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output

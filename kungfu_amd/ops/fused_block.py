@@ -106,20 +106,22 @@ def _flip_cache(space) -> _FlipCache:
 
 
 def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: Optional[torch.Tensor] = None,
-           bn=None):
+           bn=None, out_mask: Optional[torch.Tensor] = None):
     """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given).
 
     ``bn = (ws, bn_x, fcoef, mask)``: the result is the gradient of a BN(+ReLU) output whose
     input is ``bn_x``; the kernel epilogue also accumulates that BN's backward sums into
-    ``ws`` (only on the MFMA path -- returns whether it did via ``_dgrad.fused``)."""
+    ``ws`` (only on the MFMA path -- returns whether it did via ``_dgrad.fused``).
+    ``out_mask`` (stride 1, with ``out``): accumulate into ``out * out_mask`` (1-bit ReLU mask)."""
     H = hip()
     if stride == 1:
         wt = flipped if flipped is not None else H.conv_flip_weight(w)
         if bn is not None:
             ws, bx, fc, mk = bn
             _dgrad.fused = True
-            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk)
-        return H.conv(dy, wt, 1, None, out)
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask)
+        return H.conv(dy, wt, 1, None, out, acc_mask=out_mask)
+    assert out_mask is None
     _dgrad.fused = False
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
@@ -217,7 +219,11 @@ class _BottleneckFn(torch.autograd.Function):
         if tail.ready and not use3:
             tail.ws.zero_()  # sums of a gradient that is not the one we got: discard
         tail.ready, tail.y3, tail.mask = False, None, None
-        dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, True,
+        # identity block whose output gradient is our own buffer (the next block's conv1 data
+        # gradient): the residual gradient dout * relu' is never written -- conv1's data
+        # gradient below accumulates into dout in place, masking it on the fly
+        in_place = use3 and not spec.ds
+        dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, not in_place,
                                             ws[2] if use3 else None)
         dbn[2] = (dg3, db3)
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None))
@@ -235,16 +241,20 @@ class _BottleneckFn(torch.autograd.Function):
             dbn[3] = (dgd, dbd)
             dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
             dw[3] = _wgrad(dyd, x, w[3], s, 0)
+        elif in_place:
+            dx = dout  # raw output gradient; masked by mask3 inside conv1's data-gradient epilogue
         else:
             dx = didt  # the identity gradient: conv1's data gradient is accumulated into it
+        om = mask3 if in_place else None
         prev = ctx.prev
         if prev is not None and prev.y3 is not None and prev.y3.shape == dx.shape:
             # conv1's data gradient completes the gradient of the previous block's output:
             # its epilogue also accumulates that block's BN3 backward sums
-            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask))
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask),
+                        out_mask=om)
             prev.ready, prev.dx_ptr = True, dx.data_ptr()
         else:
-            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0])
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], out_mask=om)
         dw[0] = _wgrad(dy1, x, w[0], 1, 0)
         grads: List[Optional[torch.Tensor]] = []
         for i in range(nb):
