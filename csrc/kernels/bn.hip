@@ -288,24 +288,40 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
         sh[k] = coef[C + cv * 8 + k];
     }
     const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();  // multiple of CVEC
-    for (int64_t i = tid; i < nvec; i += stride) {
-        float f[8];
-        unpack8(x[i], f);
-        float rr[8];
-        if (RES) unpack8(res[i], rr);
-        uint32_t m = 0;
+    // two vectors per trip, both loads issued before either is used (bytes in flight per lane)
+    constexpr int U = 2;
+    for (int64_t i0 = tid; i0 < nvec; i0 += U * stride) {
+        uint4 xr[U], rr4[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            float v = f[k] * sc[k] + sh[k];
-            if (RES) v += rr[k];
-            if (RELU) {
-                m |= (v > 0.f ? 1u : 0u) << k;
-                v = v > 0.f ? v : 0.f;
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < nvec) {
+                xr[u] = x[i];
+                if (RES) rr4[u] = res[i];
             }
-            f[k] = v;
         }
-        y[i] = pack8(f);
-        if (RES && RELU) mask[i] = static_cast<uint8_t>(m);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= nvec) break;
+            float f[8];
+            unpack8(xr[u], f);
+            float rr[8];
+            if (RES) unpack8(rr4[u], rr);
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                float v = f[k] * sc[k] + sh[k];
+                if (RES) v += rr[k];
+                if (RELU) {
+                    m |= (v > 0.f ? 1u : 0u) << k;
+                    v = v > 0.f ? v : 0.f;
+                }
+                f[k] = v;
+            }
+            y[i] = pack8(f);
+            if (RES && RELU) mask[i] = static_cast<uint8_t>(m);
+        }
     }
 }
 
@@ -614,16 +630,33 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
     }
     load_fwd_coef<CVEC, RM>(fcoef, cv, sc, sh);
     const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();
-    for (int64_t i = tid; i < nvec; i += stride) {
-        float g[8], xv[8];
-        grad.get(grad.template fetch<CVEC>(i, i / CVEC, cv), g);
-        unpack8(x[i], xv);
-        relu_gate<RM>(g, xv, sc, sh, mask, i);
-        if (DRES) dres[i] = pack8(g);
-        float o[8];
+    // two vectors per trip, every load issued before any is used (bytes in flight per lane)
+    constexpr int U = 2;
+    for (int64_t i0 = tid; i0 < nvec; i0 += U * stride) {
+        typename G::Raw gr[U];
+        uint4 xr[U];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] = k1[k] * g[k] + k2[k] * xv[k] + k3[k];
-        dx[i] = pack8(o);
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i < nvec) {
+                gr[u] = grad.template fetch<CVEC>(i, i / CVEC, cv);
+                xr[u] = x[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * stride;
+            if (i >= nvec) break;
+            float g[8], xv[8];
+            grad.get(gr[u], g);
+            unpack8(xr[u], xv);
+            relu_gate<RM>(g, xv, sc, sh, mask, i);
+            if (DRES) dres[i] = pack8(g);
+            float o[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) o[k] = k1[k] * g[k] + k2[k] * xv[k] + k3[k];
+            dx[i] = pack8(o);
+        }
     }
 }
 

@@ -98,7 +98,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int NSUM = GATE ? 1 : 2;  // the gate needs sum(y) only
     constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     constexpr int GROUPS = NT / VPR;
-    constexpr int EPI_BYTES = BM * CROW + (STATS ? NSUM * GROUPS * BN * 4 : 0);
+    // the statistics reduction reuses the C tile's LDS once the last tile is stored
+    constexpr int RED_BYTES = STATS ? NSUM * GROUPS * BN * 4 : 0;
+    constexpr int EPI_BYTES = BM * CROW > RED_BYTES ? BM * CROW : RED_BYTES;
     constexpr int LDS_BYTES = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
@@ -358,7 +360,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     }  // m-tile loop
     if constexpr (STATS) {
         // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
-        float *red = reinterpret_cast<float *>(lds + BM * CROW);
+        float *red = reinterpret_cast<float *>(lds);
         __syncthreads();
         const int grp = tid / VPR;
 #pragma unroll
@@ -479,10 +481,15 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     if constexpr (STATS) {
         // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
         // statistics flush per block instead of per tile
-        static const int cap = [] {
+        // (KUNGFU_CONV_PERSIST_BLOCKS, default 4 per CU, fewer when the tile's LDS allows less)
+        static const int env_cap = [] {
             const char *v = std::getenv("KUNGFU_CONV_PERSIST_BLOCKS");
-            return v ? std::atoi(v) : 1024;
+            return v ? std::atoi(v) : 0;
         }();
+        constexpr int kRow = 128, STG = ST * (BM + BN) * kRow, CT = BM * (BN * 2 + 16);
+        constexpr int LDS = STG > CT ? STG : CT;
+        constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
+        const int cap = env_cap > 0 ? env_cap : 256 * (OCC < 1 ? 1 : OCC);
         const int per_n = cap / g.ntiles;
         if (cap > 0 && per_n >= 1 && g.mtiles > 2 * per_n) {
             conv_kernel<KS, WM, WN, ST, EPI, TM, TN, true><<<per_n * g.ntiles, 64 * WM * WN, 0, s>>>(
@@ -495,27 +502,26 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
 }
 
 // Tuning-only tile variants instantiate the plain epilogue; the defaults every fused one.
-template <int KS, int WM, int WN, int ST, bool ALL>
+template <int KS, int WM, int WN, int ST, bool ALL, int TM = 4, int TN = 4>
 void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
                     hipStream_t s) {
     if constexpr (!ALL) {
         if (epi != 0) throw std::invalid_argument("conv: fused epilogues need the default tile variant");
-        launch_epi<KS, WM, WN, ST, 0>(x, w, y, g, ea, s);
+        launch_epi<KS, WM, WN, ST, 0, TM, TN>(x, w, y, g, ea, s);
     } else {
+        constexpr int A = kEpiAccum, M = kEpiAccMask, B = kEpiBwdBits, C = kEpiBwdCoef;
         switch (epi) {
-        case 0: launch_epi<KS, WM, WN, ST, 0>(x, w, y, g, ea, s); break;
-        case kEpiFwdStats: launch_epi<KS, WM, WN, ST, kEpiFwdStats>(x, w, y, g, ea, s); break;
-        case kEpiAccum: launch_epi<KS, WM, WN, ST, kEpiAccum>(x, w, y, g, ea, s); break;
-        case kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiBwdCoef>(x, w, y, g, ea, s); break;
-        case kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiBwdBits>(x, w, y, g, ea, s); break;
-        case kEpiAccum | kEpiBwdBits: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdBits>(x, w, y, g, ea, s); break;
-        case kEpiAccum | kEpiBwdCoef: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiBwdCoef>(x, w, y, g, ea, s); break;
-        case kEpiAccum | kEpiAccMask: launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiAccMask>(x, w, y, g, ea, s); break;
-        case kEpiAccum | kEpiAccMask | kEpiBwdBits:
-            launch_epi<KS, WM, WN, ST, kEpiAccum | kEpiAccMask | kEpiBwdBits>(x, w, y, g, ea, s);
-            break;
-        case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu>(x, w, y, g, ea, s); break;
-        case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate>(x, w, y, g, ea, s); break;
+        case 0: launch_epi<KS, WM, WN, ST, 0, TM, TN>(x, w, y, g, ea, s); break;
+        case kEpiFwdStats: launch_epi<KS, WM, WN, ST, kEpiFwdStats, TM, TN>(x, w, y, g, ea, s); break;
+        case A: launch_epi<KS, WM, WN, ST, A, TM, TN>(x, w, y, g, ea, s); break;
+        case C: launch_epi<KS, WM, WN, ST, C, TM, TN>(x, w, y, g, ea, s); break;
+        case B: launch_epi<KS, WM, WN, ST, B, TM, TN>(x, w, y, g, ea, s); break;
+        case A | B: launch_epi<KS, WM, WN, ST, A | B, TM, TN>(x, w, y, g, ea, s); break;
+        case A | C: launch_epi<KS, WM, WN, ST, A | C, TM, TN>(x, w, y, g, ea, s); break;
+        case A | M: launch_epi<KS, WM, WN, ST, A | M, TM, TN>(x, w, y, g, ea, s); break;
+        case A | M | B: launch_epi<KS, WM, WN, ST, A | M | B, TM, TN>(x, w, y, g, ea, s); break;
+        case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu, TM, TN>(x, w, y, g, ea, s); break;
+        case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate, TM, TN>(x, w, y, g, ea, s); break;
         default: throw std::invalid_argument("conv: unsupported epilogue combination");
         }
     }
@@ -524,13 +530,15 @@ void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
 template <int KS>
 void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi, hipStream_t s,
                int variant) {
-    // default per shape class (tools/bench_conv3x3.py, tools/bench_conv.py): 3x3 -> 256x128 /
-    // 8 waves / 3 stages when Cout allows; 1x1 (1-16 K-steps) -> 128x128 / 4 waves / 2 stages
-    // (two blocks per CU keep more HBM traffic in flight); Cout = 64 -> 256x64 / 4 waves
-    // 3x3 without a fused epilogue and Cout % 256 == 0 (VGG's compute-bound layers): 256x256 /
-    // 8 waves of 64x128 (tools/bench_vgg_conv.py: 1.15-1.17 PF/s vs 1.06-1.12 for 256x128).
-    const bool big_ok = epi == 0 || epi == kEpiBiasRelu || epi == kEpiGate;  // epilogues of the 256x256 tile
-    if (variant < 0) variant = g.K % 128 == 0 ? (KS == 1 ? 0 : (big_ok && g.K % 256 == 0 ? 7 : 1)) : 2;
+    // default per shape (re-measured with the fused epilogues, tools/bench_conv1x1_variants.py
+    // [KS3=1]; VGG's compute-bound 3x3 layers: tools/bench_vgg_conv.py, 1.15-1.17 PF/s): 256x256 /
+    // 8 waves whenever Cout % 256 == 0 and there are >= 128 such tiles (64->256 at 56x56 161 ->
+    // 123 us, 3x3 256->256 at 14x14 70 -> 57 us; fewer tiles under-fill the chip: 3x3 512->512 at
+    // 7x7 62 -> 100 us), else 256x128 / 8 waves (1x1 included: 4-13 % over 128x128), else 256x64
+    if (variant < 0) {
+        const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);
+        variant = g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
+    }
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
             [[fallthrough]];
@@ -543,13 +551,10 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     case 6: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
             launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 128x64 3st
     // larger wave tiles (tuning candidates for the compute-bound 3x3 shapes)
-    case 7: if (!big_ok || g.K % 256) throw std::invalid_argument("conv variant 7: epi 0/bias-relu/gate, Cout % 256");
-            if (epi == kEpiBiasRelu) launch_epi<KS, 4, 2, 2, kEpiBiasRelu, 4, 8>(x, w, y, g, ea, s);  // 256x256, 8w, 64x128
-            else if (epi == kEpiGate) launch_epi<KS, 4, 2, 2, kEpiGate, 4, 8>(x, w, y, g, ea, s);
-            else launch_epi<KS, 4, 2, 2, 0, 4, 8>(x, w, y, g, ea, s);
-            break;
-    case 8: if (epi || g.K % 256) throw std::invalid_argument("conv variant 8: epi 0, Cout % 256");    // 256x256, 8w, 128x64
-            launch_epi<KS, 2, 4, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
+    case 7: if (g.K % 256) throw std::invalid_argument("conv variant 7: Cout % 256");
+            launch_variant<KS, 4, 2, 2, true, 4, 8>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 64x128
+    case 8: if (g.K % 256) throw std::invalid_argument("conv variant 8: Cout % 256");
+            launch_variant<KS, 2, 4, 2, true, 8, 4>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 128x64
     case 9: if (epi || g.K % 128) throw std::invalid_argument("conv variant 9: epi 0, Cout % 128");    // 256x128, 4w, 128x64
             launch_epi<KS, 2, 2, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
     default: if (epi || g.K % 128) throw std::invalid_argument("conv variant 10: epi 0, Cout % 128");  // 128x128, 2w, 64x128 3st

@@ -10,9 +10,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from kungfu_amd._lib import hip  # noqa: E402
 
 H_ = hip()
-# (H, Cin, Cout, stride)
+# (H, Cin, Cout, stride[, ks]); KS3=1 adds ResNet-50's stride-1 3x3 shapes
 SHAPES = [(56, 64, 64, 1), (56, 64, 256, 1), (56, 256, 64, 1), (56, 256, 128, 1), (28, 128, 512, 1),
           (28, 512, 128, 1), (14, 256, 1024, 1), (14, 1024, 256, 1), (7, 512, 2048, 1), (7, 2048, 512, 1)]
+if os.environ.get("KS3") == "1":
+    SHAPES = [(56, 64, 64, 1, 3), (28, 128, 128, 1, 3), (14, 256, 256, 1, 3), (7, 512, 512, 1, 3)]
 
 
 def cl(t):
@@ -35,13 +37,15 @@ def timeit(f, n=20):
 N = int(os.environ.get("BATCH", "256"))
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,5,6").split(",")]
 MODES = os.environ.get("MODES", "st,").split(",")
-for Hh, C, K, s in SHAPES:
+for shp in SHAPES:
+    Hh, C, K, s = shp[:4]
+    ks = shp[4] if len(shp) > 4 else 1
     x = cl(torch.randn(N, C, Hh, Hh, device="cuda")).bfloat16()
-    w = cl(torch.randn(K, C, 1, 1, device="cuda") * 0.05).bfloat16()
+    w = cl(torch.randn(K, C, ks, ks, device="cuda") * 0.05).bfloat16()
     st = torch.zeros(H_.conv_stat_slots * 2 * K, dtype=torch.float64, device="cuda")
     M = N * (Hh // s) * (Hh // s)
     nbytes = 2.0 * (N * Hh * Hh * C + M * K)
-    flop = 2.0 * M * K * C
+    flop = 2.0 * M * K * C * ks * ks
     res = []
     OH = Hh // s
     out = cl(torch.randn(N, K, OH, OH, device="cuda")).bfloat16()
@@ -58,5 +62,5 @@ for Hh, C, K, s in SHAPES:
                 us = timeit(lambda: f(v))
             except Exception:  # noqa: BLE001
                 continue
-            res.append("v%d%s:%.0fus/%.1fTB/s" % (v, tag, us, (nbytes + extra) / us / 1e6))
-    print("H=%2d %4d->%4d  %6.0fMB %5.1fGF  %s" % (Hh, C, K, nbytes / 1e6, flop / 1e9, " ".join(res)), flush=True)
+            res.append("v%d%s:%.0fus/%.1fTB/s/%.0fTF" % (v, tag, us, (nbytes + extra) / us / 1e6, flop / us / 1e6))
+    print("H=%2d %4d->%4d k%d  %6.0fMB %5.1fGF  %s" % (Hh, C, K, ks, nbytes / 1e6, flop / 1e9, " ".join(res)), flush=True)
