@@ -427,6 +427,45 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c
     return dw;
 }
 
+// Fused self-attention: qkv [B, S, 3*H*64] bf16 contiguous -> (out [B, S, H*64] bf16, lse [B, H, S] f32)
+std::vector<at::Tensor> attention_forward(at::Tensor qkv, int64_t heads, double scale, int64_t seed, double p_drop) {
+    TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
+                    qkv.size(2) == 3 * heads * 64 && kfk::attention_supported(qkv.size(1), 64),
+                "attention_forward: qkv must be a contiguous bf16 [B, S, 3*H*64] GPU tensor with S in {64, 128}");
+    c10::DeviceGuard gd(qkv.device());
+    const int B = qkv.size(0), S = qkv.size(1), H = static_cast<int>(heads);
+    auto out = at::empty({B, S, H * 64}, qkv.options());
+    auto lse = at::empty({B, H, S}, qkv.options().dtype(at::kFloat));
+    kfk::launch_attention_forward(reinterpret_cast<const uint16_t *>(qkv.data_ptr()),
+                                  reinterpret_cast<uint16_t *>(out.data_ptr()), lse.data_ptr<float>(), B, S, H,
+                                  static_cast<float>(scale), static_cast<uint32_t>(seed), static_cast<float>(p_drop),
+                                  stream_of(qkv, 0));
+    return {out, lse};
+}
+
+at::Tensor attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at::Tensor dout, int64_t heads,
+                              double scale, int64_t seed, double p_drop) {
+    TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
+                    qkv.size(2) == 3 * heads * 64 && kfk::attention_supported(qkv.size(1), 64),
+                "attention_backward: qkv must be a contiguous bf16 [B, S, 3*H*64] GPU tensor with S in {64, 128}");
+    const int B = qkv.size(0), S = qkv.size(1), H = static_cast<int>(heads);
+    TORCH_CHECK(out.sizes() == at::IntArrayRef({B, S, H * 64}) && out.is_contiguous() &&
+                    out.scalar_type() == at::kBFloat16,
+                "attention_backward: out must be the forward's [B, S, H*64] output");
+    if (!dout.is_contiguous()) dout = dout.contiguous();
+    TORCH_CHECK(dout.sizes() == out.sizes() && dout.scalar_type() == at::kBFloat16, "attention_backward: dout");
+    TORCH_CHECK(lse.sizes() == at::IntArrayRef({B, H, S}) && lse.scalar_type() == at::kFloat && lse.is_contiguous(),
+                "attention_backward: lse must be the forward's [B, H, S] f32");
+    c10::DeviceGuard gd(qkv.device());
+    auto dqkv = at::empty_like(qkv);
+    kfk::launch_attention_backward(reinterpret_cast<const uint16_t *>(qkv.data_ptr()),
+                                   reinterpret_cast<const uint16_t *>(out.data_ptr()), lse.data_ptr<float>(),
+                                   reinterpret_cast<const uint16_t *>(dout.data_ptr()),
+                                   reinterpret_cast<uint16_t *>(dqkv.data_ptr()), B, S, H, static_cast<float>(scale),
+                                   static_cast<uint32_t>(seed), static_cast<float>(p_drop), stream_of(qkv, 0));
+    return dqkv;
+}
+
 static void check_bias_act(const at::Tensor &y, const char *name) {
     TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kBFloat16 && y.dim() == 4 &&
                     y.is_contiguous(at::MemoryFormat::ChannelsLast) && kfk::bias_act_supported(y.size(1)),
@@ -1147,6 +1186,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("bias_act_backward", &bias_act_backward, "(dy * (y > 0), its per-channel sum) in one pass",
           py::arg("dy"), py::arg("y"), py::arg("relu") = true);
     m.def("conv_wgrad_variants", &kfk::conv_wgrad_variants);
+    m.def("attention_supported", &kfk::attention_supported);
+    m.def("attention_forward", &attention_forward, "fused self-attention forward (S 64/128, head dim 64, dropout)",
+          py::arg("qkv"), py::arg("heads"), py::arg("scale"), py::arg("seed"), py::arg("p_drop"));
+    m.def("attention_backward", &attention_backward, "fused self-attention backward -> dqkv", py::arg("qkv"),
+          py::arg("out"), py::arg("lse"), py::arg("dout"), py::arg("heads"), py::arg("scale"), py::arg("seed"),
+          py::arg("p_drop"));
     m.def("conv_wgrad_max_pixels", &kfk::conv_wgrad_max_pixels, py::arg("N"), py::arg("H"), py::arg("W"),
           py::arg("Cin"), py::arg("Cout"), py::arg("ks"), py::arg("stride"));
     m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {

@@ -251,4 +251,15 @@ void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const floa
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,
                                 hipStream_t s, double *gate_stats = nullptr);
 
+// Fused self-attention (attention.hip): qkv [B, S, 3, H, 64] bf16 (the fused projection's
+// output), out [B, S, H*64] bf16, lse [B, H, S] f32; dropout p_drop on the probabilities from a
+// counter hash of (seed, b*H + h, query, key); S = 64 or 128, head dim 64, no mask.
+bool attention_supported(int S, int head_dim);
+void launch_attention_forward(const uint16_t *qkv, uint16_t *out, float *lse, int B, int S, int H, float scale,
+                              uint32_t seed, float p_drop, hipStream_t s);
+// dqkv [B, S, 3, H, 64] (every element written)
+void launch_attention_backward(const uint16_t *qkv, const uint16_t *out, const float *lse, const uint16_t *dout,
+                               uint16_t *dqkv, int B, int S, int H, float scale, uint32_t seed, float p_drop,
+                               hipStream_t s);
+
 }  // namespace kfk

@@ -1,12 +1,15 @@
 """BERT-base encoder for masked-LM pre-training throughput (BASELINE.json config 5:
 "BERT-base SynchronousSGD + gradient-noise-scale monitor + elastic resize").
 12 layers, hidden 768, 12 heads, FFN 3072, vocab 30522, ~110 M parameters.
-Attention uses torch's scaled_dot_product_attention (flash kernels on ROCm)."""
+Attention: the fused HIP kernels of ops/attention.py (S 64/128, no mask), else torch's
+scaled_dot_product_attention."""
 import math
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.attention import self_attention
 
 
 class BertLayer(nn.Module):
@@ -27,10 +30,15 @@ class BertLayer(nn.Module):
 
     def forward(self, x, mask=None):
         B, S, D = x.shape
-        q, k, v = self.qkv(x).view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask,
-                                           dropout_p=self.dropout if self.training else 0.0)
-        a = a.transpose(1, 2).reshape(B, S, D)
+        p = self.dropout if self.training else 0.0
+        qkv = self.qkv(x)
+        if mask is None:
+            # fused HIP attention straight from / into the projections' layouts (SDPA off that path)
+            a = self_attention(qkv, self.heads, p)
+        else:
+            q, k, v = qkv.view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
+            a = a.transpose(1, 2).reshape(B, S, D)
         x = self.ln1(x, F.dropout(self.out(a), self.dropout, self.training))
         h = self.fc2(F.gelu(self.fc1(x)))
         return self.ln2(x, F.dropout(h, self.dropout, self.training))

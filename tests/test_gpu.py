@@ -1083,3 +1083,36 @@ def test_conv_flip_weights_multi_matches_single(H):
     H.conv_flip_weights(srcs, dsts)
     for w, d in zip(srcs, dsts):
         torch.testing.assert_close(d, w.flip(2, 3).transpose(0, 1), rtol=0, atol=0)
+
+
+@needs_gpu
+@pytest.mark.parametrize("S,p", [(128, 0.0), (64, 0.0), (128, 0.1), (64, 0.25)])
+def test_fused_attention_matches_fp32(S, p):
+    """Fused self-attention (csrc/kernels/attention.hip) forward and dq/dk/dv vs an f32 torch
+    composition with the SAME dropout mask (the kernels' counter hash, reproduced by
+    ops.attention.dropout_keep)."""
+    from kungfu_amd.ops.attention import _AttnFn, dropout_keep
+
+    torch.manual_seed(41)
+    B, H = 3, 4
+    qkv = (torch.randn(B, S, 3 * H * 64, device="cuda") * 1.5).bfloat16().requires_grad_(True)
+    seed = 12345
+    out = _AttnFn.apply(qkv, H, p, seed)
+    gout = torch.randn_like(out)
+    out.backward(gout)
+    x = qkv.detach().float().requires_grad_(True)
+    q, k, v = x.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
+    P = torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1)
+    keep = dropout_keep(seed, B, H, S, p, device="cuda")
+    if p > 0:
+        frac = keep.float().mean().item()
+        assert abs(frac - (1 - p)) < 0.01, frac
+    Pd = P * keep / (1 - p)
+    ref = (Pd @ v).transpose(1, 2).reshape(B, S, H * 64)
+    ref.backward(gout.float())
+    assert _rel(out, ref) < 2e-2
+    assert _rel(qkv.grad, x.grad) < 3e-2
+    for t in range(3):  # q, k, v blocks separately
+        a = qkv.grad.view(B, S, 3, H * 64)[:, :, t]
+        r = x.grad.view(B, S, 3, H * 64)[:, :, t]
+        assert ((a.float() - r).norm() / r.norm()).item() < 2e-2, t
