@@ -1,0 +1,71 @@
+"""``F.linear`` whose weight gradient runs on the split-K MFMA kernel of conv_wgrad.hip.
+
+A linear layer's weight gradient ``dW[o][i] = sum_t dy[t][o] x[t][i]`` over T = batch*seq tokens
+is exactly the 1x1-convolution weight gradient over T "pixels" (both operands token-major,
+the "NT" layout that kernel stages unchanged).  hipBLASLt's choices for these long-K, small
+M x N products are poor on BERT-base at 16 K tokens (r8 profile: 768x768 out-projection 147 us
+= 130 TF/s, 3072x768 FFN 185 us = 417 TF/s); the split-K kernel runs them as a 1x1 conv wgrad.
+Forward and data gradient stay on hipBLASLt (``F.linear`` / ``mm``).
+
+Eligible: CUDA bf16 activations and weight, in/out features multiples of 64, < 2^23 tokens;
+anything else is plain ``F.linear``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._lib import hip, hip_available
+
+_MAX_TOKENS = 1 << 23
+
+
+def _as_nhwc(t2: torch.Tensor) -> torch.Tensor:
+    """[T, C] row-major -> [1, C, 1, T] channels_last view of the same memory."""
+    T, C = t2.shape
+    return t2.as_strided((1, C, 1, T), (T * C, 1, T * C, C))
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        ctx.b_dtype = b.dtype if b is not None else None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        out_f, in_f = w.shape
+        dy2 = dy.reshape(-1, out_f)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        x2 = x.reshape(-1, in_f)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
+        return dx, dw, db
+
+
+def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return False
+    out_f, in_f = w.shape
+    if out_f % 64 or in_f % 64 or x.shape[-1] != in_f or x.numel() // in_f >= _MAX_TOKENS:
+        return False
+    return hip_available() and hip().conv_wgrad_supported(int(in_f), int(out_f), 1, 1)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:
+    """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible."""
+    if eligible(x, w) and (b is None or b.dtype in (torch.bfloat16, torch.float32)):
+        y = _LinearFn.apply(x, w, b)
+        return y
+    return F.linear(x, w, b)

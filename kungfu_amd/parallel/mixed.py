@@ -94,7 +94,10 @@ def _conv_forward(self, x):
 
 
 def _linear_forward(self, x):
-    return F.linear(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
+    from ..ops.linear import linear
+
+    # bf16 shadow weights: the weight gradient takes the split-K MFMA kernel (ops/linear.py)
+    return linear(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
 
 
 class ImmediateSink:

@@ -1116,3 +1116,27 @@ def test_fused_attention_matches_fp32(S, p):
         a = qkv.grad.view(B, S, 3, H * 64)[:, :, t]
         r = x.grad.view(B, S, 3, H * 64)[:, :, t]
         assert ((a.float() - r).norm() / r.norm()).item() < 2e-2, t
+
+
+@needs_gpu
+@pytest.mark.parametrize("T,i,o", [(1000, 768, 768), (4096, 768, 3072), (333, 128, 64)])
+def test_linear_mfma_wgrad_matches_fp32(T, i, o):
+    """ops.linear: F.linear forward, weight gradient on the split-K MFMA kernel (a linear
+    layer's dW is the 1x1-conv weight gradient over tokens), data and bias gradients via torch;
+    all vs f32 torch."""
+    from kungfu_amd.ops.linear import eligible, linear
+
+    torch.manual_seed(42)
+    x = torch.randn(2, T, i, device="cuda").bfloat16().requires_grad_(True)
+    w = (torch.randn(o, i, device="cuda") * 0.05).bfloat16().requires_grad_(True)
+    b = torch.randn(o, device="cuda").bfloat16().requires_grad_(True)
+    assert eligible(x, w)
+    y = linear(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yf = torch.nn.functional.linear(xf, wf, bf)
+    yf.backward(g.float())
+    for a, r in ((y, yf), (x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
+        assert a.dtype == torch.bfloat16
+        assert ((a.float() - r).norm() / r.norm()).item() < 1e-2
