@@ -65,10 +65,11 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// 32-byte column-group swizzle of an LDS image row (ROW = 128 or 256 bytes).
+// 32-byte column-group swizzle of an LDS image row (ROW = 128, 256 or 512 bytes; a 512-byte
+// row spans two 256-byte bank cycles, so the 3-bit swizzle of 256-byte rows serves it too).
 template <int ROW>
 __device__ __forceinline__ int hswz(int row) {
-    if constexpr (ROW == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+    if constexpr (ROW >= 256) return (row & 3) | (((row >> 3) & 1) << 2);
     else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
 }
 
@@ -79,14 +80,14 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t *p0, const uint8_t *p1) 
     return __builtin_bit_cast(bf16x8, v);
 }
 
-// WM x WN waves (wave tile 64 co x 64 ci), STAGES-deep global_load_lds ring; S = stride.
-template <int KS, int S, int WM, int WN, int STAGES>
+// WM x WN waves (wave tile 64 co x 16*TN ci), STAGES-deep global_load_lds ring; S = stride.
+template <int KS, int S, int WM, int WN, int STAGES, int TN = 4>
 __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__restrict__ dy,
                                                              const uint16_t *__restrict__ x,
                                                              float *__restrict__ part, void *__restrict__ dw,
                                                              const uint16_t *__restrict__ zero, WGeo g,
                                                              int out_f32, int accumulate, int atomic_out) {
-    constexpr int BM = 64 * WM, BN = 64 * WN, NW = WM * WN, NT = 64 * NW;
+    constexpr int BM = 64 * WM, BN = 16 * TN * WN, NW = WM * WN, NT = 64 * NW;
     constexpr int PAD = (KS - 1) / 2;
     constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per staged pixel row
     constexpr int CPRA = ROWA / 16, CPRB = ROWB / 16;
@@ -167,24 +168,23 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     const int wm = wave / WN, wn = wave % WN;
     const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
     const int rowa0 = 8 * fg + fq;  // hswz is the same for rows rowa0 + {0, 4, 32, 36}
-    int aoff[4], boff[4];
+    int aoff[4], boff[TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        aoff[i] = rowa0 * ROWA + 32 * ((wm * 4 + i) ^ hswz<ROWA>(rowa0)) + 8 * fp;
-        boff[i] = rowa0 * ROWB + 32 * ((wn * 4 + i) ^ hswz<ROWB>(rowa0)) + 8 * fp;
-    }
+    for (int i = 0; i < 4; ++i) aoff[i] = rowa0 * ROWA + 32 * ((wm * 4 + i) ^ hswz<ROWA>(rowa0)) + 8 * fp;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) boff[j] = rowa0 * ROWB + 32 * ((wn * TN + j) ^ hswz<ROWB>(rowa0)) + 8 * fp;
 
-    f32x4 acc[4][4];
+    f32x4 acc[4][TN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[TN]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     };
 
@@ -200,17 +200,15 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *abase = lds + buf * STAGE;
         const uint8_t *bbase = abase + A_BYTES;
-        bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+        bf16x8 af0[4], bf0[TN], af1[4], bf1[TN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            af0[i] = tr_frag(abase + aoff[i], abase + aoff[i] + 4 * ROWA);
-            bf0[i] = tr_frag(bbase + boff[i], bbase + boff[i] + 4 * ROWB);
-        }
+        for (int i = 0; i < 4; ++i) af0[i] = tr_frag(abase + aoff[i], abase + aoff[i] + 4 * ROWA);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            af1[i] = tr_frag(abase + aoff[i] + 32 * ROWA, abase + aoff[i] + 36 * ROWA);
-            bf1[i] = tr_frag(bbase + boff[i] + 32 * ROWB, bbase + boff[i] + 36 * ROWB);
-        }
+        for (int j = 0; j < TN; ++j) bf0[j] = tr_frag(bbase + boff[j], bbase + boff[j] + 4 * ROWB);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af1[i] = tr_frag(abase + aoff[i] + 32 * ROWA, abase + aoff[i] + 36 * ROWA);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf1[j] = tr_frag(bbase + boff[j] + 32 * ROWB, bbase + boff[j] + 36 * ROWB);
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
         if (ks + STAGES - 1 < nsteps) {
@@ -230,11 +228,11 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-                    const int ci = n0 + wn * 64 + j * 16 + (lane & 15);
+                    const int ci = n0 + wn * 16 * TN + j * 16 + (lane & 15);
                     const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
                     atomicAdd(static_cast<float *>(dw) + e, acc[i][j][r]);
                 }
@@ -242,11 +240,11 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-                    const int ci = n0 + wn * 64 + j * 16 + (lane & 15);
+                    const int ci = n0 + wn * 16 * TN + j * 16 + (lane & 15);
                     const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
                     float v = acc[i][j][r];
                     if (out_f32) {
@@ -263,7 +261,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * NT);
+            for (int j = 0; j < TN; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * TN + j) * NT);
     }
 }
 
@@ -473,10 +471,10 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
 // Block = 256 threads = OUT float4 outputs x SG split groups (SG = 256 / OUT, a power of
 // two <= splits): a few K outputs with hundreds of splits (the 56x56 layers) still keep
 // every CU's loads in flight; the SG partial sums meet in LDS.
-template <int WM, int WN>
+template <int WM, int WN, int TN = 4>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restrict__ part, void *__restrict__ dw,
                                                            WGeo g, int out_f32, int accumulate, int sg_log2) {
-    constexpr int BM = 64 * WM, BN = 64 * WN, NT = 64 * WM * WN;
+    constexpr int BM = 64 * WM, BN = 16 * TN * WN, NT = 64 * WM * WN;
     constexpr int TILE4 = BM * BN / 4;
     __shared__ f32x4 red[256];
     const int SG = 1 << sg_log2, OUT = 256 >> sg_log2;
@@ -509,8 +507,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
         const int mt = r2 / g.ntiles, nt = r2 - mt * g.ntiles;
         const int lane = tid & 63, wave = tid >> 6;
         const int wm = wave / WN, wn = wave % WN;
-        const int i = ij >> 2, j = ij & 3;
-        const int ci = nt * BN + wn * 64 + j * 16 + (lane & 15);
+        const int i = ij / TN, j = ij % TN;
+        const int ci = nt * BN + wn * 16 * TN + j * 16 + (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = mt * BM + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
@@ -529,11 +527,14 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 }
 
 struct Tile {
-    int wm, wn;
+    int wm, wn, tn;  // waves (co, ci) and 16-channel ci blocks per wave
+    constexpr int bm() const { return 64 * wm; }
+    constexpr int bn() const { return 16 * tn * wn; }
 };
-// variant -> tile (co x ci): 0 128x128, 1 128x64, 2 64x128, 3 64x64, 4 256x128, 5 128x256
-constexpr Tile kTiles[] = {{2, 2}, {2, 1}, {1, 2}, {1, 1}, {4, 2}, {2, 4}};
-constexpr int kNumVariants = 7;  // + 6: wgrad_rows_kernel (3x3 / stride 1, 9 taps per workgroup)
+// variant -> tile (co x ci): 0 128x128, 1 128x64, 2 64x128, 3 64x64, 4 256x128, 5 128x256,
+// 6 the row-image kernel (below), 7 256x256 (8 waves of 64x128: twice the MFMAs per staged byte)
+constexpr Tile kTiles[] = {{2, 2, 4}, {2, 1, 4}, {1, 2, 4}, {1, 1, 4}, {4, 2, 4}, {2, 4, 4}, {0, 0, 0}, {4, 2, 8}};
+constexpr int kNumVariants = 8;
 constexpr int kRowsVariant = 6;
 
 bool rows_supported(int Cin, int Cout, int ks, int stride) {
@@ -583,8 +584,8 @@ WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const 
     g.m_hw = magic40(g.HW);
     g.m_ow = magic40(g.OW);
     const Tile t = kTiles[plan.variant];
-    g.mtiles = Cout / (64 * t.wm);
-    g.ntiles = Cin / (64 * t.wn);
+    g.mtiles = Cout / t.bm();
+    g.ntiles = Cin / t.bn();
     g.taps = ks * ks;
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.splits = plan.splits;
@@ -592,20 +593,22 @@ WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const 
     return g;
 }
 
-template <int KS, int S, int WM, int WN>
+template <int KS, int S, int WM, int WN, int TN = 4>
 void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, const WGeo &g, bool out_f32,
               bool accumulate, bool atomic_out, hipStream_t s) {
     // 3-deep global_load_lds ring (tools/bench_wgrad.py --sweep: 2 stages starve the 8-wave
-    // 256x128 tiles, 4 stages cost the 1-2 wave tiles their second/third workgroup per CU)
-    constexpr int STAGES = 3;
-    wgrad_kernel<KS, S, WM, WN, STAGES><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
+    // 256x128 tiles, 4 stages cost the 1-2 wave tiles their second/third workgroup per CU);
+    // 2 for the 256x256 tile (64 KB per stage)
+    constexpr int STAGE_BYTES = 64 * (64 * WM + 16 * TN * WN) * 2;
+    constexpr int STAGES = 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
+    wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
         dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out);
     if (g.splits > 1 && !atomic_out) {
-        const int64_t total = static_cast<int64_t>(g.tiles) * (64 * WM) * (64 * WN) / 4;
+        const int64_t total = static_cast<int64_t>(g.tiles) * (64 * WM) * (16 * TN * WN) / 4;
         int sgl = 0;  // split groups: enough blocks for the chip, at most 64 groups, <= splits
         while (sgl < 6 && (2 << sgl) <= g.splits && (total << (sgl + 1)) <= int64_t(256) * 2048) ++sgl;
         const int64_t grid = (total + (256 >> sgl) - 1) / (256 >> sgl);
-        wgrad_reduce_kernel<WM, WN><<<static_cast<int>(grid), 256, 0, s>>>(part, dw, g, out_f32, accumulate, sgl);
+        wgrad_reduce_kernel<WM, WN, TN><<<static_cast<int>(grid), 256, 0, s>>>(part, dw, g, out_f32, accumulate, sgl);
     }
 }
 
@@ -618,7 +621,8 @@ void launch_ks(const uint16_t *dy, const uint16_t *x, void *dw, float *part, con
     case 2: launch_t<KS, S, 1, 2>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
     case 3: launch_t<KS, S, 1, 1>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
     case 4: launch_t<KS, S, 4, 2>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
-    default: launch_t<KS, S, 2, 4>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    case 5: launch_t<KS, S, 2, 4>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
+    default: launch_t<KS, S, 4, 2, 8>(dy, x, dw, part, g, out_f32, accumulate, atomic_out, s); break;
     }
 }
 
@@ -657,7 +661,11 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
     if (variant < 0) {
         // tools/bench_wgrad.py --sweep (profiles/README.md): 8-wave 256x128 tiles once the
         // GEMM is big enough, else the largest 4/2/1-wave tile the channel counts allow
-        if (Cout % 256 == 0 && Cin % 128 == 0 && work >= 131072) variant = 4;
+        // tools/bench_wgrad_1x1.py: 256x256 for the large long-K linear-layer products (BERT-base
+        // 768x3072 at 16 K tokens: 133 -> 87 us); ResNet's 1x1 shapes keep 256x128 (their split-K
+        // partials of 256x256 tiles cost more than the extra MFMA density saves)
+        if (Cout % 256 == 0 && Cin % 256 == 0 && work >= 1500000 && ks == 1) variant = 7;
+        else if (Cout % 256 == 0 && Cin % 128 == 0) variant = 4;
         else if (Cout % 128 == 0 && Cin % 256 == 0 && work >= 131072) variant = 5;
         else if (Cout % 128 == 0 && Cin % 128 == 0) variant = 0;
         else if (Cout % 128 == 0) variant = 1;
@@ -665,13 +673,13 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
         else variant = 3;
     }
     const Tile t = kTiles[variant];
-    if (Cout % (64 * t.wm) != 0 || Cin % (64 * t.wn) != 0) throw std::invalid_argument("conv_wgrad: tile/channel mismatch");
+    if (t.wm == 0 || Cout % t.bm() != 0 || Cin % t.bn() != 0) throw std::invalid_argument("conv_wgrad: tile/channel mismatch");
     pl.variant = variant;
     const int pad = (ks - 1) / 2;
     const int OH = (H + 2 * pad - ks) / stride + 1, OW = (W + 2 * pad - ks) / stride + 1;
     const int64_t P = static_cast<int64_t>(N) * OH * OW;
     const int ksteps = static_cast<int>((P + kBK - 1) / kBK);
-    const int tiles = (Cout / (64 * t.wm)) * (Cin / (64 * t.wn)) * ks * ks;
+    const int tiles = (Cout / t.bm()) * (Cin / t.bn()) * ks * ks;
     if (splits < 0) {
         // workgroups per launch: one per CU for the 4/8-wave tiles (2 for 3x3), more for the
         // 1-2 wave tiles, so every CU keeps >= ~48 KB of loads in flight; >= 4 K-steps per split
@@ -688,7 +696,7 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
     splits = std::max(1, std::min(splits, ksteps));
     pl.kps = (ksteps + splits - 1) / splits;
     pl.splits = (ksteps + pl.kps - 1) / pl.kps;  // no empty split
-    pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * tiles * (64 * t.wm) * (64 * t.wn) : 0;
+    pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * tiles * t.bm() * t.bn() : 0;
     return pl;
 }
 

@@ -12,12 +12,15 @@ anything else is plain ``F.linear``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .._lib import hip, hip_available
 
 _MAX_TOKENS = 1 << 23
+_ENABLED = os.environ.get("KUNGFU_LINEAR_WGRAD", "1") != "0"
 
 
 def _as_nhwc(t2: torch.Tensor) -> torch.Tensor:
@@ -55,7 +58,7 @@ class _LinearFn(torch.autograd.Function):
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2):
+    if not (_ENABLED and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2):
         return False
     out_f, in_f = w.shape
     if out_f % 64 or in_f % 64 or x.shape[-1] != in_f or x.numel() // in_f >= _MAX_TOKENS:
