@@ -741,7 +741,8 @@ BNCommon bn_common(int C, const at::Tensor &weight, const at::Tensor &bias,
 std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
                                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                    double momentum, double eps, bool training, bool relu,
-                                   c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> sums) {
+                                   c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> sums,
+                                   c10::optional<at::Tensor> res_coef, bool apply) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
@@ -752,12 +753,19 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                     "bn: residual must match x (bf16, channels_last)");
         rp = reinterpret_cast<const uint16_t *>(res->data_ptr());
     }
+    const float *rc = nullptr;
+    if (res_coef && res_coef->defined()) {
+        TORCH_CHECK(rp && res_coef->scalar_type() == at::kFloat && res_coef->numel() == 2 * C && res_coef->is_contiguous(),
+                    "bn: res_coef must be the residual BN's f32 [scale(C); shift(C)] coefficients");
+        rc = res_coef->data_ptr<float>();
+    }
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
-    auto y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    at::Tensor y;
+    if (apply) y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
     at::Tensor mask;
-    if (rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
+    if (apply && rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
     double *sp = nullptr;
     if (training && sums && sums->defined()) {
         TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->numel() == 2 * C * kfk::kStatSlots &&
@@ -768,11 +776,11 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
     at::Tensor partial;
     if (training && !sp) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     kfk::launch_bn_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, weight.data_ptr<float>(),
-                           bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                           bias.data_ptr<float>(), apply ? reinterpret_cast<uint16_t *>(y.data_ptr()) : nullptr,
                            mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, sh, relu, training, b.rm, b.rv,
                            static_cast<float>(momentum), static_cast<float>(eps),
                            partial.defined() ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp);
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp, rc, apply);
     return {y, mean, invstd, coef, mask};
 }
 
@@ -1210,7 +1218,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "fused NHWC BN(+residual)(+ReLU) forward -> (y, mean, invstd, coef, relu mask or None)", py::arg("x"),
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
-          py::arg("num_batches") = py::none(), py::arg("sums") = py::none());
+          py::arg("num_batches") = py::none(), py::arg("sums") = py::none(), py::arg("res_coef") = py::none(),
+          py::arg("apply") = true);
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
           py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none());

@@ -232,13 +232,21 @@ __global__ void bn_sums_finalize(double *sums, int C, int64_t rows, const float 
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (num_batches && c == 0) num_batches[0] += 1;
     if (c >= C) return;
-    double s = 0, q = 0;
+    // every slot load issued before the zeroing stores (the compiler cannot prove the stores do
+    // not alias later loads, so an interleaved loop serialises 32 load latencies)
+    double vs[kStatSlots], vq[kStatSlots];
+#pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
-        double *sl = sums + k * 2 * C;
-        s += sl[c];
-        q += sl[C + c];
-        sl[c] = 0.0;
-        sl[C + c] = 0.0;
+        vs[k] = sums[k * 2 * C + c];
+        vq[k] = sums[k * 2 * C + C + c];
+    }
+    double s = 0, q = 0;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        s += vs[k];
+        q += vq[k];
+        sums[k * 2 * C + c] = 0.0;
+        sums[k * 2 * C + C + c] = 0.0;
     }
     const double m = s / rows;
     double var = q / rows - m * m;
@@ -273,19 +281,26 @@ __global__ void bn_eval_coef(int C, const float *gamma, const float *beta, const
 // ---------------------------------------------------------------- forward apply
 
 // y = act(x*scale + shift [+ res]); with RES && RELU also a 1-bit mask per
-// element (one byte per 8-channel vector) for the backward.
-template <int CVEC, bool RES, bool RELU>
+// element (one byte per 8-channel vector) for the backward.  RESC: the residual is itself a
+// BN input -- res*rscale + rshift with the coefficients rcoef (the downsample branch's BN, so
+// its output is never materialised).
+template <int CVEC, bool RES, bool RELU, bool RESC = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restrict__ x, const uint4 *__restrict__ res,
                                                           const float *__restrict__ coef, uint4 *__restrict__ y,
-                                                          uint8_t *__restrict__ mask, int64_t nvec) {
+                                                          uint8_t *__restrict__ mask, int64_t nvec,
+                                                          const float *__restrict__ rcoef = nullptr) {
     constexpr int C = CVEC * 8;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
-    float sc[8], sh[8];
+    float sc[8], sh[8], rsc[8], rsh[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         sc[k] = coef[cv * 8 + k];
         sh[k] = coef[C + cv * 8 + k];
+        if (RESC) {
+            rsc[k] = rcoef[cv * 8 + k];
+            sh[k] += rcoef[C + cv * 8 + k];
+        }
     }
     const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();  // multiple of CVEC
     // two vectors per trip, both loads issued before either is used (bytes in flight per lane)
@@ -312,7 +327,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 float v = f[k] * sc[k] + sh[k];
-                if (RES) v += rr[k];
+                if (RESC) v += rr[k] * rsc[k];
+                else if (RES) v += rr[k];
                 if (RELU) {
                     m |= (v > 0.f ? 1u : 0u) << k;
                     v = v > 0.f ? v : 0.f;
@@ -584,13 +600,19 @@ __global__ void bn_bwd_finalize_sums(double *sums, int C, int64_t rows, const fl
                                      const float *invstd, float *dgamma, float *dbeta, float *coef, bool training) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
-    double s0 = 0, s1 = 0;
+    double v0[kStatSlots], v1[kStatSlots];
+#pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
-        double *sl = sums + k * 2 * C;
-        s0 += sl[c];
-        s1 += sl[C + c];
-        sl[c] = 0.0;
-        sl[C + c] = 0.0;
+        v0[k] = sums[k * 2 * C + c];
+        v1[k] = sums[k * 2 * C + C + c];
+    }
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        s0 += v0[k];
+        s1 += v1[k];
+        sums[k * 2 * C + c] = 0.0;
+        sums[k * 2 * C + C + c] = 0.0;
     }
     const double db = s0, dg = static_cast<double>(invstd[c]) * (s1 - static_cast<double>(mean[c]) * db);
     dgamma[c] = static_cast<float>(dg);
@@ -775,7 +797,7 @@ int bn_num_chunks(BNShape sh) { return chunking(sh).nchunks; }
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
-                       int64_t *num_batches, hipStream_t s, double *sums) {
+                       int64_t *num_batches, hipStream_t s, double *sums, const float *res_coef, bool apply) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     if (training && sums) {
@@ -787,6 +809,7 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
     } else {
         bn_eval_coef<<<(C + 255) / 256, 256, 0, s>>>(C, gamma, beta, run_mean, run_var, eps, mean, invstd, coef);
     }
+    if (!apply) return;
     const int g = apply_grid(nvec, cvec);
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
@@ -794,7 +817,10 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
         const uint4 *xv = reinterpret_cast<const uint4 *>(x);
         const uint4 *rv = reinterpret_cast<const uint4 *>(res);
         uint4 *yv = reinterpret_cast<uint4 *>(y);
-        if (res) {
+        if (res && res_coef) {
+            if (relu) bn_apply_kernel<CV, true, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef);
+            else bn_apply_kernel<CV, true, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef);
+        } else if (res) {
             if (relu) bn_apply_kernel<CV, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
             else bn_apply_kernel<CV, true, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
         } else {

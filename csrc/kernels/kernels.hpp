@@ -193,8 +193,11 @@ int bn_num_chunks(BNShape sh);  // partial scratch = 2 * nchunks * C floats
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
-                       int64_t *num_batches, hipStream_t s, double *sums = nullptr);
-// (sums: f64 [2C] batch sums from a conv epilogue -> no statistics pass; re-zeroed.)
+                       int64_t *num_batches, hipStream_t s, double *sums = nullptr, const float *res_coef = nullptr,
+                       bool apply = true);
+// (sums: f64 [2C] batch sums from a conv epilogue -> no statistics pass; re-zeroed.
+//  res_coef: the residual is res*res_coef[c] + res_coef[C+c] (another BN's input and
+//  coefficients); apply = false: statistics / coefficients only, y untouched.)
 // dz = dy * relu'(.)  -- from mask bits if given, else recomputed as x*fcoef[0:C] + fcoef[C:2C] > 0
 // (fcoef = the forward's coef) ; dgamma/dbeta (f32) ; dx = k1*dz + k2*x + k3 ; dres = dz.
 // coef scratch: 3C floats.

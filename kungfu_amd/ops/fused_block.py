@@ -168,10 +168,10 @@ class _BottleneckFn(torch.autograd.Function):
         s = spec.stride
         outs = []
 
-        def bn(i, y, res, relu):
+        def bn(i, y, res, relu, res_coef=None, apply=True):
             m = spec.bns[i]
             return H.bn_forward(y, res, gam[i], bet[i], m.running_mean, m.running_var, m.momentum, m.eps, True, relu,
-                                m.num_batches_tracked, _sums(m, dev))
+                                m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply)
 
         y1 = H.conv(x, ws_bf[0], 1, _sums(spec.bns[0], dev))
         z1, m1, i1, c1, _ = bn(0, y1, None, True)
@@ -179,12 +179,14 @@ class _BottleneckFn(torch.autograd.Function):
         z2, m2, i2, c2, _ = bn(1, y2, None, True)
         y3 = H.conv(z2, ws_bf[2], 1, _sums(spec.bns[2], dev))
         if spec.ds:
+            # the downsample BN is folded into the tail's residual read (coefficients only here):
+            # out = relu(bn3(y3) + bn_d(yd)) without materialising bn_d(yd)
             yd = H.conv(x, ws_bf[3], s, _sums(spec.bns[3], dev))
-            idt, md, idd, cd, _ = bn(3, yd, None, False)
+            _, md, idd, cd, _ = bn(3, yd, None, False, apply=False)
+            out, m3, i3, c3, mask3 = bn(2, y3, yd, True, res_coef=cd)
         else:
             yd = md = idd = cd = None
-            idt = x
-        out, m3, i3, c3, mask3 = bn(2, y3, idt, True)
+            out, m3, i3, c3, mask3 = bn(2, y3, x, True)
         # cross-block BN3 backward fusion: the previous block's tail (if x is its output)
         ctx.prev = getattr(x, "_kf_tail", None)
         ctx.tail = _TailSlot(_sums(spec.bns[2], dev), y3, mask3)
