@@ -846,15 +846,19 @@ std::vector<at::Tensor> bn_pool_forward(at::Tensor x, at::Tensor weight, at::Ten
     auto yp = at::empty({x.size(0), C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
     auto arg = at::empty({x.size(0) * OH * OW * C}, x.options().dtype(at::kByte));
     auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
-    at::Tensor partial;
-    if (training) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    at::Tensor partial, xarg;
+    if (training) {
+        partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+        xarg = at::empty_like(yp, at::MemoryFormat::ChannelsLast);
+    }
     kfk::launch_bn_pool_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), weight.data_ptr<float>(),
                                 bias.data_ptr<float>(), reinterpret_cast<uint16_t *>(yp.data_ptr()),
                                 arg.data_ptr<uint8_t>(), sh, H, W, training, b.rm, b.rv, static_cast<float>(momentum),
                                 static_cast<float>(eps), training ? partial.data_ptr<float>() : nullptr,
                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt,
-                                stream_of(x, 0), sp);
-    return {yp, mean, invstd, coef, arg};
+                                stream_of(x, 0), sp,
+                                xarg.defined() ? reinterpret_cast<uint16_t *>(xarg.data_ptr()) : nullptr);
+    return {yp, mean, invstd, coef, arg, xarg};
 }
 
 // ---- ResNet stem (stem.hip) ----
@@ -936,7 +940,8 @@ at::Tensor stem_wgrad(at::Tensor dy, at::Tensor x4, int64_t splits) {
 
 // Returns (dx, dweight, dbias).
 std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Tensor x, at::Tensor mean,
-                                         at::Tensor invstd, at::Tensor weight, at::Tensor fcoef, bool training) {
+                                         at::Tensor invstd, at::Tensor weight, at::Tensor fcoef, bool training,
+                                         c10::optional<at::Tensor> xarg) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     const int H = static_cast<int>(x.size(2)), W = static_cast<int>(x.size(3));
@@ -952,12 +957,22 @@ std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Ten
     auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
     auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    const bool pooled = training && xarg && xarg->defined();
+    at::Tensor sums;
+    if (pooled) {
+        TORCH_CHECK(xarg->sizes() == dyp.sizes() && xarg->scalar_type() == at::kBFloat16 &&
+                        xarg->is_contiguous(at::MemoryFormat::ChannelsLast),
+                    "bn_pool_backward: xarg must be the forward's pooled pre-BN values");
+        sums = at::zeros({2 * C * kfk::kStatSlots}, x.options().dtype(at::kDouble));
+    }
     kfk::launch_bn_pool_backward(reinterpret_cast<const uint16_t *>(dyp.data_ptr()), arg.data_ptr<uint8_t>(),
                                  reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(),
                                  mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, H, W,
                                  training, partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
                                  coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
-                                 stream_of(x, 0));
+                                 stream_of(x, 0),
+                                 pooled ? reinterpret_cast<const uint16_t *>(xarg->data_ptr()) : nullptr,
+                                 pooled ? sums.data_ptr<double>() : nullptr);
     return {dx, dw, db};
 }
 
@@ -1241,7 +1256,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("weight"), py::arg("x4"), py::arg("training") = true, py::arg("splits") = -1);
     m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient (split-K MFMA)", py::arg("dy"), py::arg("x4"),
           py::arg("splits") = -1);
-    m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)");
+    m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)",
+          py::arg("dy"), py::arg("arg"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
+          py::arg("fcoef"), py::arg("training"), py::arg("xarg") = py::none());
     m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
     m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");
     m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");

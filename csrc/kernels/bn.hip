@@ -347,10 +347,12 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
 // from L2 -- neighbouring outputs share 3-6 of them), BN+ReLU per element, max.
 // Emits the pooled bf16 map and the window argmax (0..8) per element as bytes.
 template <int CVEC>
+// xarg (optional): the pre-BN input value of each window's chosen element, so the backward's
+// BN sums can run over the pooled map (bn_pool_bwd_sums_kernel) instead of a full-resolution gather.
 __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__restrict__ x,
                                                                const float *__restrict__ coef, uint4 *__restrict__ yp,
                                                                uint2 *__restrict__ arg, int H, int W, int OH, int OW,
-                                                               int64_t nout_vec) {
+                                                               int64_t nout_vec, uint4 *__restrict__ xarg) {
     constexpr int C = CVEC * 8;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
@@ -367,12 +369,13 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__re
         const int64_t t = p / OW;
         const int oh = static_cast<int>(t % OH);
         const int64_t n = t / OH;
-        float best[8];
+        float best[8], xb[8];
         uint32_t a[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             best[k] = -1.f;  // post-ReLU values are >= 0
             a[k] = 0;
+            xb[k] = 0.f;
         }
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
@@ -391,6 +394,7 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__re
                     if (v > best[k]) {
                         best[k] = v;
                         a[k] = kh * 3 + kw;
+                        xb[k] = f[k];
                     }
                 }
             }
@@ -398,6 +402,61 @@ __global__ __launch_bounds__(kBlock) void bn_pool_apply_kernel(const uint4 *__re
         yp[i] = pack8(best);
         arg[i] = make_uint2(a[0] | (a[1] << 8) | (a[2] << 16) | (a[3] << 24),
                             a[4] | (a[5] << 8) | (a[6] << 16) | (a[7] << 24));
+        if (xarg) xarg[i] = pack8(xb);  // exact: bf16 inputs re-packed
+    }
+}
+
+// BN backward sums of the stem's BN+ReLU+MaxPool in POOLED space: every window hands its
+// gradient to exactly one input element (its argmax), so
+//   sum_p dz[p] = sum_w dy[w] * relu'(x_w),   sum_p dz[p] x[p] = sum_w dy[w] * relu'(x_w) * x_w
+// with x_w = xarg[w] -- two reads of the pooled map instead of the full-resolution gather
+// (exact up to f32 summation order).  Sums go to f64 slots [kStatSlots][2][C].
+template <int CVEC>
+__global__ __launch_bounds__(kBlock) void bn_pool_bwd_sums_kernel(const uint4 *__restrict__ dy,
+                                                                  const uint4 *__restrict__ xarg,
+                                                                  const float *__restrict__ fcoef,
+                                                                  double *__restrict__ sums, int64_t nvec) {
+    constexpr int C = CVEC * 8, NT = bn_threads<CVEC>();
+    const int64_t tid = static_cast<int64_t>(blockIdx.x) * NT + threadIdx.x;
+    const int cv = static_cast<int>(tid % CVEC);
+    float sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        sc[k] = fcoef[cv * 8 + k];
+        sh[k] = fcoef[C + cv * 8 + k];
+        s1[k] = s2[k] = 0.f;
+    }
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * NT;
+    for (int64_t i = tid; i < nvec; i += stride) {
+        float g[8], xv[8];
+        unpack8(dy[i], g);
+        unpack8(xarg[i], xv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float dz = xv[k] * sc[k] + sh[k] > 0.f ? g[k] : 0.f;
+            s1[k] += dz;
+            s2[k] += dz * xv[k];
+        }
+    }
+    __shared__ float red[kBlock][17];
+    if (threadIdx.x < NT) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            red[threadIdx.x][k] = s1[k];
+            red[threadIdx.x][8 + k] = s2[k];
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) {
+        const int cvi = c >> 3, k = c & 7;
+        double a1 = 0, a2 = 0;
+        for (int u = cvi; u < NT; u += CVEC) {
+            a1 += red[u][k];
+            a2 += red[u][8 + k];
+        }
+        double *sl = sums + (blockIdx.x % kStatSlots) * 2 * C;
+        atomicAdd(sl + c, a1);
+        atomicAdd(sl + C + c, a2);
     }
 }
 
@@ -847,7 +906,7 @@ bool bn_pool_supported(BNShape sh, int H, int W) {
 void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
                             BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
                             float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
-                            hipStream_t s, double *sums) {
+                            hipStream_t s, double *sums, uint16_t *xarg) {
     const int C = sh.channels, cvec = C / 8;
     if (training && sums) {
         bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
@@ -866,14 +925,26 @@ void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *
         constexpr int CV = decltype(cvc)::value;
         bn_pool_apply_kernel<CV><<<g, bn_threads<CV>(), 0, s>>>(reinterpret_cast<const uint4 *>(x), coef,
                                                       reinterpret_cast<uint4 *>(yp), reinterpret_cast<uint2 *>(arg), H,
-                                                      W, OH, OW, nout);
+                                                      W, OH, OW, nout, reinterpret_cast<uint4 *>(xarg));
     });
 }
 
 void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                             hipStream_t s) {
+                             hipStream_t s, const uint16_t *xarg, double *sums) {
+    if (xarg && sums && training) {
+        const int C = sh.channels, cvec = C / 8;
+        const int64_t nvec = sh.rows / (static_cast<int64_t>(H) * W) * pool_out(H) * pool_out(W) * cvec;
+        const int g = apply_grid(nvec, cvec);
+        dispatch_cvec(cvec, [&](auto cvc) {
+            constexpr int CV = decltype(cvc)::value;
+            bn_pool_bwd_sums_kernel<CV><<<g, bn_threads<CV>(), 0, s>>>(
+                reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint4 *>(xarg), fcoef, sums, nvec);
+        });
+    } else {
+        sums = nullptr;
+    }
     const uint64_t m_hw = (uint64_t(1) << 40) / (static_cast<uint64_t>(H) * W) + 1;
     const uint64_t m_w = (uint64_t(1) << 40) / static_cast<uint64_t>(W) + 1;
     if (static_cast<uint64_t>(sh.rows) * H * W >= (uint64_t(1) << 40))
@@ -881,7 +952,7 @@ void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint
     PoolGrad pg{reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint2 *>(arg), H, W, pool_out(H),
                 pool_out(W), m_hw, m_w};
     launch_backward_impl(pg, x, fcoef, nullptr, mean, invstd, gamma, sh, RM_COEF, training, partial, dgamma, dbeta,
-                         coef, dx, nullptr, s);
+                         coef, dx, nullptr, s, sums);
 }
 
 }  // namespace kfk

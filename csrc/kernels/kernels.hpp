@@ -214,11 +214,13 @@ bool bn_pool_supported(BNShape sh, int H, int W);
 void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *beta, uint16_t *yp, uint8_t *arg,
                             BNShape sh, int H, int W, bool training, float *run_mean, float *run_var, float momentum,
                             float eps, float *partial, float *mean, float *invstd, float *coef, int64_t *num_batches,
-                            hipStream_t s, double *sums = nullptr);
+                            hipStream_t s, double *sums = nullptr, uint16_t *xarg = nullptr);
+// xarg + sums (zeroed f64 [slots][2][C]): the BN sums come from the pooled map (exact identity,
+// see bn_pool_bwd_sums_kernel) instead of the full-resolution reduce pass.
 void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                             hipStream_t s);
+                             hipStream_t s, const uint16_t *xarg = nullptr, double *sums = nullptr);
 
 // Conv bias (+ ReLU) on NHWC bf16 [rows, C] (bias_act.hip): forward in place; backward
 // dz = dy * (y > 0) (relu) and dbias[c] = sum over rows (f32, zeroed first).

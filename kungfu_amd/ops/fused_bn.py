@@ -80,17 +80,19 @@ class _BNActFn(torch.autograd.Function):
 class _BNActPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, training, nbt, sums):
-        y, mean, invstd, coef, arg = hip().bn_pool_forward(x, weight, bias, running_mean, running_var, momentum, eps,
-                                                           training, nbt, sums)
-        ctx.save_for_backward(x, mean, invstd, weight, coef, arg)
+        y, mean, invstd, coef, arg, xarg = hip().bn_pool_forward(x, weight, bias, running_mean, running_var, momentum,
+                                                                 eps, training, nbt, sums)
+        # xarg (training): pre-BN value of each window's argmax -> the backward's BN sums run
+        # over the pooled map
+        ctx.save_for_backward(x, mean, invstd, weight, coef, arg, xarg)
         ctx.training = training
         ctx.direct = _direct(weight, bias)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, mean, invstd, weight, coef, arg = ctx.saved_tensors
-        dx, dw, db = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training)
+        x, mean, invstd, weight, coef, arg, xarg = ctx.saved_tensors
+        dx, dw, db = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training, xarg)
         dw, db = _param_grads(ctx, dw, db)
         return dx, dw, db, None, None, None, None, None, None, None
 

@@ -93,7 +93,7 @@ class _StemBlockFn(torch.autograd.Function):
             wb = wb.contiguous(memory_format=torch.channels_last)
         st = sums if training else None
         y = H.stem_forward(x4, H.stem_pack_weight(wb), st)
-        yp, mean, invstd, coef, arg = H.bn_pool_forward(y, gamma, beta, running_mean, running_var, momentum, eps,
+        yp, mean, invstd, coef, arg, _ = H.bn_pool_forward(y, gamma, beta, running_mean, running_var, momentum, eps,
                                                          training, nbt, st)
         ctx.save_for_backward(x4, y, mean, invstd, gamma, coef, arg)
         ctx.training = training

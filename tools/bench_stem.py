@@ -57,7 +57,7 @@ from kungfu_amd.ops.fused_bn import BatchNormAct2d  # noqa: E402
 bn = BatchNormAct2d(64).cuda()
 st = torch.zeros(H_.conv_stat_slots * 2 * 64, dtype=torch.float64, device="cuda")
 yc = H_.stem_forward(x4, wp, st)
-yp, mean, invstd, coef, arg = H_.bn_pool_forward(yc, bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.1, 1e-5,
+yp, mean, invstd, coef, arg, xarg = H_.bn_pool_forward(yc, bn.weight, bn.bias, bn.running_mean, bn.running_var, 0.1, 1e-5,
                                                  True, None, st)
 dyp = torch.randn_like(yp)
 t2 = {

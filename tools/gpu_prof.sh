@@ -12,9 +12,10 @@ cd /tmp && export TMPDIR=/tmp
 for M in $MODELS; do
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_${M}_prof" -o prof --output-format csv -- \
     python3 "$GRAFT_REPO_ROOT/bench.py" --model $M --steps 6 --warmup 3 > "$OUT/${TAG}_${M}_prof.log" 2>&1 || exit $?
-  python3 "$GRAFT_REPO_ROOT/tools/prof_summary.py" "$OUT/${TAG}_${M}_prof/prof_kernel_trace.csv" --top 40 \
+  MK=sgd; case $M in bert*) MK=adam;; esac
+  python3 "$GRAFT_REPO_ROOT/tools/prof_summary.py" "$OUT/${TAG}_${M}_prof/prof_kernel_trace.csv" --top 40 --marker $MK \
     > "$OUT/${TAG}_${M}_summary.md" 2>&1
-  python3 "$GRAFT_REPO_ROOT/tools/prof_shapes.py" "$OUT/${TAG}_${M}_prof/prof_kernel_trace.csv" --top 70 \
+  python3 "$GRAFT_REPO_ROOT/tools/prof_shapes.py" "$OUT/${TAG}_${M}_prof/prof_kernel_trace.csv" --top 70 --marker $MK \
     > "$OUT/${TAG}_${M}_shapes.md" 2>&1
   head -24 "$OUT/${TAG}_${M}_summary.md"
 done
