@@ -787,7 +787,8 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
 // Returns (dx, dres or undefined, dweight, dbias).
 std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd,
                                     at::Tensor weight, at::Tensor fcoef, c10::optional<at::Tensor> mask, bool relu,
-                                    bool training, bool want_dres, c10::optional<at::Tensor> sums) {
+                                    bool training, bool want_dres, c10::optional<at::Tensor> sums,
+                                    c10::optional<at::Tensor> dres_x, c10::optional<at::Tensor> dres_sums) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -813,12 +814,23 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
     }
     at::Tensor partial;
     if (!sp) partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
+    const uint16_t *dsx = nullptr;
+    double *dsp = nullptr;
+    if (dres_x && dres_x->defined()) {
+        TORCH_CHECK(want_dres && dres_sums && dres_sums->defined() && dres_x->sizes() == x.sizes() &&
+                        dres_x->scalar_type() == at::kBFloat16 && dres_x->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                        dres_sums->scalar_type() == at::kDouble && dres_sums->numel() == 2 * C * kfk::kStatSlots,
+                    "bn_backward: dres_x (second BN's input) needs want_dres and its f64 sums workspace");
+        dsx = reinterpret_cast<const uint16_t *>(dres_x->data_ptr());
+        dsp = dres_sums->data_ptr<double>();
+    }
     kfk::launch_bn_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                             reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(), mp,
                             mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, relu,
                             training, partial.defined() ? partial.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
                             db.data_ptr<float>(), coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
-                            want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0), sp);
+                            want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0), sp,
+                            dsx, dsp);
     return {dx, dres, dw, db};
 }
 
@@ -1237,7 +1249,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("apply") = true);
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
-          py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none());
+          py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none(),
+          py::arg("dres_x") = py::none(), py::arg("dres_sums") = py::none());
     m.def("bn_pool_supported", [](int64_t C, int64_t H, int64_t W) {
         return kfk::bn_pool_supported(kfk::BNShape{H * W, static_cast<int>(C)}, static_cast<int>(H),
                                       static_cast<int>(W));

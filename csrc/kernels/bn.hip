@@ -693,12 +693,17 @@ __global__ void bn_bwd_finalize_sums(double *sums, int C, int64_t rows, const fl
 
 // ---------------------------------------------------------------- backward apply
 
+// DRES && dsx: the residual gradient also feeds a second BN (the downsample branch's, input dsx,
+// no ReLU): its backward sums sum(dres) and sum(dres * dsx) (of the bf16-rounded dres, as that
+// BN's own pass would read it) go to the f64 slots dsums, so that BN skips its reduce pass.
 template <int CVEC, int RM, bool DRES, class G>
 __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint4 *__restrict__ x,
                                                               const float *__restrict__ fcoef,
                                                               const uint8_t *__restrict__ mask,
                                                               const float *__restrict__ coef, uint4 *__restrict__ dx,
-                                                              uint4 *__restrict__ dres, int64_t nvec) {
+                                                              uint4 *__restrict__ dres, int64_t nvec,
+                                                              const uint4 *__restrict__ dsx = nullptr,
+                                                              double *__restrict__ dsums = nullptr) {
     constexpr int C = CVEC * 8;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
@@ -710,6 +715,10 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
         k3[k] = coef[2 * C + cv * 8 + k];
     }
     load_fwd_coef<CVEC, RM>(fcoef, cv, sc, sh);
+    float d1[8], d2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d1[k] = d2[k] = 0.f;
+    const bool dsum = DRES && dsx != nullptr;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * bn_threads<CVEC>();
     // two vectors per trip, every load issued before any is used (bytes in flight per lane)
     constexpr int U = 2;
@@ -732,11 +741,47 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
             grad.get(gr[u], g);
             unpack8(xr[u], xv);
             relu_gate<RM>(g, xv, sc, sh, mask, i);
-            if (DRES) dres[i] = pack8(g);
+            if (DRES) {
+                const uint4 gr = pack8(g);
+                dres[i] = gr;
+                if (dsum) {
+                    float gq[8], sx[8];
+                    unpack8(gr, gq);
+                    unpack8(dsx[i], sx);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        d1[k] += gq[k];
+                        d2[k] += gq[k] * sx[k];
+                    }
+                }
+            }
             float o[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) o[k] = k1[k] * g[k] + k2[k] * xv[k] + k3[k];
             dx[i] = pack8(o);
+        }
+    }
+    if (dsum) {
+        constexpr int NT = bn_threads<CVEC>();
+        __shared__ float red[kBlock][17];
+        if (threadIdx.x < NT) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                red[threadIdx.x][k] = d1[k];
+                red[threadIdx.x][8 + k] = d2[k];
+            }
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < C; c += NT) {
+            const int cvi = c >> 3, k = c & 7;
+            double a1 = 0, a2 = 0;
+            for (int u = cvi; u < NT; u += CVEC) {
+                a1 += red[u][k];
+                a2 += red[u][8 + k];
+            }
+            double *sl = dsums + (blockIdx.x % kStatSlots) * 2 * C;
+            atomicAdd(sl + c, a1);
+            atomicAdd(sl + C + c, a2);
         }
     }
 }
@@ -791,7 +836,7 @@ template <class G>
 void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const uint8_t *mask, const float *mean,
                           const float *invstd, const float *gamma, BNShape sh, int rm, bool training, float *partial,
                           float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s,
-                          double *sums = nullptr) {
+                          double *sums = nullptr, const uint16_t *dres_x = nullptr, double *dres_sums = nullptr) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     Chunking ch = chunking(sh);
@@ -821,7 +866,9 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
         auto go = [&](auto rmc, auto drc) {
             constexpr int RM = decltype(rmc)::value;
             constexpr bool DR = decltype(drc)::value;
-            bn_bwd_apply_kernel<CV, RM, DR, G><<<g, bn_threads<CV>(), 0, s>>>(grad, xx, fcoef, mask, coef, o, r, nvec);
+            bn_bwd_apply_kernel<CV, RM, DR, G><<<g, bn_threads<CV>(), 0, s>>>(
+                grad, xx, fcoef, mask, coef, o, r, nvec, DR ? reinterpret_cast<const uint4 *>(dres_x) : nullptr,
+                DR ? dres_sums : nullptr);
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -892,10 +939,10 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
 void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                        uint16_t *dres, hipStream_t s, double *sums) {
+                        uint16_t *dres, hipStream_t s, double *sums, const uint16_t *dres_x, double *dres_sums) {
     const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
     launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy)}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
-                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums);
+                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums);
 }
 
 bool bn_pool_supported(BNShape sh, int H, int W) {

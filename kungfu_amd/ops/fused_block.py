@@ -225,8 +225,11 @@ class _BottleneckFn(torch.autograd.Function):
         # gradient): the residual gradient dout * relu' is never written -- conv1's data
         # gradient below accumulates into dout in place, masking it on the fly
         in_place = use3 and not spec.ds
+        # downsample block: the residual gradient also feeds the downsample BN, whose backward
+        # sums are accumulated by this same pass (that BN then skips its reduce)
         dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, not in_place,
-                                            ws[2] if use3 else None)
+                                            ws[2] if use3 else None, dres_x=yd if spec.ds else None,
+                                            dres_sums=ws[3] if spec.ds else None)
         dbn[2] = (dg3, db3)
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None))
         dw[2] = _wgrad(dy3, z2, w[2], 1, 0)
@@ -239,7 +242,7 @@ class _BottleneckFn(torch.autograd.Function):
                                          ws[0] if fused1 else None)
         dbn[0] = (dg1, db1)
         if spec.ds:
-            dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False)
+            dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False, ws[3])
             dbn[3] = (dgd, dbd)
             dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
             dw[3] = _wgrad(dyd, x, w[3], s, 0)
