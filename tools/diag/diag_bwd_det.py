@@ -6,7 +6,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import kungfu_amd as kf  # noqa: E402
 from kungfu_amd.models import resnet18  # noqa: E402
 from kungfu_amd.ops import conv as conv_ops  # noqa: E402
