@@ -288,7 +288,7 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
                 c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
-                c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask) {
+                c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask, bool acc_even) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -375,10 +375,70 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
         ea.amask = acc_mask->data_ptr<uint8_t>();
         epi |= kfk::kEpiAccMask;
     }
+    if (acc_even) {
+        // out holds a stride-2 1x1 data gradient at its even pixels only (conv_dgrad_s2)
+        TORCH_CHECK(accum && stride == 1 && !(epi & (kfk::kEpiAccMask | kfk::kEpiBwdCoef)),
+                    "conv: acc_even needs out, stride 1 and no acc_mask / bn_fcoef");
+        epi |= kfk::kEpiAccEven;
+    }
     kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
                      reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), ea, epi,
                      stream_of(x, 0), static_cast<int>(variant));
     return y;
+}
+
+// Data gradient of a stride-2 1x1 (pad 0) / 3x3 (pad 1) convolution with an even input:
+// dy [N, Cout, OH, OW] -> dx [N, Cin, 2OH, 2OW] (channels_last bf16), wt = conv_flip_weight(w)
+// [Cin, Cout, ks, ks].  ks = 3: every pixel written (four parity-phase GEMMs); bn_x + stats
+// (+ bn_fcoef or bn_mask) also accumulate the backward sums of the BN whose input is bn_x, as
+// conv().  ks = 1: only the even pixels are written -- complete dx with a stride-1 data
+// gradient conv(..., out=dx, acc_even=True).
+at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional<at::Tensor> stats,
+                         c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_fcoef,
+                         c10::optional<at::Tensor> bn_mask) {
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                    dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_dgrad_s2: dy must be a 4-D channels_last bf16 GPU tensor");
+    TORCH_CHECK(ks == 1 || ks == 3, "conv_dgrad_s2: ks must be 1 or 3");
+    TORCH_CHECK(wt.scalar_type() == at::kBFloat16 && wt.dim() == 4 && wt.size(2) == ks && wt.size(3) == ks &&
+                    wt.size(1) == dy.size(1) && wt.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    wt.device() == dy.device(),
+                "conv_dgrad_s2: wt must be the flipped [Cin, Cout, ks, ks] channels_last bf16 weight");
+    const int N = dy.size(0), K = dy.size(1), OH = dy.size(2), OW = dy.size(3), C = wt.size(0);
+    TORCH_CHECK(kfk::conv_supported(K, C, static_cast<int>(ks), 1), "conv_dgrad_s2: unsupported channels");
+    TORCH_CHECK(static_cast<int64_t>(N) * 4 * OH * OW * C < (int64_t(1) << 31), "conv_dgrad_s2: tensor too large");
+    c10::DeviceGuard gd(dy.device());
+    auto dx = at::empty({N, C, 2 * OH, 2 * OW}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::EpiArgs ea;
+    int epi = 0;
+    if (bn_x && bn_x->defined()) {
+        TORCH_CHECK(ks == 3, "conv_dgrad_s2: BN sums need every pixel (ks = 3)");
+        TORCH_CHECK(stats && stats->defined() && stats->scalar_type() == at::kDouble &&
+                        stats->numel() == 2 * C * kfk::kStatSlots && stats->is_contiguous() &&
+                        stats->device() == dy.device(),
+                    "conv_dgrad_s2: BN-backward sums need the f64 stats workspace");
+        TORCH_CHECK(bn_x->scalar_type() == at::kBFloat16 && bn_x->sizes() == dx.sizes() &&
+                        bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) && bn_x->device() == dy.device(),
+                    "conv_dgrad_s2: bn_x must be the BN input (bf16 channels_last, dx's shape)");
+        ea.stats = stats->data_ptr<double>();
+        ea.bx = reinterpret_cast<const uint16_t *>(bn_x->data_ptr());
+        if (bn_mask && bn_mask->defined()) {
+            TORCH_CHECK(bn_mask->scalar_type() == at::kByte && bn_mask->numel() == dx.numel() / 8,
+                        "conv_dgrad_s2: bn_mask must hold one byte per 8 elements");
+            ea.bmask = bn_mask->data_ptr<uint8_t>();
+            epi = kfk::kEpiBwdBits;
+        } else {
+            TORCH_CHECK(bn_fcoef && bn_fcoef->defined() && bn_fcoef->scalar_type() == at::kFloat &&
+                            bn_fcoef->numel() >= 2 * C && bn_fcoef->device() == dy.device(),
+                        "conv_dgrad_s2: bn_fcoef (forward [scale; shift], f32) or bn_mask required");
+            ea.fcoef = bn_fcoef->data_ptr<float>();
+            epi = kfk::kEpiBwdCoef;
+        }
+    }
+    kfk::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                              reinterpret_cast<const uint16_t *>(wt.data_ptr()), reinterpret_cast<uint16_t *>(dx.data_ptr()),
+                              N, OH, OW, K, C, static_cast<int>(ks), ea, epi, stream_of(dy, 0));
+    return dx;
 }
 
 // Weight gradient of conv(x, w, stride, pad (ks-1)/2): dw [Cout, Cin, ks, ks] channels_last
@@ -1199,7 +1259,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
-          py::arg("gate") = false, py::arg("acc_mask") = py::none());
+          py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false);
+    m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
+          "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
+          py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none());
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);

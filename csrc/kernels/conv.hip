@@ -57,6 +57,11 @@ struct Geo {
     int M;       // N*OH*OW
     int mtiles;  // ceil(M / BM)
     int ntiles;  // K / BN
+    // strided data gradient as parity phases (launch_conv_dgrad_s2):
+    int wtaps;   // taps per weight row (B row stride = wtaps * C)
+    int tapmap;  // -1: tap t reads weight tap t; else weight tap of tap t = nibble t
+    int scat;    // 1: output row m -> pixel (2*(m/OW) + pr, 2*(m%OW) + pc) of a 2OH x 2OW image
+    int pr, pc;
 };
 
 template <int N>
@@ -65,7 +70,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
-// KS = 3 (pad 1) or 1 (pad 0).  EPI flags (kernels.hpp ConvEpi):
+// KS = 3 (pad 1) or 1 (pad 0); KS = 0xHW (>= 16): an H x W window with no padding (taps read
+// rows oh..oh+H-1, out-of-range rows are zero) -- the parity phases of a stride-2 3x3 data
+// gradient (launch_conv_dgrad_s2).  EPI flags (kernels.hpp ConvEpi):
 //   kEpiAccum     y += conv (accumulate into the existing bf16 tensor, a residual gradient);
 //   kEpiFwdStats  per-channel sum / sum-of-squares of the bf16 outputs (the following BN's
 //                 batch statistics) -> f64 atomics into ea.stats[slot][2][K];
@@ -85,7 +92,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     // wave tile (16*TM) x (16*TN): TM x TN accumulators of one 16x16x32 MFMA each
     constexpr int WTM = 16 * TM, WTN = 16 * TN;
     constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
-    constexpr int TAPS = KS * KS, PAD = (KS - 1) / 2;
+    constexpr int KH = KS >= 16 ? (KS >> 4) : KS, KW = KS >= 16 ? (KS & 15) : KS;
+    constexpr int TAPS = KH * KW, PAD = KS >= 16 ? 0 : (KS - 1) / 2;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
     constexpr int STAGE = A_BYTES + B_BYTES;
     constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
@@ -152,12 +160,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
             uint32_t ok = 0;
 #pragma unroll
-            for (int kh = 0; kh < KS; ++kh)
+            for (int kh = 0; kh < KH; ++kh)
 #pragma unroll
-                for (int kw = 0; kw < KS; ++kw)
+                for (int kw = 0; kw < KW; ++kw)
                     if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
                         static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
-                        ok |= 1u << (kh * KS + kw);
+                        ok |= 1u << (kh * KW + kw);
             a_ok[j] = ok;
         }
     }
@@ -165,15 +173,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll
     for (int j = 0; j < B_INST; ++j) {
         const int r = (wave * B_INST + j) * 8 + srow;
-        b_off[j] = (n0 + r) * TAPS * g.C + schunk * 8;
+        b_off[j] = (n0 + r) * g.wtaps * g.C + schunk * 8;
     }
     const int csteps = g.C / kBK;
     const int ksteps = TAPS * csteps;
 
     auto stage = [&](int ks, int buf) {
         const int tap = ks / csteps, cc = ks - tap * csteps;
-        const int kh = tap / KS, kw = tap - kh * KS;
+        const int kh = tap / KW, kw = tap - kh * KW;
         const int toff = (kh * g.W + kw) * g.C + cc * kBK;  // wave-uniform
+        const int wtap = g.tapmap < 0 ? tap : (g.tapmap >> (4 * tap)) & 15;
         uint8_t *abase = lds + buf * STAGE;
         uint8_t *bbase = abase + A_BYTES;
 #pragma unroll
@@ -184,7 +193,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
-            const uint16_t *src = w + static_cast<uint32_t>(b_off[j] + tap * g.C + cc * kBK);
+            const uint16_t *src = w + static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK);
             __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
         }
     };
@@ -287,11 +296,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         const int row = v / VPR;
         const int m = m0 + row;
         if (m < g.M) {
-            const int64_t e = static_cast<int64_t>(m) * g.K + n0 + cv * 8;
+            int pix = m;
+            if (g.scat) {
+                const int t = m / g.OW, ow = m - t * g.OW;
+                pix = (2 * t + g.pr) * (2 * g.OW) + 2 * ow + g.pc;
+            }
+            const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
             uint4 *dst = reinterpret_cast<uint4 *>(y + e);
             uint4 val = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
             if constexpr ((EPI & kEpiAccum) != 0) {
-                uint4 old = *dst;
+                bool here = true;
+                if constexpr ((EPI & kEpiAccEven) != 0) {
+                    // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
+                    const int t = m / g.OW, ow = m - t * g.OW;
+                    here = ((ow | (t % g.OH)) & 1) == 0;
+                }
+                uint4 old = here ? *dst : make_uint4(0u, 0u, 0u, 0u);
                 if constexpr ((EPI & kEpiAccMask) != 0) {
                     const uint32_t mb = ea.amask[e >> 3];  // 8 channels from an 8-aligned e
                     uint32_t *ow = reinterpret_cast<uint32_t *>(&old);
@@ -520,6 +540,8 @@ void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
         case A | C: launch_epi<KS, WM, WN, ST, A | C, TM, TN>(x, w, y, g, ea, s); break;
         case A | M: launch_epi<KS, WM, WN, ST, A | M, TM, TN>(x, w, y, g, ea, s); break;
         case A | M | B: launch_epi<KS, WM, WN, ST, A | M | B, TM, TN>(x, w, y, g, ea, s); break;
+        case A | kEpiAccEven: launch_epi<KS, WM, WN, ST, A | kEpiAccEven, TM, TN>(x, w, y, g, ea, s); break;
+        case A | kEpiAccEven | B: launch_epi<KS, WM, WN, ST, A | kEpiAccEven | B, TM, TN>(x, w, y, g, ea, s); break;
         case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu, TM, TN>(x, w, y, g, ea, s); break;
         case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate, TM, TN>(x, w, y, g, ea, s); break;
         default: throw std::invalid_argument("conv: unsupported epilogue combination");
@@ -573,8 +595,59 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.OW = (W + 2 * pad - ks) / stride + 1;
     g.M = N * g.OH * g.OW;
     g.mtiles = g.ntiles = 0;
+    g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
     if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
+}
+
+// One parity phase of a stride-2 data gradient: the fused epilogues it needs (none, or the BN
+// backward sums of the BN that produced the forward input), 256x128 tiles when Cin % 128 == 0.
+template <int KS>
+void launch_phase(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, const EpiArgs &ea, int epi,
+                  hipStream_t s) {
+    constexpr int C = kEpiBwdCoef, B = kEpiBwdBits;
+    if (epi != 0 && epi != C && epi != B) throw std::invalid_argument("conv_dgrad_s2: unsupported epilogue");
+    if (g.K % 128 == 0) {
+        if (epi == 0) launch_epi<KS, 4, 2, 3, 0>(dy, wt, dx, g, ea, s);
+        else if (epi == C) launch_epi<KS, 4, 2, 3, C>(dy, wt, dx, g, ea, s);
+        else launch_epi<KS, 4, 2, 3, B>(dy, wt, dx, g, ea, s);
+    } else {
+        if (epi == 0) launch_epi<KS, 4, 1, 2, 0>(dy, wt, dx, g, ea, s);
+        else if (epi == C) launch_epi<KS, 4, 1, 2, C>(dy, wt, dx, g, ea, s);
+        else launch_epi<KS, 4, 1, 2, B>(dy, wt, dx, g, ea, s);
+    }
+}
+
+void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s) {
+    // dx pixel (2a + pr, 2b + pc) only sees forward taps kh = 1 (pr = 0) or kh = 2 at dy row a and
+    // kh = 0 at dy row a + 1 (pr = 1); same for columns.  Flipped-weight tap index = 2 - kh.
+    Geo g;
+    g.N = N, g.H = OH, g.W = OW, g.C = Cout, g.K = Cin, g.stride = 1;
+    g.OH = OH, g.OW = OW, g.M = N * OH * OW;
+    g.mtiles = g.ntiles = 0;
+    g.wtaps = ks * ks, g.scat = 1;
+    if (ks == 1) {
+        g.tapmap = -1, g.pr = g.pc = 0;
+        launch_phase<1>(dy, wt, dx, g, ea, epi, s);
+        return;
+    }
+    if (ks != 3) throw std::invalid_argument("conv_dgrad_s2: ks must be 1 or 3");
+    for (int pr = 0; pr < 2; ++pr)
+        for (int pc = 0; pc < 2; ++pc) {
+            const int nh = pr ? 2 : 1, nw = pc ? 2 : 1;
+            int map = 0;
+            for (int th = 0; th < nh; ++th)
+                for (int tw = 0; tw < nw; ++tw) {
+                    const int rh = pr ? (th == 0 ? 0 : 2) : 1, rw = pc ? (tw == 0 ? 0 : 2) : 1;
+                    map |= (rh * 3 + rw) << (4 * (th * nw + tw));
+                }
+            g.tapmap = map, g.pr = pr, g.pc = pc;
+            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, ea, epi, s);
+            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, ea, epi, s);
+            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, ea, epi, s);
+            else launch_phase<0x22>(dy, wt, dx, g, ea, epi, s);
+        }
 }
 
 void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,

@@ -106,7 +106,7 @@ bool conv_supported(int Cin, int Cout, int ks, int stride);
 // backward need not write dz (ResNet identity blocks).
 enum ConvEpi : int {
     kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
-    kEpiAccMask = 64
+    kEpiAccMask = 64, kEpiAccEven = 128
 };
 struct EpiArgs {
     const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
@@ -118,6 +118,16 @@ struct EpiArgs {
 };
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
                  int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);
+// kEpiAccEven (with kEpiAccum): accumulate only at pixels with even (h, w) -- the only ones a
+// stride-2 1x1 data gradient wrote (launch_conv_dgrad_s2) -- and plain-store the others.
+// Data gradient of a stride-2 KS x KS (KS = 1 pad 0 | 3 pad 1) convolution with an even input
+// (H = 2*OH, W = 2*OW): dy [N, OH, OW, Cout] -> dx [N, 2OH, 2OW, Cin], wt = the flipped weight
+// [Cin][KS*KS][Cout] (conv_flip_weight).  KS = 3: four parity-phase implicit GEMMs (1, 2, 2 and
+// 4 taps) write every dx pixel once (epi: 0 or kEpiBwdCoef/kEpiBwdBits -- BN backward sums
+// over dx, as launch_conv).  KS = 1: only the even pixels are written (the rest is left for a
+// kEpiAccEven stride-1 data gradient into the same dx).
+void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s);
 // Multi-tensor flip (one launch for a whole model's conv weights).
 struct FlipTable {
     static constexpr int kMax = 64;

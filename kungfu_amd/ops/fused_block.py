@@ -17,7 +17,10 @@ forward (training)
 backward
 * stride-1 data gradients are the same MFMA kernel on transposed/flipped weights, whose
   epilogue also accumulates the backward sums (sum dz, sum dz*x under the ReLU gate) of the
-  BN that produced the conv input -> that BN's backward skips its reduction pass; across
+  BN that produced the conv input -> that BN's backward skips its reduction pass; stride-2
+  data gradients (conv2 3x3 and the downsample 1x1 of layers 2-4) are parity-phase GEMMs on
+  the same kernel (``conv_dgrad_s2``: each output pixel parity sees 1, 2 or 4 taps; the 1x1's
+  even-pixel gradient is completed by conv1's data gradient, no zero fill); across
   blocks, the next block's conv1 data gradient does this for the previous block's BN3
   (``_TailSlot``);
 * the block-input gradient is formed IN PLACE: conv1's data-gradient kernel
@@ -106,22 +109,40 @@ def _flip_cache(space) -> _FlipCache:
 
 
 def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: Optional[torch.Tensor] = None,
-           bn=None, out_mask: Optional[torch.Tensor] = None):
-    """Data gradient; MFMA kernel for stride 1 (accumulating into ``out`` if given).
+           bn=None, out_mask: Optional[torch.Tensor] = None, acc_even: bool = False):
+    """Data gradient on the MFMA kernels (accumulating into ``out`` if given).
 
     ``bn = (ws, bn_x, fcoef, mask)``: the result is the gradient of a BN(+ReLU) output whose
     input is ``bn_x``; the kernel epilogue also accumulates that BN's backward sums into
-    ``ws`` (only on the MFMA path -- returns whether it did via ``_dgrad.fused``).
-    ``out_mask`` (stride 1, with ``out``): accumulate into ``out * out_mask`` (1-bit ReLU mask)."""
+    ``ws`` (returns whether it did via ``_dgrad.fused``).
+    ``out_mask`` (stride 1, with ``out``): accumulate into ``out * out_mask`` (1-bit ReLU mask).
+    ``acc_even`` (stride 1, with ``out``): ``out`` holds a stride-2 1x1 data gradient at its even
+    pixels only (``_dgrad_s2``); the other pixels are plainly stored.
+    Stride 2 with an even input: parity-phase GEMMs (``conv_dgrad_s2``); odd inputs fall back
+    to the library kernel."""
     H = hip()
+    wt = flipped if flipped is not None else None
     if stride == 1:
-        wt = flipped if flipped is not None else H.conv_flip_weight(w)
+        wt = wt if wt is not None else H.conv_flip_weight(w)
+        _dgrad.fused = bn is not None
         if bn is not None:
             ws, bx, fc, mk = bn
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even)
+        return H.conv(dy, wt, 1, None, out, acc_mask=out_mask, acc_even=acc_even)
+    assert out_mask is None and not acc_even
+    ks = w.shape[2]
+    if stride == 2 and out is None and _even_s2(x, dy, ks):
+        wt = wt if wt is not None else H.conv_flip_weight(w)
+        if ks == 3 and bn is not None:
+            ws, bx, fc, mk = bn
             _dgrad.fused = True
-            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask)
-        return H.conv(dy, wt, 1, None, out, acc_mask=out_mask)
-    assert out_mask is None
+            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk)
+        _dgrad.fused = False
+        dx = H.conv_dgrad_s2(dy, wt, ks)
+        if ks == 1:  # odd pixels get no gradient from a 1x1 stride-2 conv
+            dx.view(dx.shape[0], dx.shape[1], dx.shape[2] // 2, 2, dx.shape[3] // 2, 2)[:, :, :, 1:, :, :].zero_()
+            dx.view(dx.shape[0], dx.shape[1], dx.shape[2] // 2, 2, dx.shape[3] // 2, 2)[:, :, :, 0, :, 1:].zero_()
+        return dx
     _dgrad.fused = False
     dx = torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                              [True, False, False])[0]
@@ -129,6 +150,20 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
         out.add_(dx)
         return out
     return _cl(dx)
+
+
+def _even_s2(x, dy, ks) -> bool:
+    """Stride-2 data gradient on the parity-phase kernels: the input is exactly twice the output."""
+    return (x.shape[2] == 2 * dy.shape[2] and x.shape[3] == 2 * dy.shape[3] and ks in (1, 3)
+            and hip().conv_supported(dy.shape[1], x.shape[1], ks, 1))
+
+
+def _dgrad_s2_even(dy, x, w, flipped=None):
+    """Stride-2 1x1 data gradient written at the even pixels only (the caller completes the
+    tensor with a stride-1 data gradient ``_dgrad(..., out=dx, acc_even=True)``)."""
+    H = hip()
+    wt = flipped if flipped is not None else H.conv_flip_weight(w)
+    return H.conv_dgrad_s2(dy, wt, 1)
 
 
 class _TailSlot:
@@ -211,7 +246,7 @@ class _BottleneckFn(torch.autograd.Function):
         fl = [None] * nb
         if spec.wsrc is not None:
             for k, src in enumerate(spec.wsrc):
-                if src is not None and (k != 1 or s == 1) and (k != 3 or s == 1):
+                if src is not None:
                     fl[k] = src[0].get(src[1])
         dbn = [None] * nb  # (dgamma, dbeta)
         dw = [None] * nb
@@ -241,10 +276,16 @@ class _BottleneckFn(torch.autograd.Function):
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
                                          ws[0] if fused1 else None)
         dbn[0] = (dg1, db1)
+        acc_even = False
         if spec.ds:
             dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False, ws[3])
             dbn[3] = (dgd, dbd)
-            dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
+            if s == 2 and _even_s2(x, dyd, 1):
+                # even pixels only; conv1's data gradient below stores the odd ones
+                dx = _dgrad_s2_even(dyd, x, w[3], flipped=fl[3])
+                acc_even = True
+            else:
+                dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
             dw[3] = _wgrad(dyd, x, w[3], s, 0)
         elif in_place:
             dx = dout  # raw output gradient; masked by mask3 inside conv1's data-gradient epilogue
@@ -256,10 +297,10 @@ class _BottleneckFn(torch.autograd.Function):
             # conv1's data gradient completes the gradient of the previous block's output:
             # its epilogue also accumulates that block's BN3 backward sums
             dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask),
-                        out_mask=om)
+                        out_mask=om, acc_even=acc_even)
             prev.ready, prev.dx_ptr = True, dx.data_ptr()
         else:
-            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], out_mask=om)
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], out_mask=om, acc_even=acc_even)
         dw[0] = _wgrad(dy1, x, w[0], 1, 0)
         grads: List[Optional[torch.Tensor]] = []
         for i in range(nb):

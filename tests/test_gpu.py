@@ -514,7 +514,7 @@ def test_resnet_ssgd_bf16_shadow_matches_autocast():
         return ((a.double() - b.double()).norm() / b.double().norm()).item()
 
     # MIOpen's split-K kernels are not deterministic and ResNet-18 at batch 8 amplifies it: two
-    # stock runs measured 0.6 %-9 % apart (tools/diag_bwd_det.py, also on the pre-r12 build)
+    # stock runs measured 0.6 %-9 % apart (tools/diag/diag_bwd_det.py, also on the pre-r12 build)
     noise = fro(g_b, g_a)
     assert fro(g_s, g_a) < max(3 * noise, 0.12), (noise, fro(g_s, g_a))
     # later steps memorise the 8-image batch: same trajectory shape, loose values
@@ -733,7 +733,7 @@ def test_inception_fused_bn_matches_torch_bn():
     """Inception-v3 with the HIP BN+ReLU (the channel counts it supports) against the stock
     BatchNorm2d+ReLU model with the same weights, layer by layer on the same inputs (bf16
     autocast, training mode): end-to-end outputs of a random-init 47-layer net amplify bf16
-    rounding differences chaotically (tools/diag_inception_bn.py: 4e-3 per layer, 0.5 at the
+    rounding differences chaotically (tools/diag/diag_inception_bn.py: 4e-3 per layer, 0.5 at the
     logits), so the per-layer error is what is pinned.  Plus one layer's backward."""
     from kungfu_amd.models import get_model
     from kungfu_amd.models.inception import BasicConv2d
@@ -943,7 +943,7 @@ def test_avgpool3x3s1_matches_torch(shape):
     x = torch.randn(*shape, device="cuda").bfloat16().to(memory_format=torch.channels_last)
     dy = torch.randn(*shape, device="cuda").bfloat16().to(memory_format=torch.channels_last)
     # reference in float64 on the CPU (NCHW): on this ROCm build the GPU NHWC avg_pool2d
-    # BACKWARD returns the gradient shifted by the padding (tools/dbg_avgpool.py: its dx(0,0)
+    # BACKWARD returns the gradient shifted by the padding (tools/diag/dbg_avgpool.py: its dx(0,0)
     # equals the true dx(1,1)), so torch-on-GPU cannot be the reference for the gradient
     xr = x.double().cpu().contiguous().requires_grad_(True)
     yr = F.avg_pool2d(xr, 3, 1, 1)
@@ -983,6 +983,55 @@ def H_slots():
     from kungfu_amd._lib import hip
 
     return hip().conv_stat_slots
+
+
+@needs_gpu
+@pytest.mark.parametrize("N,OH,K,C", [(4, 7, 128, 64), (8, 14, 256, 128), (2, 28, 512, 256), (16, 4, 64, 192)])
+def test_conv_dgrad_s2_matches_torch(N, OH, K, C):
+    """Stride-2 data gradients on the parity-phase MFMA kernels vs the float32 torch data
+    gradient: 3x3/pad 1 (four phases, every pixel; with the BN-backward sums epilogue vs
+    float64 sums of the gated gradient) and 1x1 (even pixels) completed by a stride-1 1x1 data
+    gradient accumulated with acc_even (the ResNet downsample block's block-input gradient)."""
+    import torch.nn.functional as F
+
+    from kungfu_amd._lib import hip
+
+    H = hip()
+    torch.manual_seed(21)
+    dy = torch.randn(N, K, OH, OH, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, C, 2 * OH, 2 * OH, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    for ks in (3, 1):
+        w = (torch.randn(K, C, ks, ks, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+        ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [2, 2], [(ks - 1) // 2] * 2,
+                                                  [1, 1], False, [0, 0], 1, [True, False, False])[0]
+        wt = H.conv_flip_weight(w)
+        if ks == 3:
+            dx = H.conv_dgrad_s2(dy, wt, 3)
+            assert _rel(dx, ref) < 1e-2, ks
+            # BN backward sums of a BN+ReLU whose input is bx, forward coefficients fc
+            bx = torch.randn_like(x)
+            fc = torch.cat([torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2])
+            st = torch.zeros(H_slots() * 2 * C, dtype=torch.float64, device="cuda")
+            dx2 = H.conv_dgrad_s2(dy, wt, 3, st, bx, fc)
+            assert torch.equal(dx2, dx)
+            xd = bx.double().permute(0, 2, 3, 1).reshape(-1, C)
+            gd = dx.double().permute(0, 2, 3, 1).reshape(-1, C)
+            on = (bx.float().permute(0, 2, 3, 1).reshape(-1, C) * fc[:C] + fc[C:]) > 0
+            dz = torch.where(on, gd, torch.zeros_like(gd))
+            sums = st.view(-1, 2, C).sum(0)
+            torch.testing.assert_close(sums[0], dz.sum(0), rtol=1e-5, atol=1e-2)
+            torch.testing.assert_close(sums[1], (dz * xd).sum(0), rtol=1e-5, atol=1e-2)
+        else:
+            dx = H.conv_dgrad_s2(dy, wt, 1)
+            ev = dx[:, :, 0::2, 0::2]
+            assert _rel(ev, ref[:, :, 0::2, 0::2]) < 1e-2
+            # complete it: + the stride-1 1x1 data gradient of a second conv over all pixels
+            dy1 = torch.randn(N, K, 2 * OH, 2 * OH, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+            w1 = (torch.randn(K, C, 1, 1, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+            ref1 = F.conv_transpose2d(dy1.float(), w1.float())
+            out = H.conv(dy1, H.conv_flip_weight(w1), 1, None, dx, acc_even=True)
+            assert out.data_ptr() == dx.data_ptr()
+            assert _rel(out, ref + ref1) < 1e-2
 
 
 @needs_gpu
