@@ -395,7 +395,7 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
 // gradient conv(..., out=dx, acc_even=True).
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional<at::Tensor> stats,
                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_fcoef,
-                         c10::optional<at::Tensor> bn_mask) {
+                         c10::optional<at::Tensor> bn_mask, int64_t variant) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_dgrad_s2: dy must be a 4-D channels_last bf16 GPU tensor");
@@ -437,7 +437,8 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
     }
     kfk::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                               reinterpret_cast<const uint16_t *>(wt.data_ptr()), reinterpret_cast<uint16_t *>(dx.data_ptr()),
-                              N, OH, OW, K, C, static_cast<int>(ks), ea, epi, stream_of(dy, 0));
+                              N, OH, OW, K, C, static_cast<int>(ks), ea, epi, stream_of(dy, 0),
+                              static_cast<int>(variant));
     return dx;
 }
 
@@ -635,6 +636,33 @@ at::Tensor maxpool3s2_backward(at::Tensor dy, at::Tensor arg, int64_t H, int64_t
                                     reinterpret_cast<uint16_t *>(dx.data_ptr()), dy.size(0), static_cast<int>(H),
                                     static_cast<int>(W), static_cast<int>(dy.size(1)), static_cast<int>(pad),
                                     stream_of(dy, 0));
+    return dx;
+}
+
+// Global average pool of a channels_last bf16 [N, C, H, W] -> [N, C] bf16 (and its backward).
+at::Tensor global_avgpool_forward(at::Tensor x) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) % 8 == 0 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "global_avgpool: x must be a channels_last bf16 [N, C, H, W] GPU tensor with C % 8 == 0");
+    c10::DeviceGuard gd(x.device());
+    auto y = at::empty({x.size(0), x.size(1)}, x.options());
+    kfk::launch_global_avgpool_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()),
+                                       reinterpret_cast<uint16_t *>(y.data_ptr()), x.size(0),
+                                       static_cast<int>(x.size(2) * x.size(3)), static_cast<int>(x.size(1)),
+                                       stream_of(x, 0));
+    return y;
+}
+
+at::Tensor global_avgpool_backward(at::Tensor dy, int64_t H, int64_t W) {
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.size(1) % 8 == 0 &&
+                    H > 0 && W > 0,
+                "global_avgpool_backward: dy must be a bf16 [N, C] GPU tensor with C % 8 == 0");
+    dy = dy.contiguous();
+    c10::DeviceGuard gd(dy.device());
+    auto dx = at::empty({dy.size(0), dy.size(1), H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_global_avgpool_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                        reinterpret_cast<uint16_t *>(dx.data_ptr()), dy.size(0), static_cast<int>(H * W),
+                                        static_cast<int>(dy.size(1)), stream_of(dy, 0));
     return dx;
 }
 
@@ -1262,7 +1290,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false);
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
-          py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none());
+          py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
+          py::arg("variant") = -1);
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
@@ -1278,6 +1307,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("layernorm_forward", &layernorm_forward, "fused residual-add + LayerNorm (bf16 rows) -> (y, s, mean, rstd)",
           py::arg("x"), py::arg("r"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
     m.def("layernorm_backward", &layernorm_backward, "LayerNorm backward -> (ds, dgamma, dbeta)");
+    m.def("global_avgpool_forward", &global_avgpool_forward, "global average pool, NHWC bf16 -> [N, C]");
+    m.def("global_avgpool_backward", &global_avgpool_backward, "global average pool backward -> NHWC bf16",
+          py::arg("dy"), py::arg("H"), py::arg("W"));
     m.def("avgpool3s1", &avgpool3s1, "3x3/s1/p1 average pool, count_include_pad (also its own gradient on dy)");
     m.def("bias_act_forward_", &bias_act_forward_, "y = relu(y + bias) in place (NHWC bf16, f32 bias)",
           py::arg("y"), py::arg("bias"), py::arg("relu") = true);

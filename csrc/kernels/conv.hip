@@ -602,24 +602,48 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
 
 // One parity phase of a stride-2 data gradient: the fused epilogues it needs (none, or the BN
 // backward sums of the BN that produced the forward input), 256x128 tiles when Cin % 128 == 0.
+template <int KS, int WM, int WN, int ST, int TM = 4, int TN = 4>
+void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, const EpiArgs &ea, int epi,
+                    hipStream_t s) {
+    constexpr int C = kEpiBwdCoef, B = kEpiBwdBits;
+    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
+    if (g.K % BN) throw std::invalid_argument("conv_dgrad_s2: Cin not a multiple of the tile");
+    g.mtiles = (g.M + BM - 1) / BM;
+    g.ntiles = g.K / BN;
+    const int grid = g.mtiles * g.ntiles;
+    const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
+    if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
+    else if (epi == C) conv_kernel<KS, WM, WN, ST, C, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
+    else if (epi == B) conv_kernel<KS, WM, WN, ST, B, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
+    else throw std::invalid_argument("conv_dgrad_s2: unsupported epilogue");
+}
+
+// Tile for the short-K phase GEMMs (variant >= 0 to override; tools/bench_dgrad_s2.py): 128x128
+// / 4 waves for the large-M 3x3 phases (>= 1024 such tiles: two blocks per CU overlap one
+// block's prologue/epilogue with the other's MFMAs), else 256x128 / 8 waves; 256x64 when
+// Cin % 128 != 0.  (One grid holding all four phases, per-block tap count, measured 5-50 %
+// slower than four launches.)
 template <int KS>
 void launch_phase(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, const EpiArgs &ea, int epi,
-                  hipStream_t s) {
-    constexpr int C = kEpiBwdCoef, B = kEpiBwdBits;
-    if (epi != 0 && epi != C && epi != B) throw std::invalid_argument("conv_dgrad_s2: unsupported epilogue");
-    if (g.K % 128 == 0) {
-        if (epi == 0) launch_epi<KS, 4, 2, 3, 0>(dy, wt, dx, g, ea, s);
-        else if (epi == C) launch_epi<KS, 4, 2, 3, C>(dy, wt, dx, g, ea, s);
-        else launch_epi<KS, 4, 2, 3, B>(dy, wt, dx, g, ea, s);
-    } else {
-        if (epi == 0) launch_epi<KS, 4, 1, 2, 0>(dy, wt, dx, g, ea, s);
-        else if (epi == C) launch_epi<KS, 4, 1, 2, C>(dy, wt, dx, g, ea, s);
-        else launch_epi<KS, 4, 1, 2, B>(dy, wt, dx, g, ea, s);
+                  hipStream_t s, int v) {
+    if (v < 0) {
+        const int64_t t128 = ((static_cast<int64_t>(g.M) + 127) / 128) * (g.K / 128);
+        v = g.K % 128 ? 2 : (KS != 1 && t128 >= 1024) ? 0 : 1;
+    }
+    switch (v) {
+    case 0: if (g.K % 128 == 0) { launch_phase_t<KS, 2, 2, 2>(dy, wt, dx, g, ea, epi, s); break; }  // 128x128
+            [[fallthrough]];
+    case 5: launch_phase_t<KS, 2, 1, 2>(dy, wt, dx, g, ea, epi, s); break;                           // 128x64
+    case 1: if (g.K % 128 == 0) { launch_phase_t<KS, 4, 2, 3>(dy, wt, dx, g, ea, epi, s); break; }  // 256x128
+            [[fallthrough]];
+    default: launch_phase_t<KS, 4, 1, 2>(dy, wt, dx, g, ea, epi, s); break;                         // 256x64
     }
 }
 
 void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
-                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s) {
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant) {
+    // variant: -1 = default; else the tile variant (0 128x128, 1 256x128, 2 256x64, 5 128x64)
+    const int tv = variant;
     // dx pixel (2a + pr, 2b + pc) only sees forward taps kh = 1 (pr = 0) or kh = 2 at dy row a and
     // kh = 0 at dy row a + 1 (pr = 1); same for columns.  Flipped-weight tap index = 2 - kh.
     Geo g;
@@ -629,7 +653,7 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     g.wtaps = ks * ks, g.scat = 1;
     if (ks == 1) {
         g.tapmap = -1, g.pr = g.pc = 0;
-        launch_phase<1>(dy, wt, dx, g, ea, epi, s);
+        launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
         return;
     }
     if (ks != 3) throw std::invalid_argument("conv_dgrad_s2: ks must be 1 or 3");
@@ -643,10 +667,10 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
                     map |= (rh * 3 + rw) << (4 * (th * nw + tw));
                 }
             g.tapmap = map, g.pr = pr, g.pc = pc;
-            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, ea, epi, s);
-            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, ea, epi, s);
-            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, ea, epi, s);
-            else launch_phase<0x22>(dy, wt, dx, g, ea, epi, s);
+            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
+            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, ea, epi, s, tv);
+            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, ea, epi, s, tv);
+            else launch_phase<0x22>(dy, wt, dx, g, ea, epi, s, tv);
         }
 }
 

@@ -127,7 +127,7 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
 // over dx, as launch_conv).  KS = 1: only the even pixels are written (the rest is left for a
 // kEpiAccEven stride-1 data gradient into the same dx).
 void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
-                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s);
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);
 // Multi-tensor flip (one launch for a whole model's conv weights).
 struct FlipTable {
     static constexpr int kMax = 64;
@@ -253,6 +253,10 @@ void launch_maxpool3s2_forward(const uint16_t *x, uint16_t *y, uint8_t *arg, int
 void launch_maxpool3s2_backward(const uint16_t *dy, const uint8_t *arg, uint16_t *dx, int64_t N, int H, int W, int C,
                                 int pad, hipStream_t s);
 void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, int C, hipStream_t s);
+// Global average pool over the H*W pixels of an NHWC bf16 tensor (C % 8 == 0): y [N, C];
+// backward dx[n, p, c] = dy[n, c] / HW.
+void launch_global_avgpool_forward(const uint16_t *x, uint16_t *y, int64_t N, int HW, int C, hipStream_t s);
+void launch_global_avgpool_backward(const uint16_t *dy, uint16_t *dx, int64_t N, int HW, int C, hipStream_t s);
 
 // Fused residual-add + LayerNorm over rows of D (layernorm.hip): bf16 x, r (optional), y, s
 // (= x + r, saved for backward), f32 gamma/beta/mean/rstd; backward -> ds (bf16) and

@@ -272,6 +272,60 @@ __global__ __launch_bounds__(kBlock) void avgpool3s1_kernel(const uint4 *__restr
     }
 }
 
+// Global average pool (the ResNet / Inception head), NHWC: y[n, c] = mean over the HW pixels.
+// One thread per (n, 8-channel group); adjacent threads read adjacent 16-byte vectors of a
+// pixel, the HW pixels are walked with 4 loads in flight.
+__global__ __launch_bounds__(kBlock) void gap_fwd_kernel(const uint4 *__restrict__ x, uint4 *__restrict__ y, int HW,
+                                                         int CV, int64_t n, float inv) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * kBlock) {
+        const int cv = static_cast<int>(i % CV);
+        const int64_t nn = i / CV;
+        const uint4 *p = x + nn * HW * CV + cv;
+        float acc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+        int q = 0;
+        for (; q + 4 <= HW; q += 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = p[static_cast<int64_t>(q + u) * CV];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += (k & 1) ? hi16(bits_of(v[u], k >> 1)) : lo16(bits_of(v[u], k >> 1));
+        }
+        for (; q < HW; ++q) {
+            const uint4 v = p[static_cast<int64_t>(q) * CV];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += (k & 1) ? hi16(bits_of(v, k >> 1)) : lo16(bits_of(v, k >> 1));
+        }
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k] * inv)) |
+                   (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1] * inv)) << 16);
+        y[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// dx[n, p, c] = dy[n, c] / HW for every pixel p: one 16-byte store per thread
+__global__ __launch_bounds__(kBlock) void gap_bwd_kernel(const uint4 *__restrict__ dy, uint4 *__restrict__ dx, int HW,
+                                                         int CV, int64_t n, float inv) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * kBlock) {
+        const int cv = static_cast<int>(i % CV);
+        const int64_t nn = i / (static_cast<int64_t>(CV) * HW);
+        const uint4 d = dy[nn * CV + cv];
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = static_cast<uint32_t>(f32_to_bf16(lo16(bits_of(d, k)) * inv)) |
+                   (static_cast<uint32_t>(f32_to_bf16(hi16(bits_of(d, k)) * inv)) << 16);
+        dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+}
+
 PoolGeo pool_geo(int64_t N, int H, int W, int C) {
     if (C % 8 || H % 2 || W % 2) throw std::invalid_argument("maxpool2x2: needs C % 8 == 0 and even H, W");
     PoolGeo g;
@@ -344,6 +398,22 @@ void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, 
     if (n <= 0) return;
     avgpool3s1_kernel<<<pool_grid(n), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), reinterpret_cast<uint4 *>(y),
                                                        H, W, C / 8, n);
+}
+
+void launch_global_avgpool_forward(const uint16_t *x, uint16_t *y, int64_t N, int HW, int C, hipStream_t s) {
+    if (C % 8 || HW <= 0) throw std::invalid_argument("global_avgpool: needs C % 8 == 0");
+    const int64_t n = N * (C / 8);
+    if (n <= 0) return;
+    gap_fwd_kernel<<<pool_grid(n), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(x), reinterpret_cast<uint4 *>(y), HW,
+                                                    C / 8, n, 1.f / HW);
+}
+
+void launch_global_avgpool_backward(const uint16_t *dy, uint16_t *dx, int64_t N, int HW, int C, hipStream_t s) {
+    if (C % 8 || HW <= 0) throw std::invalid_argument("global_avgpool: needs C % 8 == 0");
+    const int64_t n = N * HW * (C / 8);
+    if (n <= 0) return;
+    gap_bwd_kernel<<<pool_grid(n), kBlock, 0, s>>>(reinterpret_cast<const uint4 *>(dy), reinterpret_cast<uint4 *>(dx), HW,
+                                                    C / 8, n, 1.f / HW);
 }
 
 }  // namespace kfk

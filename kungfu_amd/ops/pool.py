@@ -1,5 +1,6 @@
-"""Pooling on the HIP kernels of csrc/kernels/pool.hip: VGG-16's 2x2/s2 max-pool, and
-Inception-v3's 3x3/s2 max-pool and 3x3/s1/p1 average pool (see the section below).
+"""Pooling on the HIP kernels of csrc/kernels/pool.hip: VGG-16's 2x2/s2 max-pool,
+Inception-v3's 3x3/s2 max-pool and 3x3/s1/p1 average pool (see the section below), and the
+global average pool of the ResNet / Inception heads.
 
 2x2 / stride-2 max-pool:
 
@@ -113,3 +114,28 @@ class MaxPool3x3s2(nn.MaxPool2d):
 
     def forward(self, x):
         return max_pool3x3s2(x, self.padding)
+
+
+# ---------------------------------------------------------------- global average pool (heads)
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """mean over H, W of an NHWC bf16 tensor -> [N, C]; the backward writes dy / HW to every
+    pixel with 16-byte stores (torch's expand + channels_last copy took ~100 us for ResNet-50's
+    7x7x2048 head at batch 256)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return hip().global_avgpool_forward(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return hip().global_avgpool_backward(dy.to(torch.bfloat16), *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)``."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and hip_available()):
+        return _GlobalAvgPoolFn.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

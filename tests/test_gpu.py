@@ -1189,3 +1189,25 @@ def test_linear_mfma_wgrad_matches_fp32(T, i, o):
     for a, r in ((y, yf), (x.grad, xf.grad), (w.grad, wf.grad), (b.grad, bf.grad)):
         assert a.dtype == torch.bfloat16
         assert ((a.float() - r).norm() / r.norm()).item() < 1e-2
+
+
+@needs_gpu
+@pytest.mark.parametrize("N,C,Hh", [(8, 2048, 7), (3, 64, 5), (2, 768, 8)])
+def test_global_avg_pool_matches_torch(N, C, Hh):
+    """Global average pool (ResNet / Inception head) on pool.hip vs the float32 torch mean, and
+    its backward (dy / HW broadcast to every pixel) vs autograd of the float32 mean."""
+    from kungfu_amd.ops.pool import global_avg_pool
+
+    torch.manual_seed(5)
+    x = torch.randn(N, C, Hh, Hh, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    xa = x.clone().requires_grad_(True)
+    y = global_avg_pool(xa)
+    assert y.grad_fn is not None and "GlobalAvgPool" in type(y.grad_fn).__name__
+    xr = x.float().requires_grad_(True)
+    yr = xr.mean((2, 3))
+    assert _rel(y, yr) < 1e-2
+    dy = torch.randn(N, C, device="cuda").bfloat16()
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(xa.grad, xr.grad) < 1e-2

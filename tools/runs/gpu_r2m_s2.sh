@@ -5,8 +5,10 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out
 TAG=${1:-s2}
 mkdir -p "$OUT"
 export MIOPEN_USER_DB_PATH=$PWD/kungfu_amd/tuning/miopen
-timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu -k "dgrad_s2 or bottleneck or resnet50_fused or persistent" > "$OUT/${TAG}_pytest.log" 2>&1 || { tail -60 "$OUT/${TAG}_pytest.log"; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -v --timeout 200 --timeout-method thread -m gpu -k "dgrad_s2 or bottleneck or resnet50_fused or persistent or global_avg" > "$OUT/${TAG}_pytest.log" 2>&1 || { tail -60 "$OUT/${TAG}_pytest.log"; exit 1; }
 tail -1 "$OUT/${TAG}_pytest.log"
+timeout -k 10 200 python tools/bench_dgrad_s2.py > "$OUT/${TAG}_dg.log" 2>&1 || exit 1
+cat "$OUT/${TAG}_dg.log"
 for M in resnet50; do
   timeout -k 10 300 python bench.py --model $M --steps 20 --warmup 5 > "$OUT/${TAG}_${M}.log" 2>&1 || { tail -20 "$OUT/${TAG}_${M}.log"; exit 1; }
   tail -1 "$OUT/${TAG}_${M}.log" | cut -c1-230
