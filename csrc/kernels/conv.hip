@@ -123,16 +123,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     const int n0 = nt * BN;
     const int mstride = PERSIST ? nwg / g.ntiles : g.mtiles;  // nwg % ntiles == 0 when persistent
     const int cv = tid % (BN / 8);  // the epilogue's fixed 8-channel group of this thread
-    float s1[8], s2[8], sc[8], sh[8];
+    float s1[8], s2[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-    if constexpr ((EPI & kEpiBwdCoef) != 0) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[k] = ea.fcoef[n0 + cv * 8 + k];
-            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
-        }
-    }
     int mt_last = mt_first;
     for (int mt = mt_first; mt < g.mtiles; mt += mstride) {
     mt_last = mt;
@@ -292,35 +285,77 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
     // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
     static_assert(NT % VPR == 0, "fixed channel group per thread");
-    for (int v = tid; v < BM * VPR; v += NT) {
-        const int row = v / VPR;
-        const int m = m0 + row;
-        if (m < g.M) {
+    // The global reads of the epilogue (old value, BN input, masks) of U rows are all issued
+    // before any of them is consumed: one load round trip per U rows instead of per row (the
+    // loop is otherwise a chain of dependent HBM latencies -- the stores to y may alias later
+    // reads as far as the compiler knows).
+    constexpr int ITER = BM * VPR / NT;
+    static_assert(ITER * NT == BM * VPR, "whole store iterations");
+    constexpr bool LD_OLD = (EPI & kEpiAccum) != 0;
+    constexpr bool LD_BX = GATE || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
+    // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
+    // the 256x256 tile, whose 16 coefficient registers would otherwise spill)
+    constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
+    float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
+    if constexpr ((EPI & kEpiBwdCoef) != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sc[k] = ea.fcoef[n0 + cv * 8 + k];
+            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
+        }
+    }
+    for (int it0 = 0; it0 < ITER; it0 += U) {
+        uint4 val[U], old[U], bxv[U];
+        uint32_t amb[U], bmb[U];
+        int64_t ee[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int v = tid + (it0 + u) * NT;
+            const int row = v / VPR;
+            const int m = m0 + row;
+            ok[u] = m < g.M;
             int pix = m;
             if (g.scat) {
                 const int t = m / g.OW, ow = m - t * g.OW;
                 pix = (2 * t + g.pr) * (2 * g.OW) + 2 * ow + g.pc;
             }
             const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
-            uint4 *dst = reinterpret_cast<uint4 *>(y + e);
-            uint4 val = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
-            if constexpr ((EPI & kEpiAccum) != 0) {
-                bool here = true;
-                if constexpr ((EPI & kEpiAccEven) != 0) {
-                    // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
-                    const int t = m / g.OW, ow = m - t * g.OW;
-                    here = ((ow | (t % g.OH)) & 1) == 0;
+            ee[u] = e;
+            val[u] = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
+            old[u] = bxv[u] = make_uint4(0u, 0u, 0u, 0u);
+            amb[u] = 0u;
+            bmb[u] = 0xffu;
+            if (ok[u]) {
+                if constexpr (LD_OLD) {
+                    bool here = true;
+                    if constexpr ((EPI & kEpiAccEven) != 0) {
+                        // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
+                        const int t = m / g.OW, ow = m - t * g.OW;
+                        here = ((ow | (t % g.OH)) & 1) == 0;
+                    }
+                    if (here) old[u] = *reinterpret_cast<const uint4 *>(y + e);
+                    if constexpr ((EPI & kEpiAccMask) != 0) amb[u] = ea.amask[e >> 3];  // 8 channels, 8-aligned e
                 }
-                uint4 old = here ? *dst : make_uint4(0u, 0u, 0u, 0u);
+                if constexpr (LD_BX) bxv[u] = *reinterpret_cast<const uint4 *>(ea.bx + e);
+                if constexpr ((EPI & kEpiBwdBits) != 0) bmb[u] = ea.bmask[e >> 3];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            uint4 v = val[u];
+            if constexpr (LD_OLD) {
+                uint4 o0 = old[u];
                 if constexpr ((EPI & kEpiAccMask) != 0) {
-                    const uint32_t mb = ea.amask[e >> 3];  // 8 channels from an 8-aligned e
-                    uint32_t *ow = reinterpret_cast<uint32_t *>(&old);
+                    const uint32_t mb = amb[u];
+                    uint32_t *ow = reinterpret_cast<uint32_t *>(&o0);
 #pragma unroll
                     for (int k = 0; k < 4; ++k)
                         ow[k] &= (((mb >> (2 * k)) & 1u) ? 0xffffu : 0u) | (((mb >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
                 }
-                const uint32_t *a = reinterpret_cast<const uint32_t *>(&val);
-                const uint32_t *b = reinterpret_cast<const uint32_t *>(&old);
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(&v);
+                const uint32_t *b = reinterpret_cast<const uint32_t *>(&o0);
                 uint32_t o[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -330,13 +365,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                                      bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
                     o[k] = static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
                 }
-                val = make_uint4(o[0], o[1], o[2], o[3]);
+                v = make_uint4(o[0], o[1], o[2], o[3]);
             }
             if constexpr (GATE) {
                 // gradient of a ReLU output: keep y where bx > 0 (NaN passes), sum the kept values
-                const uint4 bv = *reinterpret_cast<const uint4 *>(ea.bx + e);
-                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bv);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&val);
+                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bxv[u]);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
@@ -344,10 +378,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                     vw[k] &= keep;
                 }
             }
-            *dst = val;
+            *reinterpret_cast<uint4 *>(y + ee[u]) = v;
             if constexpr (STATS) {
                 float f[8];
-                unpack_bf16x8(val, f);
+                unpack_bf16x8(v, f);
                 if constexpr (GATE) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) s1[k] += f[k];
@@ -361,9 +395,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                     // BN backward sums of the BN whose input is ea.bx:
                     //   dz = grad * relu'(.) ; s1 += dz ; s2 += dz * x
                     float xv[8];
-                    unpack_bf16x8(*reinterpret_cast<const uint4 *>(ea.bx + e), xv);
-                    uint32_t mbits = 0xffu;
-                    if constexpr ((EPI & kEpiBwdBits) != 0) mbits = ea.bmask[e >> 3];
+                    unpack_bf16x8(bxv[u], xv);
+                    const uint32_t mbits = bmb[u];
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         bool on;

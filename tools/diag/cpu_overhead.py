@@ -1,0 +1,70 @@
+"""Is the training step CPU-bound?  Runs the bench's ResNet-50 S-SGD step (same setup as
+bench.py) and reports, per step, the host time spent enqueueing it (no synchronisation) next
+to the GPU time per step (events).  If the host time is close to the GPU time, the GPU starves
+wherever the host falls behind (the fwd/bwd boundary gaps in the kernel trace).
+Also times the forward / backward / optimizer phases on the host."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(os.path.dirname(sys.path[0]), "kungfu_amd", "tuning",
+                                                          "miopen"))
+import torch
+import torch.nn.functional as F
+
+import kungfu_amd as kf
+from kungfu_amd.models import get_model
+from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+
+def main():
+    model_name = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
+    kf.init()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    model = get_model(model_name, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
+    base = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(), force_comm=True)
+    enable_bf16_shadow(model, opt)
+    x = torch.randn(256, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (256,), device=dev)
+    ph = {"zero": 0.0, "fwd": 0.0, "bwd": 0.0, "step": 0.0}
+
+    def step():
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        t1 = time.perf_counter()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(model(x).float(), y)
+        t2 = time.perf_counter()
+        loss.backward()
+        t3 = time.perf_counter()
+        opt.step()
+        t4 = time.perf_counter()
+        for k, a, b in (("zero", t0, t1), ("fwd", t1, t2), ("bwd", t2, t3), ("step", t3, t4)):
+            ph[k] += b - a
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    for k in ph:
+        ph[k] = 0.0
+    n = 20
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    h0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    h1 = time.perf_counter()
+    e1.record()
+    torch.cuda.synchronize()
+    h2 = time.perf_counter()
+    print("host enqueue %.2f ms/step, wall %.2f ms/step, gpu %.2f ms/step" % (
+        1e3 * (h1 - h0) / n, 1e3 * (h2 - h0) / n, e0.elapsed_time(e1) / n))
+    print("host phases (ms/step): " + ", ".join("%s %.2f" % (k, 1e3 * v / n) for k, v in ph.items()))
+    kf.finalize()
+
+
+if __name__ == "__main__":
+    main()
