@@ -730,15 +730,53 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy,
 
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
 at::Tensor conv_flip_weight(at::Tensor w) {
-    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
                     w.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "conv_flip_weight: [Cout, Cin, KS, KS] channels_last bf16 required");
-    const int K = w.size(0), C = w.size(1), ks = w.size(2);
+                "conv_flip_weight: [Cout, Cin, KH, KW] channels_last bf16 required");
+    const int K = w.size(0), C = w.size(1), kh = w.size(2), kw = w.size(3);
     c10::DeviceGuard gd(w.device());
-    auto wt = at::empty({C, K, ks, ks}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
-    kfk::launch_conv_flip_weight(reinterpret_cast<const uint16_t *>(w.data_ptr()),
-                                 reinterpret_cast<uint16_t *>(wt.data_ptr()), K, C, ks, stream_of(w, 0));
+    auto wt = at::empty({C, K, kh, kw}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_conv_flip_weight_taps(reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                                      reinterpret_cast<uint16_t *>(wt.data_ptr()), K, C, kh * kw, stream_of(w, 0));
     return wt;
+}
+
+// KH x KW convolution with zero padding (ph, pw) on the MFMA kernel (Inception-v3 shapes,
+// kfk::conv_rect_supported); stats: optional f64 [kStatSlots*2*Cout] BN-statistics workspace.
+at::Tensor conv_rect(at::Tensor x, at::Tensor w, int64_t stride, int64_t ph, int64_t pw,
+                     c10::optional<at::Tensor> stats) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_rect: x must be a 4-D channels_last bf16 GPU tensor");
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(1) == x.size(1) &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == x.device(),
+                "conv_rect: w must be [Cout, Cin, KH, KW] channels_last bf16 on x's device");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3), K = w.size(0);
+    const int kh = w.size(2), kw = w.size(3);
+    TORCH_CHECK(kfk::conv_rect_supported(C, K, kh, kw, static_cast<int>(stride)) && ph >= 0 && pw >= 0 &&
+                    ph < kh && pw < kw,
+                "conv_rect: unsupported channels/window/stride/padding");
+    const int OH = (H + 2 * static_cast<int>(ph) - kh) / static_cast<int>(stride) + 1;
+    const int OW = (W + 2 * static_cast<int>(pw) - kw) / static_cast<int>(stride) + 1;
+    TORCH_CHECK(OH > 0 && OW > 0, "conv_rect: empty output");
+    TORCH_CHECK(static_cast<int64_t>(N) * H * W * C < (int64_t(1) << 31) &&
+                    static_cast<int64_t>(N) * OH * OW * K < (int64_t(1) << 31),
+                "conv_rect: tensor too large for 32-bit offsets");
+    c10::DeviceGuard gd(x.device());
+    kfk::EpiArgs ea;
+    int epi = 0;
+    if (stats && stats->defined()) {
+        TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->numel() == 2 * K * kfk::kStatSlots &&
+                        stats->is_contiguous() && stats->device() == x.device(),
+                    "conv_rect: stats must be the f64 [kStatSlots*2*Cout] workspace");
+        ea.stats = stats->data_ptr<double>();
+        epi = kfk::kEpiFwdStats;
+    }
+    auto y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_conv_rect(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                          reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, kh, kw, static_cast<int>(ph),
+                          static_cast<int>(pw), static_cast<int>(stride), ea, epi, stream_of(x, 0));
+    return y;
 }
 
 // dsts[i] = conv_flip_weight(srcs[i]) for a list of bf16 conv weights, in as few launches as
@@ -753,7 +791,7 @@ void conv_flip_weights(std::vector<at::Tensor> srcs, std::vector<at::Tensor> dst
     for (size_t i = 0; i < srcs.size(); ++i) {
         const auto &w = srcs[i];
         const auto &d = dsts[i];
-        TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == w.size(3) &&
+        TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 &&
                         w.is_contiguous(at::MemoryFormat::ChannelsLast) && w.device() == srcs[0].device(),
                     "conv_flip_weights: [Cout, Cin, KS, KS] channels_last bf16 sources on one device");
         TORCH_CHECK(d.scalar_type() == at::kBFloat16 && d.dim() == 4 && d.size(0) == w.size(1) &&
@@ -1288,6 +1326,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
           py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false);
+    m.def("conv_rect", &conv_rect, "KH x KW NHWC bf16 convolution with zero padding (MFMA implicit GEMM; "
+          "Inception-v3 windows) with an optional BN-statistics epilogue", py::arg("x"), py::arg("w"),
+          py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none());
+    m.def("conv_rect_supported", &kfk::conv_rect_supported);
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),

@@ -62,6 +62,7 @@ struct Geo {
     int tapmap;  // -1: tap t reads weight tap t; else weight tap of tap t = nibble t
     int scat;    // 1: output row m -> pixel (2*(m/OW) + pr, 2*(m%OW) + pc) of a 2OH x 2OW image
     int pr, pc;
+    int ph, pw;  // zero padding (rows, columns)
 };
 
 template <int N>
@@ -70,9 +71,9 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
-// KS = 3 (pad 1) or 1 (pad 0); KS = 0xHW (>= 16): an H x W window with no padding (taps read
-// rows oh..oh+H-1, out-of-range rows are zero) -- the parity phases of a stride-2 3x3 data
-// gradient (launch_conv_dgrad_s2).  EPI flags (kernels.hpp ConvEpi):
+// KS = 3 or 1: square window; KS = 0xHW (>= 16): an H x W window (Inception's 1x7 / 7x1 / 1x3 /
+// 3x1 / 5x5, and the parity phases of a stride-2 3x3 data gradient, launch_conv_dgrad_s2).  The
+// zero padding is g.ph / g.pw (out-of-range taps read the zero page).  EPI flags (kernels.hpp ConvEpi):
 //   kEpiAccum     y += conv (accumulate into the existing bf16 tensor, a residual gradient);
 //   kEpiFwdStats  per-channel sum / sum-of-squares of the bf16 outputs (the following BN's
 //                 batch statistics) -> f64 atomics into ea.stats[slot][2][K];
@@ -93,7 +94,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int WTM = 16 * TM, WTN = 16 * TN;
     constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
     constexpr int KH = KS >= 16 ? (KS >> 4) : KS, KW = KS >= 16 ? (KS & 15) : KS;
-    constexpr int TAPS = KH * KW, PAD = KS >= 16 ? 0 : (KS - 1) / 2;
+    constexpr int TAPS = KH * KW;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
     constexpr int STAGE = A_BYTES + B_BYTES;
     constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         a_ok[j] = 0;
         if (m < g.M) {
             const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
-            const int ih0 = oh * g.stride - PAD, iw0 = ow * g.stride - PAD;
+            const int ih0 = oh * g.stride - g.ph, iw0 = ow * g.stride - g.pw;
             a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
             uint32_t ok = 0;
 #pragma unroll
@@ -629,8 +630,56 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.M = N * g.OH * g.OW;
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
+    g.ph = g.pw = pad;
     if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
+}
+
+// Rectangular windows (Inception-v3): plain or BN-statistics epilogue, 256x128 / 8 waves when
+// Cout % 128 == 0, else 256x64.
+template <int KS>
+void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
+                   hipStream_t s) {
+    if (epi != 0 && epi != kEpiFwdStats) throw std::invalid_argument("conv_rect: epilogue must be none or stats");
+    if (g.K % 128 == 0) {
+        if (epi) launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s);
+        else launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s);
+    } else {
+        if (epi) launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s);
+        else launch_epi<KS, 4, 1, 2, 0>(x, w, y, g, ea, s);
+    }
+}
+
+bool conv_rect_supported(int Cin, int Cout, int kh, int kw, int stride) {
+    if (Cin % 64 || Cout % 64 || Cin < 64 || !(stride == 1 || stride == 2)) return false;
+    return (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 7) || (kh == 7 && kw == 1) ||
+           (kh == 1 && kw == 3) || (kh == 3 && kw == 1) || (kh == 5 && kw == 5);
+}
+
+void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
+                      int kh, int kw, int ph, int pw, int stride, const EpiArgs &ea, int epi, hipStream_t s) {
+    if (!conv_rect_supported(Cin, Cout, kh, kw, stride)) throw std::invalid_argument("conv_rect: unsupported shape");
+    Geo g;
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
+    g.OH = (H + 2 * ph - kh) / stride + 1;
+    g.OW = (W + 2 * pw - kw) / stride + 1;
+    g.M = N * g.OH * g.OW;
+    g.mtiles = g.ntiles = 0;
+    g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
+    g.ph = ph, g.pw = pw;
+    if (kh == 1 && kw == 1) {
+        launch_ks<1>(x, w, y, g, ea, epi, s, -1);
+        return;
+    }
+    if (kh == 3 && kw == 3) {
+        launch_ks<3>(x, w, y, g, ea, epi, s, -1);
+        return;
+    }
+    if (kh == 1 && kw == 7) launch_rect_t<0x17>(x, w, y, g, ea, epi, s);
+    else if (kh == 7 && kw == 1) launch_rect_t<0x71>(x, w, y, g, ea, epi, s);
+    else if (kh == 1 && kw == 3) launch_rect_t<0x13>(x, w, y, g, ea, epi, s);
+    else if (kh == 3 && kw == 1) launch_rect_t<0x31>(x, w, y, g, ea, epi, s);
+    else launch_rect_t<0x55>(x, w, y, g, ea, epi, s);
 }
 
 // One parity phase of a stride-2 data gradient: the fused epilogues it needs (none, or the BN
@@ -684,6 +733,7 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     g.OH = OH, g.OW = OW, g.M = N * OH * OW;
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.scat = 1;
+    g.ph = g.pw = 0;
     if (ks == 1) {
         g.tapmap = -1, g.pr = g.pc = 0;
         launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
@@ -713,10 +763,14 @@ void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, in
 }
 
 void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s) {
-    const int64_t n = static_cast<int64_t>(Cout) * ks * ks * Cin;
+    launch_conv_flip_weight_taps(w, wt, Cout, Cin, ks * ks, s);
+}
+
+void launch_conv_flip_weight_taps(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int taps, hipStream_t s) {
+    const int64_t n = static_cast<int64_t>(Cout) * taps * Cin;
     int grid = static_cast<int>((n + 255) / 256);
     if (grid > 4096) grid = 4096;
-    conv_flip_kernel<<<grid, 256, 0, s>>>(w, wt, Cout, Cin, ks * ks);
+    conv_flip_kernel<<<grid, 256, 0, s>>>(w, wt, Cout, Cin, taps);
 }
 
 void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s) {

@@ -128,6 +128,12 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
 // kEpiAccEven stride-1 data gradient into the same dx).
 void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
                           int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);
+// KH x KW window with zero padding (ph, pw), stride 1|2 (Inception-v3's 1x1, 3x3 pad 0|1, 1x7,
+// 7x1, 1x3, 3x1, 5x5): the same implicit GEMM, K = KH*KW*Cin tap-major; epilogue none or
+// kEpiFwdStats.  Cin, Cout multiples of 64.
+bool conv_rect_supported(int Cin, int Cout, int kh, int kw, int stride);
+void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
+                      int kh, int kw, int ph, int pw, int stride, const EpiArgs &ea, int epi, hipStream_t s);
 // Multi-tensor flip (one launch for a whole model's conv weights).
 struct FlipTable {
     static constexpr int kMax = 64;
@@ -141,6 +147,8 @@ struct FlipTable {
 void launch_conv_flip_multi(const FlipTable &tab, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,KS-1-kh,KS-1-kw,ci]: stride-1 data gradient = conv(dy, wt).
 void launch_conv_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int ks, hipStream_t s);
+// Any KH x KW window: the flattened tap index is reversed (taps = KH*KW).
+void launch_conv_flip_weight_taps(const uint16_t *w, uint16_t *wt, int Cout, int Cin, int taps, hipStream_t s);
 // wt[ci,kh,kw,co] = w[co,2-kh,2-kw,ci]: stride-1 data gradient = conv3x3(dy, wt).
 void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s);
 

@@ -30,6 +30,19 @@ class BasicConv2d(nn.Module):
             self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
     def forward(self, x):
+        if self.fused and not self.pool_after_conv and self.training and self.bn.track_running_stats:
+            # MFMA conv whose epilogue accumulates the BN batch statistics: the BN skips its
+            # statistics pass (ops/conv.py conv2d_stats; None if the shape is not on the kernel)
+            from ..ops.conv import conv2d_stats
+            from ..parallel.mixed import shadow
+
+            c = self.conv
+            w = shadow(c.weight)
+            if w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
+                ws = self.bn.stats_workspace(x.device)
+                y = conv2d_stats(x, w, c.stride, c.padding, ws)
+                if y is not None:
+                    return self.bn(y, sums=ws)
         y = self.conv(x)
         if self.pool_after_conv:
             if self.fused:  # HIP 3x3/s1/p1 stencil (forward and backward)

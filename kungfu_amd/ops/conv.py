@@ -152,9 +152,82 @@ class _BiasActFn(torch.autograd.Function):
         return dz, db, None
 
 
+def _pair(v):
+    return (int(v), int(v)) if isinstance(v, int) else (int(v[0]), int(v[1]))
+
+
+def rect_eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups) -> bool:
+    """KH x KW windows the MFMA kernel takes (1x1, 3x3, 1x7, 7x1, 1x3, 3x1, 5x5; Cin, Cout
+    multiples of 64, equal strides 1|2, padding < window): Inception-v3's convolutions."""
+    if not (_ENABLED and _RECT) or not x.is_cuda or groups != 1 or w.dim() != 4 or x.dim() != 4:
+        return False
+    st, pd, dl = _pair(stride), _pair(padding), _pair(dilation)
+    if st[0] != st[1] or dl != (1, 1) or pd[0] >= w.shape[2] or pd[1] >= w.shape[3]:
+        return False
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not hip_available():
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last) or not w.is_contiguous(memory_format=torch.channels_last):
+        return False
+    return hip().conv_rect_supported(int(x.shape[1]), int(w.shape[0]), int(w.shape[2]), int(w.shape[3]), st[0])
+
+
+class _ConvRectFn(torch.autograd.Function):
+    """KH x KW convolution on the MFMA kernel (``_hip.conv_rect``).  Backward: stride 1 data
+    gradient = the same kernel on the flipped weights with padding (KH-1-ph, KW-1-pw); stride 2
+    via MIOpen; weight gradient via :func:`wgrad` (MFMA for 1x1 / 3x3-pad-1, MIOpen otherwise).
+    ``stats``: the BN statistics workspace of a following BN (epilogue sums, see ``bn_act``)."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, ph, pw, stats):
+        ctx.save_for_backward(x, w)
+        ctx.geo = (stride, ph, pw)
+        return hip().conv_rect(x, w, stride, ph, pw, stats)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        s, ph, pw = ctx.geo
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        kh, kw = int(w.shape[2]), int(w.shape[3])
+        if ctx.needs_input_grad[0]:
+            if s == 1:
+                dx = hip().conv_rect(dy, hip().conv_flip_weight(w), 1, kh - 1 - ph, kw - 1 - pw)
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
+                                                         [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            if kh == kw and ph == pw == (kh - 1) // 2:
+                dw = wgrad(dy, x, w, s, ph)
+            else:
+                dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
+                                                         [False, True, False])[1]
+        return dx, dw, None, None, None, None
+
+
+_RECT = os.environ.get("KUNGFU_CONV_RECT", "1") != "0"
+
+
+def conv2d_stats(x, w, stride, padding, stats: torch.Tensor):
+    """conv2d whose MFMA epilogue also accumulates the per-channel batch statistics of its bf16
+    output into ``stats`` (a following BN's workspace, ``BatchNormAct2d.stats_workspace``).
+    Returns None when the shape is not on the MFMA kernel (the caller runs the plain path)."""
+    if not rect_eligible(x, w, stride, padding, 1, 1):
+        return None
+    st, pd = _pair(stride), _pair(padding)
+    return _ConvRectFn.apply(x, w, st[0], pd[0], pd[1], stats)
+
+
 def conv2d(x, w, bias, stride, padding, dilation, groups, relu: bool = False):
-    """F.conv2d (+ ReLU) with the 3x3 MFMA fast path; there the bias (+ ReLU) is one in-place
-    HIP pass over the conv output (``_BiasActFn``) when the channel count allows."""
+    """F.conv2d (+ ReLU) with the MFMA fast paths: 3x3/pad 1 (there the bias (+ ReLU) is one
+    in-place HIP pass over the conv output, ``_BiasActFn``, when the channel count allows) and
+    the other KH x KW windows of :func:`rect_eligible` (no bias)."""
+    if bias is None and not eligible(x, w, stride, padding, dilation, groups) and \
+            rect_eligible(x, w, stride, padding, dilation, groups):
+        st, pd = _pair(stride), _pair(padding)
+        y = _ConvRectFn.apply(x, w, st[0], pd[0], pd[1], None)
+        return F.relu(y) if relu else y
     if eligible(x, w, stride, padding, dilation, groups):
         y = _Conv3x3Fn.apply(x, w, int(stride if isinstance(stride, int) else stride[0]))
         if bias is not None and hip().bias_act_supported(int(y.shape[1])):

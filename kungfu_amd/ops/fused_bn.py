@@ -60,9 +60,9 @@ def _direct(weight, bias):
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu, nbt):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu, nbt, sums=None):
         y, mean, invstd, coef, mask = hip().bn_forward(x, res, weight, bias, running_mean, running_var, momentum, eps,
-                                                       training, relu, nbt)
+                                                       training, relu, nbt, sums)
         ctx.save_for_backward(x, mean, invstd, weight, coef, mask)
         ctx.relu, ctx.training, ctx.has_res = relu, training, res is not None
         ctx.direct = _direct(weight, bias)
@@ -74,7 +74,7 @@ class _BNActFn(torch.autograd.Function):
         dx, dres, dw, db = hip().bn_backward(dy, x, mean, invstd, weight, coef, mask, ctx.relu, ctx.training,
                                              ctx.has_res)
         dw, db = _param_grads(ctx, dw, db)
-        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None, None
+        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None, None, None
 
 
 class _BNActPoolFn(torch.autograd.Function):
@@ -99,13 +99,17 @@ class _BNActPoolFn(torch.autograd.Function):
 
 def bn_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
            relu: bool = True, res: Optional[torch.Tensor] = None,
-           num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
+           num_batches_tracked: Optional[torch.Tensor] = None, sums: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Functional fused BN(+res)(+ReLU); falls back to torch ops when not fusable.
 
-    ``num_batches_tracked`` (if given, training mode) is incremented on device."""
+    ``num_batches_tracked`` (if given, training mode) is incremented on device.  ``sums``
+    (training): batch statistics already accumulated by the producing conv's epilogue
+    (``ops.conv.conv2d_stats``), consumed and re-zeroed -- no statistics pass."""
     if _fusable(x, res) and weight is not None and momentum is not None:
         return _BNActFn.apply(x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu,
-                              num_batches_tracked if training else None)
+                              num_batches_tracked if training else None, sums if training else None)
+    if sums is not None:
+        sums.zero_()  # not consumed by the fallback below
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
     y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
@@ -143,9 +147,19 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return (self.weight, self.bias, self.running_mean if stats else None, self.running_var if stats else None,
                 use_batch, self.momentum, self.eps), (self.num_batches_tracked if track else None)
 
-    def forward(self, x):
+    def forward(self, x, sums: Optional[torch.Tensor] = None):
+        """``sums``: batch statistics from the producing conv's epilogue (training only)."""
         a, nbt = self._args()
-        return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt)
+        return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt, sums=sums if a[4] else None)
+
+    def stats_workspace(self, dev) -> torch.Tensor:
+        """Zeroed f64 [slots, 2, C] workspace a conv epilogue accumulates this BN's batch
+        statistics into (consumed and re-zeroed by the BN kernels)."""
+        ws = getattr(self, "_kf_sums", None)
+        if ws is None or ws.device != dev:
+            ws = torch.zeros(hip().conv_stat_slots * 2 * self.num_features, dtype=torch.float64, device=dev)
+            self._kf_sums = ws
+        return ws
 
     def forward_pool(self, x, sums: Optional[torch.Tensor] = None):
         """relu(bn(x)) followed by MaxPool2d(3, stride 2, padding 1), fused (``sums``: batch

@@ -1211,3 +1211,95 @@ def test_global_avg_pool_matches_torch(N, C, Hh):
     yr.backward(dy.float())
     assert xa.grad.is_contiguous(memory_format=torch.channels_last)
     assert _rel(xa.grad, xr.grad) < 1e-2
+
+
+@needs_gpu
+@pytest.mark.parametrize("kh,kw,ph,pw,stride,C,K,Hh", [(1, 7, 0, 3, 1, 128, 192, 12), (7, 1, 3, 0, 1, 192, 128, 12),
+                                                       (1, 3, 0, 1, 1, 384, 384, 5), (3, 1, 1, 0, 1, 384, 384, 5),
+                                                       (5, 5, 2, 2, 1, 64, 64, 9), (3, 3, 0, 0, 2, 192, 320, 12),
+                                                       (3, 3, 0, 0, 1, 64, 128, 10), (1, 1, 0, 0, 1, 768, 192, 12)])
+def test_conv_rect_matches_torch(kh, kw, ph, pw, stride, C, K, Hh):
+    """Inception-v3 windows on the MFMA kernel (``ops.conv._ConvRectFn``): forward with the
+    BN-statistics epilogue, data and weight gradients, all vs the float32 torch convolution;
+    the statistics vs float64 sums of the bf16 output."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.conv import conv2d_stats, rect_eligible
+
+    torch.manual_seed(33)
+    N = 4
+    x = torch.randn(N, C, Hh, Hh, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, kh, kw, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+    assert rect_eligible(x, w, stride, (ph, pw), 1, 1)
+    st = torch.zeros(H_slots() * 2 * K, dtype=torch.float64, device="cuda")
+    xa, wa = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = conv2d_stats(xa, wa, stride, (ph, pw), st)
+    xr, wr = x.float().requires_grad_(True), w.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=stride, padding=(ph, pw))
+    assert y.shape == yr.shape and _rel(y, yr) < 1e-2
+    yd = y.double().permute(0, 2, 3, 1).reshape(-1, K)
+    sums = st.view(-1, 2, K).sum(0)
+    torch.testing.assert_close(sums[0], yd.sum(0), rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(sums[1], (yd * yd).sum(0), rtol=1e-6, atol=1e-3)
+    dy = torch.randn_like(yr)
+    y.backward(dy.bfloat16().contiguous(memory_format=torch.channels_last))
+    yr.backward(dy)
+    assert _rel(xa.grad, xr.grad) < 2e-2
+    assert _rel(wa.grad, wr.grad) < 2e-2
+
+
+@needs_gpu
+@pytest.mark.parametrize("cin,cout,kw", [(128, 192, dict(kernel_size=(1, 7), padding=(0, 3))),
+                                         (768, 192, dict(kernel_size=1)),
+                                         (448, 384, dict(kernel_size=3, padding=1)),
+                                         (192, 320, dict(kernel_size=3, stride=2))])
+def test_inception_basicconv_mfma_stats_path(monkeypatch, cin, cout, kw):
+    """Inception BasicConv2d on the MFMA conv with the BN-statistics epilogue (the path taken
+    with bf16 shadow weights) vs the stock conv + BatchNorm2d + ReLU module in float32:
+    output, input / weight / gamma / beta gradients and the running statistics."""
+    import copy
+
+    import kungfu_amd.parallel.mixed as mixed
+    from kungfu_amd.models import inception as inc
+
+    torch.manual_seed(12)
+    inc._FUSED_BN[0] = True
+    try:
+        fused = inc.BasicConv2d(cin, cout, **kw).cuda().to(memory_format=torch.channels_last)
+    finally:
+        inc._FUSED_BN[0] = False
+    ref = inc.BasicConv2d(cin, cout, **kw).cuda().to(memory_format=torch.channels_last)
+    ref.load_state_dict(fused.state_dict())
+    with torch.no_grad():
+        fused.bn.weight.uniform_(0.5, 1.5)
+        fused.bn.bias.uniform_(-0.2, 0.2)
+        ref.bn.weight.copy_(fused.bn.weight)
+        ref.bn.bias.copy_(fused.bn.bias)
+    # the bf16 compute weight the shadow machinery would hand over (a differentiable cast here)
+    monkeypatch.setattr(mixed, "shadow", lambda p: p.bfloat16().contiguous(memory_format=torch.channels_last))
+    lay = copy.deepcopy(ref)  # stock conv + BN in bf16 autocast: the bf16 error baseline
+    x = torch.randn(4, cin, 12, 12, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    xf, xr, xl = x.clone().requires_grad_(True), x.float().requires_grad_(True), x.clone().requires_grad_(True)
+    y = fused(xf)
+    assert fused.bn._kf_sums is not None  # the statistics came from the conv epilogue
+    yr = ref(xr)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yl = lay(xl)
+
+    def nrel(a, b):  # norm-relative: bf16 activations through a BN backward
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+    def close(a, l, r, what):
+        assert nrel(a, r) <= max(1.5 * nrel(l, r), 1e-2), (what, nrel(a, r), nrel(l, r))
+
+    close(y, yl, yr, "out")
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g)
+    yl.float().backward(g)
+    close(xf.grad, xl.grad, xr.grad, "dx")
+    for (n, p), (_, q), (_, l) in zip(fused.named_parameters(), ref.named_parameters(), lay.named_parameters()):
+        close(p.grad, l.grad, q.grad, n)
+    assert torch.allclose(fused.bn.running_mean, ref.bn.running_mean, rtol=1e-2, atol=1e-3)
+    assert torch.allclose(fused.bn.running_var, ref.bn.running_var, rtol=1e-2, atol=1e-3)
+    assert int(fused.bn.num_batches_tracked) == 1
