@@ -163,13 +163,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             a_ok[j] = ok;
         }
     }
+    // Channel counts that are not multiples of the tile (Inception's 48, 80, 96, 160, ...): the
+    // K-step's 8-channel chunks past Cin and the B rows past Cout read the zero page.
     int b_off[B_INST];
+    uint32_t b_ok = 0;
 #pragma unroll
     for (int j = 0; j < B_INST; ++j) {
         const int r = (wave * B_INST + j) * 8 + srow;
         b_off[j] = (n0 + r) * g.wtaps * g.C + schunk * 8;
+        if (n0 + r < g.K) b_ok |= 1u << j;
     }
-    const int csteps = g.C / kBK;
+    const int csteps = (g.C + kBK - 1) / kBK;
     const int ksteps = TAPS * csteps;
 
     auto stage = [&](int ks, int buf) {
@@ -177,17 +181,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         const int kh = tap / KW, kw = tap - kh * KW;
         const int toff = (kh * g.W + kw) * g.C + cc * kBK;  // wave-uniform
         const int wtap = g.tapmap < 0 ? tap : (g.tapmap >> (4 * tap)) & 15;
+        const bool cin_ok = cc * kBK + schunk * 8 < g.C;
         uint8_t *abase = lds + buf * STAGE;
         uint8_t *bbase = abase + A_BYTES;
 #pragma unroll
         for (int j = 0; j < A_INST; ++j) {
-            const bool ok = (a_ok[j] >> tap) & 1u;
+            const bool ok = ((a_ok[j] >> tap) & 1u) && cin_ok;
             const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
             __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
-            const uint16_t *src = w + static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK);
+            const bool ok = ((b_ok >> j) & 1u) && cin_ok;
+            const uint16_t *src = ok ? w + static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK) : zero;
             __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
         }
     };
@@ -297,8 +303,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
     // the 256x256 tile, whose 16 coefficient registers would otherwise spill)
     constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
+    const bool col_ok = n0 + cv * 8 < g.K;  // this thread's 8 channels exist (Cout % BN != 0)
     float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
     if constexpr ((EPI & kEpiBwdCoef) != 0) {
+        if (col_ok)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             sc[k] = ea.fcoef[n0 + cv * 8 + k];
@@ -315,7 +323,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             const int v = tid + (it0 + u) * NT;
             const int row = v / VPR;
             const int m = m0 + row;
-            ok[u] = m < g.M;
+            ok[u] = m < g.M && col_ok;
             int pix = m;
             if (g.scat) {
                 const int t = m / g.OW, ow = m - t * g.OW;
@@ -431,8 +439,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 if constexpr (NSUM == 2) t2 += red[(GROUPS + p) * BN + col];
             }
             double *sl = ea.stats + ((mt_last + wg) % kStatSlots) * 2 * g.K;  // spread atomics over slots
-            atomicAdd(sl + n0 + col, t1);
-            if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
+            if (n0 + col < g.K) {
+                atomicAdd(sl + n0 + col, t1);
+                if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
+            }
         }
     }
 }
@@ -528,9 +538,9 @@ const void *zero_page() {
 template <int KS, int WM, int WN, int ST, int EPI, int TM = 4, int TN = 4>
 void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
     constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    if (g.K % BN) throw std::invalid_argument("conv: Cout not a multiple of the tile");
+    if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv: Cin and Cout must be multiples of 8");
     g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = g.K / BN;
+    g.ntiles = (g.K + BN - 1) / BN;
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
     if constexpr (STATS) {
         // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
@@ -592,7 +602,7 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     // 123 us, 3x3 256->256 at 14x14 70 -> 57 us; fewer tiles under-fill the chip: 3x3 512->512 at
     // 7x7 62 -> 100 us), else 256x128 / 8 waves (1x1 included: 4-13 % over 128x128), else 256x64
     if (variant < 0) {
-        const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);
+        const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);  // (K % 256 == 0 only)
         variant = g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
     }
     switch (variant) {
@@ -651,7 +661,8 @@ void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, con
 }
 
 bool conv_rect_supported(int Cin, int Cout, int kh, int kw, int stride) {
-    if (Cin % 64 || Cout % 64 || Cin < 64 || !(stride == 1 || stride == 2)) return false;
+    // channel counts: multiples of 8 (16-byte chunks); the last K-step / N-tile is zero-padded
+    if (Cin % 8 || Cout % 8 || Cin < 16 || Cout < 16 || !(stride == 1 || stride == 2)) return false;
     return (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 7) || (kh == 7 && kw == 1) ||
            (kh == 1 && kw == 3) || (kh == 3 && kw == 1) || (kh == 5 && kw == 5);
 }

@@ -40,7 +40,7 @@ class BasicConv2d(nn.Module):
             w = shadow(c.weight)
             if w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
                 ws = self.bn.stats_workspace(x.device)
-                y = conv2d_stats(x, w, c.stride, c.padding, ws)
+                y = conv2d_stats(x, w, c.stride, c.padding, ws, master=c.weight)
                 if y is not None:
                     return self.bn(y, sums=ws)
         y = self.conv(x)

@@ -178,9 +178,10 @@ class _ConvRectFn(torch.autograd.Function):
     ``stats``: the BN statistics workspace of a following BN (epilogue sums, see ``bn_act``)."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, ph, pw, stats):
+    def forward(ctx, x, w, stride, ph, pw, stats, flip=None):
         ctx.save_for_backward(x, w)
         ctx.geo = (stride, ph, pw)
+        ctx.flip = flip
         return hip().conv_rect(x, w, stride, ph, pw, stats)
 
     @staticmethod
@@ -193,7 +194,9 @@ class _ConvRectFn(torch.autograd.Function):
         kh, kw = int(w.shape[2]), int(w.shape[3])
         if ctx.needs_input_grad[0]:
             if s == 1:
-                dx = hip().conv_rect(dy, hip().conv_flip_weight(w), 1, kh - 1 - ph, kw - 1 - pw)
+                # flipped weights: from the flat space's per-step multi-tensor flip when registered
+                wt = ctx.flip[0].get(ctx.flip[1]) if ctx.flip is not None else hip().conv_flip_weight(w)
+                dx = hip().conv_rect(dy, wt, 1, kh - 1 - ph, kw - 1 - pw)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
@@ -203,20 +206,32 @@ class _ConvRectFn(torch.autograd.Function):
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 _RECT = os.environ.get("KUNGFU_CONV_RECT", "1") != "0"
 
 
-def conv2d_stats(x, w, stride, padding, stats: torch.Tensor):
+def conv2d_stats(x, w, stride, padding, stats: torch.Tensor, master: torch.Tensor = None):
     """conv2d whose MFMA epilogue also accumulates the per-channel batch statistics of its bf16
     output into ``stats`` (a following BN's workspace, ``BatchNormAct2d.stats_workspace``).
+    ``master``: the f32 parameter ``w`` shadows -- its flipped copy for the data gradient then
+    comes from the flat space's one-launch-per-step multi-tensor flip.
     Returns None when the shape is not on the MFMA kernel (the caller runs the plain path)."""
     if not rect_eligible(x, w, stride, padding, 1, 1):
         return None
     st, pd = _pair(stride), _pair(padding)
-    return _ConvRectFn.apply(x, w, st[0], pd[0], pd[1], stats)
+    flip = None
+    if master is not None and st[0] == 1:
+        from ..parallel.mixed import direct_target
+        from .fused_block import _flip_cache
+
+        tc = direct_target(master)
+        if tc is not None and w is not master:
+            fc = _flip_cache(tc[0])
+            fc.register(tc[1], w)
+            flip = (fc, tc[1])
+    return _ConvRectFn.apply(x, w, st[0], pd[0], pd[1], stats, flip)
 
 
 def conv2d(x, w, bias, stride, padding, dilation, groups, relu: bool = False):

@@ -1217,7 +1217,12 @@ def test_global_avg_pool_matches_torch(N, C, Hh):
 @pytest.mark.parametrize("kh,kw,ph,pw,stride,C,K,Hh", [(1, 7, 0, 3, 1, 128, 192, 12), (7, 1, 3, 0, 1, 192, 128, 12),
                                                        (1, 3, 0, 1, 1, 384, 384, 5), (3, 1, 1, 0, 1, 384, 384, 5),
                                                        (5, 5, 2, 2, 1, 64, 64, 9), (3, 3, 0, 0, 2, 192, 320, 12),
-                                                       (3, 3, 0, 0, 1, 64, 128, 10), (1, 1, 0, 0, 1, 768, 192, 12)])
+                                                       (3, 3, 0, 0, 1, 64, 128, 10), (1, 1, 0, 0, 1, 768, 192, 12),
+                                                       # channel counts off the 64 grid (zero-padded K / N)
+                                                       (3, 3, 0, 0, 1, 80, 192, 12), (5, 5, 2, 2, 1, 48, 64, 9),
+                                                       (1, 1, 0, 0, 1, 192, 48, 12), (3, 3, 1, 1, 1, 96, 96, 10),
+                                                       (1, 7, 0, 3, 1, 160, 160, 12), (3, 3, 0, 0, 2, 288, 384, 12),
+                                                       (3, 3, 0, 0, 1, 32, 32, 13)])
 def test_conv_rect_matches_torch(kh, kw, ph, pw, stride, C, K, Hh):
     """Inception-v3 windows on the MFMA kernel (``ops.conv._ConvRectFn``): forward with the
     BN-statistics epilogue, data and weight gradients, all vs the float32 torch convolution;
@@ -1252,7 +1257,9 @@ def test_conv_rect_matches_torch(kh, kw, ph, pw, stride, C, K, Hh):
 @pytest.mark.parametrize("cin,cout,kw", [(128, 192, dict(kernel_size=(1, 7), padding=(0, 3))),
                                          (768, 192, dict(kernel_size=1)),
                                          (448, 384, dict(kernel_size=3, padding=1)),
-                                         (192, 320, dict(kernel_size=3, stride=2))])
+                                         (192, 320, dict(kernel_size=3, stride=2)),
+                                         (48, 64, dict(kernel_size=5, padding=2)),
+                                         (768, 160, dict(kernel_size=1))])
 def test_inception_basicconv_mfma_stats_path(monkeypatch, cin, cout, kw):
     """Inception BasicConv2d on the MFMA conv with the BN-statistics epilogue (the path taken
     with bf16 shadow weights) vs the stock conv + BatchNorm2d + ReLU module in float32:
