@@ -488,6 +488,41 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c
     return dw;
 }
 
+// Weight gradient of a KH x KW convolution with zero padding (ph, pw): dw [Cout, Cin, KH, KW]
+// channels_last bf16 (kfk::conv_wgrad_rect_supported: Inception-v3's windows / channel counts).
+at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, int64_t stride, int64_t ph,
+                           int64_t pw) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                    x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_wgrad_rect: x must be a 4-D channels_last bf16 GPU tensor");
+    const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+    const int OH = (H + 2 * static_cast<int>(ph) - static_cast<int>(kh)) / static_cast<int>(stride) + 1;
+    const int OW = (W + 2 * static_cast<int>(pw) - static_cast<int>(kw)) / static_cast<int>(stride) + 1;
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N &&
+                    dy.size(2) == OH && dy.size(3) == OW && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dy.device() == x.device(),
+                "conv_wgrad_rect: dy must be the [N, Cout, OH, OW] channels_last bf16 output gradient");
+    const int K = dy.size(1);
+    TORCH_CHECK(kfk::conv_wgrad_rect_supported(C, K, static_cast<int>(kh), static_cast<int>(kw), static_cast<int>(stride)) &&
+                    ph >= 0 && pw >= 0 && ph < kh && pw < kw,
+                "conv_wgrad_rect: unsupported channels/window/stride/padding");
+    TORCH_CHECK(static_cast<int64_t>(N) * H * W * C < (int64_t(1) << 31) &&
+                    static_cast<int64_t>(N) * OH * OW * K < (int64_t(1) << 31),
+                "conv_wgrad_rect: tensor too large for 32-bit offsets");
+    c10::DeviceGuard gd(x.device());
+    auto dw = at::empty({K, C, kh, kw}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    const auto plan = kfk::conv_wgrad_rect_plan(N, H, W, C, K, static_cast<int>(kh), static_cast<int>(kw),
+                                                static_cast<int>(ph), static_cast<int>(pw), static_cast<int>(stride));
+    at::Tensor ws;
+    if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, x.options().dtype(at::kFloat));
+    kfk::launch_conv_wgrad_rect(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                reinterpret_cast<const uint16_t *>(x.data_ptr()), dw.data_ptr(),
+                                plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, N, H, W, C, K, static_cast<int>(kh),
+                                static_cast<int>(kw), static_cast<int>(ph), static_cast<int>(pw),
+                                static_cast<int>(stride), plan, false, false, stream_of(x, 0));
+    return dw;
+}
+
 // Fused self-attention: qkv [B, S, 3*H*64] bf16 contiguous -> (out [B, S, H*64] bf16, lse [B, H, S] f32)
 std::vector<at::Tensor> attention_forward(at::Tensor qkv, int64_t heads, double scale, int64_t seed, double p_drop) {
     TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
@@ -1334,6 +1369,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1);
+    m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "
+          "(split-K MFMA GEMM, any channel count % 8)", py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
+          py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0);
+    m.def("conv_wgrad_rect_supported", &kfk::conv_wgrad_rect_supported);
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);

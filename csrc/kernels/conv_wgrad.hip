@@ -54,6 +54,7 @@ struct WGeo {
     int P, HW;
     uint64_t m_hw, m_ow;  // floor(p / d) = (p * m) >> 40, exact for p * d < 2^40
     int mtiles, ntiles, taps, tiles, splits, kps;
+    int kwin, ph, pw;  // KS == 0 (any window): taps per kernel row and the zero padding
 };
 
 __device__ __forceinline__ int fdiv(int p, uint64_t m) {
@@ -81,6 +82,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t *p0, const uint8_t *p1) 
 }
 
 // WM x WN waves (wave tile 64 co x 16*TN ci), STAGES-deep global_load_lds ring; S = stride.
+// KS = 1 | 3 (pad (KS-1)/2), or 0: a KH x KW window with padding (g.kwin, g.ph, g.pw) at run
+// time (Inception-v3's 1x7 / 7x1 / 1x3 / 3x1 / 5x5 / 3x3-pad-0).  Channel counts that are not
+// multiples of the tile: channels past Cout / Cin read the zero page, their outputs are dropped.
 template <int KS, int S, int WM, int WN, int STAGES, int TN = 4>
 __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__restrict__ dy,
                                                              const uint16_t *__restrict__ x,
@@ -88,7 +92,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                                                              const uint16_t *__restrict__ zero, WGeo g,
                                                              int out_f32, int accumulate, int atomic_out) {
     constexpr int BM = 64 * WM, BN = 16 * TN * WN, NW = WM * WN, NT = 64 * NW;
-    constexpr int PAD = (KS - 1) / 2;
+    constexpr int PAD = KS > 0 ? (KS - 1) / 2 : 0;
     constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per staged pixel row
     constexpr int CPRA = ROWA / 16, CPRB = ROWB / 16;
     constexpr int RPIA = 64 / CPRA, RPIB = 64 / CPRB;  // rows per 1 KB glds instruction
@@ -107,7 +111,9 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     const int mn = g.mtiles * g.ntiles;
     const int tap = tile / mn, rem = tile - tap * mn;
     const int mt = rem / g.ntiles, nt = rem - mt * g.ntiles;
-    const int kh = tap / KS, kw = tap - kh * KS;
+    const int kwin = KS > 0 ? KS : g.kwin;
+    const int kh = tap / kwin, kw = tap - kh * kwin;
+    const int pad_h = KS > 0 ? PAD : g.ph, pad_w = KS > 0 ? PAD : g.pw;
     const int m0 = mt * BM, n0 = nt * BN;
     const int p_begin = split * g.kps * kBK;
     int nsteps = (g.P - p_begin + kBK - 1) / kBK;
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int j = 0; j < A_INST; ++j) {
             const int p = p0 + a_row[j];
-            const uint16_t *src = p < g.P ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
+            const uint16_t *src = p < g.P && a_col[j] < g.K ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
             __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
         }
 #pragma unroll
@@ -148,14 +154,14 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
             const int p = p0 + b_row[j];
             const uint16_t *src = zero;
             if constexpr (IDENT) {
-                if (p < g.P) src = x + static_cast<uint32_t>(p * g.C + b_col[j]);
+                if (p < g.P && b_col[j] < g.C) src = x + static_cast<uint32_t>(p * g.C + b_col[j]);
             } else {
                 const int n = fdiv(p, g.m_hw);
                 const int r = p - n * g.HW;
                 const int oh = fdiv(r, g.m_ow);
                 const int ow = r - oh * g.OW;
-                const int ih = oh * S + kh - PAD, iw = ow * S + kw - PAD;
-                if (p < g.P && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                const int ih = oh * S + kh - pad_h, iw = ow * S + kw - pad_w;
+                if (p < g.P && b_col[j] < g.C && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
                     static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
                     src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
             }
@@ -233,6 +239,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                 for (int r = 0; r < 4; ++r) {
                     const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
                     const int ci = n0 + wn * 16 * TN + j * 16 + (lane & 15);
+                    if (co >= g.K || ci >= g.C) continue;
                     const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
                     atomicAdd(static_cast<float *>(dw) + e, acc[i][j][r]);
                 }
@@ -245,6 +252,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                 for (int r = 0; r < 4; ++r) {
                     const int co = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
                     const int ci = n0 + wn * 16 * TN + j * 16 + (lane & 15);
+                    if (co >= g.K || ci >= g.C) continue;
                     const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
                     float v = acc[i][j][r];
                     if (out_f32) {
@@ -512,6 +520,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = mt * BM + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            if (co >= g.K || ci >= g.C) continue;
             const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
             float v = s[r];
             if (out_f32) {
@@ -587,6 +596,7 @@ WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const 
     g.mtiles = Cout / t.bm();
     g.ntiles = Cin / t.bn();
     g.taps = ks * ks;
+    g.kwin = ks, g.ph = g.pw = pad;
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.splits = plan.splits;
     g.kps = plan.kps;
@@ -733,6 +743,76 @@ void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *p
     } else {
         if (stride == 1) launch_ks<3, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
         else launch_ks<3, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+    }
+}
+
+// ---- any KH x KW window, padding, channel counts % 8 (Inception-v3) -----------------------
+
+bool conv_wgrad_rect_supported(int Cin, int Cout, int kh, int kw, int stride) {
+    return Cin % 8 == 0 && Cout % 8 == 0 && Cin >= 16 && Cout >= 16 && (stride == 1 || stride == 2) && kh >= 1 &&
+           kw >= 1 && kh * kw <= 49;
+}
+
+namespace {
+// tile: 128 rows where the channel count reaches it (less zero padding otherwise)
+int rect_variant(int Cin, int Cout) { return Cout >= 128 ? (Cin >= 128 ? 0 : 1) : (Cin >= 128 ? 2 : 3); }
+
+WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride, int variant) {
+    WGeo g{};
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
+    g.OH = (H + 2 * ph - kh) / stride + 1;
+    g.OW = (W + 2 * pw - kw) / stride + 1;
+    g.HW = g.OH * g.OW;
+    g.P = N * g.HW;
+    g.m_hw = magic40(g.HW);
+    g.m_ow = magic40(g.OW);
+    const Tile t = kTiles[variant];
+    g.mtiles = (Cout + t.bm() - 1) / t.bm();
+    g.ntiles = (Cin + t.bn() - 1) / t.bn();
+    g.taps = kh * kw;
+    g.tiles = g.mtiles * g.ntiles * g.taps;
+    g.kwin = kw, g.ph = ph, g.pw = pw;
+    return g;
+}
+}  // namespace
+
+WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride) {
+    WgradPlan pl;
+    pl.variant = rect_variant(Cin, Cout);
+    WGeo g = make_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, stride, pl.variant);
+    const Tile t = kTiles[pl.variant];
+    const int ksteps = (g.P + kBK - 1) / kBK;
+    const int nw = t.wm * t.wn;
+    int target = 256 * (nw >= 4 ? 1 : 2) * (g.taps > 1 ? 2 : 1);
+    int splits = (target + g.tiles / 2) / g.tiles;
+    splits = std::max(1, std::min(splits, ksteps / 4));
+    splits = std::max(1, std::min(splits, ksteps));
+    pl.kps = (ksteps + splits - 1) / splits;
+    pl.splits = (ksteps + pl.kps - 1) / pl.kps;
+    pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * g.tiles * t.bm() * t.bn() : 0;
+    return pl;
+}
+
+void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W,
+                            int Cin, int Cout, int kh, int kw, int ph, int pw, int stride, const WgradPlan &plan,
+                            bool out_f32, bool accumulate, hipStream_t s) {
+    if (!conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) throw std::invalid_argument("conv_wgrad_rect: unsupported");
+    const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
+    WGeo g = make_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, stride, plan.variant);
+    g.splits = plan.splits;
+    g.kps = plan.kps;
+    if (static_cast<int64_t>(g.P) * g.HW >= (int64_t(1) << 40) || g.P >= (1 << 23))
+        throw std::invalid_argument("conv_wgrad_rect: too many pixels for the 40-bit division");
+    if (g.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad_rect: needs the workspace");
+    const bool k1 = kh == 1 && kw == 1 && ph == 0 && pw == 0, k3 = kh == 3 && kw == 3 && ph == 1 && pw == 1;
+    if (stride == 1) {
+        if (k1) launch_ks<1, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else if (k3) launch_ks<3, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else launch_ks<0, 1>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+    } else {
+        if (k1) launch_ks<1, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else if (k3) launch_ks<3, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
+        else launch_ks<0, 2>(dy, x, dw, part, g, plan.variant, out_f32, accumulate, atomic_out, s);
     }
 }
 

@@ -174,7 +174,8 @@ def rect_eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, g
 class _ConvRectFn(torch.autograd.Function):
     """KH x KW convolution on the MFMA kernel (``_hip.conv_rect``).  Backward: stride 1 data
     gradient = the same kernel on the flipped weights with padding (KH-1-ph, KW-1-pw); stride 2
-    via MIOpen; weight gradient via :func:`wgrad` (MFMA for 1x1 / 3x3-pad-1, MIOpen otherwise).
+    via MIOpen; weight gradient on the split-K MFMA kernel (:func:`wgrad` for the ResNet-shaped
+    1x1 / 3x3-pad-1 ones, ``_hip.conv_wgrad_rect`` for any other window / channel count).
     ``stats``: the BN statistics workspace of a following BN (epilogue sums, see ``bn_act``)."""
 
     @staticmethod
@@ -201,8 +202,13 @@ class _ConvRectFn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            if kh == kw and ph == pw == (kh - 1) // 2:
-                dw = wgrad(dy, x, w, s, ph)
+            cin, cout = int(x.shape[1]), int(dy.shape[1])
+            if kh == kw and ph == pw == (kh - 1) // 2 and cin % 64 == 0 and cout % 64 == 0:
+                dw = wgrad(dy, x, w, s, ph)  # ResNet-tuned planner (row-image 3x3 kernel etc.)
+            elif (_WGRAD and _WGRAD_RECT and min(cin, cout) >= 64 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
+                  and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):
+                # (narrow channel counts stay on MIOpen: their zero-padded 64-wide tiles lose)
+                dw = hip().conv_wgrad_rect(dy, x, kh, kw, s, ph, pw)
             else:
                 dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [False, True, False])[1]
@@ -210,6 +216,7 @@ class _ConvRectFn(torch.autograd.Function):
 
 
 _RECT = os.environ.get("KUNGFU_CONV_RECT", "1") != "0"
+_WGRAD_RECT = os.environ.get("KUNGFU_WGRAD_RECT", "1") != "0"
 
 
 def conv2d_stats(x, w, stride, padding, stats: torch.Tensor, master: torch.Tensor = None):

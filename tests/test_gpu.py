@@ -1225,7 +1225,8 @@ def test_global_avg_pool_matches_torch(N, C, Hh):
                                                        (3, 3, 0, 0, 1, 32, 32, 13)])
 def test_conv_rect_matches_torch(kh, kw, ph, pw, stride, C, K, Hh):
     """Inception-v3 windows on the MFMA kernel (``ops.conv._ConvRectFn``): forward with the
-    BN-statistics epilogue, data and weight gradients, all vs the float32 torch convolution;
+    BN-statistics epilogue, data and weight gradients (``conv_wgrad_rect`` for the windows /
+    channel counts the ResNet planner does not take), all vs the float32 torch convolution;
     the statistics vs float64 sums of the bf16 output."""
     import torch.nn.functional as F
 

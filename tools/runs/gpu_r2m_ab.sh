@@ -13,6 +13,6 @@ tail -1 "$OUT/${TAG}_pytest.log"
 for r in 1 2; do
   for v in 0 1; do
     env $VAR=$v timeout -k 10 300 python bench.py --model ${MODEL:-resnet50} --steps 30 --warmup 5 > "$OUT/${TAG}_${v}_$r.log" 2>&1 || { tail -20 "$OUT/${TAG}_${v}_$r.log"; exit 1; }
-    echo "$VAR=$v: $(tail -1 "$OUT/${TAG}_${v}_$r.log" | cut -c100-175)"
+    echo "$VAR=$v: $(tail -1 "$OUT/${TAG}_${v}_$r.log" | grep -o "\"value\": [0-9.]*")"
   done
 done
