@@ -645,17 +645,20 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
 }
 
-// Rectangular windows (Inception-v3): plain or BN-statistics epilogue, 256x128 / 8 waves when
+// Rectangular windows (Inception-v3): plain, BN-statistics or accumulate epilogue, 256x128 / 8 waves when
 // Cout % 128 == 0, else 256x64.
 template <int KS>
 void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
                    hipStream_t s) {
-    if (epi != 0 && epi != kEpiFwdStats) throw std::invalid_argument("conv_rect: epilogue must be none or stats");
+    if (epi != 0 && epi != kEpiFwdStats && epi != kEpiAccum)
+        throw std::invalid_argument("conv_rect: epilogue must be none, stats or accumulate");
     if (g.K % 128 == 0) {
-        if (epi) launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s);
+        if (epi == kEpiFwdStats) launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s);
+        else if (epi == kEpiAccum) launch_epi<KS, 4, 2, 3, kEpiAccum>(x, w, y, g, ea, s);
         else launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s);
     } else {
-        if (epi) launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s);
+        if (epi == kEpiFwdStats) launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s);
+        else if (epi == kEpiAccum) launch_epi<KS, 4, 1, 2, kEpiAccum>(x, w, y, g, ea, s);
         else launch_epi<KS, 4, 1, 2, 0>(x, w, y, g, ea, s);
     }
 }

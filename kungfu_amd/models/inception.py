@@ -56,6 +56,26 @@ class BasicConv2d(nn.Module):
         return F.relu(self.bn(y), inplace=True)
 
 
+def _heads(x, mods):
+    """``[m(x) for m in mods]`` for BasicConv2d modules that all read ``x`` (an Inception block's
+    branch heads).  Fused training path: their convolutions are ONE autograd node on the MFMA
+    kernel (``ops.conv.sibling_convs``: the branch gradients of x are accumulated by the conv
+    epilogue instead of autograd adds), each conv's epilogue producing its BN's statistics
+    (the pool branch pools the conv output first, so its BN computes its own)."""
+    m0 = mods[0]
+    if (len(mods) > 1 and m0.fused and m0.training and x.dtype == torch.bfloat16
+            and all(m.bn.track_running_stats for m in mods)):
+        from ..ops.conv import sibling_convs
+
+        st = [None if m.pool_after_conv else m.bn.stats_workspace(x.device) for m in mods]
+        ys = sibling_convs(x, [m.conv for m in mods], st)
+        if ys is not None:
+            from ..ops.pool import avg_pool3x3s1
+
+            return [m.bn(avg_pool3x3s1(y)) if m.pool_after_conv else m.bn(y, sums=s) for m, y, s in zip(mods, ys, st)]
+    return [m(x) for m in mods]
+
+
 def _pool_module():
     """The stem's MaxPool2d(3, 2): HIP kernels (byte argmax, gather backward) in the fused model."""
     if _FUSED_BN[0]:
@@ -90,7 +110,8 @@ class InceptionA(nn.Module):
         self.bp = _branch_pool(cin, pool_features)
 
     def forward(self, x):
-        return torch.cat([self.b1(x), self.b5(x), self.b3(x), self.bp(x)], 1)
+        o1, t5, t3, op = _heads(x, [self.b1, self.b5[0], self.b3[0], self.bp])
+        return torch.cat([o1, self.b5[1](t5), self.b3[2](self.b3[1](t3)), op], 1)
 
 
 class InceptionB(nn.Module):
@@ -120,7 +141,8 @@ class InceptionC(nn.Module):
         self.bp = _branch_pool(cin, 192)
 
     def forward(self, x):
-        return torch.cat([self.b1(x), self.b7(x), self.bd(x), self.bp(x)], 1)
+        o1, t7, td, op = _heads(x, [self.b1, self.b7[0], self.bd[0], self.bp])
+        return torch.cat([o1, self.b7[2](self.b7[1](t7)), self.bd[4](self.bd[3](self.bd[2](self.bd[1](td)))), op], 1)
 
 
 class InceptionD(nn.Module):
@@ -134,7 +156,8 @@ class InceptionD(nn.Module):
                                 BasicConv2d(192, 192, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.b7(x), _max_pool3s2(x, self.fused)], 1)
+        t3, t7 = _heads(x, [self.b3[0], self.b7[0]])
+        return torch.cat([self.b3[1](t3), self.b7[3](self.b7[2](self.b7[1](t7))), _max_pool3s2(x, self.fused)], 1)
 
 
 class InceptionE(nn.Module):
@@ -151,10 +174,9 @@ class InceptionE(nn.Module):
         self.bp = _branch_pool(cin, 192)
 
     def forward(self, x):
-        b3 = self.b3_1(x)
-        bd = self.bd_2(self.bd_1(x))
-        return torch.cat([self.b1(x), self.b3_2a(b3), self.b3_2b(b3), self.bd_3a(bd), self.bd_3b(bd),
-                          self.bp(x)], 1)
+        o1, b3, bd, op = _heads(x, [self.b1, self.b3_1, self.bd_1, self.bp])
+        bd = self.bd_2(bd)
+        return torch.cat([o1] + _heads(b3, [self.b3_2a, self.b3_2b]) + _heads(bd, [self.bd_3a, self.bd_3b]) + [op], 1)
 
 
 class InceptionV3(nn.Module):

@@ -202,17 +202,84 @@ class _ConvRectFn(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            cin, cout = int(x.shape[1]), int(dy.shape[1])
-            if kh == kw and ph == pw == (kh - 1) // 2 and cin % 64 == 0 and cout % 64 == 0:
-                dw = wgrad(dy, x, w, s, ph)  # ResNet-tuned planner (row-image 3x3 kernel etc.)
-            elif (_WGRAD and _WGRAD_RECT and min(cin, cout) >= 64 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
-                  and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):
-                # (narrow channel counts stay on MIOpen: their zero-padded 64-wide tiles lose)
-                dw = hip().conv_wgrad_rect(dy, x, kh, kw, s, ph, pw)
-            else:
-                dw = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
-                                                         [False, True, False])[1]
+            dw = _rect_wgrad(dy, x, w, s, ph, pw)
         return dx, dw, None, None, None, None, None
+
+
+def _rect_wgrad(dy, x, w, s, ph, pw):
+    """Weight gradient of a KH x KW convolution: the ResNet-tuned planner for 1x1 / 3x3-pad-1 with
+    channels % 64, the runtime-window split-K kernel for other wide layers, MIOpen for narrow ones."""
+    kh, kw = int(w.shape[2]), int(w.shape[3])
+    cin, cout = int(x.shape[1]), int(dy.shape[1])
+    if kh == kw and ph == pw == (kh - 1) // 2 and cin % 64 == 0 and cout % 64 == 0:
+        return wgrad(dy, x, w, s, ph)  # ResNet-tuned planner (row-image 3x3 kernel etc.)
+    if (_WGRAD and _WGRAD_RECT and min(cin, cout) >= 64 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
+            and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):
+        # (narrow channel counts stay on MIOpen: their zero-padded 64-wide tiles lose)
+        return hip().conv_wgrad_rect(dy, x, kh, kw, s, ph, pw)
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
+
+
+class _SiblingConvFn(torch.autograd.Function):
+    """Stride-1 convolutions that all read the same input (the branch heads of an Inception
+    block) as ONE autograd node: forward = one MFMA conv per sibling (BN statistics in each
+    epilogue when a workspace is given); backward = their data gradients chained into one dx by
+    the kernel's accumulate epilogue (no autograd adds of the branch gradients: one pass each
+    fewer), weight gradients per sibling."""
+
+    @staticmethod
+    def forward(ctx, x, pads, stats, flips, *ws):
+        ys = tuple(hip().conv_rect(x, w, 1, ph, pw, st) for w, (ph, pw), st in zip(ws, pads, stats))
+        ctx.save_for_backward(x, *ws)
+        ctx.pads, ctx.flips = pads, flips
+        return ys
+
+    @staticmethod
+    def backward(ctx, *dys):
+        x, *ws = ctx.saved_tensors
+        dx = None
+        dws = []
+        for w, dy, (ph, pw), fl in zip(ws, dys, ctx.pads, ctx.flips):
+            if dy is None:
+                dws.append(None)
+                continue
+            if not dy.is_contiguous(memory_format=torch.channels_last):
+                dy = dy.contiguous(memory_format=torch.channels_last)
+            if ctx.needs_input_grad[0]:
+                wt = fl[0].get(fl[1]) if fl is not None else hip().conv_flip_weight(w)
+                kh, kw = int(w.shape[2]), int(w.shape[3])
+                dx = hip().conv_rect(dy, wt, 1, kh - 1 - ph, kw - 1 - pw, None, dx)  # dx += (first: =)
+            dws.append(_rect_wgrad(dy, x, w, 1, ph, pw))
+        return (dx, None, None, None, *dws)
+
+
+def sibling_convs(x, convs, stats):
+    """``[conv(x) for conv in convs]`` for nn.Conv2d modules (no bias, stride 1) on the MFMA
+    kernel as one autograd node (:class:`_SiblingConvFn`); ``stats[i]``: BN statistics workspace
+    for conv i's output or None.  Takes the bf16 shadow weights.  Returns None when any conv is
+    not eligible (the caller runs the modules one by one)."""
+    from ..parallel.mixed import direct_target, shadow
+
+    ws, pads, flips = [], [], []
+    for c in convs:
+        if c.bias is not None or _pair(c.stride) != (1, 1):
+            return None
+        w = shadow(c.weight)
+        if not rect_eligible(x, w, 1, c.padding, c.dilation, c.groups):
+            return None
+        ws.append(w)
+        pads.append(_pair(c.padding))
+        tc = direct_target(c.weight)
+        if tc is not None and w is not c.weight:
+            from .fused_block import _flip_cache
+
+            fc = _flip_cache(tc[0])
+            fc.register(tc[1], w)
+            flips.append((fc, tc[1]))
+        else:
+            flips.append(None)
+    return _SiblingConvFn.apply(x, tuple(pads), tuple(stats), tuple(flips), *ws)
 
 
 _RECT = os.environ.get("KUNGFU_CONV_RECT", "1") != "0"

@@ -1311,3 +1311,38 @@ def test_inception_basicconv_mfma_stats_path(monkeypatch, cin, cout, kw):
     assert torch.allclose(fused.bn.running_mean, ref.bn.running_mean, rtol=1e-2, atol=1e-3)
     assert torch.allclose(fused.bn.running_var, ref.bn.running_var, rtol=1e-2, atol=1e-3)
     assert int(fused.bn.num_batches_tracked) == 1
+
+
+@needs_gpu
+def test_sibling_convs_match_torch(monkeypatch):
+    """Inception branch heads as one autograd node (``ops.conv.sibling_convs``): outputs, the
+    input gradient (the siblings' data gradients chained by the accumulate epilogue) and the
+    weight gradients vs float32 torch convolutions of the same input."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    import kungfu_amd.parallel.mixed as mixed
+    from kungfu_amd.ops.conv import sibling_convs
+
+    torch.manual_seed(17)
+    monkeypatch.setattr(mixed, "shadow", lambda p: p.bfloat16().contiguous(memory_format=torch.channels_last))
+    convs = [nn.Conv2d(192, 64, 1, bias=False), nn.Conv2d(192, 48, 1, bias=False),
+             nn.Conv2d(192, 96, (1, 3), padding=(0, 1), bias=False), nn.Conv2d(192, 64, 3, padding=1, bias=False)]
+    convs = [c.cuda().to(memory_format=torch.channels_last) for c in convs]
+    x = torch.randn(4, 192, 12, 12, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    xa, xr = x.clone().requires_grad_(True), x.float().requires_grad_(True)
+    st = [torch.zeros(H_slots() * 2 * c.out_channels, dtype=torch.float64, device="cuda") for c in convs]
+    ys = sibling_convs(xa, convs, st)
+    assert ys is not None and len(ys) == 4
+    gs = [torch.randn(4, c.out_channels, 12, 12, device="cuda") for c in convs]
+    wr = [c.weight.detach().bfloat16().float().requires_grad_(True) for c in convs]
+    yr = [F.conv2d(xr, w, padding=c.padding) for w, c in zip(wr, convs)]
+    for y, r, s, c in zip(ys, yr, st, convs):
+        assert _rel(y, r) < 1e-2
+        sums = s.view(-1, 2, c.out_channels).sum(0)
+        torch.testing.assert_close(sums[0], y.double().sum((0, 2, 3)), rtol=1e-6, atol=1e-3)
+    sum((y.float() * g).sum() for y, g in zip(ys, gs)).backward()
+    sum((y * g).sum() for y, g in zip(yr, gs)).backward()
+    assert _rel(xa.grad, xr.grad) < 2e-2
+    for c, w in zip(convs, wr):
+        assert _rel(c.weight.grad, w.grad) < 2e-2
