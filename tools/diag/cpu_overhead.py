@@ -7,9 +7,9 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(os.path.dirname(sys.path[0]), "kungfu_amd", "tuning",
-                                                          "miopen"))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(ROOT, "kungfu_amd", "tuning", "miopen"))
 import torch
 import torch.nn.functional as F
 
@@ -63,6 +63,17 @@ def main():
     print("host enqueue %.2f ms/step, wall %.2f ms/step, gpu %.2f ms/step" % (
         1e3 * (h1 - h0) / n, 1e3 * (h2 - h0) / n, e0.elapsed_time(e1) / n))
     print("host phases (ms/step): " + ", ".join("%s %.2f" % (k, 1e3 * v / n) for k, v in ph.items()))
+    if os.environ.get("CPROFILE"):
+        import cProfile
+        import pstats
+
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(5):
+            step()
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
     kf.finalize()
 
 
