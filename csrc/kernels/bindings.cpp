@@ -779,7 +779,8 @@ at::Tensor conv_flip_weight(at::Tensor w) {
 // KH x KW convolution with zero padding (ph, pw) on the MFMA kernel (Inception-v3 shapes,
 // kfk::conv_rect_supported); stats: optional f64 [kStatSlots*2*Cout] BN-statistics workspace.
 at::Tensor conv_rect(at::Tensor x, at::Tensor w, int64_t stride, int64_t ph, int64_t pw,
-                     c10::optional<at::Tensor> stats, c10::optional<at::Tensor> out) {
+                     c10::optional<at::Tensor> stats, c10::optional<at::Tensor> out, c10::optional<at::Tensor> bn_x,
+                     c10::optional<at::Tensor> bn_fcoef) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_rect: x must be a 4-D channels_last bf16 GPU tensor");
@@ -807,15 +808,29 @@ at::Tensor conv_rect(at::Tensor x, at::Tensor w, int64_t stride, int64_t ph, int
         ea.stats = stats->data_ptr<double>();
         epi = kfk::kEpiFwdStats;
     }
+    const bool bwd = bn_x && bn_x->defined();
+    if (bwd) {
+        // the output is the gradient of a BN+ReLU output whose input is bn_x (forward coefficients
+        // bn_fcoef): stats receives that BN's backward sums (sum dz, sum dz*x) instead
+        TORCH_CHECK(ea.stats && bn_x->scalar_type() == at::kBFloat16 && bn_x->size(0) == N && bn_x->size(1) == K &&
+                        bn_x->size(2) == OH && bn_x->size(3) == OW &&
+                        bn_x->is_contiguous(at::MemoryFormat::ChannelsLast) && bn_x->device() == x.device() &&
+                        bn_fcoef && bn_fcoef->defined() && bn_fcoef->scalar_type() == at::kFloat &&
+                        bn_fcoef->numel() >= 2 * K && bn_fcoef->device() == x.device(),
+                    "conv_rect: bn_x (the BN input, output-shaped) needs stats and bn_fcoef (f32 [scale; shift])");
+        ea.bx = reinterpret_cast<const uint16_t *>(bn_x->data_ptr());
+        ea.fcoef = bn_fcoef->data_ptr<float>();
+        epi = kfk::kEpiBwdCoef;
+    }
     at::Tensor y;
     if (out && out->defined()) {
         // y = out + conv(x, w) in place (e.g. sibling convolutions' data gradients into one dx)
-        TORCH_CHECK(epi == 0 && out->scalar_type() == at::kBFloat16 && out->dim() == 4 && out->size(0) == N &&
+        TORCH_CHECK((epi == 0 || bwd) && out->scalar_type() == at::kBFloat16 && out->dim() == 4 && out->size(0) == N &&
                         out->size(1) == K && out->size(2) == OH && out->size(3) == OW &&
                         out->is_contiguous(at::MemoryFormat::ChannelsLast) && out->device() == x.device(),
                     "conv_rect: out must be the [N, Cout, OH, OW] channels_last bf16 output (no stats)");
         y = *out;
-        epi = kfk::kEpiAccum;
+        epi |= kfk::kEpiAccum;
     } else {
         y = at::empty({N, K, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
     }
@@ -1375,7 +1390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv_rect", &conv_rect, "KH x KW NHWC bf16 convolution with zero padding (MFMA implicit GEMM; "
           "Inception-v3 windows) with an optional BN-statistics epilogue", py::arg("x"), py::arg("w"),
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none(),
-          py::arg("out") = py::none());
+          py::arg("out") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none());
     m.def("conv_rect_supported", &kfk::conv_rect_supported);
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),

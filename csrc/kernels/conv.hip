@@ -645,21 +645,31 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
 }
 
-// Rectangular windows (Inception-v3): plain, BN-statistics or accumulate epilogue, 256x128 / 8 waves when
+// Rectangular windows (Inception-v3): plain, BN-statistics, accumulate and/or BN-backward-sums
+// (the gradient of a BN+ReLU output: sum dz, sum dz*x into the stats slots) epilogue, 256x128 / 8 waves when
 // Cout % 128 == 0, else 256x64.
 template <int KS>
 void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
                    hipStream_t s) {
-    if (epi != 0 && epi != kEpiFwdStats && epi != kEpiAccum)
-        throw std::invalid_argument("conv_rect: epilogue must be none, stats or accumulate");
+    constexpr int A = kEpiAccum, C = kEpiBwdCoef;
     if (g.K % 128 == 0) {
-        if (epi == kEpiFwdStats) launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s);
-        else if (epi == kEpiAccum) launch_epi<KS, 4, 2, 3, kEpiAccum>(x, w, y, g, ea, s);
-        else launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s);
+        switch (epi) {
+        case 0: launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s); break;
+        case kEpiFwdStats: launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s); break;
+        case A: launch_epi<KS, 4, 2, 3, A>(x, w, y, g, ea, s); break;
+        case C: launch_epi<KS, 4, 2, 3, C>(x, w, y, g, ea, s); break;
+        case A | C: launch_epi<KS, 4, 2, 3, A | C>(x, w, y, g, ea, s); break;
+        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
+        }
     } else {
-        if (epi == kEpiFwdStats) launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s);
-        else if (epi == kEpiAccum) launch_epi<KS, 4, 1, 2, kEpiAccum>(x, w, y, g, ea, s);
-        else launch_epi<KS, 4, 1, 2, 0>(x, w, y, g, ea, s);
+        switch (epi) {
+        case 0: launch_epi<KS, 4, 1, 2, 0>(x, w, y, g, ea, s); break;
+        case kEpiFwdStats: launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s); break;
+        case A: launch_epi<KS, 4, 1, 2, A>(x, w, y, g, ea, s); break;
+        case C: launch_epi<KS, 4, 1, 2, C>(x, w, y, g, ea, s); break;
+        case A | C: launch_epi<KS, 4, 1, 2, A | C>(x, w, y, g, ea, s); break;
+        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
+        }
     }
 }
 

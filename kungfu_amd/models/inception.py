@@ -29,7 +29,9 @@ class BasicConv2d(nn.Module):
         else:
             self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x):
+    def forward(self, x, link: bool = False):
+        """``link``: this output's only consumer is another BasicConv2d's (or a sibling group's)
+        stride-1 conv -- its data-gradient epilogue then produces this BN's backward sums."""
         if self.fused and not self.pool_after_conv and self.training and self.bn.track_running_stats:
             # MFMA conv whose epilogue accumulates the BN batch statistics: the BN skips its
             # statistics pass (ops/conv.py conv2d_stats; None if the shape is not on the kernel)
@@ -42,7 +44,7 @@ class BasicConv2d(nn.Module):
                 ws = self.bn.stats_workspace(x.device)
                 y = conv2d_stats(x, w, c.stride, c.padding, ws, master=c.weight)
                 if y is not None:
-                    return self.bn(y, sums=ws)
+                    return self.bn(y, sums=ws, link=link)
         y = self.conv(x)
         if self.pool_after_conv:
             if self.fused:  # HIP 3x3/s1/p1 stencil (forward and backward)
@@ -52,11 +54,21 @@ class BasicConv2d(nn.Module):
             else:
                 y = F.avg_pool2d(y, 3, 1, 1)
         if self.fused:
-            return self.bn(y)
+            return self.bn(y, link=link)
         return F.relu(self.bn(y), inplace=True)
 
 
-def _heads(x, mods):
+def _chain(x, mods, link_last: bool = False):
+    """``mods[-1](...mods[0](x))`` for BasicConv2d modules: every output but the last has the next
+    conv as its only consumer (BN-sums link, see BasicConv2d.forward)."""
+    for i, m in enumerate(mods):
+        nxt = mods[i + 1] if i + 1 < len(mods) else None
+        lk = link_last if nxt is None else nxt.conv.stride in (1, (1, 1))
+        x = m(x, link=lk)
+    return x
+
+
+def _heads(x, mods, links=None):
     """``[m(x) for m in mods]`` for BasicConv2d modules that all read ``x`` (an Inception block's
     branch heads).  Fused training path: their convolutions are ONE autograd node on the MFMA
     kernel (``ops.conv.sibling_convs``: the branch gradients of x are accumulated by the conv
@@ -72,8 +84,10 @@ def _heads(x, mods):
         if ys is not None:
             from ..ops.pool import avg_pool3x3s1
 
-            return [m.bn(avg_pool3x3s1(y)) if m.pool_after_conv else m.bn(y, sums=s) for m, y, s in zip(mods, ys, st)]
-    return [m(x) for m in mods]
+            lks = links or [False] * len(mods)
+            return [m.bn(avg_pool3x3s1(y)) if m.pool_after_conv else m.bn(y, sums=s, link=lk)
+                    for m, y, s, lk in zip(mods, ys, st, lks)]
+    return [m(x, link=lk) for m, lk in zip(mods, links or [False] * len(mods))]
 
 
 def _pool_module():
@@ -110,8 +124,8 @@ class InceptionA(nn.Module):
         self.bp = _branch_pool(cin, pool_features)
 
     def forward(self, x):
-        o1, t5, t3, op = _heads(x, [self.b1, self.b5[0], self.b3[0], self.bp])
-        return torch.cat([o1, self.b5[1](t5), self.b3[2](self.b3[1](t3)), op], 1)
+        o1, t5, t3, op = _heads(x, [self.b1, self.b5[0], self.b3[0], self.bp], [False, True, True, False])
+        return torch.cat([o1, self.b5[1](t5), _chain(t3, list(self.b3[1:])), op], 1)
 
 
 class InceptionB(nn.Module):
@@ -123,7 +137,7 @@ class InceptionB(nn.Module):
                                 BasicConv2d(96, 96, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), self.bd(x), _max_pool3s2(x, self.fused)], 1)
+        return torch.cat([self.b3(x), _chain(x, list(self.bd)), _max_pool3s2(x, self.fused)], 1)
 
 
 class InceptionC(nn.Module):
@@ -141,8 +155,8 @@ class InceptionC(nn.Module):
         self.bp = _branch_pool(cin, 192)
 
     def forward(self, x):
-        o1, t7, td, op = _heads(x, [self.b1, self.b7[0], self.bd[0], self.bp])
-        return torch.cat([o1, self.b7[2](self.b7[1](t7)), self.bd[4](self.bd[3](self.bd[2](self.bd[1](td)))), op], 1)
+        o1, t7, td, op = _heads(x, [self.b1, self.b7[0], self.bd[0], self.bp], [False, True, True, False])
+        return torch.cat([o1, _chain(t7, list(self.b7[1:])), _chain(td, list(self.bd[1:])), op], 1)
 
 
 class InceptionD(nn.Module):
@@ -156,8 +170,8 @@ class InceptionD(nn.Module):
                                 BasicConv2d(192, 192, kernel_size=3, stride=2))
 
     def forward(self, x):
-        t3, t7 = _heads(x, [self.b3[0], self.b7[0]])
-        return torch.cat([self.b3[1](t3), self.b7[3](self.b7[2](self.b7[1](t7))), _max_pool3s2(x, self.fused)], 1)
+        t3, t7 = _heads(x, [self.b3[0], self.b7[0]], [False, True])
+        return torch.cat([self.b3[1](t3), _chain(t7, list(self.b7[1:])), _max_pool3s2(x, self.fused)], 1)
 
 
 class InceptionE(nn.Module):
@@ -174,8 +188,9 @@ class InceptionE(nn.Module):
         self.bp = _branch_pool(cin, 192)
 
     def forward(self, x):
-        o1, b3, bd, op = _heads(x, [self.b1, self.b3_1, self.bd_1, self.bp])
-        bd = self.bd_2(bd)
+        # b3 / bd feed one sibling group each (a single autograd consumer): linked
+        o1, b3, bd, op = _heads(x, [self.b1, self.b3_1, self.bd_1, self.bp], [False, True, True, False])
+        bd = self.bd_2(bd, link=True)
         return torch.cat([o1] + _heads(b3, [self.b3_2a, self.b3_2b]) + _heads(bd, [self.bd_3a, self.bd_3b]) + [op], 1)
 
 
@@ -194,7 +209,10 @@ class InceptionV3(nn.Module):
         self.fc = nn.Linear(2048, num_classes)
 
     def forward(self, x):
-        x = self.blocks(self.stem(x))
+        st = self.stem
+        # conv -> conv links inside the stem (the pools consume stem[2] / stem[5])
+        x = st[3](_chain(x, [st[0], st[1], st[2]]))
+        x = self.blocks(st[6](_chain(x, [st[4], st[5]])))
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 

@@ -183,6 +183,7 @@ class _ConvRectFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.geo = (stride, ph, pw)
         ctx.flip = flip
+        ctx.link = getattr(x, "_kf_link", None)  # x = a BN+ReLU output with this conv its only consumer
         return hip().conv_rect(x, w, stride, ph, pw, stats)
 
     @staticmethod
@@ -197,13 +198,24 @@ class _ConvRectFn(torch.autograd.Function):
             if s == 1:
                 # flipped weights: from the flat space's per-step multi-tensor flip when registered
                 wt = ctx.flip[0].get(ctx.flip[1]) if ctx.flip is not None else hip().conv_flip_weight(w)
-                dx = hip().conv_rect(dy, wt, 1, kh - 1 - ph, kw - 1 - pw)
+                dx = _dgrad_link(dy, wt, kh - 1 - ph, kw - 1 - pw, None, ctx.link)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             dw = _rect_wgrad(dy, x, w, s, ph, pw)
         return dx, dw, None, None, None, None, None
+
+
+def _dgrad_link(dy, wt, ph, pw, out, link):
+    """Stride-1 data gradient ``conv_rect(dy, wt)`` (accumulated into ``out`` if given); with a
+    :class:`~kungfu_amd.ops.fused_bn.BNLink` its epilogue also produces the backward sums of
+    the BN that made the conv input (that BN's backward then skips its reduction)."""
+    if link is None or link.y is None:
+        return hip().conv_rect(dy, wt, 1, ph, pw, None, out)
+    dx = hip().conv_rect(dy, wt, 1, ph, pw, link.ws, out, link.y, link.coef)
+    link.ready, link.dx_ptr = True, dx.data_ptr()
+    return dx
 
 
 def _rect_wgrad(dy, x, w, s, ph, pw):
@@ -233,6 +245,7 @@ class _SiblingConvFn(torch.autograd.Function):
         ys = tuple(hip().conv_rect(x, w, 1, ph, pw, st) for w, (ph, pw), st in zip(ws, pads, stats))
         ctx.save_for_backward(x, *ws)
         ctx.pads, ctx.flips = pads, flips
+        ctx.link = getattr(x, "_kf_link", None)
         return ys
 
     @staticmethod
@@ -240,7 +253,8 @@ class _SiblingConvFn(torch.autograd.Function):
         x, *ws = ctx.saved_tensors
         dx = None
         dws = []
-        for w, dy, (ph, pw), fl in zip(ws, dys, ctx.pads, ctx.flips):
+        last = max((i for i, d in enumerate(dys) if d is not None), default=-1)
+        for i, (w, dy, (ph, pw), fl) in enumerate(zip(ws, dys, ctx.pads, ctx.flips)):
             if dy is None:
                 dws.append(None)
                 continue
@@ -249,7 +263,8 @@ class _SiblingConvFn(torch.autograd.Function):
             if ctx.needs_input_grad[0]:
                 wt = fl[0].get(fl[1]) if fl is not None else hip().conv_flip_weight(w)
                 kh, kw = int(w.shape[2]), int(w.shape[3])
-                dx = hip().conv_rect(dy, wt, 1, kh - 1 - ph, kw - 1 - pw, None, dx)  # dx += (first: =)
+                # dx += (first: =); the last one completes dx, so its epilogue may take the BN sums
+                dx = _dgrad_link(dy, wt, kh - 1 - ph, kw - 1 - pw, dx, ctx.link if i == last else None)
             dws.append(_rect_wgrad(dy, x, w, 1, ph, pw))
         return (dx, None, None, None, *dws)
 

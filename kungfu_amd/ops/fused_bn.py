@@ -58,23 +58,47 @@ def _direct(weight, bias):
     return (tw, tb) if tw is not None and tb is not None else None
 
 
+class BNLink:
+    """Link from a BN+ReLU output to the ONE convolution that consumes it (ops/conv.py): that
+    conv's data gradient IS the gradient of this output, so its epilogue can accumulate this BN's
+    backward sums (sum dz, sum dz*x under the ReLU gate) into ``ws`` -- the BN backward then skips
+    its reduction pass.  ``dx_ptr`` lets the BN check it received exactly that tensor.  Only
+    created where the model guarantees a single consumer (an in-place autograd accumulation
+    of a second consumer's gradient would otherwise keep the pointer but change the values)."""
+    __slots__ = ("ws", "y", "coef", "ready", "dx_ptr")
+
+    def __init__(self, ws, y, coef):
+        self.ws, self.y, self.coef = ws, y, coef
+        self.ready = False
+        self.dx_ptr = 0
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu, nbt, sums=None):
+    def forward(ctx, x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu, nbt, sums=None,
+                link_ws=None):
         y, mean, invstd, coef, mask = hip().bn_forward(x, res, weight, bias, running_mean, running_var, momentum, eps,
                                                        training, relu, nbt, sums)
         ctx.save_for_backward(x, mean, invstd, weight, coef, mask)
         ctx.relu, ctx.training, ctx.has_res = relu, training, res is not None
         ctx.direct = _direct(weight, bias)
+        ctx.link = BNLink(link_ws, x, coef) if link_ws is not None else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, invstd, weight, coef, mask = ctx.saved_tensors
+        link, sums = ctx.link, None
+        if link is not None:
+            if link.ready and dy.data_ptr() == link.dx_ptr:
+                sums = link.ws  # the consumer conv's epilogue produced this BN's backward sums
+            elif link.ready:
+                link.ws.zero_()  # sums of a gradient that is not the one we got: discard
+            link.ready, link.y, link.coef = False, None, None
         dx, dres, dw, db = hip().bn_backward(dy, x, mean, invstd, weight, coef, mask, ctx.relu, ctx.training,
-                                             ctx.has_res)
+                                             ctx.has_res, sums)
         dw, db = _param_grads(ctx, dw, db)
-        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None, None, None
+        return dx, (dres if ctx.has_res else None), dw, db, None, None, None, None, None, None, None, None, None
 
 
 class _BNActPoolFn(torch.autograd.Function):
@@ -99,15 +123,22 @@ class _BNActPoolFn(torch.autograd.Function):
 
 def bn_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
            relu: bool = True, res: Optional[torch.Tensor] = None,
-           num_batches_tracked: Optional[torch.Tensor] = None, sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+           num_batches_tracked: Optional[torch.Tensor] = None, sums: Optional[torch.Tensor] = None,
+           link_ws: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Functional fused BN(+res)(+ReLU); falls back to torch ops when not fusable.
 
     ``num_batches_tracked`` (if given, training mode) is incremented on device.  ``sums``
     (training): batch statistics already accumulated by the producing conv's epilogue
-    (``ops.conv.conv2d_stats``), consumed and re-zeroed -- no statistics pass."""
+    (``ops.conv.conv2d_stats``), consumed and re-zeroed -- no statistics pass.  ``link_ws``
+    (training, BN+ReLU without residual): the output gets a :class:`BNLink` (``._kf_link``) so
+    its single consuming conv produces this BN's backward sums into ``link_ws`` (zeroed)."""
     if _fusable(x, res) and weight is not None and momentum is not None:
-        return _BNActFn.apply(x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu,
-                              num_batches_tracked if training else None, sums if training else None)
+        lw = link_ws if (training and relu and res is None) else None
+        y = _BNActFn.apply(x, res, weight, bias, running_mean, running_var, momentum, eps, training, relu,
+                           num_batches_tracked if training else None, sums if training else None, lw)
+        if lw is not None and y.grad_fn is not None:
+            y._kf_link = y.grad_fn.link
+        return y
     if sums is not None:
         sums.zero_()  # not consumed by the fallback below
     if training and num_batches_tracked is not None:
@@ -147,10 +178,12 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return (self.weight, self.bias, self.running_mean if stats else None, self.running_var if stats else None,
                 use_batch, self.momentum, self.eps), (self.num_batches_tracked if track else None)
 
-    def forward(self, x, sums: Optional[torch.Tensor] = None):
-        """``sums``: batch statistics from the producing conv's epilogue (training only)."""
+    def forward(self, x, sums: Optional[torch.Tensor] = None, link: bool = False):
+        """``sums``: batch statistics from the producing conv's epilogue (training only).
+        ``link``: the output has exactly one consumer, a conv on the MFMA kernel (see bn_act)."""
         a, nbt = self._args()
-        return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt, sums=sums if a[4] else None)
+        lw = self.stats_workspace(x.device) if (link and a[4] and self.track_running_stats) else None
+        return bn_act(x, *a, relu=self.relu, num_batches_tracked=nbt, sums=sums if a[4] else None, link_ws=lw)
 
     def stats_workspace(self, dev) -> torch.Tensor:
         """Zeroed f64 [slots, 2, C] workspace a conv epilogue accumulates this BN's batch

@@ -1346,3 +1346,70 @@ def test_sibling_convs_match_torch(monkeypatch):
     assert _rel(xa.grad, xr.grad) < 2e-2
     for c, w in zip(convs, wr):
         assert _rel(c.weight.grad, w.grad) < 2e-2
+
+
+@needs_gpu
+def test_inception_bn_link_chain(monkeypatch):
+    """BasicConv2d -> BasicConv2d chain with the BN link (the second conv's data-gradient
+    epilogue produces the first BN's backward sums; that BN skips its reduction pass) vs the
+    stock modules in float32, against the bf16 autocast baseline error."""
+    import copy
+
+    import kungfu_amd.ops.fused_bn as fbn
+    import kungfu_amd.parallel.mixed as mixed
+    from kungfu_amd.models import inception as inc
+
+    torch.manual_seed(19)
+    inc._FUSED_BN[0] = True
+    try:
+        fused = [inc.BasicConv2d(64, 96, kernel_size=3, padding=1), inc.BasicConv2d(96, 160, kernel_size=(1, 7),
+                                                                                    padding=(0, 3))]
+    finally:
+        inc._FUSED_BN[0] = False
+    fused = [m.cuda().to(memory_format=torch.channels_last) for m in fused]
+    ref = [inc.BasicConv2d(64, 96, kernel_size=3, padding=1), inc.BasicConv2d(96, 160, kernel_size=(1, 7),
+                                                                              padding=(0, 3))]
+    ref = [m.cuda().to(memory_format=torch.channels_last) for m in ref]
+    for f, r in zip(fused, ref):
+        with torch.no_grad():
+            f.bn.weight.uniform_(0.5, 1.5)
+            f.bn.bias.uniform_(-0.2, 0.2)
+        r.load_state_dict(f.state_dict())
+    lay = copy.deepcopy(ref)
+    monkeypatch.setattr(mixed, "shadow", lambda p: p.bfloat16().contiguous(memory_format=torch.channels_last))
+    used = []
+    orig = fbn.hip
+
+    class _Spy:
+        def __getattr__(self, n):
+            f = getattr(orig(), n)
+            if n != "bn_backward":
+                return f
+
+            def wrapped(*a, **k):
+                used.append(len(a) > 10 and a[10] is not None)
+                return f(*a, **k)
+            return wrapped
+
+    monkeypatch.setattr(fbn, "hip", lambda: _Spy())
+    x = torch.randn(4, 64, 14, 14, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    xf, xr, xl = x.clone().requires_grad_(True), x.float().requires_grad_(True), x.clone().requires_grad_(True)
+    y = inc._chain(xf, fused)
+    assert getattr(fused[0].bn, "_kf_sums", None) is not None
+    yr = ref[1](ref[0](xr))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yl = lay[1](lay[0](xl))
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    yr.backward(g)
+    yl.float().backward(g)
+    assert used == [False, True]  # the second layer's BN reduces itself, the first takes the linked sums
+
+    def nrel(a, b):
+        return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+    assert nrel(xf.grad, xr.grad) <= max(1.5 * nrel(xl.grad, xr.grad), 1e-2)
+    for mf, mr, ml in zip(fused, ref, lay):
+        for (n, p), (_, q), (_, l) in zip(mf.named_parameters(), mr.named_parameters(), ml.named_parameters()):
+            assert nrel(p.grad, q.grad) <= max(1.5 * nrel(l.grad, q.grad), 1e-2), n
+    assert all(float(m.bn._kf_sums.abs().sum()) == 0.0 for m in fused)  # workspaces re-zeroed
