@@ -603,7 +603,7 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     // 7x7 62 -> 100 us), else 256x128 / 8 waves (1x1 included: 4-13 % over 128x128), else 256x64
     if (variant < 0) {
         const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);  // (K % 256 == 0 only)
-        variant = g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
+        variant = g.K <= 32 ? 11 : g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
     }
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
@@ -621,6 +621,7 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
             launch_variant<KS, 4, 2, 2, true, 4, 8>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 64x128
     case 8: if (g.K % 256) throw std::invalid_argument("conv variant 8: Cout % 256");
             launch_variant<KS, 2, 4, 2, true, 8, 4>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 128x64
+    case 11: launch_variant<KS, 4, 1, 2, true, 4, 2>(x, w, y, g, ea, epi, s); break;                // 256x32 (Cout <= 32)
     case 9: if (epi || g.K % 128) throw std::invalid_argument("conv variant 9: epi 0, Cout % 128");    // 256x128, 4w, 128x64
             launch_epi<KS, 2, 2, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
     default: if (epi || g.K % 128) throw std::invalid_argument("conv variant 10: epi 0, Cout % 128");  // 128x128, 2w, 64x128 3st
@@ -628,7 +629,7 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     }
 }
 
-int conv3x3_variants() { return 11; }
+int conv3x3_variants() { return 12; }
 
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
                  int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant) {
@@ -652,7 +653,16 @@ template <int KS>
 void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
                    hipStream_t s) {
     constexpr int A = kEpiAccum, C = kEpiBwdCoef;
-    if (g.K % 128 == 0) {
+    if (g.K <= 32) {  // narrow outputs (Inception's 32-channel stem / pool branch): 256x32 tiles
+        switch (epi) {
+        case 0: launch_epi<KS, 4, 1, 2, 0, 4, 2>(x, w, y, g, ea, s); break;
+        case kEpiFwdStats: launch_epi<KS, 4, 1, 2, kEpiFwdStats, 4, 2>(x, w, y, g, ea, s); break;
+        case A: launch_epi<KS, 4, 1, 2, A, 4, 2>(x, w, y, g, ea, s); break;
+        case C: launch_epi<KS, 4, 1, 2, C, 4, 2>(x, w, y, g, ea, s); break;
+        case A | C: launch_epi<KS, 4, 1, 2, A | C, 4, 2>(x, w, y, g, ea, s); break;
+        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
+        }
+    } else if (g.K % 128 == 0) {
         switch (epi) {
         case 0: launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s); break;
         case kEpiFwdStats: launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s); break;
