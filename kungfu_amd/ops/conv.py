@@ -225,9 +225,13 @@ def _rect_wgrad(dy, x, w, s, ph, pw):
     cin, cout = int(x.shape[1]), int(dy.shape[1])
     if kh == kw and ph == pw == (kh - 1) // 2 and cin % 64 == 0 and cout % 64 == 0:
         return wgrad(dy, x, w, s, ph)  # ResNet-tuned planner (row-image 3x3 kernel etc.)
-    if (_WGRAD and _WGRAD_RECT and min(cin, cout) >= 64 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
+    # measured per Inception-v3 shape (tools/bench_inception_wgrad.py, profiles/r2o_inception_wgrad.txt):
+    # the split-K kernel wins every 1x1 (2-3x) and the multi-tap windows over 128 or >= 256 input
+    # channels; MIOpen keeps the narrow multi-tap ones (48/64/80/96/160/192 inputs: the 64-wide
+    # tiles are padded or the per-tap tiles too small)
+    wide = kh * kw == 1 or cin % 128 == 0 or cin >= 256
+    if (_WGRAD and _WGRAD_RECT and wide and min(cin, cout) >= 32 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
             and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):
-        # (narrow channel counts stay on MIOpen: their zero-padded 64-wide tiles lose)
         return hip().conv_wgrad_rect(dy, x, kh, kw, s, ph, pw)
     return torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
