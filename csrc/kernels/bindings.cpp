@@ -978,7 +978,17 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
                                     c10::optional<at::Tensor> dres_x, c10::optional<at::Tensor> dres_sums) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
-    if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+    // dy may be a channel slice of a wider channels-last tensor (a concatenation's gradient):
+    // read in place with its row stride instead of a contiguous copy
+    int64_t dy_ld = 0;
+    if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) {
+        const int64_t ld = dy.dim() == 4 ? dy.stride(3) : 0;
+        const bool slice = dy.dim() == 4 && dy.stride(1) == 1 && ld >= C && ld % 8 == 0 &&
+                           dy.stride(2) == dy.size(3) * ld && dy.stride(0) == dy.size(2) * dy.size(3) * ld &&
+                           reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0;
+        if (slice) dy_ld = ld;
+        else dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+    }
     TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == x.sizes(), "bn_backward: dy must match x");
     TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() == 2 * C, "bn_backward: fcoef must be 2C f32");
     const uint8_t *mp = nullptr;
@@ -1017,7 +1027,7 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
                             training, partial.defined() ? partial.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
                             db.data_ptr<float>(), coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
                             want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0), sp,
-                            dsx, dsp);
+                            dsx, dsp, dy_ld);
     return {dx, dres, dw, db};
 }
 

@@ -475,6 +475,19 @@ struct DirectGrad {
     __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const { unpack8(r, g); }
 };
 
+// dy is a channel slice of a wider channels-last tensor (row stride ldv 16-byte vectors): the
+// gradient of a branch of a channel concatenation (Inception) read in place, no copy.
+struct StridedGrad {
+    const uint4 *dy;
+    int64_t ldv;
+    using Raw = uint4;
+    template <int CVEC>
+    __device__ __forceinline__ Raw fetch(int64_t /*i*/, int64_t row, int cv) const {
+        return dy[row * ldv + cv];
+    }
+    __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const { unpack8(r, g); }
+};
+
 // dy of the BN output gathered from the max-pool gradient: input pixel (h, w)
 // receives dy_pool of every window (<= 2x2 of them) whose argmax it is.
 struct PoolGrad {
@@ -939,8 +952,16 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
 void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoef, const uint8_t *mask,
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                        uint16_t *dres, hipStream_t s, double *sums, const uint16_t *dres_x, double *dres_sums) {
+                        uint16_t *dres, hipStream_t s, double *sums, const uint16_t *dres_x, double *dres_sums,
+                        int64_t dy_ld) {
     const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
+    if (dy_ld > 0 && dy_ld != sh.channels) {
+        if (dy_ld % 8) throw std::invalid_argument("bn_backward: dy row stride must be a multiple of 8");
+        launch_backward_impl(StridedGrad{reinterpret_cast<const uint4 *>(dy), dy_ld / 8}, x, fcoef, mask, mean, invstd,
+                             gamma, sh, rm, training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x,
+                             dres_sums);
+        return;
+    }
     launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy)}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
                          training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums);
 }

@@ -230,7 +230,8 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                         uint16_t *dres, hipStream_t s, double *sums = nullptr, const uint16_t *dres_x = nullptr,
-                        double *dres_sums = nullptr);
+                        double *dres_sums = nullptr,
+                        int64_t dy_ld = 0);
 // (dres_x / dres_sums: dres also feeds a second, ReLU-free BN with input dres_x -- its backward
 //  sums go to dres_sums, zeroed f64 [slots][2][C])
 // (sums: f64 kStatSlots x [sum dz; sum dz*x] from a conv epilogue -> no reduce pass; re-zeroed.)

@@ -1413,3 +1413,24 @@ def test_inception_bn_link_chain(monkeypatch):
         for (n, p), (_, q), (_, l) in zip(mf.named_parameters(), mr.named_parameters(), ml.named_parameters()):
             assert nrel(p.grad, q.grad) <= max(1.5 * nrel(l.grad, q.grad), 1e-2), n
     assert all(float(m.bn._kf_sums.abs().sum()) == 0.0 for m in fused)  # workspaces re-zeroed
+
+
+@needs_gpu
+@pytest.mark.parametrize("C,off,tot", [(64, 64, 288), (96, 128, 288), (192, 576, 768), (48, 0, 256)])
+def test_bn_backward_channel_slice_grad(H, C, off, tot):
+    """BN backward reading its output gradient as a channel slice of a wider channels-last tensor
+    (the gradient of an Inception concatenation) in place: bit-identical to the contiguous copy."""
+    torch.manual_seed(23)
+    x = torch.randn(4, C, 9, 11, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    w, b = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+    y, mean, invstd, coef, _ = H.bn_forward(x, None, w, b, rm, rv, 0.1, 1e-3, True, True)
+    big = torch.randn(4, tot, 9, 11, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    dy = big[:, off:off + C]
+    assert not dy.is_contiguous(memory_format=torch.channels_last)
+    a = H.bn_backward(dy, x, mean, invstd, w, coef, None, True, True, False)
+    r = H.bn_backward(dy.contiguous(memory_format=torch.channels_last), x, mean, invstd, w, coef, None, True, True,
+                      False)
+    for u, v in zip(a, r):
+        if u is not None and u.numel():
+            assert torch.equal(u, v)
