@@ -523,6 +523,24 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
     return dw;
 }
 
+// Column sums of a contiguous bf16 [T, O] (O % 8 == 0) -> [O] in `dtype` (f32 or bf16).
+at::Tensor colsum(at::Tensor x, at::ScalarType dtype) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
+                    x.size(1) % 8 == 0 && x.size(0) > 0,
+                "colsum: x must be a contiguous bf16 [T, O] GPU tensor with O % 8 == 0");
+    TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "colsum: dtype must be float32 or bfloat16");
+    c10::DeviceGuard gd(x.device());
+    const int64_t T = x.size(0);
+    const int O = static_cast<int>(x.size(1));
+    auto part = at::empty({static_cast<int64_t>(kfk::colsum_chunks(T)) * O}, x.options().dtype(at::kFloat));
+    auto out = at::empty({O}, x.options().dtype(dtype));
+    kfk::launch_colsum_bf16(reinterpret_cast<const uint16_t *>(x.data_ptr()), T, O, part.data_ptr<float>(),
+                            dtype == at::kFloat ? out.data_ptr<float>() : nullptr,
+                            dtype == at::kBFloat16 ? reinterpret_cast<uint16_t *>(out.data_ptr()) : nullptr,
+                            stream_of(x, 0));
+    return out;
+}
+
 // Fused self-attention: qkv [B, S, 3*H*64] bf16 contiguous -> (out [B, S, H*64] bf16, lse [B, H, S] f32)
 std::vector<at::Tensor> attention_forward(at::Tensor qkv, int64_t heads, double scale, int64_t seed, double p_drop) {
     TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
@@ -1406,6 +1424,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1);
+    m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
+          py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "
           "(split-K MFMA GEMM, any channel count % 8)", py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0);

@@ -226,4 +226,79 @@ void launch_gns_update(const float *sumsq_small, const float *sumsq_big, float b
     gns_update_kernel<<<1, 1, 0, s>>>(sumsq_small, sumsq_big, b_small, b_big, alpha, state);
 }
 
+// ---- column sums of a bf16 [T, O] matrix (a linear layer's bias gradient) ---------------
+// Stage 1: block = (row chunk, 64 column vectors of 8): each thread sums its 8 columns over the
+// chunk's rows with 4 rows' loads in flight; partial f32 [chunks][O].  Stage 2: one thread per
+// column sums the chunk partials in order (deterministic).
+namespace {
+constexpr int kColVec = 64;  // 8-column vectors per block (512 columns)
+
+__device__ __forceinline__ void add8(const uint4 &q, float (&acc)[8]) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(w[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+    }
+}
+
+__global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x, int64_t T, int OV, int rows_per,
+                                                     float *__restrict__ part) {
+    const int v = blockIdx.y * kColVec + (threadIdx.x % kColVec);
+    const int rsub = threadIdx.x / kColVec;  // 4 row lanes
+    const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per;
+    int64_t r1 = r0 + rows_per;
+    if (r1 > T) r1 = T;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    if (v < OV) {
+        int64_t r = r0 + rsub;
+        for (; r + 12 < r1; r += 16) {
+            uint4 q[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) q[u] = x[(r + 4 * u) * OV + v];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) add8(q[u], acc);
+        }
+        for (; r < r1; r += 4) {
+            add8(x[r * OV + v], acc);
+        }
+    }
+    __shared__ float red[4][kColVec * 8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[rsub][(threadIdx.x % kColVec) * 8 + k] = acc[k];
+    __syncthreads();
+    const int O = OV * 8;
+    for (int c = threadIdx.x; c < kColVec * 8; c += 256) {
+        const int col = blockIdx.y * kColVec * 8 + c;
+        if (col < O) part[static_cast<int64_t>(blockIdx.x) * O + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    }
+}
+
+__global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int chunks, int O, float *out_f32,
+                                                     uint16_t *out_bf16) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= O) return;
+    float s = 0.f;
+    for (int k = 0; k < chunks; ++k) s += part[static_cast<int64_t>(k) * O + c];
+    if (out_f32) out_f32[c] = s;
+    else out_bf16[c] = f32_to_bf16(s);
+}
+}  // namespace
+
+int colsum_chunks(int64_t T) {
+    int64_t c = (T + 255) / 256;  // >= 256 rows per chunk
+    return static_cast<int>(c < 1 ? 1 : (c > 128 ? 128 : c));
+}
+
+void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float *out_f32, uint16_t *out_bf16,
+                        hipStream_t s) {
+    const int OV = O / 8, chunks = colsum_chunks(T);
+    const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
+    dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
+    colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(x), T, OV, rows_per, part);
+    colsum_stage2<<<(O + 255) / 256, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+}
+
 }  // namespace kfk

@@ -1434,3 +1434,18 @@ def test_bn_backward_channel_slice_grad(H, C, off, tot):
     for u, v in zip(a, r):
         if u is not None and u.numel():
             assert torch.equal(u, v)
+
+
+@needs_gpu
+@pytest.mark.parametrize("T,O", [(16384, 768), (16384, 3072), (300, 2304), (5, 64)])
+def test_colsum_matches_torch(H, T, O):
+    """Bias-gradient column sums (norms.hip) vs the float64 torch sum, f32 and bf16 outputs,
+    and run-to-run bit equality (deterministic two-stage reduction)."""
+    torch.manual_seed(29)
+    x = torch.randn(T, O, device="cuda").bfloat16()
+    ref = x.double().sum(0)
+    a = H.colsum(x, torch.float32)
+    torch.testing.assert_close(a.double(), ref, rtol=1e-4, atol=1e-3)
+    assert torch.equal(a, H.colsum(x, torch.float32))
+    b = H.colsum(x, torch.bfloat16)
+    assert b.dtype == torch.bfloat16 and torch.allclose(b.double(), ref, rtol=1e-2, atol=1e-1)
