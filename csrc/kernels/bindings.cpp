@@ -532,7 +532,7 @@ at::Tensor colsum(at::Tensor x, at::ScalarType dtype) {
     c10::DeviceGuard gd(x.device());
     const int64_t T = x.size(0);
     const int O = static_cast<int>(x.size(1));
-    auto part = at::empty({static_cast<int64_t>(kfk::colsum_chunks(T)) * O}, x.options().dtype(at::kFloat));
+    auto part = at::empty({static_cast<int64_t>(kfk::colsum_chunks(T, O)) * O}, x.options().dtype(at::kFloat));
     auto out = at::empty({O}, x.options().dtype(dtype));
     kfk::launch_colsum_bf16(reinterpret_cast<const uint16_t *>(x.data_ptr()), T, O, part.data_ptr<float>(),
                             dtype == at::kFloat ? out.data_ptr<float>() : nullptr,

@@ -42,7 +42,7 @@ void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, f
 // `partials` needs 2*kMaxGrid floats of scratch.
 // Column sums of a row-major bf16 [T, O] matrix (O % 8 == 0) into f32 or bf16 [O]: a linear
 // layer's bias gradient.  Deterministic two-stage; part: f32 [colsum_chunks(T) * O] scratch.
-int colsum_chunks(int64_t T);
+int colsum_chunks(int64_t T, int O);
 void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float *out_f32, uint16_t *out_bf16,
                         hipStream_t s);
 void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s);

@@ -276,29 +276,44 @@ __global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x
     }
 }
 
+// one block per 32 columns: 8 chunk lanes per column each sum every 8th chunk partial, then the
+// 8 lane sums meet in LDS in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int chunks, int O, float *out_f32,
                                                      uint16_t *out_bf16) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= O) return;
+    __shared__ float red[8][33];
+    const int cl = threadIdx.x & 31, lane = threadIdx.x >> 5;
+    const int c = blockIdx.x * 32 + cl;
     float s = 0.f;
-    for (int k = 0; k < chunks; ++k) s += part[static_cast<int64_t>(k) * O + c];
-    if (out_f32) out_f32[c] = s;
-    else out_bf16[c] = f32_to_bf16(s);
+    if (c < O)
+        for (int k = lane; k < chunks; k += 8) s += part[static_cast<int64_t>(k) * O + c];
+    red[lane][cl] = s;
+    __syncthreads();
+    if (lane == 0 && c < O) {
+        float t = 0.f;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) t += red[l][cl];
+        if (out_f32) out_f32[c] = t;
+        else out_bf16[c] = f32_to_bf16(t);
+    }
 }
 }  // namespace
 
-int colsum_chunks(int64_t T) {
-    int64_t c = (T + 255) / 256;  // >= 256 rows per chunk
-    return static_cast<int>(c < 1 ? 1 : (c > 128 ? 128 : c));
+int colsum_chunks(int64_t T, int O) {
+    // ~512 stage-1 blocks (2 per CU), >= 16 rows per chunk
+    const int colblocks = (O / 8 + kColVec - 1) / kColVec;
+    int64_t c = 512 / colblocks;
+    const int64_t cap = (T + 15) / 16;
+    if (c > cap) c = cap;
+    return static_cast<int>(c < 1 ? 1 : (c > 1024 ? 1024 : c));
 }
 
 void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float *out_f32, uint16_t *out_bf16,
                         hipStream_t s) {
-    const int OV = O / 8, chunks = colsum_chunks(T);
+    const int OV = O / 8, chunks = colsum_chunks(T, O);
     const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(x), T, OV, rows_per, part);
-    colsum_stage2<<<(O + 255) / 256, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+    colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
 }
 
 }  // namespace kfk
