@@ -113,7 +113,7 @@ class ImmediateSink:
 
 def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> int:
     """Switch ``model``'s conv/linear weights to bf16 shadow compute and direct
-    gradients (and, with ``bn_direct``, the fused BN's gamma/beta gradients).
+    gradients (and, with ``bn_direct``, the fused BN's / AddLayerNorm's gamma/beta gradients).
 
     ``optimizer`` is a kungfu_amd optimizer with a flat space (or the space
     itself).  Returns the number of parameters switched to direct gradients.
@@ -140,6 +140,7 @@ def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> i
         return True
 
     from ..ops.fused_bn import BatchNormAct2d
+    from ..ops.layernorm import AddLayerNorm
 
     for m in model.modules():
         if getattr(type(m), "kf_shadow_forward", False):  # takes shadow() in its own forward
@@ -155,7 +156,8 @@ def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> i
                 if m.bias is not None:
                     register(m.bias)
                 m.forward = types.MethodType(_linear_forward, m)
-        elif bn_direct and isinstance(m, BatchNormAct2d):
+        elif bn_direct and isinstance(m, (BatchNormAct2d, AddLayerNorm)):
+            # the fused BN / residual+LayerNorm kernels hand their f32 gamma/beta gradients to the sink
             register(m.weight)
             register(m.bias)
     if getattr(model, "_kf_shadow_hook", None) is None:
