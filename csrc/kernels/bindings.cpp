@@ -732,7 +732,7 @@ at::Tensor avgpool3s1(at::Tensor x) {
 // y, s, mean, rstd = layernorm(x [+ r]) over the last dim (bf16 rows, f32 affine)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_forward(at::Tensor x, c10::optional<at::Tensor> r,
                                                                              at::Tensor gamma, at::Tensor beta,
-                                                                             double eps) {
+                                                                             double eps, double p, int64_t seed) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.is_contiguous(),
                 "layernorm: x must be a contiguous bf16 GPU tensor");
     const int D = static_cast<int>(x.size(-1));
@@ -755,12 +755,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_forward(at:
     kfk::launch_layernorm_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), rp, gamma.data_ptr<float>(),
                                   beta.data_ptr<float>(), reinterpret_cast<uint16_t *>(y.data_ptr()),
                                   rp ? reinterpret_cast<uint16_t *>(sv.data_ptr()) : nullptr, mean.data_ptr<float>(),
-                                  rstd.data_ptr<float>(), rows, D, static_cast<float>(eps), stream_of(x, 0));
+                                  rstd.data_ptr<float>(), rows, D, static_cast<float>(eps), stream_of(x, 0),
+                                  static_cast<float>(p), static_cast<uint32_t>(seed));
     return {y, sv, mean, rstd};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy, at::Tensor s, at::Tensor gamma,
-                                                                  at::Tensor mean, at::Tensor rstd) {
+// Returns (ds, dgamma, dbeta, dr): dr (p > 0 only, else undefined) is the gradient of the dropped
+// residual input.
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy, at::Tensor s,
+                                                                              at::Tensor gamma, at::Tensor mean,
+                                                                              at::Tensor rstd, double p, int64_t seed) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && s.sizes() == dy.sizes() &&
                     s.scalar_type() == at::kBFloat16 && s.is_contiguous(),
                 "layernorm_backward: contiguous bf16 dy and s of equal shape");
@@ -773,12 +777,16 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy,
     auto partial = at::empty({kfk::layernorm_bwd_blocks(rows), 2, D}, dy.options().dtype(at::kFloat));
     auto dgamma = at::empty({D}, dy.options().dtype(at::kFloat));
     auto dbeta = at::empty({D}, dy.options().dtype(at::kFloat));
+    at::Tensor dr;
+    if (p > 0) dr = at::empty_like(dy);
     kfk::launch_layernorm_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                                    reinterpret_cast<const uint16_t *>(s.data_ptr()), gamma.data_ptr<float>(),
                                    mean.data_ptr<float>(), rstd.data_ptr<float>(),
                                    reinterpret_cast<uint16_t *>(ds.data_ptr()), partial.data_ptr<float>(),
-                                   dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, stream_of(dy, 0));
-    return {ds, dgamma, dbeta};
+                                   dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, stream_of(dy, 0),
+                                   dr.defined() ? reinterpret_cast<uint16_t *>(dr.data_ptr()) : nullptr,
+                                   static_cast<float>(p), static_cast<uint32_t>(seed));
+    return {ds, dgamma, dbeta, dr};
 }
 
 // [Cout, Cin, KS, KS] channels_last -> flipped/transposed [Cin, Cout, KS, KS] channels_last
@@ -1443,8 +1451,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("maxpool3s2_backward", &maxpool3s2_backward, "3x3/s2 max-pool gradient (gather via the argmax bytes)");
     m.def("layernorm_supported", &kfk::layernorm_supported);
     m.def("layernorm_forward", &layernorm_forward, "fused residual-add + LayerNorm (bf16 rows) -> (y, s, mean, rstd)",
-          py::arg("x"), py::arg("r"), py::arg("gamma"), py::arg("beta"), py::arg("eps"));
-    m.def("layernorm_backward", &layernorm_backward, "LayerNorm backward -> (ds, dgamma, dbeta)");
+          py::arg("x"), py::arg("r"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p") = 0.0,
+          py::arg("seed") = 0);
+    m.def("layernorm_backward", &layernorm_backward, "LayerNorm backward -> (ds, dgamma, dbeta, dr or None)",
+          py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("p") = 0.0,
+          py::arg("seed") = 0);
     m.def("global_avgpool_forward", &global_avgpool_forward, "global average pool, NHWC bf16 -> [N, C]");
     m.def("global_avgpool_backward", &global_avgpool_backward, "global average pool backward -> NHWC bf16",
           py::arg("dy"), py::arg("H"), py::arg("W"));

@@ -279,16 +279,20 @@ void launch_avgpool3s1(const uint16_t *x, uint16_t *y, int64_t N, int H, int W, 
 void launch_global_avgpool_forward(const uint16_t *x, uint16_t *y, int64_t N, int HW, int C, hipStream_t s);
 void launch_global_avgpool_backward(const uint16_t *dy, uint16_t *dx, int64_t N, int HW, int C, hipStream_t s);
 
+// (p > 0: dropout on the residual input r with a hashed keep mask of (seed, element); the
+// backward then also writes dr, the dropped residual's gradient.)
 // Fused residual-add + LayerNorm over rows of D (layernorm.hip): bf16 x, r (optional), y, s
 // (= x + r, saved for backward), f32 gamma/beta/mean/rstd; backward -> ds (bf16) and
 // dgamma/dbeta (f32) through [blocks][2][D] f32 partials.
 bool layernorm_supported(int D);
 int layernorm_bwd_blocks(int64_t rows);
 void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
-                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st);
+                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st,
+                              float p = 0.f, uint32_t seed = 0);
 void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
                                const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
-                               int64_t rows, int D, hipStream_t st);
+                               int64_t rows, int D, hipStream_t st,
+                               uint16_t *dr = nullptr, float p = 0.f, uint32_t seed = 0);
 // gate_stats != nullptr: x is a ReLU output, dx = that ReLU's input gradient (window max > 0 only)
 // and the per-channel sums of dx go to gate_stats[slot][0][C] (kStatSlots x 2 x C f64, zeroed)
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,

@@ -11,6 +11,11 @@
 // step (profiles/r2b_bert_base_gns.md).  Here the residual stream stays bf16 and each
 // direction is one pass over the activations plus a tiny column reduction.
 //
+// Residual dropout (BERT's dropout(dense(x)) before the add): with p > 0 the residual input r
+// is dropped and scaled in the forward, r' = keep(e) ? r / (1 - p) : 0, from a counter hash
+// of (seed, element index) -- no mask tensor; the backward recomputes keep(e) and writes
+// dr = keep(e) ? ds / (1 - p) : 0 beside ds (replacing torch's dropout and masked-scale passes).
+//
 // Layout: rows of D contiguous elements (D % 256 == 0, D <= 4096).  One wave64 per row;
 // lane l owns the 4-element groups l, l + 64, l + 128, ... (8-byte accesses, coalesced
 // across the wave), so each lane's columns are FIXED: the backward accumulates its
@@ -39,13 +44,30 @@ __device__ __forceinline__ uint2 pack4(const float (&f)[4]) {
                       static_cast<uint32_t>(f32_to_bf16(f[2])) | (static_cast<uint32_t>(f32_to_bf16(f[3])) << 16));
 }
 
+struct LnDrop {
+    uint32_t seed = 0, thresh = 0;  // keep(e) <=> hash(seed, e) >= thresh (thresh = p * 2^32)
+    float inv_keep = 1.f;
+    bool on = false;
+};
+
+__device__ __forceinline__ bool ln_keep(const LnDrop &d, int64_t e) {
+    uint32_t h = static_cast<uint32_t>(e) * 0x9E3779B1u ^ static_cast<uint32_t>(e >> 32) * 0x7FEB352Du ^ d.seed;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h >= d.thresh;
+}
+
 template <int G>  // G = D / 256 four-element groups per lane
 __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const uint2 *__restrict__ x,
                                                                const uint2 *__restrict__ r,
                                                                const float *__restrict__ gamma,
                                                                const float *__restrict__ beta, uint2 *__restrict__ y,
                                                                uint2 *__restrict__ s_out, float *__restrict__ mean,
-                                                               float *__restrict__ rstd, int64_t rows, float eps) {
+                                                               float *__restrict__ rstd, int64_t rows, float eps,
+                                                               LnDrop drop) {
     constexpr int D = 256 * G;
     const int lane = threadIdx.x & 63;
     float gm[G][4], bt[G][4];
@@ -67,6 +89,11 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const uint2 *__re
             if (r) {
                 float t[4];
                 unpack4(r[base + j * 64 + lane], t);
+                if (drop.on) {
+                    const int64_t e0 = (base + j * 64 + lane) * 4;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) t[k] = ln_keep(drop, e0 + k) ? t[k] * drop.inv_keep : 0.f;
+                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) v[j][k] += t[k];
             }
@@ -107,7 +134,8 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
                                                                const float *__restrict__ gamma,
                                                                const float *__restrict__ mean,
                                                                const float *__restrict__ rstd, uint2 *__restrict__ ds,
-                                                               float *__restrict__ partial, int64_t rows) {
+                                                               float *__restrict__ partial, int64_t rows,
+                                                               uint2 *__restrict__ dr, LnDrop drop) {
     constexpr int D = 256 * G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float gm[G][4], dg[G][4], db[G][4];
@@ -146,6 +174,12 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
 #pragma unroll
             for (int k = 0; k < 4; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
             ds[base + j * 64 + lane] = pack4(o);
+            if (dr) {  // gradient of the dropped residual input
+                const int64_t e0 = (base + j * 64 + lane) * 4;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k] = ln_keep(drop, e0 + k) ? o[k] * drop.inv_keep : 0.f;
+                dr[base + j * 64 + lane] = pack4(o);
+            }
         }
     }
     // block reduction of the per-lane column sums -> partial[block][2][D]
@@ -220,8 +254,22 @@ int layernorm_bwd_blocks(int64_t rows) {
     return static_cast<int>(b < 1 ? 1 : b);
 }
 
+static LnDrop make_drop(float p, uint32_t seed) {
+    LnDrop d;
+    if (p > 0.f) {
+        if (p >= 1.f) throw std::invalid_argument("layernorm: dropout p must be < 1");
+        d.on = true;
+        d.seed = seed;
+        d.thresh = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
+        d.inv_keep = 1.f / (1.f - p);
+    }
+    return d;
+}
+
 void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
-                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st) {
+                              uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st,
+                              float p, uint32_t seed) {
+    const LnDrop drop = make_drop(r ? p : 0.f, seed);
     if (rows <= 0) return;
     int64_t blocks = (rows + kLnWaves - 1) / kLnWaves;
     if (blocks > 8192) blocks = 8192;
@@ -229,20 +277,22 @@ void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float 
         constexpr int G = decltype(gc)::value;
         ln_fwd_kernel<G><<<static_cast<int>(blocks), 64 * kLnWaves, 0, st>>>(
             reinterpret_cast<const uint2 *>(x), reinterpret_cast<const uint2 *>(r), gamma, beta,
-            reinterpret_cast<uint2 *>(y), reinterpret_cast<uint2 *>(s), mean, rstd, rows, eps);
+            reinterpret_cast<uint2 *>(y), reinterpret_cast<uint2 *>(s), mean, rstd, rows, eps, drop);
     });
 }
 
 void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
                                const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
-                               int64_t rows, int D, hipStream_t st) {
+                               int64_t rows, int D, hipStream_t st, uint16_t *dr, float p, uint32_t seed) {
     if (rows <= 0) return;
+    const LnDrop drop = make_drop(dr ? p : 0.f, seed);
     const int blocks = layernorm_bwd_blocks(rows);
     dispatch_g(D, [&](auto gc) {
         constexpr int G = decltype(gc)::value;
         ln_bwd_kernel<G><<<blocks, 64 * kLnWaves, 0, st>>>(reinterpret_cast<const uint2 *>(dy),
                                                             reinterpret_cast<const uint2 *>(s), gamma, mean, rstd,
-                                                            reinterpret_cast<uint2 *>(ds), partial, rows);
+                                                            reinterpret_cast<uint2 *>(ds), partial, rows,
+                                                            reinterpret_cast<uint2 *>(dr), drop);
     });
     ln_colsum_kernel<<<(2 * D + 63) / 64, 64 * kColGroups, 0, st>>>(partial, blocks, 2 * D, dgamma, dbeta, D);
 }

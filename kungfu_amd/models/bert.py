@@ -39,9 +39,10 @@ class BertLayer(nn.Module):
             q, k, v = qkv.view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
             a = a.transpose(1, 2).reshape(B, S, D)
-        x = self.ln1(x, F.dropout(self.out(a), self.dropout, self.training))
+        # residual dropout fused into the add + LayerNorm kernels (ops/layernorm.py)
+        x = self.ln1(x, self.out(a), dropout=self.dropout)
         h = self.fc2(F.gelu(self.fc1(x)))
-        return self.ln2(x, F.dropout(h, self.dropout, self.training))
+        return self.ln2(x, h, dropout=self.dropout)
 
 
 class BertForPreTraining(nn.Module):

@@ -20,12 +20,13 @@ from .._lib import hip, hip_available
 
 class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps):
+    def forward(ctx, x, r, gamma, beta, eps, p=0.0, seed=0):
         from ..parallel.mixed import direct_target
 
-        y, s, mean, rstd = hip().layernorm_forward(x, r, gamma, beta, eps)
+        y, s, mean, rstd = hip().layernorm_forward(x, r, gamma, beta, eps, p, seed)
         ctx.save_for_backward(s, gamma, mean, rstd)
         ctx.has_r = r is not None
+        ctx.p, ctx.seed = (p, seed) if r is not None else (0.0, 0)
         tg, tb = direct_target(gamma), direct_target(beta)
         ctx.direct = (tg, tb) if tg is not None and tb is not None else None
         return y
@@ -33,7 +34,7 @@ class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         s, gamma, mean, rstd = ctx.saved_tensors
-        ds, dg, db = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd)
+        ds, dg, db, dr = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd, ctx.p, ctx.seed)
         if ctx.direct is not None:
             # gamma / beta gradients to the flat space's sink (landed with their bucket by one
             # multi-tensor kernel instead of an AccumulateGrad add each: 48 launches in BERT-base)
@@ -42,8 +43,10 @@ class _AddLayerNormFn(torch.autograd.Function):
             deliver(ctx.direct[0], dg)
             deliver(ctx.direct[1], db)
             dg = db = None
-        # d(x + r)/dx = d(x + r)/dr = 1: both inputs receive ds
-        return ds, (ds if ctx.has_r else None), dg, db, None
+        # d(x + r)/dx = d(x + r)/dr = 1: both inputs receive ds (the dropped r: ds * keep / (1-p))
+        if ctx.has_r and dr is None:
+            dr = ds
+        return ds, (dr if ctx.has_r else None), dg, db, None, None, None
 
 
 def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bool:
@@ -55,16 +58,22 @@ def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bo
 
 
 def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, bias: torch.Tensor,
-                   eps: float = 1e-5) -> torch.Tensor:
-    """``F.layer_norm(x + residual, (D,), weight, bias, eps)``."""
+                   eps: float = 1e-5, dropout: float = 0.0, training: bool = False) -> torch.Tensor:
+    """``F.layer_norm(x + F.dropout(residual, dropout, training), (D,), weight, bias, eps)``; on the
+    HIP kernels the dropout is fused (hashed keep mask, recomputed in the backward)."""
+    p = float(dropout) if training and residual is not None else 0.0
     if _eligible(x, residual, weight):
-        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps))
+        seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if p > 0 else 0  # CPU generator: no device sync
+        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed)
+    if p > 0:
+        residual = F.dropout(residual, p, True)
     s = x if residual is None else x + residual
     return F.layer_norm(s, s.shape[-1:], weight, bias, eps)
 
 
 class AddLayerNorm(nn.LayerNorm):
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, dropout: float = 0.0):
+        """``layer_norm(x + dropout(residual))`` (``dropout`` active in training mode only)."""
         if residual is not None and residual.dtype != x.dtype and x.is_cuda:
             residual = residual.to(x.dtype)  # e.g. an f32 dropout output beside a bf16 stream
-        return add_layer_norm(x, residual, self.weight, self.bias, self.eps)
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout, self.training)

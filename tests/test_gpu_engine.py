@@ -287,3 +287,42 @@ def test_add_layernorm_matches_fp32(D, rows, res):
     assert rel(xa.grad, xr.grad) < 2e-2 and rel(wa.grad, wr.grad) < 1e-2 and rel(ba.grad, br.grad) < 1e-3
     if res:
         assert torch.equal(xa.grad, ra.grad) and rel(ra.grad, rr.grad) < 2e-2
+
+
+@needs_gpu
+def test_add_layernorm_fused_residual_dropout():
+    """Residual dropout fused into the add + LayerNorm kernels: the hashed keep mask (recomputed
+    in torch below) reproduces y = LN(x + r * keep / (1 - p)) and the gradients (dx = ds,
+    dr = ds * keep / (1 - p)) of the float32 composition; keep rate ~ 1 - p."""
+    import torch.nn.functional as F
+
+    from kungfu_amd._lib import hip
+    from kungfu_amd.ops.layernorm import _AddLayerNormFn
+
+    torch.manual_seed(31)
+    rows, D, p, seed = 4096, 768, 0.1, 12345
+    x = torch.randn(rows, D, device="cuda").bfloat16()
+    r = torch.randn(rows, D, device="cuda").bfloat16()
+    g, b = torch.rand(D, device="cuda") + 0.5, torch.randn(D, device="cuda") * 0.1
+    M = 0xFFFFFFFF
+    e = torch.arange(rows * D, device="cuda", dtype=torch.int64)
+    h = (((e & M) * 0x9E3779B1) & M) ^ ((((e >> 32) * 0x7FEB352D) & M)) ^ seed
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M
+    h ^= h >> 16
+    keep = (h >= int(p * 2**32)).view(rows, D)
+    assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+    xa, ra = x.clone().requires_grad_(True), r.clone().requires_grad_(True)
+    y = _AddLayerNormFn.apply(xa, ra, g, b, 1e-12, p, seed)
+    xr, rr = x.float().requires_grad_(True), r.float().requires_grad_(True)
+    yr = F.layer_norm(xr + rr * keep / (1 - p), (D,), g, b, 1e-12)
+    assert ((y.float() - yr).norm() / yr.norm()).item() < 1e-2
+    dy = torch.randn(rows, D, device="cuda")
+    y.backward(dy.bfloat16())
+    yr.backward(dy)
+    for a, c in ((xa.grad, xr.grad), (ra.grad, rr.grad)):
+        assert ((a.float() - c).norm() / c.norm()).item() < 2e-2
+    assert torch.equal(ra.grad == 0, ~keep | (xa.grad == 0))
+    del hip
