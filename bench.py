@@ -65,11 +65,55 @@ def _setup_env():
     os.environ.setdefault("MIOPEN_USER_DB_PATH", tdir)
     os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", tdir)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # failure detection: a stalled RCCL collective or host op ends the run with a
+    # message naming the op and rank (exit 3) instead of hanging until an outer timeout
+    os.environ.setdefault("KUNGFU_RCCL_TIMEOUT_S", "300")
+    os.environ.setdefault("KUNGFU_OP_TIMEOUT_S", "900")
+
+
+def _launcher_env() -> bool:
+    return "KUNGFU_SELF_SPEC" in os.environ or "WORLD_SIZE" in os.environ
+
+
+def _self_launch(n: int) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N ranks (one per GPU) with
+    ``torch.distributed.run`` as CHILD processes and return their exit status.  The
+    parent never touches the GPU (no HIP call before or after), so nothing is
+    re-exec'd from a process holding a device context; rank 0's JSON line reaches
+    stdout through the inherited file descriptors."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench.py: launching %d ranks: %s" % (n, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def _replica_checksum(opt, model):
+    """(sum, weighted sum) in float64 over every trainable parameter -- equal on every
+    rank iff the replicas are (bitwise up to f64 summation) identical."""
+    import torch
+
+    space = getattr(opt, "space", None)
+    ps = [space.flat_param] if space is not None else [p.detach().reshape(-1) for p in model.parameters()]
+    tot = torch.zeros(2, dtype=torch.float64, device=ps[0].device)
+    for f in ps:
+        f64 = f.detach().double()
+        w = torch.arange(1, f64.numel() + 1, device=f64.device, dtype=torch.float64).remainder_(977.0).add_(1.0)
+        tot[0] += f64.sum()
+        tot[1] += (f64 * w).sum()
+    return tot.cpu()
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (ranks) on this node; > 1 without a launcher env self-launches N ranks")
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--batch", type=int, default=None, help="images (sequences) per GPU: 256 (BERT: 128)")
@@ -87,7 +131,13 @@ def main():
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--json-out", default=None)
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
+    p.add_argument("--image-size", type=int, default=224)
     a = p.parse_args()
+    if a.gpus is not None and a.gpus > 1 and not _launcher_env():
+        sys.exit(_self_launch(a.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "0")) or None
     bert = a.model.startswith("bert")
     if a.batch is None:
         a.batch = 128 if bert else 256
@@ -103,11 +153,26 @@ def main():
 
     kf.init()
     rank, size = kf.current_rank(), kf.current_cluster_size()
+    if a.gpus is None:
+        a.gpus = size
+    if size != a.gpus or (world_env is not None and world_env != size):
+        print("bench.py: --gpus %d but the job has %d ranks (WORLD_SIZE=%s); refusing to report a mislabelled "
+              "number" % (a.gpus, size, world_env), file=sys.stderr, flush=True)
+        sys.exit(2)
     dev_idx = kf.get_hip_index()
-    torch.cuda.set_device(dev_idx)
-    dev = torch.device("cuda", dev_idx)
+    cuda = a.device == "cuda"
+    if cuda:
+        torch.cuda.set_device(dev_idx)
+        dev = torch.device("cuda", dev_idx)
+    else:
+        dev = torch.device("cpu")
+        a.bf16_shadow = 0
+
+    def sync():
+        if cuda:
+            sync()
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode + in-tree find-db
-    torch.manual_seed(1234)
+    torch.manual_seed(1234)  # same init everywhere (broadcast_parameters makes it exact)
 
     fused_bn = a.fused_bn
     if fused_bn < 0:
@@ -118,7 +183,7 @@ def main():
              else get_model(a.model))
     model = model.to(dev)
     if not bert:
-        model = model.to(memory_format=torch.channels_last)
+        model = model.to(memory_format=torch.channels_last) if cuda else model
     if a.adam:
         base = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
         opt_desc = "AdamW lr=1e-4 wd=0.01"
@@ -150,6 +215,9 @@ def main():
 
         enable_bf16_shadow(model, opt)
 
+    # every rank draws its own synthetic batch, so identical replicas at the end prove
+    # that the gradient exchange (not identical inputs) kept them in step
+    torch.manual_seed(1234 + 7919 * rank)
     if bert:
         from kungfu_amd.models.bert import pretraining_loss, synthetic_pretraining_batch
 
@@ -158,7 +226,8 @@ def main():
         def compute_loss():
             return pretraining_loss(model, data)
     else:
-        x = torch.randn(a.batch, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+        x = torch.randn(a.batch, 3, a.image_size, a.image_size, device=dev)
+        x = x.to(memory_format=torch.channels_last) if cuda else x
         y = torch.randint(0, 1000, (a.batch,), device=dev)
 
         def compute_loss():
@@ -166,7 +235,7 @@ def main():
 
     def step():
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=cuda):
             loss = compute_loss()
         loss.backward()
         opt.step()
@@ -178,23 +247,53 @@ def main():
         l0 = step()
         if i == 0:
             first_loss = float(l0.detach())
-    torch.cuda.synchronize()
+    sync()
     warm_s = time.time() - t_w0
 
     kf.run_barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     kf.run_barrier()
     dt = time.perf_counter() - t0
-    # max over ranks
-    dt_t = torch.tensor([dt], dtype=torch.float64)
-    dt_max = float(kf.ops.all_reduce(dt_t, op="max")[0]) if size > 1 else dt
+    # max over ranks (host transport, outside the timed region); per-rank spread
+    dt_all = (kf.ops.all_gather(torch.tensor([dt], dtype=torch.float64)).view(-1).tolist() if size > 1 else [dt])
+    dt_max = max(dt_all)
     value = a.batch * size * a.steps / dt_max
     reducer = getattr(opt, "reducer", None)
     comm_info = reducer.describe() if reducer is not None else {"comm_ranks": size}
+    # replica consistency: after synchronous training every rank holds the same weights
+    ck = _replica_checksum(opt, model)
+    cks = kf.ops.all_gather(ck).view(size, 2) if size > 1 else ck.view(1, 2)
+    sync_algo = a.optimizer in ("ssgd", "gns")
+    consistent = bool((cks == cks[0:1]).all()) if sync_algo else None
+    try:
+        rccl_ver = kf.show_rccl_version()
+    except Exception:
+        rccl_ver = None
+    from kungfu_amd._lib import hip as _hip_mod
+
+    try:
+        wd = dict(_hip_mod().rccl_watchdog_info())
+    except Exception:
+        wd = None
+    verify = {
+        "launch": kf.launch_mode(),
+        "world_size": size,
+        "comm_ranks": comm_info.get("comm_ranks", size),
+        "comm_plane": comm_info.get("comm_plane"),
+        "rccl_version": rccl_ver,
+        "per_rank_img_s": {"min": round(a.batch * a.steps / max(dt_all), 2),
+                           "max": round(a.batch * a.steps / min(dt_all), 2)},
+        "replicas_consistent": consistent,
+        "replica_checksum": [float(x) for x in cks[0].tolist()],
+        "rccl_watchdog": ({"ops_watched": wd["registered"], "pending": wd["pending"], "timeout_s": wd["timeout_s"]}
+                          if wd else None),
+    }
+    if sync_algo and not consistent:
+        print("bench.py: REPLICAS DIVERGED: per-rank checksums %s" % cks.tolist(), file=sys.stderr, flush=True)
     metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
     unit = "sequences/sec (aggregate over n_gpus)" if bert else "images/sec (aggregate over n_gpus)"
     res = {
@@ -208,16 +307,16 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": round(value / (base_per_gpu * size), 3) if base_per_gpu else None,
-        "dtype": "bf16",
+        "dtype": "bf16" if cuda else "f32",
         "data": ("synthetic (random token ids, 20 masked positions per sequence, random MLM/NSP labels; "
                  "random-init weights)" if bert else
-                 "synthetic (random 224x224x3 images, random labels; random-init weights)"),
+                 "synthetic (random %dx%dx3 images, random labels; random-init weights)" % (a.image_size, a.image_size)),
         "config": {
             "model": a.model,
             "global_batch": a.batch * size,
             "per_gpu_batch": a.batch,
             "seq_len": a.seq_len if bert else None,
-            "image_size": None if bert else 224,
+            "image_size": None if bert else a.image_size,
             "parallelism": "dp%d" % size,
             "optimizer": "%s(%s)" % (a.optimizer, opt_desc),
             "fused_bn_hip": bool(fused_bn),
@@ -231,6 +330,7 @@ def main():
             "final_loss": round(float(loss.detach()), 4),
             "comm": comm_info,
         },
+        "verify": verify,
     }
     if rank == 0:
         line = json.dumps(res)
@@ -239,6 +339,8 @@ def main():
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     kf.finalize()
+    if sync_algo and not consistent:
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstdint>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -49,6 +50,27 @@ class StallDetector {
     bool done_ = false;
     std::thread th_;
 };
+
+// Host-op watchdog (parity: the reference's stall detector around every collective,
+// srcs/go/libkungfu-comm/main.go:163-179, turned into a failure detector).  Every
+// collective of the host runtime holds an OpWatch for its duration; one process-wide
+// thread checks them and, when an op has run longer than KUNGFU_OP_TIMEOUT_S (a
+// duration: "90", "2m"; unset or 0 = disabled), prints the op name and this peer's
+// label and terminates the process with exit status 3 (a hung peer would otherwise
+// block the whole job until an outer timeout, leaving nothing to diagnose).
+class OpWatch {
+  public:
+    explicit OpWatch(const std::string &name);
+    ~OpWatch();
+    OpWatch(const OpWatch &) = delete;
+    OpWatch &operator=(const OpWatch &) = delete;
+
+  private:
+    uint64_t id_ = 0;
+};
+void op_watchdog_set_label(const std::string &label);
+double op_watchdog_timeout();  // seconds, 0 = disabled
+void op_watchdog_set_timeout(double seconds);
 
 // Scoped timer aggregated per name; report printed at process exit when
 // KUNGFU_CONFIG_ENABLE_TRACE is set.

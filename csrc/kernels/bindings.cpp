@@ -1289,39 +1289,45 @@ at::Tensor ipc_open(py::bytes handle, int64_t numel, int64_t device) {
 
 class Comm {
   public:
-    Comm(py::bytes id, int rank, int size, int device) : c_(new kfk::RcclComm(std::string(id), rank, size, device)) {}
+    Comm(py::bytes id, int rank, int size, int device, double init_timeout_s) {
+        std::string sid(id);
+        py::gil_scoped_release nogil;  // init polls its deadline; other threads keep running
+        c_.reset(new kfk::RcclComm(sid, rank, size, device, init_timeout_s));
+    }
     int rank() const { return c_->rank(); }
     int size() const { return c_->size(); }
     bool valid() const { return c_->valid(); }
-    void all_reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t stream) {
+    bool blocking() const { return c_->blocking(); }
+    void all_reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t stream, const std::string &tag) {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(in.numel() == out.numel(), "all_reduce: size mismatch");
         c_->all_reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
-                       stream_of(in, stream));
+                       stream_of(in, stream), tag.c_str());
     }
-    void broadcast(at::Tensor t, int64_t root, int64_t stream) {
+    void broadcast(at::Tensor t, int64_t root, int64_t stream, const std::string &tag) {
         check_gpu(t, "t");
         c_->broadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(root),
-                      stream_of(t, stream));
+                      stream_of(t, stream), tag.c_str());
     }
-    void reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t root, int64_t stream) {
+    void reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t root, int64_t stream, const std::string &tag) {
         check_gpu(in, "in");
         c_->reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
-                   static_cast<int>(root), stream_of(in, stream));
+                   static_cast<int>(root), stream_of(in, stream), tag.c_str());
     }
-    void all_gather(at::Tensor in, at::Tensor out, int64_t stream) {
+    void all_gather(at::Tensor in, at::Tensor out, int64_t stream, const std::string &tag) {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(out.numel() == in.numel() * c_->size(), "all_gather: out must hold size*numel(in)");
-        c_->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), stream_of(in, stream));
+        c_->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), stream_of(in, stream),
+                       tag.c_str());
     }
-    void reduce_scatter(at::Tensor in, at::Tensor out, int64_t op, int64_t stream) {
+    void reduce_scatter(at::Tensor in, at::Tensor out, int64_t op, int64_t stream, const std::string &tag) {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(in.numel() == out.numel() * c_->size(), "reduce_scatter: in must hold size*numel(out)");
         c_->reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), dtype_code(in), static_cast<int>(op),
-                           stream_of(in, stream));
+                           stream_of(in, stream), tag.c_str());
     }
     void send(at::Tensor t, int64_t peer, int64_t stream) {
         check_gpu(t, "t");
@@ -1331,6 +1337,12 @@ class Comm {
         check_gpu(t, "t");
         c_->recv(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
     }
+    void group_start() { c_->group_start(); }
+    void group_end() { c_->group_end(); }
+    void watch(int64_t stream, const std::string &what) {
+        c_->watch(reinterpret_cast<hipStream_t>(stream), what);
+    }
+    int async_error() { return c_->async_error(); }
     // Graph all-reduce on the device: one round = one grouped batch of send/recv
     // (kungfu::plan_graph_all_reduce), then the K1 reduce kernel for every received
     // partial (buf[off:off+len] = op(buf[...], scratch[sc:sc+len])).  Every rank must run
@@ -1366,7 +1378,7 @@ class Comm {
         auto s = stream_of(buf, stream);
         for (const auto &r : rounds) {
             if (r.empty()) continue;
-            kfk::RcclComm::group_start();
+            c_->group_start();
             for (const auto &x : r) {
                 const int peer = std::get<1>(x);
                 const int64_t off = std::get<2>(x), len = std::get<3>(x), sc = std::get<4>(x);
@@ -1377,7 +1389,7 @@ class Comm {
                     c_->send(base + off * esz, len, dt, peer, s);
                 }
             }
-            kfk::RcclComm::group_end();
+            c_->group_end();
             for (const auto &x : r) {
                 const int64_t off = std::get<2>(x), len = std::get<3>(x), sc = std::get<4>(x);
                 if (std::get<0>(x) && sc >= 0)
@@ -1385,8 +1397,12 @@ class Comm {
                                        static_cast<int>(op), s);
             }
         }
+        c_->watch(s, "GraphAllReduce(" + std::to_string(rounds.size()) + " rounds, " + std::to_string(n) + " elems)");
     }
-    void destroy() { c_->destroy(); }
+    void destroy() {
+        py::gil_scoped_release nogil;
+        c_->destroy();
+    }
     void abort() { c_->abort(); }
 
   private:
@@ -1521,21 +1537,39 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");
     m.def("rccl_unique_id", [] { return py::bytes(kfk::RcclComm::unique_id()); });
     m.def("rccl_version", &kfk::RcclComm::version);
-    m.def("rccl_group_start", &kfk::RcclComm::group_start);
-    m.def("rccl_group_end", &kfk::RcclComm::group_end);
+    m.def("rccl_watchdog_info", [] {
+        const auto i = kfk::watchdog_info();
+        py::dict d;
+        d["registered"] = i.registered;
+        d["completed"] = i.completed;
+        d["pending"] = i.pending;
+        d["oldest_s"] = i.oldest_s;
+        d["timeout_s"] = i.timeout_s;
+        return d;
+    });
+    m.def("rccl_watchdog_set_label", &kfk::watchdog_set_label);
+    m.def("rccl_watchdog_set_timeout", &kfk::watchdog_set_timeout);
     py::class_<Comm>(m, "RcclComm")
-        .def(py::init<py::bytes, int, int, int>())
+        .def(py::init<py::bytes, int, int, int, double>(), py::arg("uid"), py::arg("rank"), py::arg("size"),
+             py::arg("device"), py::arg("init_timeout_s") = 0.0)
         .def("rank", &Comm::rank)
         .def("size", &Comm::size)
         .def("valid", &Comm::valid)
+        .def("blocking", &Comm::blocking)
         .def("all_reduce", &Comm::all_reduce, py::arg("input"), py::arg("output"), py::arg("op") = 0,
-             py::arg("stream") = 0)
-        .def("broadcast", &Comm::broadcast, py::arg("tensor"), py::arg("root") = 0, py::arg("stream") = 0)
+             py::arg("stream") = 0, py::arg("tag") = "")
+        .def("broadcast", &Comm::broadcast, py::arg("tensor"), py::arg("root") = 0, py::arg("stream") = 0,
+             py::arg("tag") = "")
         .def("reduce", &Comm::reduce, py::arg("input"), py::arg("output"), py::arg("op") = 0, py::arg("root") = 0,
-             py::arg("stream") = 0)
-        .def("all_gather", &Comm::all_gather, py::arg("input"), py::arg("output"), py::arg("stream") = 0)
+             py::arg("stream") = 0, py::arg("tag") = "")
+        .def("all_gather", &Comm::all_gather, py::arg("input"), py::arg("output"), py::arg("stream") = 0,
+             py::arg("tag") = "")
         .def("reduce_scatter", &Comm::reduce_scatter, py::arg("input"), py::arg("output"), py::arg("op") = 0,
-             py::arg("stream") = 0)
+             py::arg("stream") = 0, py::arg("tag") = "")
+        .def("group_start", &Comm::group_start)
+        .def("group_end", &Comm::group_end)
+        .def("watch", &Comm::watch, py::arg("stream"), py::arg("what"))
+        .def("async_error", &Comm::async_error)
         .def("send", &Comm::send, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
         .def("recv", &Comm::recv, py::arg("tensor"), py::arg("peer"), py::arg("stream") = 0)
         .def("graph_run", &Comm::graph_run, "grouped send/recv rounds + K1 reduce (device graph all-reduce)",

@@ -1,6 +1,9 @@
 #include <kungfu/log.hpp>
 
 #include <dlfcn.h>
+#include <unistd.h>
+
+#include <algorithm>
 
 #include <cstdio>
 #include <cstdlib>
@@ -141,6 +144,77 @@ StallDetector::~StallDetector() {
     cv_.notify_all();
     th_.join();
 }
+
+namespace {
+class OpWatchdog {
+  public:
+    static OpWatchdog &get() {
+        static OpWatchdog *w = new OpWatchdog();  // never destroyed (used until _exit)
+        return *w;
+    }
+    uint64_t begin(const std::string &name) {
+        if (timeout_.load() <= 0) return 0;
+        std::lock_guard<std::mutex> lk(mu_);
+        const uint64_t id = ++next_;
+        ops_.emplace(id, Op{name, std::chrono::steady_clock::now()});
+        if (!started_) {
+            started_ = true;
+            std::thread([this] { loop(); }).detach();
+        }
+        return id;
+    }
+    void end(uint64_t id) {
+        if (!id) return;
+        std::lock_guard<std::mutex> lk(mu_);
+        ops_.erase(id);
+    }
+    void set_label(const std::string &l) {
+        std::lock_guard<std::mutex> lk(mu_);
+        label_ = l;
+    }
+    double timeout() const { return timeout_.load(); }
+    void set_timeout(double t) { timeout_.store(t); }
+
+  private:
+    struct Op {
+        std::string name;
+        std::chrono::steady_clock::time_point t0;
+    };
+    OpWatchdog() : timeout_(env_duration_sec("KUNGFU_OP_TIMEOUT_S", 0)) {}
+    void loop() {
+        for (;;) {
+            const double t = timeout_.load();
+            std::this_thread::sleep_for(std::chrono::duration<double>(t > 0 ? std::min(0.25, std::max(0.01, t / 20)) : 0.25));
+            if (t <= 0) continue;
+            std::lock_guard<std::mutex> lk(mu_);
+            const auto now = std::chrono::steady_clock::now();
+            for (const auto &kv : ops_) {
+                const double age = std::chrono::duration<double>(now - kv.second.t0).count();
+                if (age <= t) continue;
+                std::fprintf(stderr,
+                             "[F] kungfu op watchdog (%s): host op '%s' has not completed after %.1f s "
+                             "(KUNGFU_OP_TIMEOUT_S=%g); %zu op(s) in flight; exiting with status 3\n",
+                             label_.empty() ? "?" : label_.c_str(), kv.second.name.c_str(), age, t, ops_.size());
+                std::fflush(stderr);
+                std::fflush(stdout);
+                ::_exit(3);
+            }
+        }
+    }
+    std::mutex mu_;
+    std::map<uint64_t, Op> ops_;
+    uint64_t next_ = 0;
+    bool started_ = false;
+    std::string label_;
+    std::atomic<double> timeout_;
+};
+}  // namespace
+
+OpWatch::OpWatch(const std::string &name) : id_(OpWatchdog::get().begin(name)) {}
+OpWatch::~OpWatch() { OpWatchdog::get().end(id_); }
+void op_watchdog_set_label(const std::string &label) { OpWatchdog::get().set_label(label); }
+double op_watchdog_timeout() { return OpWatchdog::get().timeout(); }
+void op_watchdog_set_timeout(double seconds) { OpWatchdog::get().set_timeout(seconds); }
 
 bool trace_enabled() {
     static bool on = env_bool("KUNGFU_CONFIG_ENABLE_TRACE", false);

@@ -82,6 +82,7 @@ uint64_t Peer::uid() const {
 void Peer::start() {
     if (started_) return;
     started_ = true;
+    op_watchdog_set_label("peer " + cfg_.self.str());
     if (!cfg_.single) {
         server_->start();
         if (Monitor::get().enabled()) {

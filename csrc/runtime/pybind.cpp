@@ -374,6 +374,9 @@ PYBIND11_MODULE(_kungfu, m) {
     m.def("metrics_text", [] { return Monitor::get().metrics_text(); });
     m.def("trace_report", [] { return trace_report(); });
     m.def("trace_enabled", [] { return trace_enabled(); });
+    m.def("op_watchdog_timeout", [] { return op_watchdog_timeout(); });
+    m.def("op_watchdog_set_timeout", [](double t) { op_watchdog_set_timeout(t); });
+    m.def("op_watchdog_set_label", [](const std::string &l) { op_watchdog_set_label(l); });
     m.def("trace_push", [](const std::string &name) { trace_push(name.c_str()); });
     m.def("trace_pop", [] { trace_pop(); });
     m.def("trace_record", [](const std::string &name, double seconds) { trace_record(name, seconds); });

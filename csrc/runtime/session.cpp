@@ -287,6 +287,7 @@ void Session::run_strategies(const Workspace &w, StrategyList &sl, bool monitore
 
 void Session::barrier() {
     KF_TRACE_SCOPE("session::barrier");
+    OpWatch watch("barrier");
     std::vector<uint8_t> x(peers_.size(), 0), y(peers_.size(), 0);
     Workspace w{x.data(), y.data(), x.size(), DType::U8, ReduceOp::SUM, "kungfu::barrier"};
     StrategyList sl;
@@ -311,6 +312,7 @@ bool Session::bytes_consensus(const void *data, size_t len, const std::string &n
 
 void Session::all_reduce(const Workspace &w) {
     KF_TRACE_SCOPE("session::all_reduce");
+    OpWatch watch("all_reduce(" + w.name + ")");
     StrategyList sl;
     {
         std::lock_guard<std::mutex> lk(strat_mu_);
@@ -320,6 +322,7 @@ void Session::all_reduce(const Workspace &w) {
 }
 
 void Session::monitored_all_reduce(const Workspace &w, const std::vector<int> *tree) {
+    OpWatch watch("monitored_all_reduce(" + w.name + ")");
     StrategyList sl;
     if (tree && !tree->empty()) {
         Graph g;
@@ -336,9 +339,13 @@ void Session::monitored_all_reduce(const Workspace &w, const std::vector<int> *t
 
 void Session::all_reduce_with(const std::vector<int> &forest, const Workspace &w) { monitored_all_reduce(w, &forest); }
 
-void Session::cross_all_reduce(const Workspace &w) { run_strategies(w, cross_, false); }
+void Session::cross_all_reduce(const Workspace &w) {
+    OpWatch watch("cross_all_reduce(" + w.name + ")");
+    run_strategies(w, cross_, false);
+}
 
 void Session::reduce(const Workspace &w) {
+    OpWatch watch("reduce(" + w.name + ")");
     GraphPair s;
     {
         std::lock_guard<std::mutex> lk(strat_mu_);
@@ -348,6 +355,7 @@ void Session::reduce(const Workspace &w) {
 }
 
 void Session::broadcast(const Workspace &w) {
+    OpWatch watch("broadcast(" + w.name + ")");
     GraphPair s;
     {
         std::lock_guard<std::mutex> lk(strat_mu_);
@@ -356,10 +364,17 @@ void Session::broadcast(const Workspace &w) {
     run_graphs(w, {&s.bcast});
 }
 
-void Session::local_reduce(const Workspace &w) { run_graphs(w, {&local_[0].reduce}); }
-void Session::local_broadcast(const Workspace &w) { run_graphs(w, {&local_[0].bcast}); }
+void Session::local_reduce(const Workspace &w) {
+    OpWatch watch("local_reduce(" + w.name + ")");
+    run_graphs(w, {&local_[0].reduce});
+}
+void Session::local_broadcast(const Workspace &w) {
+    OpWatch watch("local_broadcast(" + w.name + ")");
+    run_graphs(w, {&local_[0].bcast});
+}
 
 void Session::gather(const Workspace &w) {
+    OpWatch watch("gather(" + w.name + ")");
     const size_t nbytes = w.bytes();
     if (rank_ != 0) {
         router_->client().send(peers_[0], ConnType::COLLECTIVE, w.name, w.send, nbytes, kWaitRecvBuf);
@@ -379,6 +394,7 @@ void Session::gather(const Workspace &w) {
 }
 
 void Session::all_gather(const Workspace &w) {
+    OpWatch watch("all_gather(" + w.name + ")");
     const size_t nbytes = w.bytes();
     std::vector<std::function<void()>> fs;
     for (int r = 0; r < size(); ++r) {
@@ -468,17 +484,35 @@ void Session::all_gather_transform(const void *send, size_t count, DType dtype, 
     const size_t esz = dtype_size(dtype);
     std::vector<char> gathered(rank_ == 0 ? count * esz * size() : 0);
     gather(Workspace{send, gathered.data(), count, dtype, ReduceOp::SUM, name + ":gather"});
-    if (rank_ == 0) f(gathered.data(), out);
+    // A transform that throws on the root must not leave the other peers blocked in the
+    // broadcast: the root always broadcasts a status byte first, then everyone raises.
+    std::exception_ptr err;
+    uint8_t failed = 0;
+    if (rank_ == 0) {
+        try {
+            f(gathered.data(), out);
+        } catch (...) {
+            err = std::current_exception();
+            failed = 1;
+        }
+    }
+    broadcast(Workspace{&failed, &failed, 1, DType::U8, ReduceOp::SUM, name + ":status"});
+    if (failed) {
+        if (err) std::rethrow_exception(err);
+        throw std::runtime_error("all_gather_transform(" + name + "): the transform failed on rank 0");
+    }
     broadcast(Workspace{out, out, out_bytes, DType::U8, ReduceOp::SUM, name + ":bcast"});
 }
 
 void Session::send_to(int rank, const std::string &name, const void *data, size_t len) {
     if (rank < 0 || rank >= size() || rank == rank_) throw std::invalid_argument("send_to: bad rank");
+    OpWatch watch("send_to(" + std::to_string(rank) + ", " + name + ")");
     router_->client().send(peers_[rank], ConnType::COLLECTIVE, name, data, len, kNoFlag);
 }
 
 void Session::recv_from(int rank, const std::string &name, void *buf, size_t len) {
     if (rank < 0 || rank >= size() || rank == rank_) throw std::invalid_argument("recv_from: bad rank");
+    OpWatch watch("recv_from(" + std::to_string(rank) + ", " + name + ")");
     std::vector<char> b = router_->collective().recv(peers_[rank], name);
     if (b.size() != len) throw std::runtime_error("kungfu: size mismatch in " + name);
     if (len) std::memcpy(buf, b.data(), len);

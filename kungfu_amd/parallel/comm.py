@@ -148,9 +148,15 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         self.rank, self.size = _scope_rank_size(scope)
         leader = self.rank == 0
         self.device = torch.cuda.current_device()
+        _colocate_env()
+        H.rccl_watchdog_set_label("rank %d/%d (cluster v%d, %s)" % (runtime.rank(), runtime.size(), self.version,
+                                                                    runtime.self_spec()))
         uid = H.rccl_unique_id() if leader else bytes(128)
         name = "kungfu::rccl_uid::%s::v%d" % (scope, self.version)
         uid = _bcast_bytes(uid, name) if scope == "global" else _local_bcast_bytes(uid, name)
+        # non-blocking init against a deadline (KUNGFU_RCCL_INIT_TIMEOUT_S): a peer that
+        # never arrives raises here instead of hanging; collectives are then watched by
+        # the native watchdog (KUNGFU_RCCL_TIMEOUT_S), see rccl_comm.hip
         self.comm = H.RcclComm(uid, self.rank, self.size, self.device)
         # Normal priority: a high-priority HIP stream measured 2x SLOWER for the
         # whole ResNet-50 step on MI355X (63 vs 32 ms, 1 GPU, profiles/README.md).
@@ -162,26 +168,26 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         s = stream if stream is not None else self.stream
         return s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
 
-    def all_reduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None, op="sum", stream=None):
+    def all_reduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None, op="sum", stream=None, tag=""):
         out = inp if out is None else out
-        self.comm.all_reduce(inp, out, op_code(op), self._s(stream))
+        self.comm.all_reduce(inp, out, op_code(op), self._s(stream), tag)
         return out
 
-    def broadcast(self, t: torch.Tensor, root: int = 0, stream=None):
-        self.comm.broadcast(t, root, self._s(stream))
+    def broadcast(self, t: torch.Tensor, root: int = 0, stream=None, tag=""):
+        self.comm.broadcast(t, root, self._s(stream), tag)
         return t
 
-    def reduce(self, inp, out=None, op="sum", root=0, stream=None):
+    def reduce(self, inp, out=None, op="sum", root=0, stream=None, tag=""):
         out = inp if out is None else out
-        self.comm.reduce(inp, out, op_code(op), root, self._s(stream))
+        self.comm.reduce(inp, out, op_code(op), root, self._s(stream), tag)
         return out
 
-    def all_gather(self, inp, out, stream=None):
-        self.comm.all_gather(inp, out, self._s(stream))
+    def all_gather(self, inp, out, stream=None, tag=""):
+        self.comm.all_gather(inp, out, self._s(stream), tag)
         return out
 
-    def reduce_scatter(self, inp, out, op="sum", stream=None):
-        self.comm.reduce_scatter(inp, out, op_code(op), self._s(stream))
+    def reduce_scatter(self, inp, out, op="sum", stream=None, tag=""):
+        self.comm.reduce_scatter(inp, out, op_code(op), self._s(stream), tag)
         return out
 
     def send(self, t, peer, stream=None):
@@ -191,10 +197,14 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         self.comm.recv(t, peer, self._s(stream))
 
     def group_start(self):
-        hip().rccl_group_start()
+        self.comm.group_start()
 
     def group_end(self):
-        hip().rccl_group_end()
+        self.comm.group_end()
+
+    def watch(self, what: str, stream=None):
+        """Register everything issued on ``stream`` so far with the native watchdog."""
+        self.comm.watch(self._s(stream), what)
 
     def graph_all_reduce(self, t: torch.Tensor, op="sum", pairs=None, stream=None, monitored: bool = False):
         """In-place all-reduce along KungFu strategy graphs (default: the session's current
@@ -295,7 +305,7 @@ class HostComm(_StreamOrdered):
             else:
                 h.floor_divide_(self.size)
 
-    def all_reduce(self, inp, out=None, op="sum", stream=None):
+    def all_reduce(self, inp, out=None, op="sum", stream=None, tag=""):
         nm = self._name("ar")
         return self._run(inp, out, stream, lambda h: self._ar(h, op, nm))
 
@@ -355,7 +365,7 @@ class HostComm(_StreamOrdered):
             runtime.record_strategy_stat(t0, time.time(), t.numel() * esz)
         return t
 
-    def broadcast(self, t, root: int = 0, stream=None):
+    def broadcast(self, t, root: int = 0, stream=None, tag=""):
         nm = self._name("bc")
         if root == 0:
             fn = runtime.broadcast if self.scope == "global" else runtime.local_broadcast
@@ -370,7 +380,7 @@ class HostComm(_StreamOrdered):
 
         return self._run(t, None, stream, f)
 
-    def reduce(self, inp, out=None, op="sum", root=0, stream=None):
+    def reduce(self, inp, out=None, op="sum", root=0, stream=None, tag=""):
         """Result on ``root`` only; the other ranks' ``out`` is left untouched (RCCL semantics)."""
         nm = self._name("rd")
         red = op if op != "avg" else "sum"
@@ -391,7 +401,7 @@ class HostComm(_StreamOrdered):
         self._run(inp, inp.detach().clone() if out is None else out.detach().clone(), stream, f, write=False)
         return inp if out is None else out
 
-    def all_gather(self, inp, out, stream=None):
+    def all_gather(self, inp, out, stream=None, tag=""):
         nm = self._name("ag")
 
         def run():
@@ -408,7 +418,7 @@ class HostComm(_StreamOrdered):
             run()
         return out
 
-    def reduce_scatter(self, inp, out, op="sum", stream=None):
+    def reduce_scatter(self, inp, out, op="sum", stream=None, tag=""):
         full = inp.detach().clone()
         self.all_reduce(full, op=op, stream=stream)
         n = out.numel()
@@ -421,12 +431,29 @@ class HostComm(_StreamOrdered):
     def group_end(self):
         pass
 
+    def watch(self, what: str, stream=None):
+        pass  # host ops are watched by the runtime's op watchdog (KUNGFU_OP_TIMEOUT_S)
+
     def destroy(self):
         self.comm = None
 
 
 # Kept for callers of the round-1 name.
 HostStagedComm = HostComm
+
+
+def _colocate_env() -> None:
+    """``KUNGFU_RCCL_COLOCATE=1``: several RCCL ranks on ONE GPU (tests on a one-GPU box).
+    RCCL rejects two ranks of one communicator on the same device of the same host
+    ("Duplicate GPU detected"); giving every rank its own host identity
+    (``NCCL_HOSTID``) makes them distinct "hosts" joined by RCCL's socket transport over
+    loopback -- a real multi-rank RCCL communicator (bootstrap, ordering, ncclAvg,
+    rebuild after resize, abort) whose bandwidth means nothing.  Must run before the
+    process's first RCCL call."""
+    if os.environ.get("KUNGFU_RCCL_COLOCATE", "0") != "1":
+        return
+    os.environ["NCCL_HOSTID"] = "kungfu-colocated-%s" % runtime.self_spec()
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 
 
 def _use_host_staging() -> bool:

@@ -146,6 +146,8 @@ class GradReducer:
         self._steps_bound = 0  # completed backward passes since the last (re)bind
         self._ordered = False
         self.rebinds = 0
+        self.steps = 0  # completed backward passes (names collectives for the watchdog)
+        self._tag = ""
         self._armed = False
         self._enabled = True
         self._hooks = []
@@ -227,8 +229,10 @@ class GradReducer:
         b = self.param_bucket[i]
         o, n = self.space.offsets[i]
         if self._enabled and b.launched:
-            self._late(i)
-        if (not self._enabled or g.dtype not in (torch.bfloat16, torch.float32)
+            self._late(i)  # raises unless no collective is in flight (one peer)
+        # a late gradient (its bucket already landed) is added now: staging it would
+        # carry it into the next step's gradient
+        if (not self._enabled or b.launched or g.dtype not in (torch.bfloat16, torch.float32)
                 or g.stride() != self.space.strides[i] or not g.is_cuda):
             with torch.no_grad():
                 self.space.grad_view(i).add_(g)
@@ -279,6 +283,8 @@ class GradReducer:
         if self.skip:
             return
         comm = self.comm
+        # names the collective for the watchdog: "bucket 3/5 of step 12"
+        self._tag = "bucket %d/%d of step %d" % (b.index, len(self.buckets), self.steps)
         comm.fence()
         g = self.space.flat_grad[b.start:b.end]
         if self.pre_reduce is not None:
@@ -303,7 +309,7 @@ class GradReducer:
             # one rank: the average IS the sum, and RCCL's in-place one-rank sum is free while
             # its one-rank average is a scaled copy of the bucket (oneRankReduce<PreMulSum>:
             # 1.4 ms/step of HBM traffic for VGG-16's 528 MB of gradients)
-            comm.all_reduce(g, op=self.op if comm.size > 1 or self.op != "avg" else "sum")
+            comm.all_reduce(g, op=self.op if comm.size > 1 or self.op != "avg" else "sum", tag=self._tag)
             return
         comm.graph_all_reduce(g, op="sum", monitored=True)
         if self.op == "avg":
@@ -327,6 +333,7 @@ class GradReducer:
         if self._expected is None:
             self._expected = list(self._fires)
         self._steps_bound += 1
+        self.steps += 1
         self._reset_buckets()
         if self.post_finish is not None:
             self.post_finish()
@@ -335,6 +342,8 @@ class GradReducer:
         for b in self.buckets:
             b.pending = sum(self._expected[i] for i in b.params) if self._expected is not None else 1
             b.launched = False
+            if b.staged:  # never carry staged gradients into another step
+                self._land(b)
         self._fires = [0] * len(self.space.params)
         if self.sched is not None:
             self.sched.reset()

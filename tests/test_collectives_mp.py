@@ -35,3 +35,4 @@ def test_all_gather_transform_mst():
     r = kungfu_run(3, [worker("agt.py")], timeout=120)
     assert r.returncode == 0, r.stdout[-3000:]
     assert r.stdout.count("AGT_OK") == 3
+    assert r.stdout.count("AGT_ERR_OK") == 3, r.stdout[-3000:]

@@ -552,6 +552,8 @@ def test_bench_torchrun_two_ranks_one_gpu_host_staged():
     assert len(lines) == 1, r.stdout[-4000:]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["parallelism"] == "dp2"
+    assert res["verify"]["comm_ranks"] == 2 and res["verify"]["comm_plane"] == "host", res["verify"]
+    assert res["verify"]["replicas_consistent"] is True, res["verify"]
 
 
 @needs_gpu
@@ -709,9 +711,9 @@ def test_resnet50_fused_block_step_matches_layerwise():
 @needs_gpu
 def test_device_graph_allreduce_two_ranks():
     """KungFu strategy graphs executed on the device plane (RCCL send/recv rounds + K1)
-    with 2 ranks; skipped when RCCL refuses two ranks on one GPU."""
+    with 2 ranks sharing the GPU as a real RCCL communicator (KUNGFU_RCCL_COLOCATE)."""
     r = kungfu_run(2, [worker("graph_gpu.py")], timeout=300, extra=["-allow-xgmi"],
-                   env={"KUNGFU_FORCE_DEVICE": "0"})
+                   env={"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_RCCL_COLOCATE": "1", "NCCL_SOCKET_IFNAME": "lo"})
     if "GRAPH_GPU_SKIP" in r.stdout:
         pytest.skip("RCCL refuses 2 ranks on one GPU: " + r.stdout[-300:])
     assert r.returncode == 0, r.stdout[-4000:]

@@ -1,0 +1,101 @@
+"""Multi-rank RCCL on ONE GPU: KUNGFU_RCCL_COLOCATE=1 gives
+each rank its own RCCL host identity, so 2-3 ranks sharing the card form a real RCCL
+communicator over RCCL's socket transport.  Bandwidth is meaningless; what runs is the
+real thing: unique-id bootstrap, non-blocking init, ncclAvg buckets issued from the
+autograd thread in the auto-learned order, the watchdog, and communicator rebuild after
+an elastic resize."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from conftest import ROOT, free_port_block, kungfu_run, worker
+
+pytestmark = pytest.mark.gpu
+needs_gpu = pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")
+COLO = {"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_RCCL_COLOCATE": "1", "NCCL_SOCKET_IFNAME": "lo"}
+
+
+@needs_gpu
+@pytest.mark.parametrize("np_", [2, 3])
+def test_rccl_colocated_collectives(np_):
+    r = kungfu_run(np_, [worker("rccl_colo.py")], timeout=240, extra=["-allow-xgmi"], env=COLO)
+    assert r.returncode == 0, r.stdout[-5000:]
+    assert r.stdout.count("RCCL_COLO_OK") == np_, r.stdout[-5000:]
+
+
+@needs_gpu
+@pytest.mark.parametrize("plane,dtype", [("rccl", "f32"), ("rccl", "bf16"), ("host", "f32")])
+def test_ssgd_matches_single_process_global_batch(plane, dtype):
+    env = dict(COLO) if plane == "rccl" else {"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"}
+    r = kungfu_run(2, [worker("ssgd_exact.py"), dtype], timeout=300, extra=["-allow-xgmi"], env=env)
+    assert r.returncode == 0, r.stdout[-5000:]
+    oks = re.findall(r"SSGD_EXACT_OK rank=\d np=2 plane=(\w+)", r.stdout)
+    assert oks == [plane, plane], r.stdout[-5000:]
+
+
+@needs_gpu
+def test_rccl_watchdog_names_stalled_bucket():
+    r = kungfu_run(2, [worker("rccl_stall.py")], timeout=240, extra=["-allow-xgmi"],
+                   env=dict(COLO, KUNGFU_RCCL_TIMEOUT_S="6"))
+    out = r.stdout
+    assert r.returncode != 0, out[-4000:]
+    assert "STALL_NOT_DETECTED rank=0" not in out, out[-4000:]
+    assert "kungfu rccl watchdog" in out and "bucket" in out and "has not completed" in out, out[-4000:]
+
+
+def _bench(env, extra=()):
+    e = dict(os.environ, PYTHONPATH=ROOT, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KUNGFU_SELF_SPEC"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
+                        "--batch", "16"] + list(extra), cwd=ROOT, env=e, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-5000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-5000:]
+    return json.loads(lines[0])
+
+
+@needs_gpu
+@pytest.mark.parametrize("plane", ["rccl", "host"])
+def test_bench_self_launch_two_ranks(plane):
+    """``bench.py --gpus 2`` with no launcher env spawns its 2 ranks itself; the JSON proves
+    2 communicating ranks on the named plane and identical replicas."""
+    env = dict(COLO) if plane == "rccl" else {"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"}
+    res = _bench(env)
+    v = res["verify"]
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2", res
+    assert v["comm_ranks"] == 2 and v["comm_plane"] == plane, v
+    assert v["replicas_consistent"] is True, v
+    if plane == "rccl":
+        assert v["rccl_watchdog"]["ops_watched"] > 0 and v["rccl_watchdog"]["pending"] == 0, v
+
+
+@needs_gpu
+def test_elastic_resize_rebuilds_rccl_communicator():
+    """kungfu-run -w, 1 -> 2 -> 1 peers with the RCCL plane: the communicator is torn down
+    and re-created for every cluster version (parity: KungfuResetNcclHelper,
+    srcs/cpp/src/tensorflow/ops/gpu/scheduler.cpp:54-68) and replicas stay identical."""
+    base = free_port_block(16)
+    cfg = base + 15
+    r = kungfu_run(1, [worker("elastic_train.py"), "--schedule", "1:2,2:3,1:2", "--max-step", "7",
+                       "--optimizer", "ssgd", "--device", "cuda", "--model", "resnet18", "--global-batch", "16"],
+                   timeout=400, port_base=base, env=COLO,
+                   extra=["-w", "-allow-xgmi", "-builtin-config-port", str(cfg), "-config-server",
+                          "http://127.0.0.1:%d/config" % cfg, "-H", "127.0.0.1:4"])
+    assert r.returncode == 0, r.stdout[-5000:]
+    steps = re.findall(r"STEP (\d+) np=(\d+) rank=(\d+) loss=(\S+) h=(\w+)", r.stdout)
+    by = {}
+    for st, np_, rk, loss, h in steps:
+        by.setdefault(int(st), []).append((int(np_), h))
+    assert sorted(by) == list(range(7)), r.stdout[-3000:]
+    for st, rows in by.items():
+        assert len(rows) == rows[0][0], (st, rows)
+        assert len({h for _, h in rows}) == 1, (st, rows)
+    assert any(rows[0][0] == 2 for rows in by.values())
+    assert "plane=rccl" in r.stdout, r.stdout[-3000:]

@@ -22,3 +22,22 @@ w = torch.tensor([abs(r - j) * 1.0 + (0 if abs(r - j) == 1 else 5.0) for j in ra
 edges = global_minimum_spanning_tree(w)
 assert sorted(tuple(sorted(e)) for e in edges.tolist()) == [(i, i + 1) for i in range(n - 1)], edges
 print("AGT_OK rank=%d" % r, flush=True)
+
+# a transform that raises on the root must not leave the other peers blocked in the
+# broadcast: every peer raises (session.cpp all_gather_transform)
+
+
+def boom(g):
+    raise ValueError("transform exploded")
+
+
+try:
+    all_gather_transform(torch.ones(3), torch.zeros(3), boom, name="agt-boom")
+    raise AssertionError("all_gather_transform did not raise")
+except AssertionError:
+    raise
+except Exception as e:  # noqa: BLE001
+    assert r != 0 or "exploded" in str(e), e
+# the session is still usable afterwards
+assert torch.equal(kf.ops.all_reduce(torch.ones(2)), torch.full((2,), float(n)))
+print("AGT_ERR_OK rank=%d" % r, flush=True)

@@ -136,6 +136,9 @@ def main():
         extra = ""
         if a.optimizer == "gns" and np_ > 1:
             extra = " gns=%s" % opt.noise_scale
+        red = getattr(opt, "reducer", None)
+        if red is not None and np_ > 1:
+            extra += " plane=%s" % red.describe()["comm_plane"]
         print("STEP %d np=%d rank=%d loss=%.6f h=%s%s" % (tr.step, np_, r, loss.item(), digest(opt.space.flat_param),
                                                          extra), flush=True)
         if tr.after_step():
