@@ -8,6 +8,7 @@
 
 #include <fcntl.h>
 #include <signal.h>
+#include <sys/prctl.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
 #include <unistd.h>
@@ -88,10 +89,15 @@ int run_once(const Proc &p, int color, bool verbose, const std::string &log_pref
     // O_CLOEXEC: workers forked later must not inherit these write ends, or
     // this worker's output pumps would not see EOF until every sibling exits.
     if (::pipe2(out_pipe, O_CLOEXEC) != 0 || ::pipe2(err_pipe, O_CLOEXEC) != 0) return 127;
+    const pid_t parent = ::getpid();
     pid_t pid = ::fork();
     if (pid < 0) return 127;
     if (pid == 0) {
         ::setpgid(0, 0);
+        // a worker never outlives its runner (the forking thread waits for it): if the
+        // launcher is SIGKILLed (an outer timeout), its GPU workers go with it
+        ::prctl(PR_SET_PDEATHSIG, SIGKILL);
+        if (::getppid() != parent) ::_exit(127);
         ::dup2(out_pipe[1], 1);
         ::dup2(err_pipe[1], 2);
         ::close(out_pipe[0]);

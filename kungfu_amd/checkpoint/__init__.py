@@ -92,7 +92,8 @@ def latest(directory: str) -> Optional[str]:
 
 def load(path: str, model: torch.nn.Module, optimizer=None) -> Dict[str, Any]:
     """Collective: restore ``model`` (and ``optimizer``) from rank 0's checkpoint on every
-    peer.  Returns ``{"step", "trained_samples", "cluster_size", "extra"}`` (agreed on by all)."""
+    peer.  Returns ``{"step", "trained_samples", "cluster_size", "extra"}``, identical on every
+    peer (``extra`` is rank 0's, broadcast)."""
     _ensure()
     meta = torch.zeros(3, dtype=torch.int64)
     extra: Dict[str, Any] = {}
@@ -116,4 +117,16 @@ def load(path: str, model: torch.nn.Module, optimizer=None) -> Dict[str, Any]:
     # every peer gets rank 0's model + optimizer state exactly as after an elastic (re)join
     broadcast_model(model, optimizer)
     meta = ops.all_reduce(meta, op="max")
+    # ``extra`` (data-loader position, scheduler state, ...) is rank 0's on every peer
+    import io
+
+    from ..initializer import broadcast_bytes
+
+    if current_rank() == 0:
+        bio = io.BytesIO()
+        torch.save(extra, bio)
+        data = bio.getvalue()
+    else:
+        data = None
+    extra = torch.load(io.BytesIO(broadcast_bytes(data)), map_location="cpu", weights_only=True)
     return {"step": int(meta[0]), "trained_samples": int(meta[1]), "cluster_size": int(meta[2]), "extra": extra}

@@ -37,9 +37,78 @@ def _scalar_holders(optimizer):
     return out
 
 
+def broadcast_bytes(data: Optional[bytes]) -> bytes:
+    """Rank 0's ``data`` on every peer (other ranks may pass None)."""
+    from ..python import current_rank
+
+    root = current_rank() == 0
+    n = torch.tensor([len(data) if root and data is not None else 0], dtype=torch.int64)
+    ops.inplace_broadcast_(n)
+    buf = torch.zeros(int(n[0]), dtype=torch.uint8)
+    if root and int(n[0]):
+        buf.copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+    if int(n[0]):
+        ops.inplace_broadcast_(buf)
+    return bytes(buf.numpy().tobytes())
+
+
+def _agree_state_layout(inner) -> None:
+    """Make every peer's per-parameter optimizer state match rank 0's LAYOUT (which
+    parameters have state, which keys, shapes, dtypes) and its non-tensor values, before
+    the per-tensor broadcasts: a freshly started (or re-joined) peer has no lazily
+    created state while rank 0 -- e.g. after a checkpoint load -- has one entry per
+    parameter, and mismatched broadcast counts would hang (RCCL) or silently pair the
+    wrong tensors (host plane).  Param-group hyper-parameters follow rank 0 too."""
+    import json
+
+    from ..python import current_rank
+
+    params = [p for g in inner.param_groups for p in g["params"]]
+    if current_rank() == 0:
+        index = {id(p): i for i, p in enumerate(params)}
+        layout = []
+        for p, st in inner.state.items():
+            if id(p) not in index:
+                continue
+            ent = {}
+            for k, v in st.items():
+                if isinstance(v, torch.Tensor):
+                    ent[k] = ["t", list(v.shape), str(v.dtype).replace("torch.", ""), v.device.type == "cpu"]
+                elif isinstance(v, (bool, int, float)) or v is None:
+                    ent[k] = ["v", v]
+            layout.append([index[id(p)], ent])
+        groups = [{k: v for k, v in g.items() if k != "params" and (isinstance(v, (bool, int, float)) or v is None)}
+                  for g in inner.param_groups]
+        data = json.dumps({"state": layout, "groups": groups}).encode()
+    else:
+        data = None
+    spec = json.loads(broadcast_bytes(data).decode())
+    for g, gv in zip(inner.param_groups, spec["groups"]):
+        g.update(gv)
+    want = {i: ent for i, ent in spec["state"]}
+    for i, p in enumerate(params):
+        ent = want.get(i)
+        if ent is None:
+            inner.state.pop(p, None)
+            continue
+        st = inner.state.setdefault(p, {})
+        for k in [k for k in st if k not in ent]:
+            del st[k]
+        for k, e in ent.items():
+            if e[0] == "v":
+                st[k] = e[1]
+                continue
+            shape, dt, on_cpu = tuple(e[1]), getattr(torch, e[2]), e[3]
+            dev = torch.device("cpu") if on_cpu else p.device
+            v = st.get(k)
+            if not (isinstance(v, torch.Tensor) and tuple(v.shape) == shape and v.dtype == dt and v.device == dev):
+                st[k] = torch.zeros(shape, dtype=dt, device=dev)
+
+
 def broadcast_optimizer_state(optimizer) -> None:
     """Broadcast optimizer state from rank 0: flat buffers (momentum, Adam moments
-    and step), per-parameter state tensors, and host-side scalars."""
+    and step), per-parameter state tensors (after agreeing on their layout), and
+    host-side scalars."""
     inner = getattr(optimizer, "inner", optimizer)
     flat_bufs = [getattr(inner, n, None) for n in ("momentum_buffer", "exp_avg", "exp_avg_sq", "_step_t")]
     for b in flat_bufs:
@@ -54,7 +123,14 @@ def broadcast_optimizer_state(optimizer) -> None:
         for h, vs in zip(holders, vals):
             h._kf_load_scalars(t[k:k + len(vs)].tolist())
             k += len(vs)
-    for p, st in inner.state.items():
+    if not hasattr(inner, "param_groups"):
+        return
+    _agree_state_layout(inner)
+    params = [p for g in inner.param_groups for p in g["params"]]
+    for p in params:  # parameter order, identical on every peer
+        st = inner.state.get(p)
+        if not st:
+            continue
         for k in sorted(st.keys()):
             v = st[k]
             if isinstance(v, torch.Tensor):
