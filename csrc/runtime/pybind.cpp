@@ -353,6 +353,7 @@ PYBIND11_MODULE(_kungfu, m) {
         py::gil_scoped_release r;
         s->recv_from(rank, name, reinterpret_cast<void *>(buf), nbytes);
     }, "named point-to-point receive (exact size)");
+    m.def("now", [] { return now_sec(); }, "the steady clock the strategy statistics use (seconds)");
     m.def("record_strategy_stat", [](double begin, double end, uint64_t bytes) {
         require_session()->record_strategy_stat(begin, end, bytes);
     }, "account a monitored collective of a device plane to the current global strategy");

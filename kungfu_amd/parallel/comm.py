@@ -89,8 +89,13 @@ class _DeviceStats:
 
     def _stat_begin(self, stream):
         if getattr(self, "_stat_base", None) is None:
+            # anchor the device timeline to the runtime's steady clock once (one host
+            # sync per communicator), so device and host-plane timings share one clock
+            # in StrategyStat's (first_begin, last_end) window
             self._stat_base = torch.cuda.Event(enable_timing=True)
             self._stat_base.record(stream)
+            self._stat_base.synchronize()
+            self._stat_base_host = runtime.now()
             self._stat_pending = []
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(stream)
@@ -112,8 +117,8 @@ class _DeviceStats:
                 keep.append((st, en, nb))
                 continue
             en.synchronize()
-            b = self._stat_base.elapsed_time(st) / 1e3
-            e = self._stat_base.elapsed_time(en) / 1e3
+            b = self._stat_base_host + self._stat_base.elapsed_time(st) / 1e3
+            e = self._stat_base_host + self._stat_base.elapsed_time(en) / 1e3
             runtime.record_strategy_stat(b, e, int(nb))
         self._stat_pending = keep
 
@@ -172,6 +177,17 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         out = inp if out is None else out
         self.comm.all_reduce(inp, out, op_code(op), self._s(stream), tag)
         return out
+
+    def monitored_all_reduce(self, t: torch.Tensor, op="sum", stream=None, tag=""):
+        """In-place all-reduce whose bytes and device time feed the strategy statistics
+        (parity: ``MonitoredAllReduce``, srcs/go/kungfu/session/monitoring.go:15-35)."""
+        s = stream if stream is not None else self.stream
+        if not hasattr(s, "cuda_stream"):
+            s = torch.cuda.ExternalStream(int(s), device=self.device)
+        st = self._stat_begin(s)
+        self.comm.all_reduce(t, t, op_code(op), s.cuda_stream, tag)
+        self._stat_end(st, s, t.numel() * t.element_size())
+        return t
 
     def broadcast(self, t: torch.Tensor, root: int = 0, stream=None, tag=""):
         self.comm.broadcast(t, root, self._s(stream), tag)
@@ -309,6 +325,17 @@ class HostComm(_StreamOrdered):
         nm = self._name("ar")
         return self._run(inp, out, stream, lambda h: self._ar(h, op, nm))
 
+    def monitored_all_reduce(self, t, op="sum", stream=None, tag=""):
+        """All-reduce along the session's current strategy with strategy statistics: CPU
+        tensors use the runtime's native monitored all-reduce; staged GPU tensors are
+        timed on the runtime's clock around the (synchronous) staged collective."""
+        if not self.staged:
+            return self.graph_all_reduce(t, op=op, monitored=True)
+        t0 = runtime.now()
+        self.all_reduce(t, op=op, stream=stream)
+        runtime.record_strategy_stat(t0, runtime.now(), t.numel() * t.element_size())
+        return t
+
     def graph_all_reduce(self, t, op="sum", pairs=None, stream=None, monitored: bool = False):
         """CPU tensors: the host runtime executes the strategy graphs itself (monitored:
         native strategy statistics).  Staged GPU tensors: the device graph plane's round
@@ -332,8 +359,6 @@ class HostComm(_StreamOrdered):
             return t
         if self.size == 1:
             return t
-        import time
-
         from .._lib import hip
 
         rounds, nscratch = _graph_plan(self, pairs, self.rank, t.numel())
@@ -342,7 +367,7 @@ class HostComm(_StreamOrdered):
         if not isinstance(s, torch.cuda.Stream):
             s = torch.cuda.ExternalStream(int(s), device=self.device)
         esz = t.element_size()
-        t0 = time.time()
+        t0 = runtime.now()
         with torch.cuda.stream(s):
             flat = t.view(-1)
             scratch = torch.empty(max(int(nscratch), 1), dtype=t.dtype, device=t.device)
@@ -362,7 +387,7 @@ class HostComm(_StreamOrdered):
                             hip().reduce(flat[off:off + ln], flat[off:off + ln], dst, op_code(op))
             s.synchronize()
         if monitored:
-            runtime.record_strategy_stat(t0, time.time(), t.numel() * esz)
+            runtime.record_strategy_stat(t0, runtime.now(), t.numel() * esz)
         return t
 
     def broadcast(self, t, root: int = 0, stream=None, tag=""):

@@ -79,7 +79,7 @@ class GradReducer:
     def __init__(self, space: FlatParamSpace, op: str = "avg", bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
                  tail_bucket_mb: float = 4.0,
-                 skip_single: bool = True):
+                 skip_single: bool = True, monitored: bool = False):
         # skip_single: with one peer the average of the gradients IS the local
         # gradient, so no collective is issued (the engine's hooks still run).
         # skip_single=False sends every bucket through the communicator even
@@ -87,6 +87,9 @@ class GradReducer:
         self.space = space
         self.op = op
         self.skip_single = skip_single
+        # monitored: every bucket's all-reduce feeds the session's strategy statistics
+        # (SynchronousSGDOptimizer(monitor=True); parity sync_sgd.py:96-97)
+        self.monitored = monitored
         cap_mb = float(os.environ.get("KUNGFU_BUCKET_MB", bucket_mb if bucket_mb is not None else 32.0))
         esz = space.flat_grad.element_size()
         if comm_dtype is not None and comm_dtype not in (torch.float32, torch.bfloat16):
@@ -309,7 +312,11 @@ class GradReducer:
             # one rank: the average IS the sum, and RCCL's in-place one-rank sum is free while
             # its one-rank average is a scaled copy of the bucket (oneRankReduce<PreMulSum>:
             # 1.4 ms/step of HBM traffic for VGG-16's 528 MB of gradients)
-            comm.all_reduce(g, op=self.op if comm.size > 1 or self.op != "avg" else "sum", tag=self._tag)
+            op = self.op if comm.size > 1 or self.op != "avg" else "sum"
+            if self.monitored:
+                comm.monitored_all_reduce(g, op=op, tag=self._tag)
+            else:
+                comm.all_reduce(g, op=op, tag=self._tag)
             return
         comm.graph_all_reduce(g, op="sum", monitored=True)
         if self.op == "avg":

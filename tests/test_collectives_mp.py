@@ -36,3 +36,11 @@ def test_all_gather_transform_mst():
     assert r.returncode == 0, r.stdout[-3000:]
     assert r.stdout.count("AGT_OK") == 3
     assert r.stdout.count("AGT_ERR_OK") == 3, r.stdout[-3000:]
+
+
+def test_monitored_ssgd_adapts_strategy_on_interference():
+    """bucket-engine S-SGD with monitor/adapt: strategy statistics accrue,
+    an injected slowdown flips the strategy on every peer at the same step."""
+    r = kungfu_run(2, [worker("adapt_ssgd.py"), "cpu"], timeout=180)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("ADAPT_OK") == 2, r.stdout[-4000:]

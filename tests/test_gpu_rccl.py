@@ -99,3 +99,15 @@ def test_elastic_resize_rebuilds_rccl_communicator():
         assert len({h for _, h in rows}) == 1, (st, rows)
     assert any(rows[0][0] == 2 for rows in by.values())
     assert "plane=rccl" in r.stdout, r.stdout[-3000:]
+
+
+@needs_gpu
+@pytest.mark.parametrize("plane", ["host", "rccl"])
+def test_monitored_ssgd_adapts_on_gpu(plane):
+    """S-SGD(monitor, adapt) on the GPU bucket engine: strategy throughputs
+    from the bucket all-reduces (device events on the RCCL plane), an injected slowdown
+    flips the strategy on both ranks at the same step."""
+    env = dict(COLO) if plane == "rccl" else {"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"}
+    r = kungfu_run(2, [worker("adapt_ssgd.py"), "cuda"], timeout=240, extra=["-allow-xgmi"], env=env)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("ADAPT_OK") == 2, r.stdout[-4000:]
