@@ -170,7 +170,7 @@ def main():
 
     def sync():
         if cuda:
-            sync()
+            torch.cuda.synchronize()
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode + in-tree find-db
     torch.manual_seed(1234)  # same init everywhere (broadcast_parameters makes it exact)
 

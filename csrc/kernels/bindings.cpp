@@ -1547,6 +1547,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["timeout_s"] = i.timeout_s;
         return d;
     });
+    kfk::watchdog_set_freeze_hook([] {
+        if (Py_IsInitialized()) PyGILState_Ensure();  // held until the process exits
+    });
     m.def("rccl_watchdog_set_label", &kfk::watchdog_set_label);
     m.def("rccl_watchdog_set_timeout", &kfk::watchdog_set_timeout);
     py::class_<Comm>(m, "RcclComm")

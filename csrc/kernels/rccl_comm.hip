@@ -157,6 +157,7 @@ class Watchdog {
     }
 
     void set_timeout(double t) { timeout_ = t; }
+    void set_freeze(void (*fn)()) { freeze_ = fn; }
 
     WatchdogInfo info() {
         std::lock_guard<std::mutex> lk(mu_);
@@ -244,6 +245,17 @@ class Watchdog {
         std::fprintf(stderr, "[F] aborting %zu communicator(s) and exiting with status 3\n", comms_.size());
         std::fflush(stderr);
         std::fflush(stdout);
+        if (freeze_) {  // stop the application's threads first (bounded: 2 s)
+            auto frozen = std::make_shared<std::atomic<bool>>(false);
+            void (*f)() = freeze_;
+            std::thread([f, frozen] {
+                f();
+                frozen->store(true);
+                for (;;) std::this_thread::sleep_for(std::chrono::seconds(1));
+            }).detach();
+            const double t_frz = now_s() + 2.0;
+            while (!frozen->load() && now_s() < t_frz) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        }
         // ncclCommAbort makes the RCCL kernels leave their wait loops, so the process
         // does not exit with waves spinning on the device; bounded, it runs detached.
         std::vector<void *> cs(comms_.begin(), comms_.end());
@@ -263,6 +275,7 @@ class Watchdog {
     std::set<void *> comms_;
     std::string label_;
     std::atomic<double> timeout_;
+    void (*freeze_)() = nullptr;
     bool started_ = false;
     long long registered_ = 0, completed_ = 0;
 };
@@ -272,6 +285,7 @@ class Watchdog {
 WatchdogInfo watchdog_info() { return Watchdog::get().info(); }
 void watchdog_set_label(const std::string &label) { Watchdog::get().set_label(label); }
 void watchdog_set_timeout(double seconds) { Watchdog::get().set_timeout(seconds); }
+void watchdog_set_freeze_hook(void (*fn)()) { Watchdog::get().set_freeze(fn); }
 
 std::string RcclComm::unique_id() {
     ncclUniqueId id;

@@ -71,5 +71,9 @@ struct WatchdogInfo {
 WatchdogInfo watchdog_info();
 void watchdog_set_label(const std::string &label);  // e.g. "rank 3/8"
 void watchdog_set_timeout(double seconds);
+// Called (on a helper thread) before the communicators are aborted: the Python binding
+// takes the GIL there and never releases it, so no Python thread runs on with results
+// of the aborted collectives during the few ms until the process exits.
+void watchdog_set_freeze_hook(void (*fn)());
 
 }  // namespace kfk

@@ -54,7 +54,11 @@ if kind == "cuda":
 ad = opt.adapter
 tps = [t for t in ad.throughputs if t]
 assert len(tps) >= 5 and all(t > 0 for t in tps[:6]), ad.throughputs
-assert ad.changed and ad.switched_at is not None and ad.switched_at >= 8, (ad.switched_at, ad.throughputs)
+assert ad.changed and ad.switched_at is not None and ad.switched_at > 3, (ad.switched_at, ad.throughputs)
+if kind == "cpu":  # the host plane on CPU is quiet enough to pin the cause: the injected slowdown
+    assert ad.switched_at >= 8, (ad.switched_at, ad.throughputs)
+# the slowdown is visible in the statistics
+assert tps[-1] < 0.5 * max(tps[2:6]), ad.throughputs
 after = runtime.global_strategy_pairs()
 assert after != before, (before, after)
 sw = kf.ops.all_gather(torch.tensor([ad.switched_at], dtype=torch.int64))

@@ -5,6 +5,7 @@ global-batch gradient is the average of the per-rank gradients.  Also pins the b
 gradient error against the f32 average (--comm-dtype bf16).
 
 argv: [f32|bf16]"""
+import os
 import sys
 
 import torch
@@ -13,6 +14,7 @@ import torch.nn.functional as F
 import kungfu_amd as kf
 
 comm_dtype = sys.argv[1] if len(sys.argv) > 1 else "f32"
+os.environ["KUNGFU_TAIL_BUCKET_MB"] = "0.05"  # several buckets for this 0.5 MB model
 kf.init()
 r, n = kf.current_rank(), kf.current_cluster_size()
 dev = torch.device("cuda", kf.get_hip_index())
@@ -43,7 +45,8 @@ for x, y in data:
 # S-SGD: each rank its contiguous shard
 m = net()
 opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4),
-                                            named_parameters=m.named_parameters(), bucket_mb=0.05,
+                                            named_parameters=m.named_parameters(), bucket_mb=0.1,
+                                            first_bucket_mb=0.05,
                                             comm_dtype=torch.bfloat16 if comm_dtype == "bf16" else None)
 kf.broadcast_parameters(m.state_dict())
 assert opt.reducer is not None and len(opt.reducer.buckets) >= 3, len(opt.reducer.buckets)
