@@ -204,9 +204,11 @@ def main():
 
         opt = KungFuOptimizer(base, named_parameters=model.named_parameters())
     elif a.optimizer == "sma":
-        opt = kf.optimizers.SynchronousAveragingOptimizer(base, named_parameters=model.named_parameters())
+        opt = kf.optimizers.SynchronousAveragingOptimizer(base, named_parameters=model.named_parameters(),
+                                                          force_comm=bool(a.force_comm))
     elif a.optimizer == "pair":
-        opt = kf.optimizers.PairAveragingOptimizer(base, named_parameters=model.named_parameters())
+        opt = kf.optimizers.PairAveragingOptimizer(base, named_parameters=model.named_parameters(),
+                                                   force_comm=bool(a.force_comm) and cuda)
     else:
         opt = kf.optimizers.AdaptiveSGDOptimizer(base, named_parameters=model.named_parameters(), change_step=10)
     kf.broadcast_parameters(model.state_dict())
@@ -263,7 +265,18 @@ def main():
     dt_max = max(dt_all)
     value = a.batch * size * a.steps / dt_max
     reducer = getattr(opt, "reducer", None)
-    comm_info = reducer.describe() if reducer is not None else {"comm_ranks": size}
+    if reducer is not None:
+        comm_info = reducer.describe()
+    elif getattr(opt, "averager", None) is not None:  # SMA / AdaSGD: model all-reduce per step
+        c = opt.averager.comm
+        comm_info = {"comm_ranks": c.size if c is not None else size, "comm_plane": c.plane if c is not None else "skip",
+                     "comm_bytes_per_step": opt.space.numel * 4 if c is not None else 0, "overlap": True}
+    elif getattr(opt, "store", None) is not None:  # pair averaging: device model store pulls
+        comm_info = {"comm_ranks": size, "comm_plane": "ipc" if size > 1 else "ipc-self",
+                     "pulls": opt.pulls, "dropped": opt.store.dropped, "prefetch": opt.prefetcher is not None,
+                     "comm_bytes_per_step": opt.space.numel * 4}
+    else:
+        comm_info = {"comm_ranks": size}
     # replica consistency: after synchronous training every rank holds the same weights
     ck = _replica_checksum(opt, model)
     cks = kf.ops.all_gather(ck).view(size, 2) if size > 1 else ck.view(1, 2)

@@ -100,41 +100,112 @@ class DeviceModelStore:
         self._pending = None
 
     def _record(self, target: int):
+        if target == self.rank:  # forced self-pull (one peer): the own advertised record
+            return (self.version % self.SLOTS, self.version) if self.version else None
         rec = torch.zeros(2, dtype=torch.int64)
         if not runtime.request(target, "", _REC + self.name, rec.data_ptr(), 16):
             return None
         return int(rec[0]), int(rec[1])
 
     @traced("pair::pull")
-    def pull(self, target: int, out: torch.Tensor) -> bool:
+    def pull(self, target: int, out: torch.Tensor, stream=None, after_event=None) -> Optional[torch.cuda.Event]:
+        """Copy ``target``'s latest advertised snapshot into ``out``.  Returns the copy's
+        completion event (None: nothing valid was pulled).  The copy runs on ``stream``
+        (default: current) after ``after_event``; this call host-waits for it (it is meant
+        to run on the prefetch thread, off the training loop's critical path)."""
         rec = self._record(target)
         if rec is None:
-            return False
+            return None
         slot, ver = rec
-        if self.local.get(target, False):
-            out.copy_(self.peer_bufs[target][slot], non_blocking=True)
-            done = torch.cuda.Event()
-            done.record()
+        if target == self.rank or self.local.get(target, False):
+            src = self.bufs[slot] if target == self.rank else self.peer_bufs[target][slot]
+            s = stream if stream is not None else torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(s):
+                if after_event is not None:
+                    s.wait_event(after_event)
+                out.copy_(src, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(s)
             done.synchronize()
             after = self._record(target)
             if after is None or after[1] - ver >= self.SLOTS - 1:
                 self.dropped += 1  # the owner may have started rewriting this slot
-                return False
+                return None
             self.last_pulled = (target, ver)
-            return True
+            return done
         h = torch.empty(self.numel, dtype=torch.float32)
         if not runtime.request(target, "", "kf:pair:model:" + self.name, h.data_ptr(), self.numel * 4):
-            return False
-        out.copy_(h)
+            return None
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(s):
+            if after_event is not None:
+                s.wait_event(after_event)
+            out.copy_(h, non_blocking=False)
+            done = torch.cuda.Event()
+            done.record(s)
+        done.synchronize()
         self.last_pulled = (target, ver)
-        return True
+        return done
+
+
+class _Prefetcher:
+    """Pulls the NEXT step's peer model on a host thread + a dedicated copy stream while
+    the training loop enqueues forward/backward (parity: the reference's
+    ``AsyncModelAveraging`` / ``AsyncRequestModel`` prefetch buffer with a callback,
+    srcs/cpp/src/tensorflow/ops/cpu/peer_to_peer.cpp:166-238,424-510).  The thread first
+    advertises the snapshot published at the end of the step (its host wait on that copy
+    happens here, not in the training loop), then pulls; the compute stream only waits on
+    the copy's event."""
+
+    def __init__(self, store: DeviceModelStore, out: torch.Tensor):
+        import threading
+
+        self.store, self.out = store, out
+        self.stream = torch.cuda.Stream(device=store.device)
+        self._threading = threading
+        self.thread = None
+        self.result: Optional[torch.cuda.Event] = None
+        self.error: Optional[BaseException] = None
+
+    def start(self, target: int, consumed: Optional[torch.cuda.Event]):
+        def run():
+            try:
+                torch.cuda.set_device(self.store.device)
+                self.store.advertise()
+                self.result = self.store.pull(target, self.out, stream=self.stream, after_event=consumed)
+            except BaseException as e:  # noqa: BLE001 -- re-raised in the training thread
+                self.error = e
+
+        self.result, self.error = None, None
+        self.thread = self._threading.Thread(target=run, name="kungfu-pair-prefetch", daemon=True)
+        self.thread.start()
+        if not getattr(self, "_atexit", False):  # never leave a pull in flight at shutdown
+            import atexit
+
+            atexit.register(self._drain)
+            self._atexit = True
+
+    def _drain(self):
+        t = self.thread
+        if t is not None:
+            t.join(timeout=60)
+
+    def finish(self) -> Optional[torch.cuda.Event]:
+        if self.thread is None:
+            return None
+        self.thread.join()
+        self.thread = None
+        if self.error is not None:
+            raise self.error
+        return self.result
 
 
 class _PairAveraging(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, fuse_requests: bool = True,
                  fused_model_name: str = "model", fused: bool = True, seed: Optional[int] = None,
-                 peer_selection: str = "random"):
+                 peer_selection: str = "random", prefetch: bool = True, force_comm: bool = False):
         super().__init__(optimizer, named_parameters, fused=fused)
+        self.force_comm = force_comm
         if peer_selection not in ("random", "roundrobin"):
             raise ValueError("peer_selection must be 'random' or 'roundrobin'")
         self.peer_selection = peer_selection
@@ -146,11 +217,18 @@ class _PairAveraging(KungFuOptimizer):
         self.step_count = 0
         self.last_target = -1
         self.store: Optional[DeviceModelStore] = None
-        if self.space is not None and self.size > 1:
+        self.prefetcher: Optional[_Prefetcher] = None
+        self.pulls = 0
+        if self.space is not None and (self.size > 1 or force_comm) and self.space.device.type == "cuda":
             self.store = DeviceModelStore(self.space.numel, self.space.device, fused_model_name)
             self._other = torch.empty_like(self.space.flat_param)
+            if prefetch:
+                self.prefetcher = _Prefetcher(self.store, self._other)
+        self._consumed: Optional[torch.cuda.Event] = None
 
     def random_peer(self) -> int:
+        if self.size == 1:
+            return 0  # force_comm: self-pull
         t = self.rng.randrange(self.size)
         return (t + 1) % self.size if t == self.rank else t
 
@@ -159,7 +237,7 @@ class _PairAveraging(KungFuOptimizer):
         (the reference's SelectionStrategy, ops/cpu/peer_to_peer.cpp:8-63)."""
         if self.peer_selection == "random":
             return self.random_peer()
-        others = [r for r in range(self.size) if r != self.rank]
+        others = [r for r in range(self.size) if r != self.rank] or [self.rank]
         t = others[self._rr % len(others)]
         self._rr += 1
         return t
@@ -193,8 +271,19 @@ class _PairAveraging(KungFuOptimizer):
                     v.add_(o.to(v.device)).mul_(0.5)
 
     # -- algorithm ----------------------------------------------------------------
+    def _average(self, done: Optional[torch.cuda.Event]):
+        if done is None:
+            return
+        cur = torch.cuda.current_stream(self.space.device)
+        cur.wait_event(done)  # normally complete already: no stall
+        hip().axpby(self.space.flat_param, self._other, None, 0.5, 0.5)
+        self.pulls += 1
+        ev = torch.cuda.Event()
+        ev.record(cur)  # the next prefetch may overwrite _other only after this kernel
+        self._consumed = ev
+
     def _before_step(self):
-        if self.size == 1:
+        if self.size == 1 and not self.force_comm:
             return
         if self.step_count == 0:
             if self.store is not None:
@@ -202,29 +291,53 @@ class _PairAveraging(KungFuOptimizer):
                 self.store.advertise()
             else:
                 self._host_save()
-            runtime.barrier()
+            if self.size > 1:
+                runtime.barrier()
+            if self.prefetcher is not None:  # first step: a synchronous pull
+                self.last_target = self.next_peer()
+                self._average(self.store.pull(self.last_target, self._other))
+                return
+        if self.prefetcher is not None:
+            self._average(self.prefetcher.finish())
+            return
         target = self.next_peer()
         self.last_target = target
         if self.store is not None:
             self.store.advertise()
-            if self.store.pull(target, self._other):
-                hip().axpby(self.space.flat_param, self._other, None, 0.5, 0.5)
+            self._average(self.store.pull(target, self._other))
         else:
             self._host_pull_average(target)
 
     def _after_step(self):
         self.step_count += 1
-        if self.size == 1:
+        if self.size == 1 and not self.force_comm:
             return
         if self.store is not None:
             self.store.publish(self.space.flat_param)
+            if self.prefetcher is not None:
+                # the next step's pull (and this step's advertisement) overlap its forward/backward
+                self.last_target = self.next_peer()
+                self.prefetcher.start(self.last_target, self._consumed)
         else:
             self._host_save()
+
+    def synchronize(self):
+        """Wait for an in-flight prefetch (e.g. before a checkpoint or a resize)."""
+        if self.prefetcher is not None and self.prefetcher.thread is not None:
+            self._average(self.prefetcher.finish())
 
 
 def PairAveragingOptimizer(optimizer, named_parameters=None, fuse_requests: bool = True,
                            fused_model_name: str = "model", fused: bool = True, name=None, use_locking=False,
-                           with_keras=False, peer_selection: str = "random"):
-    """Wrap ``optimizer`` with AD-PSGD pair averaging (see module doc)."""
+                           with_keras=False, peer_selection: str = "random", prefetch: bool = True,
+                           force_comm: bool = False):
+    """Wrap ``optimizer`` with AD-PSGD pair averaging (see module doc).
+
+    * ``prefetch=True`` (GPU): the model averaged in at step k+1 is pulled while step k+1's
+      forward/backward are enqueued (host thread + copy stream), like the reference's
+      ``AsyncModelAveraging``; ``False`` pulls synchronously at the start of each step.
+    * ``force_comm=True``: with one peer, pull the own published snapshot through the same
+      store/copy path (exercises and profiles the device store at N=1)."""
     return _PairAveraging(optimizer, named_parameters, fuse_requests=fuse_requests,
-                          fused_model_name=fused_model_name, fused=fused, peer_selection=peer_selection)
+                          fused_model_name=fused_model_name, fused=fused, peer_selection=peer_selection,
+                          prefetch=prefetch, force_comm=force_comm)

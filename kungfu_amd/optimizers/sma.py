@@ -37,8 +37,11 @@ class ModelAverager:
     """Asynchronous all-reduce (op avg) of a flat parameter buffer, re-bound after resizes.
     Shared by SMA and AdaSGD."""
 
-    def __init__(self, space):
+    def __init__(self, space, force_comm: bool = False):
         self.space = space
+        # force_comm: with one peer still snapshot + all-reduce (1-rank RCCL) + blend, so the
+        # overlap of the model all-reduce with the next forward is exercised / profiled at N=1
+        self.force_comm = force_comm
         self.comm = None
         self.key = None  # (cluster version, comm epoch) of the pending average
         self._avg = torch.empty_like(space.flat_param)
@@ -49,7 +52,7 @@ class ModelAverager:
 
     def launch(self):
         """Snapshot the parameters and start their average on the comm stream."""
-        if runtime.size() == 1:
+        if runtime.size() == 1 and not self.force_comm:
             self.key = self.current_key()
             self.comm = None
             return
@@ -58,7 +61,8 @@ class ModelAverager:
         self.comm.fence()
         with self.comm.on_stream():
             self._avg.copy_(self.space.flat_param, non_blocking=True)
-        self.comm.all_reduce(self._avg, op="avg")
+        # one rank: the in-place sum IS the average (RCCL's one-rank avg is an extra scaled copy)
+        self.comm.all_reduce(self._avg, op="avg" if self.comm.size > 1 else "sum", tag="sma model average")
 
     def blend(self, alpha: float):
         """v <- (1 - alpha) v + alpha avg(v), using the pending average if it is
@@ -77,10 +81,10 @@ class ModelAverager:
 
 class _SynchronousAveraging(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, alpha: float = 0.1, fused: bool = True,
-                 flat=None):
+                 flat=None, force_comm: bool = False):
         super().__init__(optimizer, named_parameters, fused=fused, flat=flat)
         self.alpha = alpha
-        self.averager = ModelAverager(self.space) if self.space is not None else None
+        self.averager = ModelAverager(self.space, force_comm=force_comm) if self.space is not None else None
 
     def _before_step(self):
         if self.averager is not None:
@@ -99,8 +103,10 @@ class _SynchronousAveraging(KungFuOptimizer):
 
 
 def SynchronousAveragingOptimizer(optimizer, named_parameters=None, alpha: float = 0.1, fused: bool = True,
-                                  name=None, use_locking=False, with_keras=False, flat=None):
+                                  name=None, use_locking=False, with_keras=False, flat=None, force_comm: bool = False):
     """Wrap ``optimizer`` with synchronous model averaging (alpha = weight of
     the central model).  ``name``/``use_locking``/``with_keras`` are accepted
-    for API parity with the reference and ignored."""
-    return _SynchronousAveraging(optimizer, named_parameters, alpha=alpha, fused=fused, flat=flat)
+    for API parity with the reference and ignored.  ``force_comm``: run the model
+    all-reduce even with one peer (see :class:`ModelAverager`)."""
+    return _SynchronousAveraging(optimizer, named_parameters, alpha=alpha, fused=fused, flat=flat,
+                                 force_comm=force_comm)

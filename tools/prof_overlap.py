@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--comm-regex", default=r"ncclDevKernel|rccl|oneRank|nccl")
     ap.add_argument("--marker", default="sgd")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--copies", default=None, help="rocprofv3 --memory-copy-trace CSV: count copies as comm")
     a = ap.parse_args()
     ks = []
     with open(a.trace) as f:
@@ -62,6 +63,13 @@ def main():
             e = int(_col(row, "End_Timestamp", "EndNs", "End"))
             q = row.get("Stream_Id") or row.get("Queue_Id") or row.get("Queue_ID") or "?"
             ks.append((s, e, name, q))
+    if a.copies:
+        with open(a.copies) as f:
+            for row in csv.DictReader(f):
+                s = int(_col(row, "Start_Timestamp", "BeginNs", "Start"))
+                e = int(_col(row, "End_Timestamp", "EndNs", "End"))
+                d = row.get("Direction") or row.get("Operation") or "copy"
+                ks.append((s, e, "memcpy:%s" % d, "copy"))
     ks.sort()
     marks = [s for s, e, n, q in ks if re.search(a.marker, n)]
     if len(marks) < a.steps + 1:
