@@ -94,6 +94,126 @@ def _self_launch(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def _elastic_launch(schedule: str) -> int:
+    """``--elastic`` without a launcher: run this script under ``kungfu-run -w`` (watch mode,
+    built-in config server), starting with the schedule's first size; relay the final
+    rank 0's JSON line (the launcher prefixes worker output) to stdout."""
+    import socket
+    import subprocess
+
+    sizes = [int(p.split(":")[0]) for p in schedule.split(",") if p]
+
+    def free_block(n):
+        for base in range(21000 + (os.getpid() % 97) * 211, 60000, 97):
+            ok = True
+            for q in range(base, base + n):
+                sk = socket.socket()
+                try:
+                    sk.bind(("0.0.0.0", q))
+                except OSError:
+                    ok = False
+                finally:
+                    sk.close()
+                if not ok:
+                    break
+            if ok:
+                return base
+        raise RuntimeError("no free port block")
+
+    base = free_block(max(sizes) + 8)
+    cfg = base + max(sizes) + 6
+    cmd = [os.path.join(ROOT, "bin", "kungfu-run"), "-q", "-w", "-np", str(sizes[0]), "-H", "127.0.0.1:%d" % max(sizes),
+           "-port", str(base), "-port-range", "%d-%d" % (base + 1, base + 1 + max(sizes) + 4),
+           "-builtin-config-port", str(cfg), "-config-server", "http://127.0.0.1:%d/config" % cfg,
+           sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench.py: elastic run %s: %s" % (schedule, " ".join(cmd)), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        i = line.find('{"metric"')
+        if i >= 0:
+            print(line[i:].rstrip("\n"), flush=True)
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def _elastic_loop(a, model, opt, step, sync, bert):
+    """Config 5 as one command: train through the ``--elastic`` schedule with
+    ``ElasticTrainer`` (resize via the config server, state re-broadcast, RCCL communicators
+    rebuilt for every cluster version); per phase: throughput (each phase's first step --
+    communicator setup, learned bucket order -- is not timed), replica checksum agreement,
+    the gradient noise scale; plus every resize's latency.  The final rank 0 prints one JSON.
+
+    Parity: srcs/python/kungfu/tensorflow/experimental/hook/elastic.py:68-84 (ElasticHook +
+    ResizeProfiler), benchmarks/adaptation/bench-adaptation.sh, srcs/go/kungfu/peer/peer.go:168-276."""
+    import torch
+
+    import kungfu_amd as kf
+    from kungfu_amd.elastic import ElasticTrainer
+
+    sched = kf.ops.StepBasedSchedule(a.elastic)
+    total = sum(int(p.split(":")[1]) for p in a.elastic.split(",") if p)
+    tr = ElasticTrainer(model, opt, local_batch_size=a.batch, schedule=a.elastic)
+    phases, cur = [], None
+    while True:
+        tr.before_step()
+        if tr.step >= total:
+            break
+        n, ver = kf.current_cluster_size(), kf.cluster_version()
+        if cur is None or cur["version"] != ver:
+            cur = {"version": ver, "np": n, "first_step": tr.step, "steps": 0, "times": []}
+            phases.append(cur)
+        t0 = time.perf_counter()
+        loss = step()
+        sync()
+        cur["times"].append(time.perf_counter() - t0)
+        cur["steps"] += 1
+        cur["loss"] = float(loss.detach())
+        last = tr.step + 1 >= total
+        if last or sched(tr.step + 1) != n:  # phase end: are the replicas identical?
+            ck = _replica_checksum(opt, model)
+            cks = kf.ops.all_gather(ck).view(n, 2)
+            cur["replicas_consistent"] = bool((cks == cks[0:1]).all())
+            cur["replica_checksum"] = [float(v) for v in cks[0].tolist()]
+            cur["gradient_noise_scale"] = getattr(opt, "noise_scale", None)
+        if last:
+            tr.step += 1
+            break
+        if tr.after_step():
+            break
+    if kf.detached() or kf.current_rank() != 0:
+        kf.finalize()
+        return
+    out = []
+    for ph in phases:
+        ts = ph["times"][1:] or ph["times"]
+        thr = a.batch * ph["np"] * len(ts) / sum(ts)
+        out.append({"np": ph["np"], "cluster_version": ph["version"], "first_step": ph["first_step"],
+                    "steps": ph["steps"], "timed_steps": len(ts), "value": round(thr, 2),
+                    "ms_per_step": round(1000 * sum(ts) / len(ts), 3), "final_loss": round(ph["loss"], 4),
+                    "replicas_consistent": ph.get("replicas_consistent"),
+                    "gradient_noise_scale": ph.get("gradient_noise_scale")})
+    resizes = [{"from": o, "to": nn, "seconds": round(d, 3)} for d, o, nn in tr.profiler.records]
+    unit = "sequences/sec" if bert else "images/sec"
+    res = {
+        "metric": "%s/sec %s elastic %s (%s)" % ("sequences" if bert else "images", a.model, a.optimizer, a.elastic),
+        "value": out[-1]["value"] if out else None,
+        "unit": unit + " (aggregate over the final phase's ranks)",
+        "n_gpus": out[-1]["np"] if out else None,
+        "steps": total,
+        "higher_is_better": True,
+        "dtype": "bf16" if a.device == "cuda" else "f32",
+        "data": "synthetic",
+        "config": {"model": a.model, "per_gpu_batch": a.batch, "seq_len": a.seq_len if bert else None,
+                   "optimizer": a.optimizer, "schedule": a.elastic},
+        "phases": out,
+        "resizes": resizes,
+        "all_phases_consistent": all(p["replicas_consistent"] for p in out),
+    }
+    print(json.dumps(res), flush=True)
+    kf.finalize()
+
+
 def _replica_checksum(opt, model):
     """(sum, weighted sum) in float64 over every trainable parameter -- equal on every
     rank iff the replicas are (bitwise up to f64 summation) identical."""
@@ -134,7 +254,12 @@ def main():
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
     p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--elastic", default=None, metavar="SIZE:STEPS,...",
+                   help="elastic run (config 5): resize the job along this schedule, e.g. 4:20,8:20 "
+                        "(self-launches kungfu-run -w with its built-in config server)")
     a = p.parse_args()
+    if a.elastic and not _launcher_env():
+        sys.exit(_elastic_launch(a.elastic))
     if a.gpus is not None and a.gpus > 1 and not _launcher_env():
         sys.exit(_self_launch(a.gpus))
     world_env = int(os.environ.get("WORLD_SIZE", "0")) or None
@@ -153,7 +278,7 @@ def main():
 
     kf.init()
     rank, size = kf.current_rank(), kf.current_cluster_size()
-    if a.gpus is None:
+    if a.gpus is None or a.elastic:
         a.gpus = size
     if size != a.gpus or (world_env is not None and world_env != size):
         print("bench.py: --gpus %d but the job has %d ranks (WORLD_SIZE=%s); refusing to report a mislabelled "
@@ -211,7 +336,8 @@ def main():
                                                    force_comm=bool(a.force_comm) and cuda)
     else:
         opt = kf.optimizers.AdaptiveSGDOptimizer(base, named_parameters=model.named_parameters(), change_step=10)
-    kf.broadcast_parameters(model.state_dict())
+    if not a.elastic:  # elastic: ElasticTrainer broadcasts at every membership change
+        kf.broadcast_parameters(model.state_dict())
     if a.bf16_shadow and getattr(opt, "space", None) is not None:
         from kungfu_amd.parallel.mixed import enable_bf16_shadow
 
@@ -242,6 +368,9 @@ def main():
         loss.backward()
         opt.step()
         return loss
+
+    if a.elastic:
+        return _elastic_loop(a, model, opt, step, sync, bert)
 
     t_w0 = time.time()
     first_loss = None

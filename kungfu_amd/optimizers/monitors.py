@@ -102,8 +102,8 @@ class _GradientNoiseScale(_SynchronousSGD):
 
     # per-tensor CPU path ---------------------------------------------------------
     def sync_gradients(self):
-        if self.space is not None or not self._monitoring():
-            return super().sync_gradients()
+        if self.space is not None or not self._monitoring() or self.np == 1:
+            return super().sync_gradients()  # B == b with one peer: the estimate is undefined
         grads = [p.grad for p in self.params if p.grad is not None]
         local = ops.fuse([g.detach() for g in grads]).clone()
         super().sync_gradients()
@@ -196,8 +196,8 @@ class _GradVariance(_SynchronousSGD):
             self._var_t = torch.tensor(sum(float((s[a:b] - g[a:b] * g[a:b]).norm()) for a, b in zip(o, o[1:])))
 
     def sync_gradients(self):
-        if self.space is not None or not self._monitoring():
-            return super().sync_gradients()
+        if self.space is not None or not self._monitoring() or self.np == 1:
+            return super().sync_gradients()  # B == b with one peer: the estimate is undefined
         grads = [p.grad for p in self.params if p.grad is not None]
         sq = [g.detach() * g.detach() for g in grads]
         super().sync_gradients()

@@ -51,3 +51,21 @@ def test_bench_refuses_mislabelled_world():
                 "--batch", "2", "--image-size", "32"], env={"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "refusing" in r.stderr
+
+
+def test_bench_elastic_schedule_one_command():
+    """config 5 as one command -- ``bench.py --elastic`` self-launches
+    kungfu-run -w with its config server and reports per-phase throughput, replica
+    agreement, the noise scale while 2 peers train, and the resize latencies."""
+    r = _bench(["--elastic", "1:2,2:3,1:2", "--device", "cpu", "--model", "resnet18", "--batch", "2",
+                "--image-size", "32", "--optimizer", "gns"], timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
+    res = json.loads(lines[0])
+    assert [p["np"] for p in res["phases"]] == [1, 2, 1], res["phases"]
+    assert res["all_phases_consistent"] is True
+    assert [(z["from"], z["to"]) for z in res["resizes"]] == [(1, 2), (2, 1)], res["resizes"]
+    gns = res["phases"][1]["gradient_noise_scale"]
+    assert gns is not None and gns == gns and abs(gns) != float("inf"), res["phases"][1]
+    assert all(p["value"] > 0 for p in res["phases"])

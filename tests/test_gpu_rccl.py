@@ -111,3 +111,26 @@ def test_monitored_ssgd_adapts_on_gpu(plane):
     r = kungfu_run(2, [worker("adapt_ssgd.py"), "cuda"], timeout=240, extra=["-allow-xgmi"], env=env)
     assert r.returncode == 0, r.stdout[-4000:]
     assert r.stdout.count("ADAPT_OK") == 2, r.stdout[-4000:]
+
+
+@needs_gpu
+@pytest.mark.parametrize("plane", ["host", "rccl"])
+def test_bench_elastic_bert_gns(plane):
+    """Config 5 (BERT-base + gradient noise scale + resize) as one command on one GPU:
+    1 -> 2 ranks; the RCCL run differs from the host-staged one only in the plane."""
+    env = dict(COLO) if plane == "rccl" else {"KUNGFU_FORCE_DEVICE": "0", "KUNGFU_GPU_DATAPLANE": "host"}
+    e = dict(os.environ, PYTHONPATH=ROOT, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KUNGFU_SELF_SPEC"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "bert_base", "--optimizer", "gns",
+                        "--elastic", "1:3,2:4", "--batch", "8"], cwd=ROOT, env=e, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-5000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stderr[-5000:]
+    res = json.loads(lines[0])
+    assert [p["np"] for p in res["phases"]] == [1, 2], res["phases"]
+    assert res["all_phases_consistent"] is True, res["phases"]
+    gns = res["phases"][1]["gradient_noise_scale"]
+    assert gns is not None and gns == gns, res["phases"]
+    print(json.dumps(res))
