@@ -101,7 +101,7 @@ def _linear_forward(self, x):
 
 
 class ImmediateSink:
-    """Default sink: add the gradient into the flat slot now (torch kernel)."""
+    """Add the gradient into the flat slot now (one torch kernel per gradient)."""
 
     def __init__(self, space: FlatParamSpace):
         self.space = space
@@ -109,6 +109,40 @@ class ImmediateSink:
     def put(self, i: int, g: torch.Tensor) -> None:
         with torch.no_grad():
             self.space.grad_view(i).add_(g)
+
+
+class BatchedSink(ImmediateSink):
+    """Default sink for optimizers without a bucket engine (SMA, pair averaging, AdaSGD,
+    local): stages the direct gradients of a backward and lands them ALL with one
+    multi-tensor ``grad_accumulate`` kernel when the backward ends (an autograd engine
+    callback) -- instead of one ``AccumulateGrad``-style add per weight (ResNet-50: 161
+    adds, ~1.1 ms/step in profiles/r3o_sma_summary.md)."""
+
+    def __init__(self, space: FlatParamSpace):
+        super().__init__(space)
+        self._staged, self._offs = [], []
+        self._armed = False
+
+    def put(self, i: int, g: torch.Tensor) -> None:
+        if (g.dtype not in (torch.bfloat16, torch.float32) or not g.is_cuda
+                or g.stride() != self.space.strides[i]):
+            return super().put(i, g)
+        self._staged.append(g)
+        self._offs.append(self.space.offsets[i][0])
+        if not self._armed:
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self.flush)
+                self._armed = True
+            except RuntimeError:  # not inside a backward pass: land now
+                self.flush()
+
+    def flush(self) -> None:
+        self._armed = False
+        if self._staged:
+            from .._lib import hip
+
+            hip().grad_accumulate(self.space.flat_grad, self._staged, self._offs, 1.0)
+            self._staged, self._offs = [], []
 
 
 def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> int:
@@ -124,7 +158,7 @@ def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> i
         raise ValueError("enable_bf16_shadow: optimizer has no flat parameter space (CPU model?)")
     space.enable_shadow()
     if getattr(space, "sink", None) is None:
-        space.sink = ImmediateSink(space)
+        space.sink = BatchedSink(space)
     n = 0
 
     def register(p):
