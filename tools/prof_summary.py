@@ -16,24 +16,40 @@ import re
 
 CATEGORIES = [
     ("conv fwd", r"conv_fwd|igemm_fwd|naive_conv.*fwd|ConvFwd"),
-    ("conv bwd-data", r"conv_bwd_data|igemm_bwd_|ConvBwdData"),
+    ("conv bwd-data", r"conv_bwd_data|igemm_bwd_|ConvBwdData|naive_conv.*bwd"),
     ("conv bwd-weight", r"igemm_wrw|conv_bwd_weight|batched_gemm_xdl|ConvBwdWeight|wrw"),
     ("gemm (fc/linear)", r"Cijk_|gemm|hipblaslt"),
+    ("BN finalize (ours)", r"kfk::.*(bn_sums_finalize|bn_bwd_finalize|bn_stats_finalize|bn_eval_coef|stem_bwd_finalize)"),
     ("fused BN (ours)", r"kfk::.*bn_"),
     ("conv MFMA 1x1 (ours)", r"kfk::.*conv_kernel<1,"),
     ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,"),
+    ("conv MFMA rect KHxKW (ours)", r"kfk::.*conv_kernel<1\d\d,"),
+    ("conv MFMA stride-2 dgrad phases (ours)", r"kfk::.*conv_kernel<\d\d,"),
     ("conv weight flip (ours)", r"kfk::.*conv_flip"),
     ("conv MFMA wgrad (ours)", r"kfk::.*wgrad"),
     ("conv bias+ReLU (ours)", r"kfk::.*bias_act"),
     ("max-pool 2x2 (ours)", r"kfk::.*maxpool2"),
     ("stem conv MFMA (ours)", r"kfk::.*stem"),
-    ("optimizer/flat (ours)", r"kfk::"),
+    ("LayerNorm (ours)", r"kfk::.*ln_(fwd|bwd|colsum)"),
+    ("attention (ours)", r"kfk::.*attn_"),
+    ("pool (ours)", r"kfk::.*(gap_|avgpool|maxpool3s2)"),
+    ("bias-grad colsum (ours)", r"kfk::.*colsum_stage"),
+    ("gradient landing (ours)", r"kfk::.*(grad_accumulate|multi_copy)"),
+    ("optimizer step (ours)", r"kfk::.*(sgd_f32|adam_f32|axpby_)"),
+    ("GNS / variance monitors (ours)", r"kfk::.*(sumsq2|gns_update|variance_stage|seg_variance|square_kernel|fold1|fold2)"),
+    ("casts (ours)", r"kfk::.*(cast8|cast_tail)"),
+    ("K1 reduce / scale (ours)", r"kfk::.*(reduce_f32|reduce_half|reduce_plain|scale_f32|scale_kernel)"),
+    ("other (ours)", r"kfk::"),
     ("rccl", r"ncclDevKernel|oneRankReduce|rccl"),
     ("casts", r"bfloat16tofloat32_copy|bfloat16_copy|float_to|copy_kernel"),
     ("accumulate/add", r"CUDAFunctor_add|AddFunctor"),
-    ("fill/memset/copy", r"fillBuffer|copyBuffer|FillFunctor|SubTensorOpWithScalar|Op2dTensor|Op1dTensor"),
+    ("fill/memset/copy", r"fillBuffer|copyBuffer|FillFunctor|SubTensorOp|Op2dTensor|Op1dTensor|CatArrayBatchedCopy"),
     ("pool", r"pool"),
-    ("loss/softmax", r"softmax|nll|cross_entropy|log_softmax"),
+    ("loss/softmax", r"softmax|SoftMax|nll|cross_entropy|log_softmax"),
+    ("GELU (torch)", r"Gelu"),
+    ("dropout (torch)", r"dropout|masked_scale"),
+    ("embedding grad (torch)", r"sum_and_scatter|compute_grad_weight|embedding|device_block_merge|radix_sort"),
+    ("LayerNorm (torch)", r"layer_norm|GradGammaBeta"),
     ("batchnorm (torch/MIOpen)", r"batch_norm|BatchNorm|MIOpenBatchNorm"),
     ("other elementwise", r"elementwise|reduce_kernel"),
 ]
