@@ -7,9 +7,10 @@ the torch wrapper ``srcs/python/kungfu/torch/optimizers/sync_sgd.py:6-32``.
 Data planes:
 * GPU (default): bucketed in-place RCCL all-reduce of the flat gradient
   buffer, launched from backward hooks on a comm stream (overlapped with
-  backward), op ``avg``.  ``hierarchical=True`` uses local-reduce ->
-  cross-host host all-reduce -> local-broadcast instead (reference's
-  hierarchical NCCL path, ``ops/gpu/collective.cpp:105-156``).
+  backward), op ``avg``.  ``hierarchical=True`` runs every bucket as local reduce ->
+  cross-host host all-reduce among the local roots -> local broadcast, still
+  overlapped with backward (reference's hierarchical NCCL path,
+  ``ops/gpu/collective.cpp:105-156``; see ``ddp._CrossHostStage``).
 * CPU tensors: the C++ host runtime's graph all-reduce (TCP/UDS) with the
   chosen strategy; async per tensor, then wait all.
 
@@ -76,10 +77,11 @@ class _SynchronousSGD(KungFuOptimizer):
         self.monitor = monitor or adapt
         self.hierarchical = hierarchical
         self.reducer: Optional[GradReducer] = None
-        if self.space is not None and not hierarchical and overlap:
+        if self.space is not None and overlap:
             self.reducer = GradReducer(self.space, op="avg" if op == "avg" else "sum", bucket_mb=bucket_mb,
                                        comm_dtype=comm_dtype, skip_single=not force_comm,
-                                       first_bucket_mb=first_bucket_mb, monitored=self.monitor)
+                                       first_bucket_mb=first_bucket_mb, monitored=self.monitor and not hierarchical,
+                                       hierarchical=hierarchical)
         self.adapter = InterferenceAdapter(warmup=adapt_warmup) if adapt else None
 
     def _before_step(self):

@@ -57,6 +57,8 @@ def _local_bcast_bytes(data: bytes, name: str) -> bytes:
 
 
 def _scope_rank_size(scope: str):
+    """"global", or a per-host scope ("local", "local:<purpose>" -- separate communicators
+    over the same host group, e.g. one per issuing thread)."""
     if scope == "global":
         return runtime.rank(), runtime.size()
     return runtime.local_rank(), runtime.local_size()

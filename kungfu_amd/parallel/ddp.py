@@ -75,11 +75,94 @@ class LateGradientError(RuntimeError):
     pass
 
 
+class _CrossHostStage:
+    """The middle and last steps of a hierarchical bucket all-reduce with several hosts
+    (parity: ``CrossAllReduceGpu``, srcs/cpp/src/nccl/controller.cpp:8-40): one worker
+    thread takes the buckets in launch order -- the same order on every rank -- and, on
+    the host's root, waits for the local reduce, stages the bucket through host memory,
+    all-reduces it among the local roots over the host transport and copies it back; then
+    every local rank issues the local broadcast on a SECOND local communicator from this
+    thread (each communicator is driven by exactly one thread, in one order).  Backward
+    keeps running meanwhile; ``drain`` (end of backward) waits for the queue and orders
+    the compute stream after the broadcasts."""
+
+    def __init__(self, reducer: "GradReducer", bcast_comm):
+        import queue
+        import threading
+
+        from .._lib import runtime
+
+        self.r, self.bcast = reducer, bcast_comm
+        self.cuda = reducer.space.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=reducer.space.device) if self.cuda else None
+        self.root = runtime.local_rank() == 0
+        self.size = runtime.size()
+        self.version = runtime.cluster_version()
+        self.q = queue.Queue()
+        self.err = None
+        self.seq = 0
+        self.th = threading.Thread(target=self._loop, name="kungfu-cross-host", daemon=True)
+        self.th.start()
+
+    def submit(self, g: torch.Tensor, tag: str):
+        ev = None
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(self.r.comm.stream)
+        self.seq += 1
+        self.q.put((g, ev, tag, self.seq))
+
+    def _loop(self):
+        from .._lib import dtype_code, op_code, runtime
+
+        if self.cuda:
+            torch.cuda.set_device(self.r.space.device)
+        while True:
+            item = self.q.get()
+            if item is None:
+                self.q.task_done()
+                return
+            g, ev, tag, seq = item
+            try:
+                ctx = torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
+                with ctx:
+                    if self.cuda:
+                        self.stream.wait_event(ev)
+                    if self.root:
+                        if self.cuda:
+                            ev.synchronize()
+                            h = g.to("cpu")
+                        else:
+                            h = g
+                        runtime.cross_all_reduce(h.data_ptr(), h.data_ptr(), h.numel(), dtype_code(h), op_code("sum"),
+                                                 "kf:hier:v%d:%d" % (self.version, seq))
+                        if self.r.op == "avg":
+                            h.mul_(1.0 / self.size)
+                        if self.cuda:
+                            g.copy_(h)
+                    self.bcast.broadcast(g, root=0, stream=self.stream, tag=tag + " (local broadcast)")
+            except BaseException as e:  # noqa: BLE001 -- re-raised by drain()
+                self.err = e
+            self.q.task_done()
+
+    def drain(self):
+        self.q.join()
+        if self.err is not None:
+            e, self.err = self.err, None
+            raise e
+        if self.cuda:
+            torch.cuda.current_stream(self.r.space.device).wait_stream(self.stream)
+
+    def stop(self):
+        self.q.put(None)
+        self.th.join(timeout=30)
+
+
 class GradReducer:
     def __init__(self, space: FlatParamSpace, op: str = "avg", bucket_mb: Optional[float] = None,
                  first_bucket_mb: float = 1.0, comm_dtype: Optional[torch.dtype] = None,
                  tail_bucket_mb: float = 4.0,
-                 skip_single: bool = True, monitored: bool = False):
+                 skip_single: bool = True, monitored: bool = False, hierarchical: bool = False):
         # skip_single: with one peer the average of the gradients IS the local
         # gradient, so no collective is issued (the engine's hooks still run).
         # skip_single=False sends every bucket through the communicator even
@@ -90,6 +173,12 @@ class GradReducer:
         # monitored: every bucket's all-reduce feeds the session's strategy statistics
         # (SynchronousSGDOptimizer(monitor=True); parity sync_sgd.py:96-97)
         self.monitored = monitored
+        # hierarchical: local reduce -> cross-host all-reduce among the hosts' local roots ->
+        # local broadcast, per bucket, during backward (the reference's
+        # ScheduledHierarchicalNcclAllReduce per tensor through its ordered scheduler,
+        # srcs/cpp/src/tensorflow/ops/gpu/collective.cpp:105-156)
+        self.hierarchical = hierarchical
+        self._hier = None
         cap_mb = float(os.environ.get("KUNGFU_BUCKET_MB", bucket_mb if bucket_mb is not None else 32.0))
         esz = space.flat_grad.element_size()
         if comm_dtype is not None and comm_dtype not in (torch.float32, torch.bfloat16):
@@ -177,7 +266,15 @@ class GradReducer:
             return
         size = runtime.size()
         self.skip = self.skip_single and size == 1
-        self.comm = None if self.skip else get_device_comm(device=self.space.device)
+        if self._hier is not None:
+            self._hier.stop()
+            self._hier = None
+        if self.hierarchical and not self.skip:
+            self.comm = get_device_comm("local", device=self.space.device)
+            if runtime.host_count() > 1:
+                self._hier = _CrossHostStage(self, get_device_comm("local:bcast", device=self.space.device))
+        else:
+            self.comm = None if self.skip else get_device_comm(device=self.space.device)
         # The learned collective order belongs to the old membership: start again
         # from index order; the new rank 0's arrival order is adopted after one step.
         self.sched = runtime.OrderedScheduler(len(self.buckets))
@@ -199,10 +296,11 @@ class GradReducer:
         from .._lib import runtime
 
         return {
+            "hierarchical": self.hierarchical,
             "buckets": len(self.buckets),
             "bucket_mb": round(max(b.end - b.start for b in self.buckets) * self.space.flat_grad.element_size()
                                / (1 << 20), 2),
-            "comm_ranks": (self.comm.size if self.comm is not None else runtime.size()),
+            "comm_ranks": (self.comm.size if self.comm is not None and not self.hierarchical else runtime.size()),
             "comm_plane": ("skip" if self.skip else getattr(self.comm, "plane", "?")),
             "comm_dtype": str(self.comm_dtype or self.space.flat_grad.dtype).replace("torch.", ""),
             "comm_bytes_per_step": self.bytes_per_step,
@@ -308,6 +406,8 @@ class GradReducer:
             self._reduce(comm, g)
 
     def _reduce(self, comm, g):
+        if self.hierarchical:
+            return self._reduce_hierarchical(comm, g)
         if not self.graph:
             # one rank: the average IS the sum, and RCCL's in-place one-rank sum is free while
             # its one-rank average is a scaled copy of the bucket (oneRankReduce<PreMulSum>:
@@ -323,10 +423,28 @@ class GradReducer:
             with comm.on_stream():
                 g.mul_(1.0 / comm.size)
 
+    def _reduce_hierarchical(self, comm, g):
+        """Local reduce to the host's root on the comm stream; then either (one host) the
+        local broadcast right behind it -- all stream-ordered, no host sync -- or (several
+        hosts) hand the bucket to the cross-host stage, which runs the host all-reduce among
+        the local roots and the local broadcast on its own thread and stream."""
+        from .._lib import runtime
+
+        comm.reduce(g, op="sum", root=0, tag=self._tag + " (local reduce)")
+        if self._hier is not None:
+            self._hier.submit(g, self._tag)
+            return
+        if self.op == "avg" and comm.rank == 0:
+            with comm.on_stream():
+                g.mul_(1.0 / runtime.size())
+        comm.broadcast(g, root=0, tag=self._tag + " (local broadcast)")
+
     def _finish(self):
         for j in self.sched.flush():
             if not self.buckets[j].launched:
                 self._launch(self.buckets[j])
+        if self._hier is not None:
+            self._hier.drain()
         if not self.skip:
             self.comm.join()
             if self._steps_bound == 1 and not self._ordered:

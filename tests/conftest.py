@@ -74,3 +74,31 @@ def run():
 
 def worker(name):
     return os.path.join(ROOT, "tests", "workers", name)
+
+
+def run_fake_hosts(script_args, hosts=2, per_host=2, env=None, timeout=240):
+    """Start hosts x per_host peers directly with the kungfu-run env contract, host h on
+    127.0.0.<h+1> (the runtime groups hosts by IPv4; all of 127/8 reaches this machine), so
+    multi-host code paths (cross-host stages, local communicators) run on one box.
+    Returns (returncodes, combined output)."""
+    base = free_port_block(hosts * per_host + 2)
+    peers = ["127.0.0.%d:%d" % (h + 1, base + h * per_host + i) for h in range(hosts) for i in range(per_host)]
+    procs = []
+    for p in peers:
+        e = dict(os.environ, KUNGFU_SELF_SPEC=p, KUNGFU_INIT_PEERS=",".join(peers), KUNGFU_INIT_RUNNERS="",
+                 KUNGFU_INIT_CLUSTER_VERSION="0", PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
+                 OMP_NUM_THREADS="2")
+        if env:
+            e.update(env)
+        procs.append(subprocess.Popen([sys.executable] + list(script_args), env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            outs.append(pr.communicate(timeout=timeout)[0])
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+                pr.wait()
+    return [pr.returncode for pr in procs], "\n".join(outs)

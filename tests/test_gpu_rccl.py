@@ -134,3 +134,16 @@ def test_bench_elastic_bert_gns(plane):
     gns = res["phases"][1]["gradient_noise_scale"]
     assert gns is not None and gns == gns, res["phases"]
     print(json.dumps(res))
+
+
+@needs_gpu
+def test_hierarchical_bucket_engine_two_fake_hosts_rccl():
+    """Hierarchical S-SGD on the GPU with 2 "hosts" x 2 ranks (conftest.run_fake_hosts):
+    per bucket a local RCCL reduce, the host all-reduce among the local roots on the
+    cross-host thread, a local RCCL broadcast on the second local communicator -- equal to
+    one process on the global batch."""
+    from conftest import run_fake_hosts
+
+    rcs, text = run_fake_hosts([worker("ssgd_exact.py"), "f32", "cuda", "hier"], env=COLO, timeout=300)
+    assert all(rc == 0 for rc in rcs), text[-5000:]
+    assert text.count("SSGD_EXACT_OK") == 4 and "hier=True" in text, text[-5000:]

@@ -56,3 +56,24 @@ def test_other_optimizers_train(opt):
         assert all("gns=" in x[4] and "None" not in x[4] for x in res)
     if opt == "var":
         assert all("var=" in x[4] for x in res)
+
+
+@pytest.mark.parametrize("hier", ["flat", "hier"])
+def test_bucket_engine_matches_single_process_cpu(hier):
+    """The flat bucket engine over the host plane (and its hierarchical mode: local reduce ->
+    cross-host -> local broadcast per bucket) reproduces one process on the global batch."""
+    r = kungfu_run(3, [worker("ssgd_exact.py"), "f32", "cpu", hier], timeout=240)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert r.stdout.count("SSGD_EXACT_OK") == 3, r.stdout[-4000:]
+
+
+def test_hierarchical_bucket_engine_two_fake_hosts_cpu():
+    """Hierarchical bucket engine with 2 "hosts" x 2 ranks (127.0.0.1 / 127.0.0.2, see
+    conftest.run_fake_hosts): the cross-host stage (local reduce -> host all-reduce among
+    the 2 local roots -> local broadcast from its own thread) runs and the result equals
+    one process on the global batch."""
+    from conftest import run_fake_hosts
+
+    rcs, text = run_fake_hosts([worker("ssgd_exact.py"), "f32", "cpu", "hier"])
+    assert all(rc == 0 for rc in rcs), text[-5000:]
+    assert text.count("SSGD_EXACT_OK") == 4 and "hier=True" in text, text[-5000:]

@@ -14,11 +14,17 @@ import torch.nn.functional as F
 import kungfu_amd as kf
 
 comm_dtype = sys.argv[1] if len(sys.argv) > 1 else "f32"
+device = sys.argv[2] if len(sys.argv) > 2 else "cuda"
+hier = len(sys.argv) > 3 and sys.argv[3] == "hier"
 os.environ["KUNGFU_TAIL_BUCKET_MB"] = "0.05"  # several buckets for this 0.5 MB model
 kf.init()
 r, n = kf.current_rank(), kf.current_cluster_size()
-dev = torch.device("cuda", kf.get_hip_index())
-torch.cuda.set_device(dev)
+if device == "cuda":
+    dev = torch.device("cuda", kf.get_hip_index())
+    torch.cuda.set_device(dev)
+else:
+    dev = torch.device("cpu")
+    torch.set_num_threads(2)
 B, STEPS = 8, 4
 
 
@@ -47,7 +53,8 @@ m = net()
 opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4),
                                             named_parameters=m.named_parameters(), bucket_mb=0.1,
                                             first_bucket_mb=0.05,
-                                            comm_dtype=torch.bfloat16 if comm_dtype == "bf16" else None)
+                                            comm_dtype=torch.bfloat16 if comm_dtype == "bf16" else None,
+                                            flat=True, hierarchical=hier)
 kf.broadcast_parameters(m.state_dict())
 assert opt.reducer is not None and len(opt.reducer.buckets) >= 3, len(opt.reducer.buckets)
 errs = []
@@ -60,7 +67,8 @@ for step, (x, y) in enumerate(data):
     want = ref_grads[step]
     errs.append(((got.double() - want.double()).norm() / want.double().norm()).item())
     opt.step()
-torch.cuda.synchronize()
+if device == "cuda":
+    torch.cuda.synchronize()
 w_got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).double()
 w_ref = torch.cat([p.detach().reshape(-1) for p in ref.parameters()]).double()
 werr = ((w_got - w_ref).norm() / w_ref.norm()).item()
@@ -75,6 +83,7 @@ else:
     assert max(errs) < 8e-3 and werr < 8e-3, (errs, werr)
 ck = kf.ops.all_gather(w_got.sum().reshape(1).cpu())
 assert torch.all(ck == ck[0]), ck
-print("SSGD_EXACT_OK rank=%d np=%d plane=%s dtype=%s grad_err=%.2e w_err=%.2e" % (
-    r, n, d["comm_plane"], comm_dtype, max(errs), werr), flush=True)
+assert d["hierarchical"] == hier, d
+print("SSGD_EXACT_OK rank=%d np=%d plane=%s dtype=%s hier=%s grad_err=%.2e w_err=%.2e" % (
+    r, n, d["comm_plane"], comm_dtype, hier, max(errs), werr), flush=True)
 kf.finalize()
