@@ -31,6 +31,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace kfk {
@@ -52,6 +53,39 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
     for (int i = 0; i < 4; ++i)
         w[i] = static_cast<uint32_t>(f32_to_bf16(f[2 * i])) | (static_cast<uint32_t>(f32_to_bf16(f[2 * i + 1])) << 16);
     return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Non-temporal 16-byte accesses (KUNGFU_BN_NT: bit 0 loads, bit 1 stores), for the apply passes
+// that stream every byte exactly once.  A uniform runtime flag: both paths are in one kernel.
+typedef unsigned int kf_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld16(const uint4 *p, bool nt) {
+    if (nt) {
+        const kf_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const kf_u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
+
+__device__ __forceinline__ void st16(uint4 *p, const uint4 &v, bool nt) {
+    if (nt) {
+        kf_u32x4 w;
+        w.x = v.x;
+        w.y = v.y;
+        w.z = v.z;
+        w.w = v.w;
+        __builtin_nontemporal_store(w, reinterpret_cast<kf_u32x4 *>(p));
+    } else {
+        *p = v;
+    }
+}
+
+int bn_nt_mode() {
+    static const int m = [] {
+        const char *e = std::getenv("KUNGFU_BN_NT");
+        return e ? std::atoi(e) : 0;
+    }();
+    return m;
 }
 
 struct Chunking {
@@ -288,8 +322,9 @@ template <int CVEC, bool RES, bool RELU, bool RESC = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restrict__ x, const uint4 *__restrict__ res,
                                                           const float *__restrict__ coef, uint4 *__restrict__ y,
                                                           uint8_t *__restrict__ mask, int64_t nvec,
-                                                          const float *__restrict__ rcoef = nullptr) {
+                                                          const float *__restrict__ rcoef = nullptr, int ntm = 0) {
     constexpr int C = CVEC * 8;
+    const bool ntl = ntm & 1, nts = ntm & 2;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
     float sc[8], sh[8], rsc[8], rsh[8];
@@ -311,8 +346,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
         for (int u = 0; u < U; ++u) {
             const int64_t i = i0 + u * stride;
             if (i < nvec) {
-                xr[u] = x[i];
-                if (RES) rr4[u] = res[i];
+                xr[u] = ld16(x + i, ntl);
+                if (RES) rr4[u] = ld16(res + i, ntl);
             }
         }
 #pragma unroll
@@ -335,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
                 }
                 f[k] = v;
             }
-            y[i] = pack8(f);
+            st16(y + i, pack8(f), nts);
             if (RES && RELU) mask[i] = static_cast<uint8_t>(m);
         }
     }
@@ -467,10 +502,11 @@ __global__ __launch_bounds__(kBlock) void bn_pool_bwd_sums_kernel(const uint4 *_
 // flight before any arithmetic: fetch() issues the loads, get() unpacks.
 struct DirectGrad {
     const uint4 *dy;
+    bool nt = false;
     using Raw = uint4;
     template <int CVEC>
     __device__ __forceinline__ Raw fetch(int64_t i, int64_t /*row*/, int /*cv*/) const {
-        return dy[i];
+        return ld16(dy + i, nt);
     }
     __device__ __forceinline__ void get(const Raw &r, float (&g)[8]) const { unpack8(r, g); }
 };
@@ -716,8 +752,9 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
                                                               const float *__restrict__ coef, uint4 *__restrict__ dx,
                                                               uint4 *__restrict__ dres, int64_t nvec,
                                                               const uint4 *__restrict__ dsx = nullptr,
-                                                              double *__restrict__ dsums = nullptr) {
+                                                              double *__restrict__ dsums = nullptr, int ntm = 0) {
     constexpr int C = CVEC * 8;
+    const bool ntl = ntm & 1, nts = ntm & 2;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
     const int cv = static_cast<int>(tid % CVEC);
     float k1[8], k2[8], k3[8], sc[8], sh[8];
@@ -743,7 +780,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
             const int64_t i = i0 + u * stride;
             if (i < nvec) {
                 gr[u] = grad.template fetch<CVEC>(i, i / CVEC, cv);
-                xr[u] = x[i];
+                xr[u] = ld16(x + i, ntl);
             }
         }
 #pragma unroll
@@ -756,7 +793,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
             relu_gate<RM>(g, xv, sc, sh, mask, i);
             if (DRES) {
                 const uint4 gr = pack8(g);
-                dres[i] = gr;
+                st16(dres + i, gr, nts);
                 if (dsum) {
                     float gq[8], sx[8];
                     unpack8(gr, gq);
@@ -771,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_apply_kernel(G grad, const uint
             float o[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) o[k] = k1[k] * g[k] + k2[k] * xv[k] + k3[k];
-            dx[i] = pack8(o);
+            st16(dx + i, pack8(o), nts);
         }
     }
     if (dsum) {
@@ -881,7 +918,7 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
             constexpr bool DR = decltype(drc)::value;
             bn_bwd_apply_kernel<CV, RM, DR, G><<<g, bn_threads<CV>(), 0, s>>>(
                 grad, xx, fcoef, mask, coef, o, r, nvec, DR ? reinterpret_cast<const uint4 *>(dres_x) : nullptr,
-                DR ? dres_sums : nullptr);
+                DR ? dres_sums : nullptr, bn_nt_mode());
         };
         using T = std::true_type;
         using F = std::false_type;
@@ -930,6 +967,7 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
     }
     if (!apply) return;
     const int g = apply_grid(nvec, cvec);
+    const int ntm = bn_nt_mode();
     dispatch_cvec(cvec, [&](auto cvc) {
         constexpr int CV = decltype(cvc)::value;
         constexpr int NT = bn_threads<CV>();
@@ -937,14 +975,14 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
         const uint4 *rv = reinterpret_cast<const uint4 *>(res);
         uint4 *yv = reinterpret_cast<uint4 *>(y);
         if (res && res_coef) {
-            if (relu) bn_apply_kernel<CV, true, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef);
-            else bn_apply_kernel<CV, true, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef);
+            if (relu) bn_apply_kernel<CV, true, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef, ntm);
+            else bn_apply_kernel<CV, true, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, res_coef, ntm);
         } else if (res) {
-            if (relu) bn_apply_kernel<CV, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
-            else bn_apply_kernel<CV, true, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            if (relu) bn_apply_kernel<CV, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
+            else bn_apply_kernel<CV, true, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
         } else {
-            if (relu) bn_apply_kernel<CV, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
-            else bn_apply_kernel<CV, false, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec);
+            if (relu) bn_apply_kernel<CV, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
+            else bn_apply_kernel<CV, false, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
         }
     });
 }
@@ -962,7 +1000,7 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                              dres_sums);
         return;
     }
-    launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy)}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
+    launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy), (bn_nt_mode() & 1) != 0}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
                          training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums);
 }
 

@@ -1,6 +1,6 @@
 // Streaming bandwidth of the BN-apply access pattern (x, res -> y, 1-byte mask per 16 B) on
 // MI355X: plain vs non-temporal loads/stores, unroll depth and grid size.  Standalone:
-//   hipcc -O3 --offload-arch=gfx950 tools/micro/stream_bw.hip -o /tmp/stream_bw && /tmp/stream_bw
+//   hipcc -O3 --offload-arch=gfx950 tools/stream_bw.hip -o /tmp/stream_bw && /tmp/stream_bw
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
