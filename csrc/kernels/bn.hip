@@ -80,12 +80,22 @@ __device__ __forceinline__ void st16(uint4 *p, const uint4 &v, bool nt) {
     }
 }
 
+// default 1 (non-temporal loads): ResNet-50 step 21.73 -> 21.39 ms on MI355X, while
+// non-temporal stores did not pay in the full step (profiles/README.md, r3f)
 int bn_nt_mode() {
     static const int m = [] {
         const char *e = std::getenv("KUNGFU_BN_NT");
-        return e ? std::atoi(e) : 0;
+        return e ? std::atoi(e) : 1;
     }();
     return m;
+}
+
+int bn_max_grid(int def) {
+    static const int m = [] {
+        const char *e = std::getenv("KUNGFU_BN_MAXGRID");
+        return e ? std::atoi(e) : 0;
+    }();
+    return m > 0 ? m : def;
 }
 
 struct Chunking {
@@ -622,7 +632,8 @@ template <int CVEC, int RM, class G>
 __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(G grad, const uint4 *__restrict__ x,
                                                                const float *__restrict__ fcoef,
                                                                const uint8_t *__restrict__ mask, int64_t rows,
-                                                               int64_t rows_per_chunk, float *partial) {
+                                                               int64_t rows_per_chunk, float *partial, int ntm = 0) {
+    const bool ntl = ntm & 1;
     constexpr int RPI = kBlock / CVEC;
     constexpr int C = CVEC * 8;
     __shared__ float lds[2 * RPI * C];
@@ -645,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_reduce_kernel(G grad, const uin
         for (int u = 0; u < U; ++u) {
             const int64_t row = r + u * RPI, i = row * CVEC + cv;
             gr[u] = grad.template fetch<CVEC>(i, row, cv);
-            xr[u] = x[i];
+            xr[u] = ld16(x + i, ntl);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -862,7 +873,8 @@ void dispatch_cvec(int cvec, F &&f) {
 int apply_grid(int64_t nvec, int cvec) {
     const int nt = (kBlock / cvec) * cvec;
     int64_t g = (nvec + nt - 1) / nt;
-    if (g > kMaxGrid) g = kMaxGrid;
+    const int mg = bn_max_grid(kMaxGrid);
+    if (g > mg) g = mg;
     if (g < 1) g = 1;
     return static_cast<int>(g);
 }
@@ -900,7 +912,8 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
         auto go = [&](auto rmc) {
             constexpr int RM = decltype(rmc)::value;
             bn_bwd_reduce_kernel<CV, RM, G>
-                <<<ch.nchunks, bn_threads<CV>(), 0, s>>>(grad, xx, fcoef, mask, sh.rows, ch.rows_per_chunk, partial);
+                <<<ch.nchunks, bn_threads<CV>(), 0, s>>>(grad, xx, fcoef, mask, sh.rows, ch.rows_per_chunk, partial,
+                                                          bn_nt_mode());
         };
         if (rm == RM_COEF) go(std::integral_constant<int, RM_COEF>());
         else if (rm == RM_BITS) go(std::integral_constant<int, RM_BITS>());
