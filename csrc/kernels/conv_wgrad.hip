@@ -30,6 +30,8 @@
 // tf.keras.applications ResNet-50 with TF's stock convolutions
 // (benchmarks/system/benchmark_kungfu.py:96).
 #include "common.hpp"
+
+#include <cstdlib>
 #include "kernels.hpp"
 
 #include <algorithm>
@@ -55,7 +57,19 @@ struct WGeo {
     uint64_t m_hw, m_ow;  // floor(p / d) = (p * m) >> 40, exact for p * d < 2^40
     int mtiles, ntiles, taps, tiles, splits, kps;
     int kwin, ph, pw;  // KS == 0 (any window): taps per kernel row and the zero padding
+    int nta, ntb;      // stage dy (A) / x (B) with non-temporal LDS-DMA loads (aux = 2)
 };
+
+// KUNGFU_WGRAD_NT: 0 never, 1 for an operand every byte of which is staged once (dy when
+// ntiles * taps == 1, x when mtiles * taps == 1), 2 always.
+void wgrad_set_nt(WGeo &g) {
+    static const int m = [] {
+        const char *e = std::getenv("KUNGFU_WGRAD_NT");
+        return e ? std::atoi(e) : 0;
+    }();
+    g.nta = m == 2 || (m == 1 && g.ntiles * g.taps == 1);
+    g.ntb = m == 2 || (m == 1 && g.mtiles * g.taps == 1);
+}
 
 __device__ __forceinline__ int fdiv(int p, uint64_t m) {
     return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
@@ -147,7 +161,10 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         for (int j = 0; j < A_INST; ++j) {
             const int p = p0 + a_row[j];
             const uint16_t *src = p < g.P && a_col[j] < g.K ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
-            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+            if (g.nta)
+                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
@@ -165,7 +182,10 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                     static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
                     src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
             }
-            __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
+            if (g.ntb)
+                __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
         }
     };
 
@@ -600,6 +620,7 @@ WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const 
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.splits = plan.splits;
     g.kps = plan.kps;
+    wgrad_set_nt(g);
     return g;
 }
 
@@ -772,6 +793,7 @@ WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int p
     g.taps = kh * kw;
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.kwin = kw, g.ph = ph, g.pw = pw;
+    wgrad_set_nt(g);
     return g;
 }
 }  // namespace
