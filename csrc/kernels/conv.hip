@@ -63,18 +63,7 @@ struct Geo {
     int scat;    // 1: output row m -> pixel (2*(m/OW) + pr, 2*(m%OW) + pc) of a 2OH x 2OW image
     int pr, pc;
     int ph, pw;  // zero padding (rows, columns)
-    int nta;     // 1: stage the A operand with non-temporal LDS-DMA loads (aux = 2)
 };
-
-// KUNGFU_CONV_NT_A: 0 never, 1 when the A operand (activations / output gradient) is read by
-// exactly one column of tiles (ntiles == 1: every byte staged once), 2 always.
-int conv_nt_a(int ntiles) {
-    static const int m = [] {
-        const char *e = std::getenv("KUNGFU_CONV_NT_A");
-        return e ? std::atoi(e) : 0;
-    }();
-    return m == 2 || (m == 1 && ntiles == 1) ? 1 : 0;
-}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -199,10 +188,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         for (int j = 0; j < A_INST; ++j) {
             const bool ok = ((a_ok[j] >> tap) & 1u) && cin_ok;
             const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
-            if (g.nta)
-                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 2);
-            else
-                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
@@ -555,7 +541,6 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv: Cin and Cout must be multiples of 8");
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = (g.K + BN - 1) / BN;
-    g.nta = conv_nt_a(g.ntiles);
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
     if constexpr (STATS) {
         // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
@@ -657,7 +642,6 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
     g.ph = g.pw = pad;
-    g.nta = 0;
     if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
 }
@@ -717,7 +701,6 @@ void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, 
     g.mtiles = g.ntiles = 0;
     g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
     g.ph = ph, g.pw = pw;
-    g.nta = 0;
     if (kh == 1 && kw == 1) {
         launch_ks<1>(x, w, y, g, ea, epi, s, -1);
         return;
@@ -743,7 +726,6 @@ void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g,
     if (g.K % BN) throw std::invalid_argument("conv_dgrad_s2: Cin not a multiple of the tile");
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = g.K / BN;
-    g.nta = conv_nt_a(g.ntiles);
     const int grid = g.mtiles * g.ntiles;
     const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
     if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
@@ -786,7 +768,6 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.scat = 1;
     g.ph = g.pw = 0;
-    g.nta = 0;
     if (ks == 1) {
         g.tapmap = -1, g.pr = g.pc = 0;
         launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);

@@ -30,8 +30,6 @@
 // tf.keras.applications ResNet-50 with TF's stock convolutions
 // (benchmarks/system/benchmark_kungfu.py:96).
 #include "common.hpp"
-
-#include <cstdlib>
 #include "kernels.hpp"
 
 #include <algorithm>
@@ -57,19 +55,15 @@ struct WGeo {
     uint64_t m_hw, m_ow;  // floor(p / d) = (p * m) >> 40, exact for p * d < 2^40
     int mtiles, ntiles, taps, tiles, splits, kps;
     int kwin, ph, pw;  // KS == 0 (any window): taps per kernel row and the zero padding
-    int nta, ntb;      // stage dy (A) / x (B) with non-temporal LDS-DMA loads (aux = 2)
 };
 
-// KUNGFU_WGRAD_NT: 0 never, 1 for an operand every byte of which is staged once (dy when
-// ntiles * taps == 1, x when mtiles * taps == 1), 2 always.
-void wgrad_set_nt(WGeo &g) {
-    static const int m = [] {
-        const char *e = std::getenv("KUNGFU_WGRAD_NT");
-        return e ? std::atoi(e) : 0;
-    }();
-    g.nta = m == 2 || (m == 1 && g.ntiles * g.taps == 1);
-    g.ntb = m == 2 || (m == 1 && g.mtiles * g.taps == 1);
-}
+// Cache policy of the split-K kernel's LDS-DMA operand loads: non-temporal (aux = 2).  Measured
+// on the ResNet-50 step (r3h, tools/gpu_r3_ntconv.sh): +1 % with nt on both operands; the same
+// hint on the forward / data-gradient conv kernel's activation loads cost 1.5-2 %.
+#ifndef KUNGFU_WGRAD_AUX
+#define KUNGFU_WGRAD_AUX 2
+#endif
+constexpr int kWgradAux = KUNGFU_WGRAD_AUX;
 
 __device__ __forceinline__ int fdiv(int p, uint64_t m) {
     return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
@@ -161,10 +155,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         for (int j = 0; j < A_INST; ++j) {
             const int p = p0 + a_row[j];
             const uint16_t *src = p < g.P && a_col[j] < g.K ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
-            if (g.nta)
-                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 2);
-            else
-                __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, kWgradAux);
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
@@ -182,10 +173,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                     static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
                     src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
             }
-            if (g.ntb)
-                __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 2);
-            else
-                __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, kWgradAux);
         }
     };
 
@@ -620,7 +608,6 @@ WGeo make_geo(int N, int H, int W, int Cin, int Cout, int ks, int stride, const 
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.splits = plan.splits;
     g.kps = plan.kps;
-    wgrad_set_nt(g);
     return g;
 }
 
@@ -793,7 +780,6 @@ WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int p
     g.taps = kh * kw;
     g.tiles = g.mtiles * g.ntiles * g.taps;
     g.kwin = kw, g.ph = ph, g.pw = pw;
-    wgrad_set_nt(g);
     return g;
 }
 }  // namespace
