@@ -5,14 +5,15 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 ALT=$1; TAG=$2; shift 2
+BARGS=("$@")
 SO=$(ls kungfu_amd/_hip*.so)
 cp "$SO" /tmp/_hip_main.so
 run() {  # $1 = label
-  timeout -k 10 300 python bench.py --steps 30 --warmup 8 "$@" > "$OUT/${TAG}_$1.log" 2>&1 || return $?
+  timeout -k 10 300 python bench.py --steps 30 --warmup 8 "${BARGS[@]}" > "$OUT/${TAG}_$1.log" 2>&1 || return $?
   echo "$1 $(tail -1 $OUT/${TAG}_$1.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')"
 }
 for i in 1 2; do
-  cp /tmp/_hip_main.so "$SO" && run main$i "$@" || exit $?
-  cp "$ALT" "$SO" && run alt$i "$@" || exit $?
+  cp /tmp/_hip_main.so "$SO" && run main$i || exit $?
+  cp "$ALT" "$SO" && run alt$i || exit $?
 done
 cp /tmp/_hip_main.so "$SO"
