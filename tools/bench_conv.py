@@ -87,6 +87,9 @@ for Hh, C, K, ks, s in SHAPES:
     tot["fwd_o"] += t_o
     tot["fst_o"] += t_os
     line += " | fwd miopen %6.1f ours %6.1f +stats %6.1f" % (t_m, t_o, t_os)
+    byt = 2.0 * (N * Hh * Hh * C + N * OH * OH * K + K * C * ks * ks)
+    fl = 2.0 * N * OH * OH * K * C * ks * ks
+    line += " (%.2f TB/s %.0f TF/s)" % (byt / t_o / 1e6, fl / t_o / 1e6)
     vs = []
     for v in range(H_.conv3x3_variants()):
         if v in (0, 1) and K % 128:
