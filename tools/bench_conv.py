@@ -94,7 +94,10 @@ for Hh, C, K, ks, s in SHAPES:
     for v in range(H_.conv3x3_variants()):
         if v in (0, 1) and K % 128:
             continue
-        vs.append((timeit(lambda: H_.conv(x, w, s, None, None, v)), v))
+        try:
+            vs.append((timeit(lambda: H_.conv(x, w, s, None, None, v)), v))
+        except ValueError:  # tile does not fit this shape
+            pass
     vs.sort()
     line += " [best v%d %.1f, %s]" % (vs[0][1], vs[0][0], " ".join("v%d %.0f" % (v, t) for t, v in sorted(vs, key=lambda z: z[1])))
     if s == 1:
