@@ -46,7 +46,7 @@ import torch
 import torch.nn.functional as F
 
 from .._lib import hip, hip_available
-from ..parallel.mixed import deliver, direct_target, shadow
+from ..parallel.mixed import SideStream, deliver, direct_target, shadow
 
 _ENABLED = os.environ.get("KUNGFU_FUSED_BLOCK", "1") != "0"
 
@@ -250,6 +250,15 @@ class _BottleneckFn(torch.autograd.Function):
                     fl[k] = src[0].get(src[1])
         dbn = [None] * nb  # (dgamma, dbeta)
         dw = [None] * nb
+        # weight gradients on the side stream when every one of them goes to a gradient sink
+        # (bf16 shadow weights): the sink joins the side stream before landing them
+        side = SideStream.enabled and spec.wsrc is not None and all(v is not None for v in spec.wsrc)
+
+        def wgrad(dy_, x_, w_, s_, p_):
+            if side:
+                return SideStream.run(lambda a_, b_: _wgrad(a_, b_, w_, s_, p_), dy_, x_)
+            return _wgrad(dy_, x_, w_, s_, p_)
+
         ws = [_sums(b, dout.device) for b in spec.bns]
         tail = ctx.tail
         use3 = tail.ready and dout.data_ptr() == tail.dx_ptr
@@ -267,12 +276,12 @@ class _BottleneckFn(torch.autograd.Function):
                                             dres_sums=ws[3] if spec.ds else None)
         dbn[2] = (dg3, db3)
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None))
-        dw[2] = _wgrad(dy3, z2, w[2], 1, 0)
+        dw[2] = wgrad(dy3, z2, w[2], 1, 0)
         dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1])
         dbn[1] = (dg2, db2)
         dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None))
         fused1 = _dgrad.fused
-        dw[1] = _wgrad(dy2, z1, w[1], s, 1)
+        dw[1] = wgrad(dy2, z1, w[1], s, 1)
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
                                          ws[0] if fused1 else None)
         dbn[0] = (dg1, db1)
@@ -286,7 +295,7 @@ class _BottleneckFn(torch.autograd.Function):
                 acc_even = True
             else:
                 dx = _dgrad(dyd, x, w[3], s, 0, flipped=fl[3])
-            dw[3] = _wgrad(dyd, x, w[3], s, 0)
+            dw[3] = wgrad(dyd, x, w[3], s, 0)
         elif in_place:
             dx = dout  # raw output gradient; masked by mask3 inside conv1's data-gradient epilogue
         else:
@@ -301,7 +310,7 @@ class _BottleneckFn(torch.autograd.Function):
             prev.ready, prev.dx_ptr = True, dx.data_ptr()
         else:
             dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], out_mask=om, acc_even=acc_even)
-        dw[0] = _wgrad(dy1, x, w[0], 1, 0)
+        dw[0] = wgrad(dy1, x, w[0], 1, 0)
         grads: List[Optional[torch.Tensor]] = []
         for i in range(nb):
             gw = dw[i]

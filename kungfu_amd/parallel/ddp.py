@@ -335,6 +335,9 @@ class GradReducer:
         # carry it into the next step's gradient
         if (not self._enabled or b.launched or g.dtype not in (torch.bfloat16, torch.float32)
                 or g.stride() != self.space.strides[i] or not g.is_cuda):
+            from .mixed import SideStream
+
+            SideStream.join()
             with torch.no_grad():
                 self.space.grad_view(i).add_(g)
         else:
@@ -373,7 +376,9 @@ class GradReducer:
         """Add the bucket's staged direct gradients into the flat buffer (one kernel)."""
         if b.staged:
             from .._lib import hip
+            from .mixed import SideStream
 
+            SideStream.join()  # weight gradients still running on the side stream
             hip().grad_accumulate(self.space.flat_grad, b.staged, b.staged_off, 1.0)
             b.staged, b.staged_off = [], []
 
@@ -440,11 +445,14 @@ class GradReducer:
         comm.broadcast(g, root=0, tag=self._tag + " (local broadcast)")
 
     def _finish(self):
+        from .mixed import SideStream
+
         for j in self.sched.flush():
             if not self.buckets[j].launched:
                 self._launch(self.buckets[j])
         if self._hier is not None:
             self._hier.drain()
+        SideStream.join()  # nothing computed on the side stream outlives backward
         if not self.skip:
             self.comm.join()
             if self._steps_bound == 1 and not self._ordered:

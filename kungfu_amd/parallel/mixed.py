@@ -30,6 +30,7 @@ Usage::
 """
 from __future__ import annotations
 
+import os
 import types
 from typing import Dict, Optional, Tuple
 
@@ -100,6 +101,55 @@ def _linear_forward(self, x):
     return linear(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
 
 
+class SideStream:
+    """Weight gradients on a side stream, overlapping the backward data-gradient chain
+    (``KUNGFU_WGRAD_STREAM=1``): a weight gradient depends only on its layer's output
+    gradient and input, and nothing on the critical path of backward reads it, so it can
+    run beside the next layers' data gradients and the memory-bound BN passes (filling the
+    CUs an under-sized grid leaves idle).  Its results reach the flat gradient buffer only
+    through a gradient sink, which makes the landing stream wait for every side-stream
+    event recorded so far (:meth:`join`) -- the join is deferred to the bucket launch / the
+    end of backward instead of the end of each layer."""
+
+    enabled = os.environ.get("KUNGFU_WGRAD_STREAM", "0") == "1"
+    _streams: Dict[int, torch.cuda.Stream] = {}
+    _pending: list = []
+
+    @classmethod
+    def stream(cls, dev: torch.device) -> torch.cuda.Stream:
+        k = dev.index if dev.index is not None else torch.cuda.current_device()
+        s = cls._streams.get(k)
+        if s is None:
+            s = cls._streams[k] = torch.cuda.Stream(device=k)
+        return s
+
+    @classmethod
+    def run(cls, fn, *inputs: torch.Tensor) -> torch.Tensor:
+        """``fn(*inputs)`` on the side stream after the work issued so far on the current
+        stream; the result is registered for a deferred :meth:`join`."""
+        main = torch.cuda.current_stream()
+        side = cls.stream(inputs[0].device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            out = fn(*inputs)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for t in inputs:
+            t.record_stream(side)  # main may free them while the side stream still reads
+        out.record_stream(main)  # consumed on the main stream after the join
+        cls._pending.append(ev)
+        return out
+
+    @classmethod
+    def join(cls, stream=None) -> None:
+        if not cls._pending:
+            return
+        s = stream if stream is not None else torch.cuda.current_stream()
+        for ev in cls._pending:
+            s.wait_event(ev)
+        cls._pending = []
+
+
 class ImmediateSink:
     """Add the gradient into the flat slot now (one torch kernel per gradient)."""
 
@@ -107,6 +157,7 @@ class ImmediateSink:
         self.space = space
 
     def put(self, i: int, g: torch.Tensor) -> None:
+        SideStream.join()
         with torch.no_grad():
             self.space.grad_view(i).add_(g)
 
@@ -141,6 +192,7 @@ class BatchedSink(ImmediateSink):
         if self._staged:
             from .._lib import hip
 
+            SideStream.join()
             hip().grad_accumulate(self.space.flat_grad, self._staged, self._offs, 1.0)
             self._staged, self._offs = [], []
 

@@ -327,3 +327,45 @@ def test_add_layernorm_fused_residual_dropout():
         assert ((a.float() - c).norm() / c.norm()).item() < 2e-2
     assert torch.equal(ra.grad == 0, ~keep | (xa.grad == 0))
     del hip
+
+
+@needs_gpu
+def test_wgrad_side_stream_bit_identical():
+    """Weight gradients on the side stream (KUNGFU_WGRAD_STREAM, parallel/mixed.py SideStream)
+    overlap the data-gradient chain; the deferred join before landing must make the flat
+    gradients bit-identical to the single-stream backward (same deterministic kernels)."""
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet50
+    from kungfu_amd.parallel.mixed import SideStream, enable_bf16_shadow
+
+    kf.init()
+
+    def run(side):
+        old = SideStream.enabled
+        SideStream.enabled = side
+        try:
+            torch.manual_seed(0)
+            m = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9))
+            enable_bf16_shadow(m, opt)
+            g = torch.Generator(device="cuda").manual_seed(3)
+            x = torch.randn(16, 3, 96, 96, device="cuda", generator=g).to(memory_format=torch.channels_last)
+            y = torch.randint(0, 1000, (16,), device="cuda", generator=g)
+            grads = []
+            for _ in range(3):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    F.cross_entropy(m(x).float(), y).backward()
+                grads.append(opt.space.flat_grad.clone())
+                opt.step()
+            torch.cuda.synchronize()
+            assert not SideStream._pending
+            return grads, opt.space.flat_param.clone()
+        finally:
+            SideStream.enabled = old
+
+    g0, p0 = run(False)
+    g1, p1 = run(True)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b), (a - b).abs().max()
+    assert torch.equal(p0, p1)
