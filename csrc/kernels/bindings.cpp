@@ -387,6 +387,71 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
     return y;
 }
 
+// Linear layer on the MFMA kernel: y[M, N] = x[M, K] @ w[N, K]^T (both row-major bf16).
+//   bias:            y += bias (bf16 [N]);  gelu (needs bias): returns (gelu(u), u), u = x w^T + b;
+//   out:             y = out += x w^T (accumulate into an existing [M, N] bf16 tensor);
+//   gelu_u + stats:  y = (x w^T) * gelu'(gelu_u), stats[slot][0][n] += sum_m y (a bias gradient;
+//                    stats: zeroed f64 kStatSlots x 2 x N workspace).
+std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
+                             c10::optional<at::Tensor> out, c10::optional<at::Tensor> gelu_u,
+                             c10::optional<at::Tensor> stats, int64_t variant) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+                "gemm: x must be a contiguous 2-D bf16 GPU tensor");
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 2 && w.is_contiguous() && w.size(1) == x.size(1) &&
+                    w.device() == x.device(),
+                "gemm: w must be a contiguous [N, K] bf16 tensor on x's device");
+    const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+    TORCH_CHECK(M < (int64_t(1) << 31) && kfk::gemm_supported(static_cast<int>(M), static_cast<int>(K), static_cast<int>(N)),
+                "gemm: unsupported shape (K, N multiples of 64)");
+    c10::DeviceGuard gd(x.device());
+    kfk::EpiArgs ea;
+    int epi = 0;
+    at::Tensor y, u;
+    auto check_mn = [&](const at::Tensor &t, const char *what) {
+        TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.size(0) == M && t.size(1) == N &&
+                        t.is_contiguous() && t.device() == x.device(),
+                    "gemm: ", what, " must be a contiguous [M, N] bf16 tensor on x's device");
+    };
+    if (out && out->defined()) {
+        TORCH_CHECK(!(bias && bias->defined()) && !gelu && !(gelu_u && gelu_u->defined()),
+                    "gemm: out (accumulate) excludes bias / gelu / gelu_u");
+        check_mn(*out, "out");
+        y = *out;
+        epi = kfk::kEpiAccum;
+    } else {
+        y = at::empty({M, N}, x.options());
+    }
+    if (bias && bias->defined()) {
+        TORCH_CHECK(bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous() &&
+                        bias->device() == x.device(),
+                    "gemm: bias must be a contiguous bf16 [N] tensor on x's device");
+        ea.bias = reinterpret_cast<const uint16_t *>(bias->data_ptr());
+        epi = kfk::kEpiBias;
+        if (gelu) {
+            u = at::empty({M, N}, x.options());
+            ea.aux = reinterpret_cast<uint16_t *>(u.data_ptr());
+            epi = kfk::kEpiGelu;
+        }
+    } else {
+        TORCH_CHECK(!gelu, "gemm: gelu needs a bias");
+    }
+    if (gelu_u && gelu_u->defined()) {
+        TORCH_CHECK(epi == 0, "gemm: gelu_u excludes bias / out");
+        check_mn(*gelu_u, "gelu_u");
+        TORCH_CHECK(stats && stats->defined() && stats->scalar_type() == at::kDouble && stats->is_contiguous() &&
+                        stats->numel() == 2 * N * kfk::kStatSlots && stats->device() == x.device(),
+                    "gemm: gelu_u needs the f64 stats workspace (kStatSlots x 2 x N)");
+        ea.bx = reinterpret_cast<const uint16_t *>(gelu_u->data_ptr());
+        ea.stats = stats->data_ptr<double>();
+        epi = kfk::kEpiGeluGrad;
+    }
+    kfk::launch_gemm(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                     reinterpret_cast<uint16_t *>(y.data_ptr()), static_cast<int>(M), static_cast<int>(K),
+                     static_cast<int>(N), ea, epi, stream_of(x, 0), static_cast<int>(variant));
+    if (u.defined()) return {y, u};
+    return {y};
+}
+
 // Data gradient of a stride-2 1x1 (pad 0) / 3x3 (pad 1) convolution with an even input:
 // dy [N, Cout, OH, OW] -> dx [N, Cin, 2OH, 2OW] (channels_last bf16), wt = conv_flip_weight(w)
 // [Cin, Cout, ks, ks].  ks = 3: every pixel written (four parity-phase GEMMs); bn_x + stats
@@ -1444,6 +1509,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none());
     m.def("conv_rect_supported", &kfk::conv_rect_supported);
+    m.def("gemm", &gemm, "linear layer x @ w^T on the MFMA kernel with bias / GELU / GELU-gradient(+bias-gradient "
+          "sums) / accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
+          py::arg("gelu") = false, py::arg("out") = py::none(), py::arg("gelu_u") = py::none(),
+          py::arg("stats") = py::none(), py::arg("variant") = -1);
+    m.def("gemm_supported", &kfk::gemm_supported);
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),

@@ -102,9 +102,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int LOADS = A_INST + B_INST;
     static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
     constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
     constexpr bool GATE = (EPI & kEpiGate) != 0;
-    constexpr int NSUM = GATE ? 1 : 2;  // the gate needs sum(y) only
+    constexpr bool GELU = (EPI & kEpiGelu) != 0, GELUG = (EPI & kEpiGeluGrad) != 0;
+    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias | kEpiGelu)) != 0;
+    constexpr int NSUM = (GATE || GELUG) ? 1 : 2;  // the gates need sum(y) only (a bias gradient)
     constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     constexpr int GROUPS = NT / VPR;
     // the statistics reduction reuses the C tile's LDS once the last tile is stored
@@ -271,7 +273,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         bcol[j] = 0.f;
-        if constexpr ((EPI & kEpiBiasRelu) != 0) bcol[j] = bf16_to_f32(ea.bias[n0 + wn * WTN + j * 16 + (lane & 15)]);
+        if constexpr (BIAS) {
+            const int c = n0 + wn * WTN + j * 16 + (lane & 15);
+            if (c < g.K) bcol[j] = bf16_to_f32(ea.bias[c]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -282,10 +287,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
                 const int col = wn * WTN + j * 16 + (lane & 15);
                 float v = acc[i][j][r];
-                if constexpr ((EPI & kEpiBiasRelu) != 0) {
-                    v += bcol[j];
-                    v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
-                }
+                if constexpr (BIAS) v += bcol[j];
+                if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
                 *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(v);
             }
     __syncthreads();
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int ITER = BM * VPR / NT;
     static_assert(ITER * NT == BM * VPR, "whole store iterations");
     constexpr bool LD_OLD = (EPI & kEpiAccum) != 0;
-    constexpr bool LD_BX = GATE || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
+    constexpr bool LD_BX = GATE || GELUG || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
     // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
     // the 256x256 tile, whose 16 coefficient registers would otherwise spill)
     constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
@@ -387,11 +390,44 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                     vw[k] &= keep;
                 }
             }
+            if constexpr (GELU) {
+                // v = u (bias added): saved for the backward, then y = gelu(u) in f32, one rounding
+                *reinterpret_cast<uint4 *>(ea.aux + ee[u]) = v;
+                float f[8];
+                unpack_bf16x8(v, f);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float a = f[2 * k], b = f[2 * k + 1];
+                    const float ga = 0.5f * a * (1.f + erff(a * 0.70710678118654752f));
+                    const float gb = 0.5f * b * (1.f + erff(b * 0.70710678118654752f));
+                    vw[k] = static_cast<uint32_t>(f32_to_bf16(ga)) | (static_cast<uint32_t>(f32_to_bf16(gb)) << 16);
+                }
+            }
+            if constexpr (GELUG) {
+                // gradient of gelu(u): dy * (Phi(u) + u * phi(u)), torch's GeluBackward in f32
+                float f[8], uf[8];
+                unpack_bf16x8(v, f);
+                unpack_bf16x8(bxv[u], uf);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float d[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float t = uf[2 * k + h];
+                        const float cdf = 0.5f * (1.f + erff(t * 0.70710678118654752f));
+                        const float pdf = __expf(-0.5f * t * t) * 0.39894228040143268f;
+                        d[h] = f[2 * k + h] * (cdf + t * pdf);
+                    }
+                    vw[k] = static_cast<uint32_t>(f32_to_bf16(d[0])) | (static_cast<uint32_t>(f32_to_bf16(d[1])) << 16);
+                }
+            }
             *reinterpret_cast<uint4 *>(y + ee[u]) = v;
             if constexpr (STATS) {
                 float f[8];
                 unpack_bf16x8(v, f);
-                if constexpr (GATE) {
+                if constexpr (GATE || GELUG) {
 #pragma unroll
                     for (int k = 0; k < 8; ++k) s1[k] += f[k];
                 } else if constexpr ((EPI & kEpiFwdStats) != 0) {
@@ -680,6 +716,60 @@ void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, con
         case A | C: launch_epi<KS, 4, 1, 2, A | C>(x, w, y, g, ea, s); break;
         default: throw std::invalid_argument("conv_rect: unsupported epilogue");
         }
+    }
+}
+
+// Linear layers: M tokens x K in-features -> N out-features, the 1x1 case of the kernel above
+// (H = W = 1) with the bias / GELU / GELU-gradient / accumulate epilogues.
+template <int WM, int WN, int ST, int TM, int TN>
+void launch_gemm_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
+                   hipStream_t s) {
+    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
+    if (g.K % BN) throw std::invalid_argument("gemm: out-features not a multiple of the tile");
+    g.mtiles = (g.M + BM - 1) / BM;
+    g.ntiles = g.K / BN;
+    const dim3 grid(g.mtiles * g.ntiles), block(64 * WM * WN);
+    const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
+    switch (epi) {
+    case 0: conv_kernel<1, WM, WN, ST, 0, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
+    case kEpiBias: conv_kernel<1, WM, WN, ST, kEpiBias, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
+    case kEpiGelu: conv_kernel<1, WM, WN, ST, kEpiGelu, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
+    case kEpiGeluGrad:
+        conv_kernel<1, WM, WN, ST, kEpiGeluGrad, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea);
+        break;
+    case kEpiAccum: conv_kernel<1, WM, WN, ST, kEpiAccum, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
+    default: throw std::invalid_argument("gemm: unsupported epilogue");
+    }
+}
+
+bool gemm_supported(int M, int K, int N) {
+    return M > 0 && K >= 64 && K % 64 == 0 && N % 64 == 0 && N >= 64 &&
+           static_cast<int64_t>(M) * (K > N ? K : N) < (int64_t(1) << 31);
+}
+
+void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K, int N, const EpiArgs &ea, int epi,
+                 hipStream_t s, int variant) {
+    if (!gemm_supported(M, K, N)) throw std::invalid_argument("gemm: unsupported shape");
+    Geo g;
+    g.N = M, g.H = g.W = 1, g.C = K, g.K = N, g.stride = 1;
+    g.OH = g.OW = 1, g.M = M;
+    g.mtiles = g.ntiles = 0;
+    g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0;
+    if (variant < 0) {
+        // enough 256x256 tiles to fill the chip twice, else 256x128, else 128x128 (or 128x64)
+        const int64_t t256 = N % 256 ? 0 : ((M + 255) / 256) * (N / 256);
+        const int64_t t128 = N % 128 ? 0 : ((M + 255) / 256) * (N / 128);
+        variant = t256 >= 512 ? 0 : t128 >= 512 ? 1 : 2;
+    }
+    switch (variant) {
+    case 0: if (N % 256 == 0) { launch_gemm_t<4, 2, 2, 4, 8>(x, w, y, g, ea, epi, s); break; }  // 256x256, 8 waves
+            [[fallthrough]];
+    case 1: if (N % 128 == 0) { launch_gemm_t<4, 2, 3, 4, 4>(x, w, y, g, ea, epi, s); break; }  // 256x128, 8 waves
+            [[fallthrough]];
+    case 2: if (N % 128 == 0) { launch_gemm_t<2, 2, 2, 4, 4>(x, w, y, g, ea, epi, s); break; }  // 128x128, 4 waves
+            launch_gemm_t<2, 1, 2, 4, 4>(x, w, y, g, ea, epi, s); break;                       // 128x64
+    default: if (N % 256) throw std::invalid_argument("gemm variant 3: N % 256");
+            launch_gemm_t<2, 4, 2, 8, 4>(x, w, y, g, ea, epi, s); break;                       // 256x256, 128x64 waves
     }
 }
 

@@ -109,13 +109,21 @@ bool conv_supported(int Cin, int Cout, int ks, int stride);
 // kEpiAccMask (with kEpiAccum): y = old * amask + conv -- the residual gradient dz = dout * relu'
 // formed from the raw output gradient and the 1-bit ReLU mask on the fly, so the BN3+add+ReLU
 // backward need not write dz (ResNet identity blocks).
+// Linear-layer (GEMM) epilogues, launch_gemm only:
+//   kEpiBias      y = conv + bias (bf16 bias, added in f32 before the one rounding);
+//   kEpiGelu      u = bf16(conv + bias) is written to ea.aux (the GELU's saved input) and
+//                 y = gelu(u) (erf form, torch's F.gelu default);
+//   kEpiGeluGrad  the output is the gradient of a GELU output whose input is ea.bx (= u):
+//                 y = bf16(conv) * gelu'(u) and stats[slot][0][c] += sum(y) (the bias gradient
+//                 of the layer that produced u).
 enum ConvEpi : int {
     kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
-    kEpiAccMask = 64, kEpiAccEven = 128
+    kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGelu = 512, kEpiGeluGrad = 1024
 };
 struct EpiArgs {
     const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
-    const uint16_t *bias = nullptr;  // kEpiBiasRelu: bf16 [K]
+    uint16_t *aux = nullptr;         // kEpiGelu: the pre-activation output [M, K] bf16
+    const uint16_t *bias = nullptr;  // kEpiBiasRelu / kEpiBias / kEpiGelu: bf16 [K]
     double *stats = nullptr;         // kStatSlots x [2][K] f64 (zeroed; consumed + re-zeroed by the BN)
     const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output
     const float *fcoef = nullptr;    // bwd coef: forward [scale(K); shift(K)]
@@ -136,6 +144,11 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
 // KH x KW window with zero padding (ph, pw), stride 1|2 (Inception-v3's 1x1, 3x3 pad 0|1, 1x7,
 // 7x1, 1x3, 3x1, 5x5): the same implicit GEMM, K = KH*KW*Cin tap-major; epilogue none or
 // kEpiFwdStats.  Cin, Cout multiples of 64.
+// Linear layer y[M, N] = x[M, K] w[N, K]^T (+ epilogue) on the same MFMA kernel (a 1x1 conv over
+// M "pixels"): epi 0, kEpiBias, kEpiGelu, kEpiGeluGrad, kEpiAccum (y += product).  K, N % 64.
+bool gemm_supported(int M, int K, int N);
+void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K, int N, const EpiArgs &ea, int epi,
+                 hipStream_t s, int variant = -1);
 bool conv_rect_supported(int Cin, int Cout, int kh, int kw, int stride);
 void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
                       int kh, int kw, int ph, int pw, int stride, const EpiArgs &ea, int epi, hipStream_t s);
