@@ -556,7 +556,7 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c
 // Weight gradient of a KH x KW convolution with zero padding (ph, pw): dw [Cout, Cin, KH, KW]
 // channels_last bf16 (kfk::conv_wgrad_rect_supported: Inception-v3's windows / channel counts).
 at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, int64_t stride, int64_t ph,
-                           int64_t pw) {
+                           int64_t pw, int64_t variant) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_wgrad_rect: x must be a 4-D channels_last bf16 GPU tensor");
@@ -577,7 +577,8 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
     c10::DeviceGuard gd(x.device());
     auto dw = at::empty({K, C, kh, kw}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
     const auto plan = kfk::conv_wgrad_rect_plan(N, H, W, C, K, static_cast<int>(kh), static_cast<int>(kw),
-                                                static_cast<int>(ph), static_cast<int>(pw), static_cast<int>(stride));
+                                                static_cast<int>(ph), static_cast<int>(pw), static_cast<int>(stride),
+                                                static_cast<int>(variant));
     at::Tensor ws;
     if (plan.ws_floats > 0) ws = at::empty({plan.ws_floats}, x.options().dtype(at::kFloat));
     kfk::launch_conv_wgrad_rect(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
@@ -1522,8 +1523,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "
           "(split-K MFMA GEMM, any channel count % 8)", py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
-          py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0);
+          py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("variant") = -1);
     m.def("conv_wgrad_rect_supported", &kfk::conv_wgrad_rect_supported);
+    m.def("conv_wgrad_rows_rect_supported", &kfk::conv_wgrad_rows_rect_supported, "row-image weight-gradient kernel "
+          "covers this stride-1 window (args: N, H, W, Cin, Cout, kh, kw, ph, pw, stride)");
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
           py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);

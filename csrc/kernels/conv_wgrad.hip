@@ -483,6 +483,222 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Row-image weight gradient for ANY stride-1 KH x KW window with zero padding and channel
+// counts % 8 (Inception-v3's narrow multi-tap layers: 32..192 channels, 1x7 / 7x1 / 3x3 /
+// 5x5, pad 0 or (K-1)/2), the generalisation of wgrad_rows_kernel above:
+//   * output tile 64 co x 64 ci per wave and tap; channels past Cout / Cin are staged from the
+//     zero page and their outputs dropped (48 -> one half-empty tile, 80 -> 64 + 16, ...);
+//   * a workgroup holds NWV waves = NWV consecutive taps of the window (taps > NWV: the window
+//     is split over tap groups, e.g. 5x5 = 9 + 9 + 7 taps; idle waves of the last group only
+//     stage) and shares one K-step's staging among them: dy as 64 pixel rows, the input as the
+//     (R + KH - 1) x (L + KW - 1) image around the segment of 64 output pixels;
+//   * tap (kh, kw) reads the image at row offset kh * XW + kw (transposing LDS reads with
+//     per-lane row addresses: the im2col shift is only an address offset).
+// Replaces MIOpen's igemm_wrw for these shapes (r2o_inception_wgrad.txt: 170-275 TF/s there).
+struct RRGeo {
+    int N, H, W, C, K, OH, OW;
+    int KH, KW, ph, pw, taps, tgroups;
+    int L, R, spr, gpi, nseg;
+    int XW, xrows, xpieces;
+    int mtiles, ntiles, tiles, splits, kps;
+};
+
+template <int NWV, int STAGES>
+__global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_t *__restrict__ dy,
+                                                                   const uint16_t *__restrict__ x,
+                                                                   float *__restrict__ part, void *__restrict__ dw,
+                                                                   const uint16_t *__restrict__ zero, RRGeo g,
+                                                                   int out_f32, int accumulate, int atomic_out) {
+    constexpr int ROW = 128;                      // 64 channels
+    constexpr int MAXP = (8 + 25 + NWV - 1) / NWV;  // 1 KB pieces per wave per K-step
+    constexpr int STAGE = (8 + 25 + 1) * 1024;     // dy 8 KB | input image <= 25 KB | dummy 1 KB
+    constexpr int DUMMY = (8 + 25) * 1024;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q8 = nwg >> 3, rr8 = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < rr8 ? xcd * (q8 + 1) : rr8 * (q8 + 1) + (xcd - rr8) * q8) + (orig >> 3);
+    const int mn = g.mtiles * g.ntiles;
+    const int per_split = mn * g.tgroups;
+    const int split = wg / per_split, rem0 = wg - split * per_split;
+    const int tg = rem0 / mn, ctile = rem0 - tg * mn;
+    const int mt = ctile / g.ntiles, nt = ctile - mt * g.ntiles;
+    const int m0 = mt * 64, n0 = nt * 64;
+    const int tap = tg * NWV + wave;  // >= g.taps: staging-only wave
+    const bool has_tap = tap < g.taps;
+    const int kh = has_tap ? tap / g.KW : 0, kw = has_tap ? tap - kh * g.KW : 0;
+    const int seg0 = split * g.kps;
+    int nsteps = g.nseg - seg0;
+    if (nsteps > g.kps) nsteps = g.kps;
+
+    // ---- staging descriptors: wave issues pieces wave + NWV u; piece < 8: dy, else input image
+    const int total = 8 + g.xpieces;
+    int p_kind[MAXP], p_r[MAXP], p_c[MAXP], p_col[MAXP];  // kind 0 dy, 1 x, 2 dummy
+    bool p_cok[MAXP];
+#pragma unroll
+    for (int u = 0; u < MAXP; ++u) {
+        const int pq = wave + NWV * u;
+        const int pc = lane & 7;
+        p_cok[u] = false;
+        if (pq < 8) {
+            const int t = pq * 8 + (lane >> 3);  // dy slot
+            p_kind[u] = 0;
+            p_r[u] = t / g.L;
+            p_c[u] = t - p_r[u] * g.L;
+            if (p_r[u] >= g.R) p_r[u] = 1 << 20;  // slot past the segment: invalid
+            p_col[u] = m0 + ((((pc >> 1) ^ hswz<ROW>(t)) << 1) | (pc & 1)) * 8;
+            p_cok[u] = p_col[u] < g.K;
+        } else if (pq < total) {
+            const int t = (pq - 8) * 8 + (lane >> 3);  // image row
+            p_kind[u] = 1;
+            p_r[u] = t / g.XW;
+            p_c[u] = t - p_r[u] * g.XW;
+            if (t >= g.xrows) p_r[u] = 1 << 20;
+            p_col[u] = n0 + ((((pc >> 1) ^ hswz<ROW>(t)) << 1) | (pc & 1)) * 8;
+            p_cok[u] = p_col[u] < g.C;
+        } else {
+            p_kind[u] = 2;
+            p_r[u] = p_c[u] = p_col[u] = 0;
+        }
+    }
+    const int segs_img = g.gpi * g.spr;
+    auto stage = [&](int ks, int buf) {
+        const int seg = seg0 + ks;
+        const int n = seg / segs_img, rem = seg - n * segs_img;
+        const int grp = rem / g.spr, sidx = rem - grp * g.spr;
+        const int oh0 = grp * g.R, ow0 = sidx * g.L;
+        uint8_t *base = lds + buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < MAXP; ++u) {
+            const int pq = wave + NWV * u;
+            const uint16_t *src = zero;
+            uint8_t *dst = base + DUMMY;
+            if (p_kind[u] == 0) {
+                const int oh = oh0 + p_r[u], ow = ow0 + p_c[u];
+                if (oh < g.OH && ow < g.OW && p_cok[u])
+                    src = dy + static_cast<uint32_t>(((n * g.OH + oh) * g.OW + ow) * g.K + p_col[u]);
+                dst = base + pq * 1024;
+            } else if (p_kind[u] == 1) {
+                const int ih = oh0 + p_r[u] - g.ph, iw = ow0 + p_c[u] - g.pw;
+                if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
+                    static_cast<unsigned>(iw) < static_cast<unsigned>(g.W) && p_cok[u])
+                    src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + p_col[u]);
+                dst = base + pq * 1024;
+            }
+            __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+        }
+    };
+
+    // ---- fragment addresses.  lane = 16 fg + 4 fq + fp; K-slots j = 8 fg + fq + {0, 4, 32, 36}.
+    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+    const int rowa0 = 8 * fg + fq;
+    int aoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aoff[i] = rowa0 * ROW + 32 * (i ^ hswz<ROW>(rowa0)) + 8 * fp;
+    int boff[4][4];  // [sub-read][ci block]
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int j = rowa0 + (s & 1) * 4 + (s >> 1) * 32;
+        const int r = j / g.L, c = j - r * g.L;
+        const int jrow = r < g.R ? r * g.XW + c : 0;  // slots past the segment read a staged row (dy is 0)
+        const int trow = jrow + kh * g.XW + kw;
+        const int h = hswz<ROW>(trow);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) boff[s][i] = 8192 + trow * ROW + 32 * (i ^ h) + 8 * fp;
+    }
+
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+
+#pragma unroll
+    for (int p = 0; p < STAGES - 1; ++p)
+        if (p < nsteps) stage(p, p);
+    int buf = 0;
+    for (int ks = 0; ks < nsteps; ++ks) {
+        if (ks + STAGES - 1 <= nsteps) wait_vmcnt<MAXP * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const uint8_t *base = lds + buf * STAGE;
+        if (has_tap) {  // wave-uniform
+            bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                af0[i] = tr_frag(base + aoff[i], base + aoff[i] + 4 * ROW);
+                bf0[i] = tr_frag(base + boff[0][i], base + boff[1][i]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                af1[i] = tr_frag(base + aoff[i] + 32 * ROW, base + aoff[i] + 36 * ROW);
+                bf1[i] = tr_frag(base + boff[2][i], base + boff[3][i]);
+            }
+            mfma_block(af0, bf0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + STAGES - 1 < nsteps) {
+                int nb = buf + STAGES - 1;
+                if (nb >= STAGES) nb -= STAGES;
+                stage(ks + STAGES - 1, nb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_block(af1, bf1);
+        } else if (ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
+        buf = buf + 1 == STAGES ? 0 : buf + 1;
+    }
+    wait_vmcnt<0>();
+    if (!has_tap) return;
+
+    // ---- epilogue (wgrad_kernel's three forms; tile = this wave's tap)
+    if (atomic_out || g.splits == 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = m0 + i * 16 + (lane >> 4) * 4 + r;
+                    const int ci = n0 + j * 16 + (lane & 15);
+                    if (co >= g.K || ci >= g.C) continue;
+                    const int64_t e = (static_cast<int64_t>(co) * g.taps + tap) * g.C + ci;
+                    float v = acc[i][j][r];
+                    if (atomic_out) {
+                        atomicAdd(static_cast<float *>(dw) + e, v);
+                    } else if (out_f32) {
+                        float *o = static_cast<float *>(dw) + e;
+                        *o = accumulate ? *o + v : v;
+                    } else {
+                        uint16_t *o = static_cast<uint16_t *>(dw) + e;
+                        if (accumulate) v += bf16_to_f32(*o);
+                        *o = f32_to_bf16(v);
+                    }
+                }
+    } else {
+        const int tile = tap * mn + mt * g.ntiles + nt;
+        f32x4 *dst = reinterpret_cast<f32x4 *>(part + (static_cast<int64_t>(split) * g.tiles + tile) * 4096) + lane;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * 64);
+    }
+}
+
 // Sum the split partials (workspace order of wgrad_kernel) and scatter to dw.
 // Block = 256 threads = OUT float4 outputs x SG split groups (SG = 256 / OUT, a power of
 // two <= splits): a few K outputs with hundreds of splits (the 56x56 layers) still keep
@@ -784,8 +1000,54 @@ WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int p
 }
 }  // namespace
 
-WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride) {
+namespace {
+// the row-image kernel's segments / tap groups for a stride-1 KH x KW window (xpieces > 25: unsupported)
+RRGeo rows_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw) {
+    RRGeo g{};
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
+    g.OH = H + 2 * ph - kh + 1, g.OW = W + 2 * pw - kw + 1;
+    g.KH = kh, g.KW = kw, g.ph = ph, g.pw = pw, g.taps = kh * kw;
+    const int nwv = g.taps % 7 == 0 ? 7 : 9;
+    g.tgroups = (g.taps + nwv - 1) / nwv;
+    if (g.OW >= 64) {
+        g.L = 64, g.R = 1, g.spr = (g.OW + 63) / 64, g.gpi = g.OH;
+    } else {
+        g.L = g.OW, g.R = 64 / g.OW, g.spr = 1, g.gpi = (g.OH + g.R - 1) / g.R;
+    }
+    g.nseg = N * g.gpi * g.spr;
+    g.XW = g.L + kw - 1;
+    g.xrows = (g.R + kh - 1) * g.XW;
+    g.xpieces = (g.xrows + 7) / 8;
+    g.mtiles = (Cout + 63) / 64, g.ntiles = (Cin + 63) / 64;
+    g.tiles = g.mtiles * g.ntiles * g.taps;
+    return g;
+}
+}  // namespace
+
+bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw,
+                                    int stride) {
+    if (stride != 1 || kh * kw < 2 || !conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) return false;
+    if (H + 2 * ph - kh + 1 <= 0 || W + 2 * pw - kw + 1 <= 0) return false;
+    return rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw).xpieces <= 25;
+}
+
+WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride,
+                               int variant) {
     WgradPlan pl;
+    if (variant == kRowsVariant) {
+        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+            throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
+        const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw);
+        pl.variant = variant;
+        const int ct = rg.mtiles * rg.ntiles * rg.tgroups;
+        // ~2 workgroups of 7-9 waves per CU, >= 4 segments per split
+        int splits = std::max(1, (512 + ct / 2) / ct);
+        splits = std::max(1, std::min(splits, std::max(1, rg.nseg / 4)));
+        pl.kps = (rg.nseg + splits - 1) / splits;
+        pl.splits = (rg.nseg + pl.kps - 1) / pl.kps;
+        pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * rg.tiles * 4096 : 0;
+        return pl;
+    }
     pl.variant = rect_variant(Cin, Cout);
     WGeo g = make_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, stride, pl.variant);
     const Tile t = kTiles[pl.variant];
@@ -806,6 +1068,30 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
                             bool out_f32, bool accumulate, hipStream_t s) {
     if (!conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) throw std::invalid_argument("conv_wgrad_rect: unsupported");
     const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
+    if (plan.variant == kRowsVariant) {
+        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+            throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
+        RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw);
+        rg.splits = plan.splits, rg.kps = plan.kps;
+        if (rg.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad_rect: needs the workspace");
+        const int grid = rg.mtiles * rg.ntiles * rg.tgroups * rg.splits;
+        const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
+        if (rg.taps % 7 == 0)
+            wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out);
+        else
+            wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out);
+        if (rg.splits > 1 && !atomic_out) {
+            WGeo g{};
+            g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = rg.taps, g.tiles = rg.tiles;
+            g.splits = rg.splits;
+            const int64_t tot = static_cast<int64_t>(g.tiles) * 1024;
+            int sgl = 0;
+            while (sgl < 6 && (2 << sgl) <= g.splits && (tot << (sgl + 1)) <= int64_t(256) * 2048) ++sgl;
+            const int64_t rgrid = (tot + (256 >> sgl) - 1) / (256 >> sgl);
+            wgrad_reduce_kernel<1, 1><<<static_cast<int>(rgrid), 256, 0, s>>>(part, dw, g, out_f32, accumulate, sgl);
+        }
+        return;
+    }
     WGeo g = make_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, stride, plan.variant);
     g.splits = plan.splits;
     g.kps = plan.kps;

@@ -191,7 +191,12 @@ void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *p
 // Any KH x KW window with zero padding (ph, pw), stride 1|2, Cin / Cout multiples of 8
 // (Inception-v3's windows and channel counts): same kernel, runtime window, zero-padded tiles.
 bool conv_wgrad_rect_supported(int Cin, int Cout, int kh, int kw, int stride);
-WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride);
+// variant 6 (stride 1, multi-tap): the row-image kernel (all taps of a workgroup share one staged
+// input image per 64-pixel segment), else -1 = the tap-tiled split-K kernel.
+WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride,
+                               int variant = -1);
+bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw,
+                                    int stride);
 void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W,
                             int Cin, int Cout, int kh, int kw, int ph, int pw, int stride, const WgradPlan &plan,
                             bool out_f32, bool accumulate, hipStream_t s);

@@ -70,6 +70,12 @@ def main():
             t = timeit(f)
             best = min(best, t)
             row += "  rect %7.1f%s" % (t, "" if err < 2e-2 else " ERR%.3f" % err)
+        if H.conv_wgrad_rows_rect_supported(N, h, w, cin, cout, kh, kw, pad[0], pad[1], s):
+            f = lambda: H.conv_wgrad_rect(dy, x, kh, kw, s, pad[0], pad[1], 6)  # noqa: E731
+            err = ((f().float() - ref).abs().max() / ref.abs().max()).item()
+            t = timeit(f)
+            best = min(best, t)
+            row += "  rows %7.1f%s" % (t, "" if err < 2e-2 else " ERR%.3f" % err)
         if kh == kw and pad[0] == pad[1] == (kh - 1) // 2 and H.conv_wgrad_supported(cin, cout, kh, s):
             f = lambda: H.conv_wgrad(dy, x, kh, s)  # noqa: E731
             t = timeit(f)
