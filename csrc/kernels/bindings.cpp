@@ -1021,7 +1021,7 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                    double momentum, double eps, bool training, bool relu,
                                    c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> sums,
-                                   c10::optional<at::Tensor> res_coef, bool apply) {
+                                   c10::optional<at::Tensor> res_coef, bool apply, c10::optional<at::Tensor> out) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
@@ -1041,7 +1041,21 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
     at::Tensor y;
-    if (apply) y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    int64_t y_ld = 0;
+    if (out && out->defined()) {
+        // a channel slice [N, C, H, W] of a wider channels_last bf16 tensor (a concatenation)
+        TORCH_CHECK(apply && !rp && relu && out->scalar_type() == at::kBFloat16 && out->dim() == 4 &&
+                        out->size(0) == x.size(0) && out->size(1) == C && out->size(2) == x.size(2) &&
+                        out->size(3) == x.size(3) && out->stride(1) == 1 && out->stride(3) >= C &&
+                        out->stride(3) % 8 == 0 && out->stride(2) == out->size(3) * out->stride(3) &&
+                        out->stride(0) == out->size(2) * out->stride(2) &&
+                        reinterpret_cast<uintptr_t>(out->data_ptr()) % 16 == 0 && out->device() == x.device(),
+                    "bn: out must be a 16-byte aligned channel slice of a channels_last bf16 tensor (BN+ReLU, no residual)");
+        y = *out;
+        y_ld = out->stride(3);
+    } else if (apply) {
+        y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    }
     auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
     at::Tensor mask;
     if (apply && rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
@@ -1059,7 +1073,7 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                            mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, sh, relu, training, b.rm, b.rv,
                            static_cast<float>(momentum), static_cast<float>(eps),
                            partial.defined() ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp, rc, apply);
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp, rc, apply, y_ld);
     return {y, mean, invstd, coef, mask};
 }
 
@@ -1579,7 +1593,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
           py::arg("num_batches") = py::none(), py::arg("sums") = py::none(), py::arg("res_coef") = py::none(),
-          py::arg("apply") = true);
+          py::arg("apply") = true, py::arg("out") = py::none());
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
           py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none(),

@@ -328,11 +328,14 @@ __global__ void bn_eval_coef(int C, const float *gamma, const float *beta, const
 // element (one byte per 8-channel vector) for the backward.  RESC: the residual is itself a
 // BN input -- res*rscale + rshift with the coefficients rcoef (the downsample branch's BN, so
 // its output is never materialised).
-template <int CVEC, bool RES, bool RELU, bool RESC = false>
+// SOUT: y is a channel slice of a wider NHWC tensor (row stride y_ldv 16-byte vectors): the
+// branch outputs of an Inception block written straight into their concatenation.
+template <int CVEC, bool RES, bool RELU, bool RESC = false, bool SOUT = false>
 __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restrict__ x, const uint4 *__restrict__ res,
                                                           const float *__restrict__ coef, uint4 *__restrict__ y,
                                                           uint8_t *__restrict__ mask, int64_t nvec,
-                                                          const float *__restrict__ rcoef = nullptr, int ntm = 0) {
+                                                          const float *__restrict__ rcoef = nullptr, int ntm = 0,
+                                                          int64_t y_ldv = 0) {
     constexpr int C = CVEC * 8;
     const bool ntl = ntm & 1, nts = ntm & 2;
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * bn_threads<CVEC>() + threadIdx.x;
@@ -380,7 +383,8 @@ __global__ __launch_bounds__(kBlock) void bn_apply_kernel(const uint4 *__restric
                 }
                 f[k] = v;
             }
-            st16(y + i, pack8(f), nts);
+            if constexpr (SOUT) st16(y + (i / CVEC) * y_ldv + cv, pack8(f), nts);
+            else st16(y + i, pack8(f), nts);
             if (RES && RELU) mask[i] = static_cast<uint8_t>(m);
         }
     }
@@ -966,8 +970,11 @@ int bn_num_chunks(BNShape sh) { return chunking(sh).nchunks; }
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
-                       int64_t *num_batches, hipStream_t s, double *sums, const float *res_coef, bool apply) {
+                       int64_t *num_batches, hipStream_t s, double *sums, const float *res_coef, bool apply,
+                       int64_t y_ld) {
     const int C = sh.channels, cvec = C / 8;
+    if (y_ld > 0 && (y_ld % 8 || y_ld < C || res || !relu))
+        throw std::invalid_argument("bn_forward: a strided output needs BN+ReLU without residual, row stride % 8");
     const int64_t nvec = sh.rows * cvec;
     if (training && sums) {
         bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
@@ -993,6 +1000,9 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
         } else if (res) {
             if (relu) bn_apply_kernel<CV, true, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
             else bn_apply_kernel<CV, true, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
+        } else if (y_ld > 0 && y_ld != C) {
+            bn_apply_kernel<CV, false, true, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm,
+                                                                          y_ld / 8);
         } else {
             if (relu) bn_apply_kernel<CV, false, true><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);
             else bn_apply_kernel<CV, false, false><<<g, NT, 0, s>>>(xv, rv, coef, yv, mask, nvec, nullptr, ntm);

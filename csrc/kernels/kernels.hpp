@@ -242,7 +242,8 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
                        int64_t *num_batches, hipStream_t s, double *sums = nullptr, const float *res_coef = nullptr,
-                       bool apply = true);
+                       bool apply = true, int64_t y_ld = 0);
+// (y_ld > 0: y is a channel slice of a wider NHWC tensor with that row stride (elements); BN+ReLU only.
 // (sums: f64 [2C] batch sums from a conv epilogue -> no statistics pass; re-zeroed.
 //  res_coef: the residual is res*res_coef[c] + res_coef[C+c] (another BN's input and
 //  coefficients); apply = false: statistics / coefficients only, y untouched.)

@@ -29,9 +29,12 @@ class BasicConv2d(nn.Module):
         else:
             self.bn = nn.BatchNorm2d(cout, eps=0.001)
 
-    def forward(self, x, link: bool = False):
+    def forward(self, x, link: bool = False, defer: bool = False):
         """``link``: this output's only consumer is another BasicConv2d's (or a sibling group's)
-        stride-1 conv -- its data-gradient epilogue then produces this BN's backward sums."""
+        stride-1 conv -- its data-gradient epilogue then produces this BN's backward sums.
+        ``defer`` (fused training path): return a :class:`~kungfu_amd.ops.fused_bn.Deferred` BN+ReLU
+        (conv output + BN) for a concatenation to apply straight into its channel slice."""
+        defer = defer and self.fused and self.training and self.bn.track_running_stats
         if self.fused and not self.pool_after_conv and self.training and self.bn.track_running_stats:
             # MFMA conv whose epilogue accumulates the BN batch statistics: the BN skips its
             # statistics pass (ops/conv.py conv2d_stats; None if the shape is not on the kernel)
@@ -44,6 +47,10 @@ class BasicConv2d(nn.Module):
                 ws = self.bn.stats_workspace(x.device)
                 y = conv2d_stats(x, w, c.stride, c.padding, ws, master=c.weight)
                 if y is not None:
+                    if defer:
+                        from ..ops.fused_bn import Deferred
+
+                        return Deferred(y, self.bn, ws)
                     return self.bn(y, sums=ws, link=link)
         y = self.conv(x)
         if self.pool_after_conv:
@@ -53,27 +60,41 @@ class BasicConv2d(nn.Module):
                 y = avg_pool3x3s1(y)
             else:
                 y = F.avg_pool2d(y, 3, 1, 1)
+        if defer:
+            from ..ops.fused_bn import Deferred
+
+            return Deferred(y, self.bn)
         if self.fused:
             return self.bn(y, link=link)
         return F.relu(self.bn(y), inplace=True)
 
 
-def _chain(x, mods, link_last: bool = False):
+def _chain(x, mods, link_last: bool = False, defer_last: bool = True):
     """``mods[-1](...mods[0](x))`` for BasicConv2d modules: every output but the last has the next
-    conv as its only consumer (BN-sums link, see BasicConv2d.forward)."""
+    conv as its only consumer (BN-sums link, see BasicConv2d.forward).  ``defer_last``: the last
+    BN+ReLU is left to the block's concatenation (:func:`~kungfu_amd.ops.fused_bn.bn_relu_concat`)."""
     for i, m in enumerate(mods):
         nxt = mods[i + 1] if i + 1 < len(mods) else None
         lk = link_last if nxt is None else nxt.conv.stride in (1, (1, 1))
-        x = m(x, link=lk)
+        x = m(x, link=lk, defer=defer_last and nxt is None)
     return x
 
 
-def _heads(x, mods, links=None):
+def _cat(pieces):
+    """An Inception block's channel concatenation: the deferred branch BN+ReLUs write straight into
+    their slices (fused model), else torch.cat."""
+    from ..ops.fused_bn import bn_relu_concat
+
+    return bn_relu_concat(pieces)
+
+
+def _heads(x, mods, links=None, defer=None):
     """``[m(x) for m in mods]`` for BasicConv2d modules that all read ``x`` (an Inception block's
     branch heads).  Fused training path: their convolutions are ONE autograd node on the MFMA
     kernel (``ops.conv.sibling_convs``: the branch gradients of x are accumulated by the conv
     epilogue instead of autograd adds), each conv's epilogue producing its BN's statistics
-    (the pool branch pools the conv output first, so its BN computes its own)."""
+    (the pool branch pools the conv output first, so its BN computes its own).  ``defer[i]``: head i's
+    BN+ReLU is left to the block's concatenation (a Deferred is returned)."""
     m0 = mods[0]
     if (len(mods) > 1 and m0.fused and m0.training and x.dtype == torch.bfloat16
             and all(m.bn.track_running_stats for m in mods)):
@@ -84,10 +105,18 @@ def _heads(x, mods, links=None):
         if ys is not None:
             from ..ops.pool import avg_pool3x3s1
 
+            from ..ops.fused_bn import Deferred
+
             lks = links or [False] * len(mods)
-            return [m.bn(avg_pool3x3s1(y)) if m.pool_after_conv else m.bn(y, sums=s, link=lk)
-                    for m, y, s, lk in zip(mods, ys, st, lks)]
-    return [m(x, link=lk) for m, lk in zip(mods, links or [False] * len(mods))]
+            dfs = defer or [False] * len(mods)
+            out = []
+            for m, y, s, lk, df in zip(mods, ys, st, lks, dfs):
+                if m.pool_after_conv:
+                    y = avg_pool3x3s1(y)
+                out.append(Deferred(y, m.bn, s) if df else m.bn(y, sums=s, link=lk))
+            return out
+    return [m(x, link=lk, defer=df) for m, lk, df in zip(mods, links or [False] * len(mods),
+                                                           defer or [False] * len(mods))]
 
 
 def _pool_module():
@@ -124,8 +153,9 @@ class InceptionA(nn.Module):
         self.bp = _branch_pool(cin, pool_features)
 
     def forward(self, x):
-        o1, t5, t3, op = _heads(x, [self.b1, self.b5[0], self.b3[0], self.bp], [False, True, True, False])
-        return torch.cat([o1, self.b5[1](t5), _chain(t3, list(self.b3[1:])), op], 1)
+        o1, t5, t3, op = _heads(x, [self.b1, self.b5[0], self.b3[0], self.bp], [False, True, True, False],
+                                [True, False, False, True])
+        return _cat([o1, self.b5[1](t5, defer=True), _chain(t3, list(self.b3[1:])), op])
 
 
 class InceptionB(nn.Module):
@@ -137,7 +167,7 @@ class InceptionB(nn.Module):
                                 BasicConv2d(96, 96, kernel_size=3, stride=2))
 
     def forward(self, x):
-        return torch.cat([self.b3(x), _chain(x, list(self.bd)), _max_pool3s2(x, self.fused)], 1)
+        return _cat([self.b3(x, defer=True), _chain(x, list(self.bd)), _max_pool3s2(x, self.fused)])
 
 
 class InceptionC(nn.Module):
@@ -155,8 +185,9 @@ class InceptionC(nn.Module):
         self.bp = _branch_pool(cin, 192)
 
     def forward(self, x):
-        o1, t7, td, op = _heads(x, [self.b1, self.b7[0], self.bd[0], self.bp], [False, True, True, False])
-        return torch.cat([o1, _chain(t7, list(self.b7[1:])), _chain(td, list(self.bd[1:])), op], 1)
+        o1, t7, td, op = _heads(x, [self.b1, self.b7[0], self.bd[0], self.bp], [False, True, True, False],
+                                [True, False, False, True])
+        return _cat([o1, _chain(t7, list(self.b7[1:])), _chain(td, list(self.bd[1:])), op])
 
 
 class InceptionD(nn.Module):
@@ -171,7 +202,7 @@ class InceptionD(nn.Module):
 
     def forward(self, x):
         t3, t7 = _heads(x, [self.b3[0], self.b7[0]], [False, True])
-        return torch.cat([self.b3[1](t3), _chain(t7, list(self.b7[1:])), _max_pool3s2(x, self.fused)], 1)
+        return _cat([self.b3[1](t3, defer=True), _chain(t7, list(self.b7[1:])), _max_pool3s2(x, self.fused)])
 
 
 class InceptionE(nn.Module):
@@ -189,9 +220,12 @@ class InceptionE(nn.Module):
 
     def forward(self, x):
         # b3 / bd feed one sibling group each (a single autograd consumer): linked
-        o1, b3, bd, op = _heads(x, [self.b1, self.b3_1, self.bd_1, self.bp], [False, True, True, False])
+        o1, b3, bd, op = _heads(x, [self.b1, self.b3_1, self.bd_1, self.bp], [False, True, True, False],
+                                [True, False, False, True])
         bd = self.bd_2(bd, link=True)
-        return torch.cat([o1] + _heads(b3, [self.b3_2a, self.b3_2b]) + _heads(bd, [self.bd_3a, self.bd_3b]) + [op], 1)
+        both = [True, True]
+        return _cat([o1] + _heads(b3, [self.b3_2a, self.b3_2b], defer=both) + _heads(bd, [self.bd_3a, self.bd_3b], defer=both)
+                    + [op])
 
 
 class InceptionV3(nn.Module):
@@ -211,8 +245,8 @@ class InceptionV3(nn.Module):
     def forward(self, x):
         st = self.stem
         # conv -> conv links inside the stem (the pools consume stem[2] / stem[5])
-        x = st[3](_chain(x, [st[0], st[1], st[2]]))
-        x = self.blocks(st[6](_chain(x, [st[4], st[5]])))
+        x = st[3](_chain(x, [st[0], st[1], st[2]], defer_last=False))
+        x = self.blocks(st[6](_chain(x, [st[4], st[5]], defer_last=False)))
         return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
 
 

@@ -26,6 +26,11 @@ import torch.nn.functional as F
 from .._lib import hip, hip_available
 from ..parallel.mixed import deliver, direct_target
 
+import os
+
+# KUNGFU_BN_CONCAT=0: apply deferred branch BNs and concatenate with torch.cat (A/B, tests)
+CONCAT_ENABLED = os.environ.get("KUNGFU_BN_CONCAT", "1") != "0"
+
 
 def available() -> bool:
     return torch.cuda.is_available() and hip_available()
@@ -164,6 +169,136 @@ def bn_act_pool(x, weight, bias, running_mean, running_var, training: bool, mome
     y = bn_act(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=True,
                num_batches_tracked=num_batches_tracked)
     return F.max_pool2d(y, 3, 2, 1)
+
+
+class Deferred:
+    """A BN+ReLU whose application is deferred to a concatenation (:func:`bn_relu_concat`):
+    ``y`` is the BN input (the conv output), ``bn`` the :class:`BatchNormAct2d`, ``sums`` the
+    batch statistics its producing conv's epilogue accumulated (or None)."""
+    __slots__ = ("y", "bn", "sums")
+
+    def __init__(self, y, bn, sums=None):
+        self.y, self.bn, self.sums = y, bn, sums
+
+    def materialize(self) -> torch.Tensor:
+        return self.bn(self.y, sums=self.sums)
+
+
+class _ConcatSpec:
+    __slots__ = ("items", "ctot")
+
+    def __init__(self, items, ctot):
+        self.items, self.ctot = items, ctot  # items: (bn module, sums) or None for a plain tensor
+
+
+class _BNConcatFn(torch.autograd.Function):
+    """``torch.cat([relu(bn_i(y_i)) ..., t_j ...], 1)`` without the copy: each BN+ReLU apply pass
+    writes straight into its channel slice of the concatenation (a strided HIP store), the plain
+    pieces (e.g. a max-pool branch) are copied into theirs; backward reads each slice of the
+    output gradient in place (the BN backward takes a strided gradient)."""
+
+    @staticmethod
+    def forward(ctx, spec: _ConcatSpec, *args):
+        H = hip()
+        first = args[0]
+        N, _, Hh, W = first.shape
+        out = torch.empty((N, spec.ctot, Hh, W), dtype=torch.bfloat16, device=first.device,
+                          memory_format=torch.channels_last)
+        saved, direct, k, c0 = [], [], 0, 0
+        for item in spec.items:
+            if item is not None:
+                y, g, b = args[k:k + 3]
+                k += 3
+                m, sums = item
+                a, nbt = m._args()
+                C = int(y.shape[1])
+                _, mean, invstd, coef, _ = H.bn_forward(y, None, g, b, a[2], a[3], a[5], a[6], True, True, nbt, sums,
+                                                        None, True, out[:, c0:c0 + C])
+                saved += [y, mean, invstd, g, coef]
+                direct.append(_direct(g, b))
+            else:
+                t = args[k]
+                k += 1
+                C = int(t.shape[1])
+                out[:, c0:c0 + C].copy_(t)
+            c0 += C
+        ctx.save_for_backward(*saved)
+        ctx.spec, ctx.direct = spec, direct
+        ctx.plain = [int(t.shape[1]) for t, it in zip(_plain_args(spec, args), spec.items) if it is None]
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        H = hip()
+        if not dout.is_contiguous(memory_format=torch.channels_last):
+            dout = dout.contiguous(memory_format=torch.channels_last)
+        saved = list(ctx.saved_tensors)
+        grads, c0, si, pi, bi = [], 0, 0, 0, 0
+        for item in ctx.spec.items:
+            if item is not None:
+                y, mean, invstd, g, coef = saved[si:si + 5]
+                si += 5
+                C = int(y.shape[1])
+                dx, _, dw, db = H.bn_backward(dout[:, c0:c0 + C], y, mean, invstd, g, coef, None, True, True, False,
+                                              None)
+                d = ctx.direct[bi]
+                bi += 1
+                if d is not None:
+                    deliver(d[0], dw)
+                    deliver(d[1], db)
+                    dw = db = None
+                grads += [dx, dw, db]
+            else:
+                C = ctx.plain[pi]
+                pi += 1
+                grads.append(dout[:, c0:c0 + C])
+            c0 += C
+        return (None, *grads)
+
+
+def _plain_args(spec, args):
+    """The argument (first tensor) of each piece, in piece order."""
+    out, k = [], 0
+    for item in spec.items:
+        out.append(args[k])
+        k += 3 if item is not None else 1
+    return out
+
+
+def bn_relu_concat(pieces) -> torch.Tensor:
+    """``torch.cat`` over channels of ``pieces`` (tensors and :class:`Deferred` BN+ReLUs), with every
+    deferred BN+ReLU written straight into its slice of the result when the HIP path covers the whole
+    set (bf16 channels_last pieces of one N x H x W, channel offsets % 8, training-mode BNs with
+    running statistics); otherwise the BNs are applied and the pieces concatenated by torch."""
+    ok = CONCAT_ENABLED
+    ref = None
+    c0 = 0
+    for p in (pieces if ok else ()):
+        t = p.y if isinstance(p, Deferred) else p
+        if ref is None:
+            ref = t
+        if (t.dtype != torch.bfloat16 or not t.is_cuda or t.shape[0] != ref.shape[0] or t.shape[2:] != ref.shape[2:]
+                or c0 % 8):
+            ok = False
+            break
+        if isinstance(p, Deferred):
+            m = p.bn
+            if not (m.training and m.track_running_stats and m.relu and m.momentum is not None
+                    and _fusable(t, None) and type(m).forward is BatchNormAct2d.forward):
+                ok = False
+                break
+        c0 += int(t.shape[1])
+    if not ok or not any(isinstance(p, Deferred) for p in pieces):
+        return torch.cat([p.materialize() if isinstance(p, Deferred) else p for p in pieces], 1)
+    items, args = [], []
+    for p in pieces:
+        if isinstance(p, Deferred):
+            items.append((p.bn, p.sums))
+            args += [p.y, p.bn.weight, p.bn.bias]
+        else:
+            items.append(None)
+            args.append(p)
+    return _BNConcatFn.apply(_ConcatSpec(items, c0), *args)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):

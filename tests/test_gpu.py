@@ -1451,3 +1451,45 @@ def test_colsum_matches_torch(H, T, O):
     assert torch.equal(a, H.colsum(x, torch.float32))
     b = H.colsum(x, torch.bfloat16)
     assert b.dtype == torch.bfloat16 and torch.allclose(b.double(), ref, rtol=1e-2, atol=1e-1)
+
+
+@needs_gpu
+@pytest.mark.parametrize("block", ["A", "B", "C", "D", "E"])
+def test_inception_bn_concat_matches_cat(block, monkeypatch):
+    """Inception blocks whose branch BN+ReLUs write straight into their slice of the
+    concatenation (ops.fused_bn.bn_relu_concat) against the same blocks with the BNs applied
+    separately and torch.cat: outputs, block-input and parameter gradients, running stats."""
+    import copy
+
+    from kungfu_amd.models import inception as inc
+    from kungfu_amd.ops import fused_bn
+
+    torch.manual_seed(5)
+    inc._FUSED_BN[0] = True
+    try:
+        mk = {"A": (lambda: inc.InceptionA(64, 32), 64, 13), "B": (lambda: inc.InceptionB(96), 96, 13),
+              "C": (lambda: inc.InceptionC(128, 64), 128, 9), "D": (lambda: inc.InceptionD(128), 128, 9),
+              "E": (lambda: inc.InceptionE(192), 192, 5)}[block]
+        m0 = mk[0]().cuda().to(memory_format=torch.channels_last)
+    finally:
+        inc._FUSED_BN[0] = False
+    m1 = copy.deepcopy(m0)
+    x = torch.randn(4, mk[1], mk[2], mk[2], device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    res = []
+    for m, on in ((m0, False), (m1, True)):
+        monkeypatch.setattr(fused_bn, "CONCAT_ENABLED", on)
+        xx = x.clone().requires_grad_(True)
+        y = m(xx)
+        if on:
+            assert y.grad_fn is not None and "BNConcat" in type(y.grad_fn).__name__
+        g = torch.randn_like(y.float()).bfloat16()
+        y.backward(g)
+        res.append((y.detach().float(), xx.grad.float(), [p.grad.float() for p in m.parameters()],
+                    [b.clone() for b in m.buffers()]))
+    (y0, gx0, gp0, b0), (y1, gx1, gp1, b1) = res
+    assert torch.equal(y0, y1)
+    assert ((gx1 - gx0).norm() / gx0.norm()).item() < 1e-3
+    for a, b in zip(gp0, gp1):
+        assert ((b - a).norm() / a.norm().clamp_min(1e-12)).item() < 1e-3
+    for a, b in zip(b0, b1):
+        assert torch.equal(a, b)
