@@ -1396,7 +1396,7 @@ def test_inception_bn_link_chain(monkeypatch):
     monkeypatch.setattr(fbn, "hip", lambda: _Spy())
     x = torch.randn(4, 64, 14, 14, device="cuda").bfloat16().to(memory_format=torch.channels_last)
     xf, xr, xl = x.clone().requires_grad_(True), x.float().requires_grad_(True), x.clone().requires_grad_(True)
-    y = inc._chain(xf, fused)
+    y = inc._chain(xf, fused, defer_last=False)
     assert getattr(fused[0].bn, "_kf_sums", None) is not None
     yr = ref[1](ref[0](xr))
     with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -1468,21 +1468,26 @@ def test_inception_bn_concat_matches_cat(block, monkeypatch):
     inc._FUSED_BN[0] = True
     try:
         mk = {"A": (lambda: inc.InceptionA(64, 32), 64, 13), "B": (lambda: inc.InceptionB(96), 96, 13),
-              "C": (lambda: inc.InceptionC(128, 64), 128, 9), "D": (lambda: inc.InceptionD(128), 128, 9),
+              "C": (lambda: inc.InceptionC(192, 64), 192, 9), "D": (lambda: inc.InceptionD(128), 128, 9),
               "E": (lambda: inc.InceptionE(192), 192, 5)}[block]
         m0 = mk[0]().cuda().to(memory_format=torch.channels_last)
     finally:
         inc._FUSED_BN[0] = False
+    for mod in m0.modules():
+        if isinstance(mod, inc.BasicConv2d):
+            mod.conv.to(torch.bfloat16)  # bf16 conv weights: the MFMA conv + BN-statistics path
     m1 = copy.deepcopy(m0)
     x = torch.randn(4, mk[1], mk[2], mk[2], device="cuda").bfloat16().to(memory_format=torch.channels_last)
     res = []
+    g = None
     for m, on in ((m0, False), (m1, True)):
         monkeypatch.setattr(fused_bn, "CONCAT_ENABLED", on)
         xx = x.clone().requires_grad_(True)
         y = m(xx)
         if on:
             assert y.grad_fn is not None and "BNConcat" in type(y.grad_fn).__name__
-        g = torch.randn_like(y.float()).bfloat16()
+        if g is None:
+            g = torch.randn_like(y.float()).bfloat16()
         y.backward(g)
         res.append((y.detach().float(), xx.grad.float(), [p.grad.float() for p in m.parameters()],
                     [b.clone() for b in m.buffers()]))
