@@ -460,7 +460,7 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
 // gradient conv(..., out=dx, acc_even=True).
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional<at::Tensor> stats,
                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_fcoef,
-                         c10::optional<at::Tensor> bn_mask, int64_t variant) {
+                         c10::optional<at::Tensor> bn_mask, int64_t variant, int64_t dh, int64_t dw, int64_t pad) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_dgrad_s2: dy must be a 4-D channels_last bf16 GPU tensor");
@@ -470,10 +470,19 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
                     wt.device() == dy.device(),
                 "conv_dgrad_s2: wt must be the flipped [Cin, Cout, ks, ks] channels_last bf16 weight");
     const int N = dy.size(0), K = dy.size(1), OH = dy.size(2), OW = dy.size(3), C = wt.size(0);
-    TORCH_CHECK(kfk::conv_supported(K, C, static_cast<int>(ks), 1), "conv_dgrad_s2: unsupported channels");
-    TORCH_CHECK(static_cast<int64_t>(N) * 4 * OH * OW * C < (int64_t(1) << 31), "conv_dgrad_s2: tensor too large");
+    const bool even = dh <= 0;
+    if (even) {
+        TORCH_CHECK(kfk::conv_supported(K, C, static_cast<int>(ks), 1), "conv_dgrad_s2: unsupported channels");
+        dh = 2 * OH, dw = 2 * OW, pad = ks == 3 ? 1 : 0;
+    } else {
+        // any dx size (ks = 3, pad 0 | 1): channel counts % 8
+        TORCH_CHECK(ks == 3 && (pad == 0 || pad == 1) && K % 8 == 0 && C % 8 == 0 && K >= 16 && C >= 16 && dw > 0 &&
+                        (dh + 2 * pad - 3) / 2 + 1 == OH && (dw + 2 * pad - 3) / 2 + 1 == OW,
+                    "conv_dgrad_s2: dh/dw/pad do not match a 3x3 stride-2 convolution of dy's size (channels % 8)");
+    }
+    TORCH_CHECK(static_cast<int64_t>(N) * dh * dw * C < (int64_t(1) << 31), "conv_dgrad_s2: tensor too large");
     c10::DeviceGuard gd(dy.device());
-    auto dx = at::empty({N, C, 2 * OH, 2 * OW}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+    auto dx = at::empty({N, C, dh, dw}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
     kfk::EpiArgs ea;
     int epi = 0;
     if (bn_x && bn_x->defined()) {
@@ -503,7 +512,8 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
     kfk::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                               reinterpret_cast<const uint16_t *>(wt.data_ptr()), reinterpret_cast<uint16_t *>(dx.data_ptr()),
                               N, OH, OW, K, C, static_cast<int>(ks), ea, epi, stream_of(dy, 0),
-                              static_cast<int>(variant));
+                              static_cast<int>(variant), static_cast<int>(dh), static_cast<int>(dw),
+                              static_cast<int>(pad));
     return dx;
 }
 
@@ -1532,7 +1542,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
-          py::arg("variant") = -1);
+          py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1);
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
           py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "

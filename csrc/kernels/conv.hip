@@ -60,8 +60,9 @@ struct Geo {
     // strided data gradient as parity phases (launch_conv_dgrad_s2):
     int wtaps;   // taps per weight row (B row stride = wtaps * C)
     int tapmap;  // -1: tap t reads weight tap t; else weight tap of tap t = nibble t
-    int scat;    // 1: output row m -> pixel (2*(m/OW) + pr, 2*(m%OW) + pc) of a 2OH x 2OW image
+    int scat;    // 1: output (n, a, b) of the OH x OW phase grid -> pixel (2a + pr, 2b + pc) of a dh x dw image
     int pr, pc;
+    int dh, dw;  // scat: the data-gradient image (2OH x 2OW for an even input)
     int ph, pw;  // zero padding (rows, columns)
 };
 
@@ -330,7 +331,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             int pix = m;
             if (g.scat) {
                 const int t = m / g.OW, ow = m - t * g.OW;
-                pix = (2 * t + g.pr) * (2 * g.OW) + 2 * ow + g.pc;
+                const int n = t / g.OH, a = t - n * g.OH;
+                pix = (n * g.dh + 2 * a + g.pr) * g.dw + 2 * ow + g.pc;
             }
             const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
             ee[u] = e;
@@ -676,7 +678,7 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.OW = (W + 2 * pad - ks) / stride + 1;
     g.M = N * g.OH * g.OW;
     g.mtiles = g.ntiles = 0;
-    g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
+    g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.dh = g.dw = 0;
     g.ph = g.pw = pad;
     if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
@@ -754,7 +756,7 @@ void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K
     g.N = M, g.H = g.W = 1, g.C = K, g.K = N, g.stride = 1;
     g.OH = g.OW = 1, g.M = M;
     g.mtiles = g.ntiles = 0;
-    g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0;
+    g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0, g.dh = g.dw = 0;
     if (variant < 0) {
         // enough 256x256 tiles to fill the chip twice, else 256x128, else 128x128 (or 128x64)
         const int64_t t256 = N % 256 ? 0 : ((M + 255) / 256) * (N / 256);
@@ -789,7 +791,7 @@ void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, 
     g.OW = (W + 2 * pw - kw) / stride + 1;
     g.M = N * g.OH * g.OW;
     g.mtiles = g.ntiles = 0;
-    g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0;
+    g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.dh = g.dw = 0;
     g.ph = ph, g.pw = pw;
     if (kh == 1 && kw == 1) {
         launch_ks<1>(x, w, y, g, ea, epi, s, -1);
@@ -813,9 +815,9 @@ void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g,
                     hipStream_t s) {
     constexpr int C = kEpiBwdCoef, B = kEpiBwdBits;
     constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    if (g.K % BN) throw std::invalid_argument("conv_dgrad_s2: Cin not a multiple of the tile");
+    if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv_dgrad_s2: channel counts must be multiples of 8");
     g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = g.K / BN;
+    g.ntiles = (g.K + BN - 1) / BN;  // a partial last N tile reads zero B rows, stores its valid columns
     const int grid = g.mtiles * g.ntiles;
     const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
     if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
@@ -847,33 +849,48 @@ void launch_phase(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, c
 }
 
 void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
-                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant) {
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant, int DH, int DW,
+                          int pad) {
     // variant: -1 = default; else the tile variant (0 128x128, 1 256x128, 2 256x64, 5 128x64)
     const int tv = variant;
-    // dx pixel (2a + pr, 2b + pc) only sees forward taps kh = 1 (pr = 0) or kh = 2 at dy row a and
-    // kh = 0 at dy row a + 1 (pr = 1); same for columns.  Flipped-weight tap index = 2 - kh.
+    if (DH <= 0) DH = 2 * OH;
+    if (DW <= 0) DW = 2 * OW;
     Geo g;
     g.N = N, g.H = OH, g.W = OW, g.C = Cout, g.K = Cin, g.stride = 1;
-    g.OH = OH, g.OW = OW, g.M = N * OH * OW;
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.scat = 1;
+    g.dh = DH, g.dw = DW;
     g.ph = g.pw = 0;
     if (ks == 1) {
+        if (DH != 2 * OH || DW != 2 * OW || pad != 0) throw std::invalid_argument("conv_dgrad_s2: 1x1 needs an even input");
+        g.OH = OH, g.OW = OW, g.M = N * OH * OW;
         g.tapmap = -1, g.pr = g.pc = 0;
         launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
         return;
     }
-    if (ks != 3) throw std::invalid_argument("conv_dgrad_s2: ks must be 1 or 3");
+    if (ks != 3 || (pad != 0 && pad != 1)) throw std::invalid_argument("conv_dgrad_s2: ks 3 needs pad 0 or 1");
+    if ((DH + 2 * pad - 3) / 2 + 1 != OH || (DW + 2 * pad - 3) / 2 + 1 != OW)
+        throw std::invalid_argument("conv_dgrad_s2: dy / dx sizes do not match a stride-2 3x3 convolution");
+    // dx row ih = 2a + pr sees the forward taps with 2 oh + kh = ih + pad: q = pr + pad odd -> kh = 1 at
+    // dy row a (one tap); q even -> kh = 2 at row a + q/2 - 1 and kh = 0 at row a + q/2 (two taps, the
+    // window starting q/2 - 1 rows past a, i.e. zero padding 1 - q/2).  Same for columns.  Flipped-weight
+    // tap index = 2 - kh; every dx pixel is written by exactly one phase.
     for (int pr = 0; pr < 2; ++pr)
         for (int pc = 0; pc < 2; ++pc) {
-            const int nh = pr ? 2 : 1, nw = pc ? 2 : 1;
+            const int qr = pr + pad, qc = pc + pad;
+            const int nh = (qr & 1) ? 1 : 2, nw = (qc & 1) ? 1 : 2;
+            const int PH = (DH - pr + 1) / 2, PW = (DW - pc + 1) / 2;
+            if (PH <= 0 || PW <= 0) continue;
             int map = 0;
             for (int th = 0; th < nh; ++th)
                 for (int tw = 0; tw < nw; ++tw) {
-                    const int rh = pr ? (th == 0 ? 0 : 2) : 1, rw = pc ? (tw == 0 ? 0 : 2) : 1;
+                    const int rh = nh == 1 ? 1 : (th == 0 ? 0 : 2), rw = nw == 1 ? 1 : (tw == 0 ? 0 : 2);
                     map |= (rh * 3 + rw) << (4 * (th * nw + tw));
                 }
             g.tapmap = map, g.pr = pr, g.pc = pc;
+            g.OH = PH, g.OW = PW, g.M = N * PH * PW;
+            g.ph = nh == 1 ? 0 : 1 - qr / 2;
+            g.pw = nw == 1 ? 0 : 1 - qc / 2;
             if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
             else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, ea, epi, s, tv);
             else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, ea, epi, s, tv);

@@ -139,8 +139,11 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
 // 4 taps) write every dx pixel once (epi: 0 or kEpiBwdCoef/kEpiBwdBits -- BN backward sums
 // over dx, as launch_conv).  KS = 1: only the even pixels are written (the rest is left for a
 // kEpiAccEven stride-1 data gradient into the same dx).
+// DH / DW (ks = 3): any dx size with padding `pad` (0 or 1) -- e.g. Inception's 3x3/s2/p0 on odd
+// inputs (25 -> 12); <= 0 = the even input 2OH x 2OW.  Cin / Cout multiples of 8.
 void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
-                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);
+                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1, int DH = 0,
+                          int DW = 0, int pad = 1);
 // KH x KW window with zero padding (ph, pw), stride 1|2 (Inception-v3's 1x1, 3x3 pad 0|1, 1x7,
 // 7x1, 1x3, 3x1, 5x5): the same implicit GEMM, K = KH*KW*Cin tap-major; epilogue none or
 // kEpiFwdStats.  Cin, Cout multiples of 64.

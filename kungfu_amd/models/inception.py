@@ -75,7 +75,8 @@ def _chain(x, mods, link_last: bool = False, defer_last: bool = True):
     BN+ReLU is left to the block's concatenation (:func:`~kungfu_amd.ops.fused_bn.bn_relu_concat`)."""
     for i, m in enumerate(mods):
         nxt = mods[i + 1] if i + 1 < len(mods) else None
-        lk = link_last if nxt is None else nxt.conv.stride in (1, (1, 1))
+        # stride-1 consumers, and 3x3 stride-2 ones (parity-phase data gradient), produce the BN sums
+        lk = link_last if nxt is None else (nxt.conv.stride in (1, (1, 1)) or nxt.conv.kernel_size == (3, 3))
         x = m(x, link=lk, defer=defer_last and nxt is None)
     return x
 

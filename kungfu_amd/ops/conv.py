@@ -199,6 +199,16 @@ class _ConvRectFn(torch.autograd.Function):
                 # flipped weights: from the flat space's per-step multi-tensor flip when registered
                 wt = ctx.flip[0].get(ctx.flip[1]) if ctx.flip is not None else hip().conv_flip_weight(w)
                 dx = _dgrad_link(dy, wt, kh - 1 - ph, kw - 1 - pw, None, ctx.link)
+            elif s == 2 and kh == kw == 3 and ph == pw and ph in (0, 1) and min(x.shape[1], dy.shape[1]) >= 16:
+                # parity-phase GEMMs for any input size (Inception's 3x3/s2/p0 on 25x25 / 12x12 maps)
+                wt = ctx.flip[0].get(ctx.flip[1]) if ctx.flip is not None else hip().conv_flip_weight(w)
+                H = hip()
+                lk = ctx.link
+                if lk is not None and lk.y is not None:
+                    dx = H.conv_dgrad_s2(dy, wt, 3, lk.ws, lk.y, lk.coef, None, -1, int(x.shape[2]), int(x.shape[3]), ph)
+                    lk.ready, lk.dx_ptr = True, dx.data_ptr()
+                else:
+                    dx = H.conv_dgrad_s2(dy, wt, 3, dh=int(x.shape[2]), dw=int(x.shape[3]), pad=ph)
             else:
                 dx = torch.ops.aten.convolution_backward(dy, x, w, None, [s, s], [ph, pw], [1, 1], False, [0, 0], 1,
                                                          [True, False, False])[0]
@@ -320,7 +330,7 @@ def conv2d_stats(x, w, stride, padding, stats: torch.Tensor, master: torch.Tenso
         return None
     st, pd = _pair(stride), _pair(padding)
     flip = None
-    if master is not None and st[0] == 1:
+    if master is not None:
         from ..parallel.mixed import direct_target
         from .fused_block import _flip_cache
 

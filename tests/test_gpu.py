@@ -1037,6 +1037,41 @@ def test_conv_dgrad_s2_matches_torch(N, OH, K, C):
 
 
 @needs_gpu
+@pytest.mark.parametrize("N,DH,DW,K,C,pad", [(4, 25, 25, 384, 288, 0), (4, 25, 25, 96, 96, 0), (3, 12, 12, 320, 192, 0),
+                                             (3, 13, 11, 64, 40, 1), (2, 9, 10, 128, 64, 0)])
+def test_conv_dgrad_s2_any_size_matches_torch(N, DH, DW, K, C, pad):
+    """Stride-2 3x3 data gradient for ANY input size / padding 0|1 and channel counts % 8
+    (Inception's 25x25 -> 12x12 pad-0 layers): four parity phases of different sizes vs the
+    float32 torch data gradient, and with the BN-backward sums epilogue."""
+    from kungfu_amd._lib import hip
+
+    H = hip()
+    torch.manual_seed(23)
+    OH, OW = (DH + 2 * pad - 3) // 2 + 1, (DW + 2 * pad - 3) // 2 + 1
+    dy = torch.randn(N, K, OH, OW, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(N, C, DH, DW, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    w = (torch.randn(K, C, 3, 3, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [2, 2], [pad, pad],
+                                              [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    wt = H.conv_flip_weight(w)
+    dx = H.conv_dgrad_s2(dy, wt, 3, dh=DH, dw=DW, pad=pad)
+    assert dx.shape == ref.shape
+    assert _rel(dx, ref) < 1e-2
+    bx = torch.randn_like(x)
+    fc = torch.cat([torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2])
+    st = torch.zeros(H_slots() * 2 * C, dtype=torch.float64, device="cuda")
+    dx2 = H.conv_dgrad_s2(dy, wt, 3, st, bx, fc, None, -1, DH, DW, pad)
+    assert torch.equal(dx2, dx)
+    xd = bx.double().permute(0, 2, 3, 1).reshape(-1, C)
+    gd = dx.double().permute(0, 2, 3, 1).reshape(-1, C)
+    on = (bx.float().permute(0, 2, 3, 1).reshape(-1, C) * fc[:C] + fc[C:]) > 0
+    dz = torch.where(on, gd, torch.zeros_like(gd))
+    sums = st.view(-1, 2, C).sum(0)
+    torch.testing.assert_close(sums[0], dz.sum(0), rtol=1e-5, atol=1e-2)
+    torch.testing.assert_close(sums[1], (dz * xd).sum(0), rtol=1e-5, atol=1e-2)
+
+
+@needs_gpu
 @pytest.mark.parametrize("N,Hh,C,K", [(3, 12, 64, 64), (2, 10, 64, 128), (2, 9, 128, 256), (1, 8, 256, 512)])
 def test_conv_bias_relu_and_gate_epilogues(H, N, Hh, C, K):
     """conv epilogues of the fused VGG stack: relu(conv + bias) vs f32 torch; the ReLU-gated
