@@ -285,10 +285,53 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 // input is bn_x; stats then receive sum(dz), sum(dz * x) (dz = grad * relu') for
 // bn_backward(..., sums=stats).  bn_mask (1 bit per element) or bn_fcoef (forward
 // [scale; shift]) gives the ReLU gate.
+// In-launch BN finalize of a statistics epilogue (kfk::BNFin).  mode 1 (forward):
+//   t = [arrive(int32 >= 9, zeroed), gamma, beta, mean, invstd, coef(2C), running_mean, running_var, num_batches]
+// mode 2 (backward): t = [arrive, gamma, mean, invstd, coef(3C), dgamma, dbeta]; f32 per-channel tensors.
+static void fill_fin(kfk::BNFin &f, int64_t mode, const c10::optional<std::vector<at::Tensor>> &t, int64_t rows,
+                     double momentum, double eps, bool training, int C, const at::Tensor &like) {
+    if (mode == 0) return;
+    TORCH_CHECK(t.has_value() && (mode == 1 || mode == 2), "fin: mode 1 or 2 with its tensor list");
+    const auto &v = *t;
+    TORCH_CHECK(v.size() == (mode == 1 ? 9u : 7u), "fin: wrong tensor count for the mode");
+    TORCH_CHECK(v[0].scalar_type() == at::kInt && v[0].numel() >= 9 && v[0].is_contiguous() && v[0].device() == like.device(),
+                "fin: arrive must be a zeroed int32 tensor of >= 9 words on the conv's device");
+    auto f32 = [&](const at::Tensor &a, int64_t n, const char *what) -> float * {
+        TORCH_CHECK(a.defined() && a.scalar_type() == at::kFloat && a.numel() == n && a.is_contiguous() &&
+                        a.device() == like.device(),
+                    "fin: ", what, " must be a contiguous f32 tensor of ", n, " elements on the conv's device");
+        return a.data_ptr<float>();
+    };
+    f.mode = static_cast<int>(mode);
+    f.arrive = reinterpret_cast<unsigned *>(v[0].data_ptr<int>());
+    f.rows = rows;
+    f.training = training ? 1 : 0;
+    f.momentum = static_cast<float>(momentum), f.eps = static_cast<float>(eps);
+    f.gamma = f32(v[1], C, "gamma");
+    if (mode == 1) {
+        f.beta = f32(v[2], C, "beta");
+        f.mean = f32(v[3], C, "mean");
+        f.invstd = f32(v[4], C, "invstd");
+        f.coef = f32(v[5], 2 * C, "coef");
+        f.run_mean = f32(v[6], C, "running_mean");
+        f.run_var = f32(v[7], C, "running_var");
+        TORCH_CHECK(v[8].scalar_type() == at::kLong && v[8].numel() == 1, "fin: num_batches must be int64[1]");
+        f.num_batches = v[8].data_ptr<int64_t>();
+    } else {
+        f.mean = f32(v[2], C, "mean");
+        f.invstd = f32(v[3], C, "invstd");
+        f.coef = f32(v[4], 3 * C, "coef");
+        f.dgamma = f32(v[5], C, "dgamma");
+        f.dbeta = f32(v[6], C, "dbeta");
+    }
+}
+
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
                 c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
-                c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask, bool acc_even) {
+                c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask, bool acc_even,
+                int64_t fin_mode, c10::optional<std::vector<at::Tensor>> fin, double fin_momentum, double fin_eps,
+                bool fin_training) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -381,6 +424,12 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
                     "conv: acc_even needs out, stride 1 and no acc_mask / bn_fcoef");
         epi |= kfk::kEpiAccEven;
     }
+    if (fin_mode) {
+        TORCH_CHECK((fin_mode == 1 && (epi & kfk::kEpiFwdStats)) ||
+                        (fin_mode == 2 && (epi & (kfk::kEpiBwdCoef | kfk::kEpiBwdBits))),
+                    "conv: fin mode 1 needs the statistics epilogue (stats, no bn_x), mode 2 the BN-backward sums (bn_x)");
+        fill_fin(ea.fin, fin_mode, fin, static_cast<int64_t>(N) * OH * OW, fin_momentum, fin_eps, fin_training, K, x);
+    }
     kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
                      reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), ea, epi,
                      stream_of(x, 0), static_cast<int>(variant));
@@ -460,7 +509,8 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
 // gradient conv(..., out=dx, acc_even=True).
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional<at::Tensor> stats,
                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_fcoef,
-                         c10::optional<at::Tensor> bn_mask, int64_t variant, int64_t dh, int64_t dw, int64_t pad) {
+                         c10::optional<at::Tensor> bn_mask, int64_t variant, int64_t dh, int64_t dw, int64_t pad,
+                         int64_t fin_mode, c10::optional<std::vector<at::Tensor>> fin, bool fin_training) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_dgrad_s2: dy must be a 4-D channels_last bf16 GPU tensor");
@@ -508,6 +558,10 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
             ea.fcoef = bn_fcoef->data_ptr<float>();
             epi = kfk::kEpiBwdCoef;
         }
+    }
+    if (fin_mode) {
+        TORCH_CHECK(fin_mode == 2 && epi != 0, "conv_dgrad_s2: fin mode 2 needs the BN-backward sums (bn_x)");
+        fill_fin(ea.fin, fin_mode, fin, static_cast<int64_t>(N) * dh * dw, 0.0, 0.0, fin_training, C, dy);
     }
     kfk::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                               reinterpret_cast<const uint16_t *>(wt.data_ptr()), reinterpret_cast<uint16_t *>(dx.data_ptr()),
@@ -1031,7 +1085,8 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
                                    double momentum, double eps, bool training, bool relu,
                                    c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> sums,
-                                   c10::optional<at::Tensor> res_coef, bool apply, c10::optional<at::Tensor> out) {
+                                   c10::optional<at::Tensor> res_coef, bool apply, c10::optional<at::Tensor> out,
+                                   c10::optional<std::vector<at::Tensor>> pre) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     auto b = bn_common(C, weight, bias, running_mean, running_var, num_batches, training);
@@ -1066,7 +1121,18 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
     } else if (apply) {
         y = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     }
-    auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+    at::Tensor mean, invstd, coef;
+    const bool prefin = pre.has_value();
+    if (prefin) {
+        // (mean, invstd, coef) already written from `sums` by the producing conv's in-launch finalize
+        TORCH_CHECK(pre->size() == 3 && training && sums && sums->defined(), "bn: pre = (mean, invstd, coef) with sums");
+        mean = (*pre)[0], invstd = (*pre)[1], coef = (*pre)[2];
+        TORCH_CHECK(mean.scalar_type() == at::kFloat && mean.numel() == C && invstd.numel() == C &&
+                        coef.numel() == 2 * C && coef.scalar_type() == at::kFloat,
+                    "bn: pre tensors must be f32 mean[C], invstd[C], coef[2C]");
+    } else {
+        mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+    }
     at::Tensor mask;
     if (apply && rp && relu) mask = at::empty({sh.rows * (C / 8)}, x.options().dtype(at::kByte));
     double *sp = nullptr;
@@ -1083,7 +1149,8 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
                            mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, sh, relu, training, b.rm, b.rv,
                            static_cast<float>(momentum), static_cast<float>(eps),
                            partial.defined() ? partial.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
-                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp, rc, apply, y_ld);
+                           invstd.data_ptr<float>(), coef.data_ptr<float>(), b.nbt, stream_of(x, 0), sp, rc, apply, y_ld,
+                           prefin);
     return {y, mean, invstd, coef, mask};
 }
 
@@ -1091,7 +1158,8 @@ std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, 
 std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean, at::Tensor invstd,
                                     at::Tensor weight, at::Tensor fcoef, c10::optional<at::Tensor> mask, bool relu,
                                     bool training, bool want_dres, c10::optional<at::Tensor> sums,
-                                    c10::optional<at::Tensor> dres_x, c10::optional<at::Tensor> dres_sums) {
+                                    c10::optional<at::Tensor> dres_x, c10::optional<at::Tensor> dres_sums,
+                                    c10::optional<std::vector<at::Tensor>> pre) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     // dy may be a channel slice of a wider channels-last tensor (a concatenation's gradient):
@@ -1117,7 +1185,17 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
     auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
     at::Tensor dres;
     if (want_dres) dres = at::empty_like(x, at::MemoryFormat::ChannelsLast);
-    auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
+    at::Tensor dw, db, coef;
+    const bool prefin = pre.has_value();
+    if (prefin) {
+        // (dgamma, dbeta, coef) already written from `sums` by the dgrad conv's in-launch finalize
+        TORCH_CHECK(pre->size() == 3 && sums && sums->defined(), "bn_backward: pre = (dgamma, dbeta, coef) with sums");
+        dw = (*pre)[0], db = (*pre)[1], coef = (*pre)[2];
+        TORCH_CHECK(dw.scalar_type() == at::kFloat && dw.numel() == C && db.numel() == C && coef.numel() == 3 * C,
+                    "bn_backward: pre tensors must be f32 dgamma[C], dbeta[C], coef[3C]");
+    } else {
+        dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
+    }
     double *sp = nullptr;
     if (sums && sums->defined()) {
         TORCH_CHECK(sums->is_cuda() && sums->scalar_type() == at::kDouble && sums->numel() == 2 * C * kfk::kStatSlots &&
@@ -1143,7 +1221,7 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
                             training, partial.defined() ? partial.data_ptr<float>() : nullptr, dw.data_ptr<float>(),
                             db.data_ptr<float>(), coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
                             want_dres ? reinterpret_cast<uint16_t *>(dres.data_ptr()) : nullptr, stream_of(x, 0), sp,
-                            dsx, dsp, dy_ld);
+                            dsx, dsp, dy_ld, prefin);
     return {dx, dres, dw, db};
 }
 
@@ -1528,7 +1606,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("stride") = 1, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
-          py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false);
+          py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false,
+          py::arg("fin_mode") = 0, py::arg("fin") = py::none(), py::arg("fin_momentum") = 0.1,
+          py::arg("fin_eps") = 1e-5, py::arg("fin_training") = true);
     m.def("conv_rect", &conv_rect, "KH x KW NHWC bf16 convolution with zero padding (MFMA implicit GEMM; "
           "Inception-v3 windows) with an optional BN-statistics epilogue", py::arg("x"), py::arg("w"),
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none(),
@@ -1542,7 +1622,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
-          py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1);
+          py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1,
+          py::arg("fin_mode") = 0, py::arg("fin") = py::none(), py::arg("fin_training") = true);
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
           py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "
@@ -1603,11 +1684,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("res"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
           py::arg("num_batches") = py::none(), py::arg("sums") = py::none(), py::arg("res_coef") = py::none(),
-          py::arg("apply") = true, py::arg("out") = py::none());
+          py::arg("apply") = true, py::arg("out") = py::none(), py::arg("pre") = py::none());
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
           py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none(),
-          py::arg("dres_x") = py::none(), py::arg("dres_sums") = py::none());
+          py::arg("dres_x") = py::none(), py::arg("dres_sums") = py::none(), py::arg("pre") = py::none());
     m.def("bn_pool_supported", [](int64_t C, int64_t H, int64_t W) {
         return kfk::bn_pool_supported(kfk::BNShape{H * W, static_cast<int>(C)}, static_cast<int>(H),
                                       static_cast<int>(W));

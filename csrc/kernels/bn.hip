@@ -28,6 +28,7 @@
 //
 // Statistics are two-stage and deterministic: per-chunk partial sums (f32)
 // then a per-channel fold in f64 (no float atomics).
+#include "bn_fin.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -82,6 +83,16 @@ __device__ __forceinline__ void st16(uint4 *p, const uint4 &v, bool nt) {
 
 // default 1 (non-temporal loads): ResNet-50 step 21.73 -> 21.39 ms on MI355X, while
 // non-temporal stores did not pay in the full step (profiles/README.md, r3f)
+// KUNGFU_BN_SKIP_FINALIZE=1: TIMING EXPERIMENT ONLY -- the sums-finalize kernels are not launched
+// (coefficients stay stale: wrong numerics), to bound what folding them elsewhere could save.
+bool bn_skip_finalize() {
+    static const bool b = [] {
+        const char *e = std::getenv("KUNGFU_BN_SKIP_FINALIZE");
+        return e && std::atoi(e) != 0;
+    }();
+    return b;
+}
+
 int bn_nt_mode() {
     static const int m = [] {
         const char *e = std::getenv("KUNGFU_BN_NT");
@@ -292,21 +303,7 @@ __global__ void bn_sums_finalize(double *sums, int C, int64_t rows, const float 
         sums[k * 2 * C + c] = 0.0;
         sums[k * 2 * C + C + c] = 0.0;
     }
-    const double m = s / rows;
-    double var = q / rows - m * m;
-    if (var < 0) var = 0;
-    const float is = rsqrtf(static_cast<float>(var) + eps);
-    mean[c] = static_cast<float>(m);
-    invstd[c] = is;
-    if (run_mean) {
-        const double unbiased = rows > 1 ? var * rows / (rows - 1) : var;
-        run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * static_cast<float>(m);
-        run_var[c] = (1.f - momentum) * run_var[c] + momentum * static_cast<float>(unbiased);
-    }
-    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-    const float sc = g * is;
-    coef[c] = sc;
-    coef[C + c] = b - static_cast<float>(m) * sc;
+    bn_fin_fwd_channel(c, C, s, q, rows, gamma, beta, mean, invstd, run_mean, run_var, momentum, eps, coef);
 }
 
 // Eval mode: coefficients from running stats.
@@ -737,22 +734,7 @@ __global__ void bn_bwd_finalize_sums(double *sums, int C, int64_t rows, const fl
         sums[k * 2 * C + c] = 0.0;
         sums[k * 2 * C + C + c] = 0.0;
     }
-    const double db = s0, dg = static_cast<double>(invstd[c]) * (s1 - static_cast<double>(mean[c]) * db);
-    dgamma[c] = static_cast<float>(dg);
-    dbeta[c] = static_cast<float>(db);
-    const float g = gamma ? gamma[c] : 1.f;
-    const float a = g * invstd[c];
-    if (training) {
-        const float inv_m = 1.f / static_cast<float>(rows);
-        const float k2 = -a * static_cast<float>(dg) * invstd[c] * inv_m;
-        coef[c] = a;
-        coef[C + c] = k2;
-        coef[2 * C + c] = -a * static_cast<float>(db) * inv_m - k2 * mean[c];
-    } else {
-        coef[c] = a;
-        coef[C + c] = 0.f;
-        coef[2 * C + c] = 0.f;
-    }
+    bn_fin_bwd_channel(c, C, s0, s1, rows, gamma, mean, invstd, dgamma, dbeta, coef, training);
 }
 
 // ---------------------------------------------------------------- backward apply
@@ -902,12 +884,14 @@ template <class G>
 void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const uint8_t *mask, const float *mean,
                           const float *invstd, const float *gamma, BNShape sh, int rm, bool training, float *partial,
                           float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s,
-                          double *sums = nullptr, const uint16_t *dres_x = nullptr, double *dres_sums = nullptr) {
+                          double *sums = nullptr, const uint16_t *dres_x = nullptr, double *dres_sums = nullptr,
+                          bool prefinalized = false) {
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     Chunking ch = chunking(sh);
     const uint4 *xx = reinterpret_cast<const uint4 *>(x);
     if (sums) {
+        if (!prefinalized && !bn_skip_finalize())
         bn_bwd_finalize_sums<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, mean, invstd, dgamma, dbeta,
                                                              coef, training);
     } else {
@@ -971,12 +955,13 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
                        int64_t *num_batches, hipStream_t s, double *sums, const float *res_coef, bool apply,
-                       int64_t y_ld) {
+                       int64_t y_ld, bool prefinalized) {
     const int C = sh.channels, cvec = C / 8;
     if (y_ld > 0 && (y_ld % 8 || y_ld < C || res || !relu))
         throw std::invalid_argument("bn_forward: a strided output needs BN+ReLU without residual, row stride % 8");
     const int64_t nvec = sh.rows * cvec;
     if (training && sums) {
+        if (!prefinalized && !bn_skip_finalize())
         bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
                                                          run_var, momentum, eps, coef, num_batches);
     } else if (training) {
@@ -1014,17 +999,17 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                         uint16_t *dres, hipStream_t s, double *sums, const uint16_t *dres_x, double *dres_sums,
-                        int64_t dy_ld) {
+                        int64_t dy_ld, bool prefinalized) {
     const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
     if (dy_ld > 0 && dy_ld != sh.channels) {
         if (dy_ld % 8) throw std::invalid_argument("bn_backward: dy row stride must be a multiple of 8");
         launch_backward_impl(StridedGrad{reinterpret_cast<const uint4 *>(dy), dy_ld / 8}, x, fcoef, mask, mean, invstd,
                              gamma, sh, rm, training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x,
-                             dres_sums);
+                             dres_sums, prefinalized);
         return;
     }
     launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy), (bn_nt_mode() & 1) != 0}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
-                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums);
+                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums, prefinalized);
 }
 
 bool bn_pool_supported(BNShape sh, int H, int W) {
@@ -1038,6 +1023,7 @@ void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *
                             hipStream_t s, double *sums, uint16_t *xarg) {
     const int C = sh.channels, cvec = C / 8;
     if (training && sums) {
+        if (!bn_skip_finalize())
         bn_sums_finalize<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, beta, mean, invstd, run_mean,
                                                          run_var, momentum, eps, coef, num_batches);
     } else if (training) {

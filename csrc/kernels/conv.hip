@@ -22,6 +22,7 @@
 //
 // The same kernel computes the stride-1 data gradient: dx = conv3x3(dy, w')
 // with w'[ci, kh, kw, co] = w[co, 2-kh, 2-kw, ci] (conv3x3_flip_weight).
+#include "bn_fin.hpp"
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -69,6 +70,61 @@ struct Geo {
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// In-launch BN finalize (kernels.hpp BNFin): called by every workgroup after its slot atomics.
+// Completion-ordered hand-off (MI355X_MICROARCH.md, inter-workgroup visibility: "the workgroup whose
+// add came last, told by the value its add returned", sc1 loads of the handed-off words): each wave
+// waits for its own atomics (vmcnt counts them), the workgroup joins a barrier, one lane arrives on
+// its shard counter (blockIdx % 8) and the last arriver of a shard on the top counter; the last of
+// those folds every channel's slots with sc1 loads (the f64 adds were performed at the memory side,
+// no L2 holds them) and re-zeroes slots and counters with sc1 stores for the next launch.  No fence:
+// the outputs are read by later kernels only.
+__device__ __noinline__ void bn_finalize_last(const EpiArgs &ea, int C, int nwg, int orig, int tid, int nt) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int shard = orig & 7;
+        const int nsh = nwg < 8 ? nwg : 8;
+        const unsigned nin = static_cast<unsigned>((nwg - shard + 7) / 8);
+        int last = 0;
+        const unsigned o = __hip_atomic_fetch_add(ea.fin.arrive + shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (o == nin - 1) {
+            const unsigned o2 =
+                __hip_atomic_fetch_add(ea.fin.arrive + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = o2 == static_cast<unsigned>(nsh - 1);
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    const BNFin &f = ea.fin;
+    double *sums = ea.stats;
+    for (int c = tid; c < C; c += nt) {
+        double v0[kStatSlots], v1[kStatSlots];
+#pragma unroll
+        for (int k = 0; k < kStatSlots; ++k) {
+            v0[k] = __hip_atomic_load(sums + k * 2 * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v1[k] = __hip_atomic_load(sums + k * 2 * C + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        double s0 = 0, s1 = 0;
+#pragma unroll
+        for (int k = 0; k < kStatSlots; ++k) {
+            s0 += v0[k];
+            s1 += v1[k];
+            __hip_atomic_store(sums + k * 2 * C + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sums + k * 2 * C + C + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (f.mode == 1)
+            bn_fin_fwd_channel(c, C, s0, s1, f.rows, f.gamma, f.beta, f.mean, f.invstd, f.run_mean, f.run_var,
+                               f.momentum, f.eps, f.coef);
+        else
+            bn_fin_bwd_channel(c, C, s0, s1, f.rows, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef,
+                               f.training != 0);
+    }
+    if (tid < 9) __hip_atomic_store(f.arrive + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && f.mode == 1 && f.num_batches) f.num_batches[0] += 1;
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
@@ -482,6 +538,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                 if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
             }
         }
+        if constexpr (NSUM == 2) {
+            if (ea.fin.mode != 0) bn_finalize_last(ea, g.K, nwg, orig, tid, NT);
+        }
     }
 }
 
@@ -875,8 +934,13 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     // dy row a (one tap); q even -> kh = 2 at row a + q/2 - 1 and kh = 0 at row a + q/2 (two taps, the
     // window starting q/2 - 1 rows past a, i.e. zero padding 1 - q/2).  Same for columns.  Flipped-weight
     // tap index = 2 - kh; every dx pixel is written by exactly one phase.
+    if (ea.fin.mode && (DH < 2 || DW < 2)) throw std::invalid_argument("conv_dgrad_s2: in-launch finalize needs dx >= 2x2");
+    // the BN-backward sums accumulate over all four phase launches: only the last one finalizes
+    EpiArgs ea_early = ea;
+    ea_early.fin.mode = 0;
     for (int pr = 0; pr < 2; ++pr)
         for (int pc = 0; pc < 2; ++pc) {
+            const EpiArgs &eap = (pr == 1 && pc == 1) ? ea : ea_early;
             const int qr = pr + pad, qc = pc + pad;
             const int nh = (qr & 1) ? 1 : 2, nw = (qc & 1) ? 1 : 2;
             const int PH = (DH - pr + 1) / 2, PW = (DW - pc + 1) / 2;
@@ -891,10 +955,10 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
             g.OH = PH, g.OW = PW, g.M = N * PH * PW;
             g.ph = nh == 1 ? 0 : 1 - qr / 2;
             g.pw = nw == 1 ? 0 : 1 - qc / 2;
-            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
-            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, ea, epi, s, tv);
-            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, ea, epi, s, tv);
-            else launch_phase<0x22>(dy, wt, dx, g, ea, epi, s, tv);
+            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, eap, epi, s, tv);
+            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, eap, epi, s, tv);
+            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, eap, epi, s, tv);
+            else launch_phase<0x22>(dy, wt, dx, g, eap, epi, s, tv);
         }
 }
 

@@ -120,7 +120,27 @@ enum ConvEpi : int {
     kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
     kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGelu = 512, kEpiGeluGrad = 1024
 };
+// In-launch BN finalize of a statistics epilogue (kEpiFwdStats / kEpiBwdCoef / kEpiBwdBits): every
+// workgroup waits for its slot atomics, arrives on a two-level counter (per blockIdx % 8 shard,
+// then across shards), and the LAST arriver folds the kStatSlots slots (sc1 loads: the f64 adds
+// were performed at the memory side), writes what bn_sums_finalize / bn_bwd_finalize_sums would,
+// re-zeroes the slots and the counter -- the separate finalize launch (and its kernel boundary)
+// is gone.  The BN apply that follows is told the coefficients are already there.
+struct BNFin {
+    int mode = 0;                // 0 off, 1 forward batch statistics, 2 backward sums
+    unsigned *arrive = nullptr;  // 9 zeroed words, left zeroed
+    int64_t rows = 0;            // elements per channel
+    int training = 1;            // backward: training-mode BN
+    const float *gamma = nullptr, *beta = nullptr;
+    float *mean = nullptr, *invstd = nullptr;  // forward: written; backward: read
+    float *run_mean = nullptr, *run_var = nullptr;
+    int64_t *num_batches = nullptr;
+    float momentum = 0.f, eps = 0.f;
+    float *coef = nullptr;                      // forward [scale; shift] (2C), backward (3C)
+    float *dgamma = nullptr, *dbeta = nullptr;  // backward
+};
 struct EpiArgs {
+    BNFin fin;
     const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
     uint16_t *aux = nullptr;         // kEpiGelu: the pre-activation output [M, K] bf16
     const uint16_t *bias = nullptr;  // kEpiBiasRelu / kEpiBias / kEpiGelu: bf16 [K]
@@ -245,7 +265,9 @@ void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamm
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,
                        int64_t *num_batches, hipStream_t s, double *sums = nullptr, const float *res_coef = nullptr,
-                       bool apply = true, int64_t y_ld = 0);
+                       bool apply = true, int64_t y_ld = 0, bool prefinalized = false);
+// (prefinalized: mean / invstd / coef were already written from `sums` by the producing conv's
+// in-launch finalize (BNFin) -- no finalize launch here.
 // (y_ld > 0: y is a channel slice of a wider NHWC tensor with that row stride (elements); BN+ReLU only.
 // (sums: f64 [2C] batch sums from a conv epilogue -> no statistics pass; re-zeroed.
 //  res_coef: the residual is res*res_coef[c] + res_coef[C+c] (another BN's input and
@@ -258,7 +280,7 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                         uint16_t *dres, hipStream_t s, double *sums = nullptr, const uint16_t *dres_x = nullptr,
                         double *dres_sums = nullptr,
-                        int64_t dy_ld = 0);
+                        int64_t dy_ld = 0, bool prefinalized = false);
 // (dres_x / dres_sums: dres also feeds a second, ReLU-free BN with input dres_x -- its backward
 //  sums go to dres_sums, zeroed f64 [slots][2][C])
 // (sums: f64 kStatSlots x [sum dz; sum dz*x] from a conv epilogue -> no reduce pass; re-zeroed.)

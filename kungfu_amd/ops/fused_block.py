@@ -70,6 +70,41 @@ def _sums(bn, dev) -> torch.Tensor:
     return ws
 
 
+# KUNGFU_BN_INLAUNCH_FIN=0: separate BN finalize launches (A/B); default: the statistics-producing conv
+# finalizes in its own launch (last-arriving workgroup, csrc/kernels/conv.hip bn_finalize_last)
+_INLAUNCH_FIN = os.environ.get("KUNGFU_BN_INLAUNCH_FIN", "1") != "0"
+
+
+def _arrive(bn, dev) -> torch.Tensor:
+    """Per-BN arrival counters of the in-launch finalize (9 int32 words, left zeroed by the kernel)."""
+    a = getattr(bn, "_kf_arrive", None)
+    if a is None or a.device != dev:
+        a = torch.zeros(16, dtype=torch.int32, device=dev)
+        bn._kf_arrive = a
+    return a
+
+
+def _fin_fwd(bn, gamma, beta, dev):
+    """(conv kwargs, bn_forward pre) for a forward statistics epilogue that finalizes in-launch."""
+    if not _INLAUNCH_FIN:
+        return {}, None
+    C = bn.num_features
+    f32 = dict(dtype=torch.float32, device=dev)
+    mean, invstd, coef = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(2 * C, **f32)
+    t = [_arrive(bn, dev), gamma, beta, mean, invstd, coef, bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    return dict(fin_mode=1, fin=t, fin_momentum=float(bn.momentum), fin_eps=float(bn.eps)), [mean, invstd, coef]
+
+
+def _fin_bwd(bn, gamma, mean, invstd, dev):
+    """(fin tensor list, bn_backward pre) for a BN-backward-sums epilogue that finalizes in-launch."""
+    if not _INLAUNCH_FIN:
+        return None, None
+    C = bn.num_features
+    f32 = dict(dtype=torch.float32, device=dev)
+    dg, db, coef = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(3 * C, **f32)
+    return [_arrive(bn, dev), gamma, mean, invstd, coef, dg, db], [dg, db, coef]
+
+
 def _wgrad(dy, x, w, stride, pad):
     from .conv import wgrad
 
@@ -126,17 +161,20 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
         wt = wt if wt is not None else H.conv_flip_weight(w)
         _dgrad.fused = bn is not None
         if bn is not None:
-            ws, bx, fc, mk = bn
-            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even)
+            ws, bx, fc, mk = bn[:4]
+            fin = bn[4] if len(bn) > 4 else None
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even,
+                          fin_mode=2 if fin is not None else 0, fin=fin)
         return H.conv(dy, wt, 1, None, out, acc_mask=out_mask, acc_even=acc_even)
     assert out_mask is None and not acc_even
     ks = w.shape[2]
     if stride == 2 and out is None and _even_s2(x, dy, ks):
         wt = wt if wt is not None else H.conv_flip_weight(w)
         if ks == 3 and bn is not None:
-            ws, bx, fc, mk = bn
+            ws, bx, fc, mk = bn[:4]
+            fin = bn[4] if len(bn) > 4 else None
             _dgrad.fused = True
-            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk)
+            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk, fin_mode=2 if fin is not None else 0, fin=fin)
         _dgrad.fused = False
         dx = H.conv_dgrad_s2(dy, wt, ks)
         if ks == 1:  # odd pixels get no gradient from a 1x1 stride-2 conv
@@ -172,12 +210,13 @@ class _TailSlot:
     BN3 backward sums (sum dz, sum dz*y3 under the 1-bit ReLU mask).  ``dx_ptr`` lets this
     block's backward check that the gradient it receives is exactly that tensor (no other
     consumer added to it); otherwise the sums are discarded and recomputed."""
-    __slots__ = ("ws", "y3", "mask", "ready", "dx_ptr")
+    __slots__ = ("ws", "y3", "mask", "ready", "dx_ptr", "fin", "pre")
 
-    def __init__(self, ws, y3, mask):
+    def __init__(self, ws, y3, mask, fin=None, pre=None):
         self.ws, self.y3, self.mask = ws, y3, mask
         self.ready = False
         self.dx_ptr = 0
+        self.fin, self.pre = fin, pre  # in-launch finalize of this block's BN3 backward (see _fin_bwd)
 
 
 class _Spec:
@@ -203,20 +242,27 @@ class _BottleneckFn(torch.autograd.Function):
         s = spec.stride
         outs = []
 
+        pres = [None] * len(spec.bns)
+
         def bn(i, y, res, relu, res_coef=None, apply=True):
             m = spec.bns[i]
             return H.bn_forward(y, res, gam[i], bet[i], m.running_mean, m.running_var, m.momentum, m.eps, True, relu,
-                                m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply)
+                                m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply, pre=pres[i])
 
-        y1 = H.conv(x, ws_bf[0], 1, _sums(spec.bns[0], dev))
+        def conv(i, inp, w_, st_):
+            # the conv's statistics epilogue also finalizes BN i in its own launch (_fin_fwd)
+            kw, pres[i] = _fin_fwd(spec.bns[i], gam[i], bet[i], dev)
+            return H.conv(inp, w_, st_, _sums(spec.bns[i], dev), **kw)
+
+        y1 = conv(0, x, ws_bf[0], 1)
         z1, m1, i1, c1, _ = bn(0, y1, None, True)
-        y2 = H.conv(z1, ws_bf[1], s, _sums(spec.bns[1], dev))
+        y2 = conv(1, z1, ws_bf[1], s)
         z2, m2, i2, c2, _ = bn(1, y2, None, True)
-        y3 = H.conv(z2, ws_bf[2], 1, _sums(spec.bns[2], dev))
+        y3 = conv(2, z2, ws_bf[2], 1)
         if spec.ds:
             # the downsample BN is folded into the tail's residual read (coefficients only here):
             # out = relu(bn3(y3) + bn_d(yd)) without materialising bn_d(yd)
-            yd = H.conv(x, ws_bf[3], s, _sums(spec.bns[3], dev))
+            yd = conv(3, x, ws_bf[3], s)
             _, md, idd, cd, _ = bn(3, yd, None, False, apply=False)
             out, m3, i3, c3, mask3 = bn(2, y3, yd, True, res_coef=cd)
         else:
@@ -224,7 +270,8 @@ class _BottleneckFn(torch.autograd.Function):
             out, m3, i3, c3, mask3 = bn(2, y3, x, True)
         # cross-block BN3 backward fusion: the previous block's tail (if x is its output)
         ctx.prev = getattr(x, "_kf_tail", None)
-        ctx.tail = _TailSlot(_sums(spec.bns[2], dev), y3, mask3)
+        fin3, pre3 = _fin_bwd(spec.bns[2], gam[2], m3, i3, dev)
+        ctx.tail = _TailSlot(_sums(spec.bns[2], dev), y3, mask3, fin3, pre3)
         ctx.spec = spec
         ctx.wdtypes = [w.dtype for w in ws[0::3]]
         ctx.save_for_backward(x, y1, z1, y2, z2, y3, yd, *ws_bf, *gam, m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3,
@@ -264,7 +311,9 @@ class _BottleneckFn(torch.autograd.Function):
         use3 = tail.ready and dout.data_ptr() == tail.dx_ptr
         if tail.ready and not use3:
             tail.ws.zero_()  # sums of a gradient that is not the one we got: discard
-        tail.ready, tail.y3, tail.mask = False, None, None
+            tail.pre = None  # (its in-launch finalize re-zeroed the slots; the coefficients are stale)
+        pre3 = tail.pre if use3 else None
+        tail.ready, tail.y3, tail.mask, tail.fin, tail.pre = False, None, None, None, None
         # identity block whose output gradient is our own buffer (the next block's conv1 data
         # gradient): the residual gradient dout * relu' is never written -- conv1's data
         # gradient below accumulates into dout in place, masking it on the fly
@@ -273,17 +322,19 @@ class _BottleneckFn(torch.autograd.Function):
         # sums are accumulated by this same pass (that BN then skips its reduce)
         dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, not in_place,
                                             ws[2] if use3 else None, dres_x=yd if spec.ds else None,
-                                            dres_sums=ws[3] if spec.ds else None)
+                                            dres_sums=ws[3] if spec.ds else None, pre=pre3)
         dbn[2] = (dg3, db3)
-        dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None))
+        fin2, pre2 = _fin_bwd(spec.bns[1], g[1], m2, i2, dout.device)
+        dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None, fin2))
         dw[2] = wgrad(dy3, z2, w[2], 1, 0)
-        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1])
+        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1], pre=pre2)
         dbn[1] = (dg2, db2)
-        dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None))
+        fin1, pre1 = _fin_bwd(spec.bns[0], g[0], m1, i1, dout.device)
+        dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None, fin1))
         fused1 = _dgrad.fused
         dw[1] = wgrad(dy2, z1, w[1], s, 1)
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
-                                         ws[0] if fused1 else None)
+                                         ws[0] if fused1 else None, pre=pre1 if fused1 else None)
         dbn[0] = (dg1, db1)
         acc_even = False
         if spec.ds:
@@ -305,7 +356,7 @@ class _BottleneckFn(torch.autograd.Function):
         if prev is not None and prev.y3 is not None and prev.y3.shape == dx.shape:
             # conv1's data gradient completes the gradient of the previous block's output:
             # its epilogue also accumulates that block's BN3 backward sums
-            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask),
+            dx = _dgrad(dy1, x, w[0], 1, 0, out=dx, flipped=fl[0], bn=(prev.ws, prev.y3, None, prev.mask, prev.fin),
                         out_mask=om, acc_even=acc_even)
             prev.ready, prev.dx_ptr = True, dx.data_ptr()
         else:

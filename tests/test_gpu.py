@@ -667,6 +667,60 @@ def test_fused_bottleneck_matches_fp32(cin, stride, ds, nblk):
 
 
 @needs_gpu
+@pytest.mark.parametrize("cin,stride,ds,nblk", [(256, 1, False, 2), (64, 1, True, 3), (256, 2, True, 2),
+                                                (512, 2, True, 2)])
+def test_fused_bottleneck_inlaunch_finalize_bit_identical(cin, stride, ds, nblk, monkeypatch):
+    """BN finalize folded into the statistics-producing conv's own launch (the last-arriving
+    workgroup folds the slots, conv.hip bn_finalize_last) vs the separate finalize launches:
+    the same f64 sums in the same order through the same code, so outputs, every gradient,
+    running statistics and num_batches_tracked must be bit-identical -- over two steps (the
+    slots and arrival counters must be left zeroed for the next use)."""
+    import copy
+
+    import torch.nn as nn
+
+    from kungfu_amd.models.resnet import Bottleneck, conv1x1
+    from kungfu_amd.ops import fused_block
+    from kungfu_amd.ops.fused_bn import BatchNormAct2d
+
+    torch.manual_seed(1)
+    planes = 64 if cin <= 256 else 128
+    norm = lambda c, relu: BatchNormAct2d(c, relu=relu)  # noqa: E731
+    down = nn.Sequential(conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4, relu=False)) if ds else None
+    blocks = [Bottleneck(cin, planes, stride, down, norm=norm, fused_tail=True)]
+    blocks += [Bottleneck(planes * 4, planes, 1, None, norm=norm, fused_tail=True) for _ in range(nblk - 1)]
+    blk = nn.Sequential(*blocks).cuda().to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    other = copy.deepcopy(blk)
+    hw = 28
+    res = []
+    for mod, on in ((blk, False), (other, True)):
+        monkeypatch.setattr(fused_block, "_INLAUNCH_FIN", on)
+        outs = []
+        for step in range(2):
+            torch.manual_seed(100 + step)
+            x = torch.randn(8, cin, hw, hw, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+            gout = torch.randn(8, planes * 4, hw // stride, hw // stride, device="cuda")
+            xin = x.clone().requires_grad_(True)
+            assert fused_block.eligible(mod[0], xin)
+            out = mod(xin)
+            (out.float() * gout).sum().backward()
+            outs += [out.detach().clone(), xin.grad.clone()]
+        outs += [p.grad.clone() for p in mod.parameters()] + [b.clone() for b in mod.buffers()]
+        res.append(outs)
+    for i, (a, b) in enumerate(zip(*res)):
+        assert torch.equal(a, b), i
+    for m in other.modules():  # the in-launch finalize left its workspaces zeroed
+        if getattr(m, "_kf_arrive", None) is not None:
+            assert int(m._kf_arrive.abs().sum()) == 0
+        if getattr(m, "_kf_sums", None) is not None:
+            assert float(m._kf_sums.abs().sum()) == 0.0
+
+
+@needs_gpu
 def test_resnet50_fused_block_step_matches_layerwise():
     """ResNet-50 S-SGD steps (bf16 shadow weights) with one-node fused bottlenecks: the
     first-step loss is as close to the float32 model as the per-layer bf16 path's, and
