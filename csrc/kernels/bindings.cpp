@@ -12,6 +12,7 @@
 #include <memory>
 #include <tuple>
 #include <vector>
+#include <cstring>
 
 namespace {
 
@@ -285,23 +286,24 @@ at::Tensor conv3x3(at::Tensor x, at::Tensor w, int64_t stride, int64_t variant) 
 // input is bn_x; stats then receive sum(dz), sum(dz * x) (dz = grad * relu') for
 // bn_backward(..., sums=stats).  bn_mask (1 bit per element) or bn_fcoef (forward
 // [scale; shift]) gives the ReLU gate.
-// In-launch BN finalize of a statistics epilogue (kfk::BNFin).  mode 1 (forward):
+// In-launch BN finalize descriptor (kfk::BNFin) packed on the host into a CPU uint8 tensor; the
+// caller keeps a device copy and passes it to conv / conv_dgrad_s2 as `fin`.  mode 1 (forward):
 //   t = [arrive(int32 >= 9, zeroed), gamma, beta, mean, invstd, coef(2C), running_mean, running_var, num_batches]
 // mode 2 (backward): t = [arrive, gamma, mean, invstd, coef(3C), dgamma, dbeta]; f32 per-channel tensors.
-static void fill_fin(kfk::BNFin &f, int64_t mode, const c10::optional<std::vector<at::Tensor>> &t, int64_t rows,
-                     double momentum, double eps, bool training, int C, const at::Tensor &like) {
-    if (mode == 0) return;
-    TORCH_CHECK(t.has_value() && (mode == 1 || mode == 2), "fin: mode 1 or 2 with its tensor list");
-    const auto &v = *t;
-    TORCH_CHECK(v.size() == (mode == 1 ? 9u : 7u), "fin: wrong tensor count for the mode");
-    TORCH_CHECK(v[0].scalar_type() == at::kInt && v[0].numel() >= 9 && v[0].is_contiguous() && v[0].device() == like.device(),
-                "fin: arrive must be a zeroed int32 tensor of >= 9 words on the conv's device");
+at::Tensor bn_fin_desc(int64_t mode, std::vector<at::Tensor> v, int64_t rows, double momentum, double eps,
+                       bool training) {
+    TORCH_CHECK(mode == 1 || mode == 2, "bn_fin_desc: mode 1 (forward) or 2 (backward)");
+    TORCH_CHECK(v.size() == (mode == 1 ? 9u : 7u), "bn_fin_desc: wrong tensor count for the mode");
+    TORCH_CHECK(v[0].is_cuda() && v[0].scalar_type() == at::kInt && v[0].numel() >= 9 && v[0].is_contiguous(),
+                "bn_fin_desc: arrive must be a zeroed int32 GPU tensor of >= 9 words");
+    const int C = static_cast<int>(v[1].numel());
     auto f32 = [&](const at::Tensor &a, int64_t n, const char *what) -> float * {
         TORCH_CHECK(a.defined() && a.scalar_type() == at::kFloat && a.numel() == n && a.is_contiguous() &&
-                        a.device() == like.device(),
-                    "fin: ", what, " must be a contiguous f32 tensor of ", n, " elements on the conv's device");
+                        a.device() == v[0].device(),
+                    "bn_fin_desc: ", what, " must be a contiguous f32 tensor of ", n, " elements on arrive's device");
         return a.data_ptr<float>();
     };
+    kfk::BNFin f;
     f.mode = static_cast<int>(mode);
     f.arrive = reinterpret_cast<unsigned *>(v[0].data_ptr<int>());
     f.rows = rows;
@@ -315,7 +317,7 @@ static void fill_fin(kfk::BNFin &f, int64_t mode, const c10::optional<std::vecto
         f.coef = f32(v[5], 2 * C, "coef");
         f.run_mean = f32(v[6], C, "running_mean");
         f.run_var = f32(v[7], C, "running_var");
-        TORCH_CHECK(v[8].scalar_type() == at::kLong && v[8].numel() == 1, "fin: num_batches must be int64[1]");
+        TORCH_CHECK(v[8].scalar_type() == at::kLong && v[8].numel() == 1, "bn_fin_desc: num_batches must be int64[1]");
         f.num_batches = v[8].data_ptr<int64_t>();
     } else {
         f.mean = f32(v[2], C, "mean");
@@ -324,14 +326,24 @@ static void fill_fin(kfk::BNFin &f, int64_t mode, const c10::optional<std::vecto
         f.dgamma = f32(v[5], C, "dgamma");
         f.dbeta = f32(v[6], C, "dbeta");
     }
+    auto out = at::empty({static_cast<int64_t>(sizeof(kfk::BNFin))}, at::TensorOptions().dtype(at::kByte));
+    std::memcpy(out.data_ptr<uint8_t>(), &f, sizeof(f));
+    return out;
+}
+
+static const kfk::BNFin *fin_ptr(const c10::optional<at::Tensor> &fin, const at::Tensor &like, int C) {
+    if (!fin || !fin->defined()) return nullptr;
+    TORCH_CHECK(fin->is_cuda() && fin->device() == like.device() && fin->scalar_type() == at::kByte &&
+                    fin->numel() == static_cast<int64_t>(sizeof(kfk::BNFin)) && fin->is_contiguous(),
+                "fin: must be the device copy of a bn_fin_desc descriptor on the conv's device");
+    return reinterpret_cast<const kfk::BNFin *>(fin->data_ptr<uint8_t>());
 }
 
 at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Tensor> stats,
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
                 c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
                 c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask, bool acc_even,
-                int64_t fin_mode, c10::optional<std::vector<at::Tensor>> fin, double fin_momentum, double fin_eps,
-                bool fin_training) {
+                c10::optional<at::Tensor> fin) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -424,12 +436,9 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
                     "conv: acc_even needs out, stride 1 and no acc_mask / bn_fcoef");
         epi |= kfk::kEpiAccEven;
     }
-    if (fin_mode) {
-        TORCH_CHECK((fin_mode == 1 && (epi & kfk::kEpiFwdStats)) ||
-                        (fin_mode == 2 && (epi & (kfk::kEpiBwdCoef | kfk::kEpiBwdBits))),
-                    "conv: fin mode 1 needs the statistics epilogue (stats, no bn_x), mode 2 the BN-backward sums (bn_x)");
-        fill_fin(ea.fin, fin_mode, fin, static_cast<int64_t>(N) * OH * OW, fin_momentum, fin_eps, fin_training, K, x);
-    }
+    ea.fin = fin_ptr(fin, x, K);
+    TORCH_CHECK(!ea.fin || (epi & (kfk::kEpiFwdStats | kfk::kEpiBwdCoef | kfk::kEpiBwdBits)),
+                "conv: fin needs the statistics epilogue (stats) or the BN-backward sums (stats + bn_x)");
     kfk::launch_conv(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
                      reinterpret_cast<uint16_t *>(y.data_ptr()), N, H, W, C, K, ks, static_cast<int>(stride), ea, epi,
                      stream_of(x, 0), static_cast<int>(variant));
@@ -510,7 +519,7 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
 at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional<at::Tensor> stats,
                          c10::optional<at::Tensor> bn_x, c10::optional<at::Tensor> bn_fcoef,
                          c10::optional<at::Tensor> bn_mask, int64_t variant, int64_t dh, int64_t dw, int64_t pad,
-                         int64_t fin_mode, c10::optional<std::vector<at::Tensor>> fin, bool fin_training) {
+                         c10::optional<at::Tensor> fin) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
                     dy.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_dgrad_s2: dy must be a 4-D channels_last bf16 GPU tensor");
@@ -559,10 +568,8 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
             epi = kfk::kEpiBwdCoef;
         }
     }
-    if (fin_mode) {
-        TORCH_CHECK(fin_mode == 2 && epi != 0, "conv_dgrad_s2: fin mode 2 needs the BN-backward sums (bn_x)");
-        fill_fin(ea.fin, fin_mode, fin, static_cast<int64_t>(N) * dh * dw, 0.0, 0.0, fin_training, C, dy);
-    }
+    ea.fin = fin_ptr(fin, dy, C);
+    TORCH_CHECK(!ea.fin || epi != 0, "conv_dgrad_s2: fin needs the BN-backward sums (stats + bn_x)");
     kfk::launch_conv_dgrad_s2(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                               reinterpret_cast<const uint16_t *>(wt.data_ptr()), reinterpret_cast<uint16_t *>(dx.data_ptr()),
                               N, OH, OW, K, C, static_cast<int>(ks), ea, epi, stream_of(dy, 0),
@@ -1607,8 +1614,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
           py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false,
-          py::arg("fin_mode") = 0, py::arg("fin") = py::none(), py::arg("fin_momentum") = 0.1,
-          py::arg("fin_eps") = 1e-5, py::arg("fin_training") = true);
+          py::arg("fin") = py::none());
+    m.def("bn_fin_desc", &bn_fin_desc, "pack an in-launch BN finalize descriptor (CPU uint8; copy it to the GPU)",
+          py::arg("mode"), py::arg("tensors"), py::arg("rows"), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5,
+          py::arg("training") = true);
     m.def("conv_rect", &conv_rect, "KH x KW NHWC bf16 convolution with zero padding (MFMA implicit GEMM; "
           "Inception-v3 windows) with an optional BN-statistics epilogue", py::arg("x"), py::arg("w"),
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none(),
@@ -1623,7 +1632,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "MFMA implicit GEMMs)", py::arg("dy"), py::arg("wt"), py::arg("ks"), py::arg("stats") = py::none(),
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1,
-          py::arg("fin_mode") = 0, py::arg("fin") = py::none(), py::arg("fin_training") = true);
+          py::arg("fin") = py::none());
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
           py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "

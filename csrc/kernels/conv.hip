@@ -80,7 +80,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // those folds every channel's slots with sc1 loads (the f64 adds were performed at the memory side,
 // no L2 holds them) and re-zeroes slots and counters with sc1 stores for the next launch.  No fence:
 // the outputs are read by later kernels only.
-__device__ __noinline__ void bn_finalize_last(const EpiArgs &ea, int C, int nwg, int orig, int tid, int nt) {
+__device__ __forceinline__ void bn_finalize_last(const BNFin *__restrict__ fp, double *sums, int C, int nwg, int orig,
+                                                 int tid, int nt, double *red, int red_doubles) {
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -89,42 +90,50 @@ __device__ __noinline__ void bn_finalize_last(const EpiArgs &ea, int C, int nwg,
         const int nsh = nwg < 8 ? nwg : 8;
         const unsigned nin = static_cast<unsigned>((nwg - shard + 7) / 8);
         int last = 0;
-        const unsigned o = __hip_atomic_fetch_add(ea.fin.arrive + shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned *arrive = fp->arrive;
+        const unsigned o = __hip_atomic_fetch_add(arrive + shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (o == nin - 1) {
-            const unsigned o2 =
-                __hip_atomic_fetch_add(ea.fin.arrive + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned o2 = __hip_atomic_fetch_add(arrive + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             last = o2 == static_cast<unsigned>(nsh - 1);
         }
         s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
-    const BNFin &f = ea.fin;
-    double *sums = ea.stats;
-    for (int c = tid; c < C; c += nt) {
-        double v0[kStatSlots], v1[kStatSlots];
-#pragma unroll
-        for (int k = 0; k < kStatSlots; ++k) {
-            v0[k] = __hip_atomic_load(sums + k * 2 * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v1[k] = __hip_atomic_load(sums + k * 2 * C + C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // channel chunks staged through LDS (the main loop's buffers are free): every slot word of the
+    // chunk loaded once (sc1, all independent) and re-zeroed, then each channel folded in slot order
+    // k = 0..15 -- the order of bn_sums_finalize / bn_bwd_finalize_sums, so bit-identical to them
+    constexpr int KS2 = 2 * kStatSlots;
+    const int chunk = red_doubles / KS2 < C ? red_doubles / KS2 : C;
+    for (int c0 = 0; c0 < C; c0 += chunk) {
+        const int ch = C - c0 < chunk ? C - c0 : chunk;
+        const int items = KS2 * ch;
+#pragma unroll 8
+        for (int it = tid; it < items; it += nt) {
+            const int kw = it / ch, cc = it - kw * ch;  // kw = 2 k + which
+            double *a = sums + static_cast<int64_t>(kw) * C + c0 + cc;
+            red[it] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        double s0 = 0, s1 = 0;
-#pragma unroll
-        for (int k = 0; k < kStatSlots; ++k) {
-            s0 += v0[k];
-            s1 += v1[k];
-            __hip_atomic_store(sums + k * 2 * C + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(sums + k * 2 * C + C + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        for (int cc = tid; cc < ch; cc += nt) {
+            double s0 = 0, s1 = 0;
+            for (int k = 0; k < kStatSlots; ++k) {
+                s0 += red[(2 * k) * ch + cc];
+                s1 += red[(2 * k + 1) * ch + cc];
+            }
+            const int c = c0 + cc;
+            if (fp->mode == 1)
+                bn_fin_fwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
+                                   fp->run_var, fp->momentum, fp->eps, fp->coef);
+            else
+                bn_fin_bwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta,
+                                   fp->coef, fp->training != 0);
         }
-        if (f.mode == 1)
-            bn_fin_fwd_channel(c, C, s0, s1, f.rows, f.gamma, f.beta, f.mean, f.invstd, f.run_mean, f.run_var,
-                               f.momentum, f.eps, f.coef);
-        else
-            bn_fin_bwd_channel(c, C, s0, s1, f.rows, f.gamma, f.mean, f.invstd, f.dgamma, f.dbeta, f.coef,
-                               f.training != 0);
+        __syncthreads();
     }
-    if (tid < 9) __hip_atomic_store(f.arrive + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0 && f.mode == 1 && f.num_batches) f.num_batches[0] += 1;
+    if (tid < 9) __hip_atomic_store(fp->arrive + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0 && fp->mode == 1 && fp->num_batches) fp->num_batches[0] += 1;
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
@@ -539,7 +548,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
             }
         }
         if constexpr (NSUM == 2) {
-            if (ea.fin.mode != 0) bn_finalize_last(ea, g.K, nwg, orig, tid, NT);
+            if (ea.fin != nullptr)
+                bn_finalize_last(ea.fin, ea.stats, g.K, nwg, orig, tid, NT, reinterpret_cast<double *>(lds),
+                                 LDS_BYTES / 8);
         }
     }
 }
@@ -934,10 +945,10 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     // dy row a (one tap); q even -> kh = 2 at row a + q/2 - 1 and kh = 0 at row a + q/2 (two taps, the
     // window starting q/2 - 1 rows past a, i.e. zero padding 1 - q/2).  Same for columns.  Flipped-weight
     // tap index = 2 - kh; every dx pixel is written by exactly one phase.
-    if (ea.fin.mode && (DH < 2 || DW < 2)) throw std::invalid_argument("conv_dgrad_s2: in-launch finalize needs dx >= 2x2");
+    if (ea.fin && (DH < 2 || DW < 2)) throw std::invalid_argument("conv_dgrad_s2: in-launch finalize needs dx >= 2x2");
     // the BN-backward sums accumulate over all four phase launches: only the last one finalizes
     EpiArgs ea_early = ea;
-    ea_early.fin.mode = 0;
+    ea_early.fin = nullptr;
     for (int pr = 0; pr < 2; ++pr)
         for (int pc = 0; pc < 2; ++pc) {
             const EpiArgs &eap = (pr == 1 && pc == 1) ? ea : ea_early;

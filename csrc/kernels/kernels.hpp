@@ -125,7 +125,8 @@ enum ConvEpi : int {
 // then across shards), and the LAST arriver folds the kStatSlots slots (sc1 loads: the f64 adds
 // were performed at the memory side), writes what bn_sums_finalize / bn_bwd_finalize_sums would,
 // re-zeroes the slots and the counter -- the separate finalize launch (and its kernel boundary)
-// is gone.  The BN apply that follows is told the coefficients are already there.
+// is gone.  The BN apply that follows is told the coefficients are already there.  Passed as a
+// pointer to a device copy (bn_fin_desc packs one on the host).
 struct BNFin {
     int mode = 0;                // 0 off, 1 forward batch statistics, 2 backward sums
     unsigned *arrive = nullptr;  // 9 zeroed words, left zeroed
@@ -140,7 +141,9 @@ struct BNFin {
     float *dgamma = nullptr, *dbeta = nullptr;  // backward
 };
 struct EpiArgs {
-    BNFin fin;
+    // device-resident descriptor (a kernel-argument copy of BNFin costs every statistics kernel
+    // ~25 spilled SGPRs: the compiler loads all kernel arguments up front)
+    const BNFin *fin = nullptr;
     const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
     uint16_t *aux = nullptr;         // kEpiGelu: the pre-activation output [M, K] bf16
     const uint16_t *bias = nullptr;  // kEpiBiasRelu / kEpiBias / kEpiGelu: bf16 [K]

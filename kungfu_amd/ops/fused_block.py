@@ -75,34 +75,70 @@ def _sums(bn, dev) -> torch.Tensor:
 _INLAUNCH_FIN = os.environ.get("KUNGFU_BN_INLAUNCH_FIN", "1") != "0"
 
 
-def _arrive(bn, dev) -> torch.Tensor:
-    """Per-BN arrival counters of the in-launch finalize (9 int32 words, left zeroed by the kernel)."""
-    a = getattr(bn, "_kf_arrive", None)
-    if a is None or a.device != dev:
-        a = torch.zeros(16, dtype=torch.int32, device=dev)
-        bn._kf_arrive = a
-    return a
+class _BNFinState:
+    """Per-BN in-launch finalize state: the arrival counters and a ring of ``RING`` generations of
+    (output buffers, device descriptor) -- the forward's mean / invstd / coefficients and the
+    backward's dgamma / dbeta / coefficients live in persistent buffers the descriptors point at
+    (packed once, rebuilt only when a pointer or the row count changes).  A generation is reused
+    ``RING`` forwards later, so up to that many forwards may be outstanding before their backward."""
+    RING = 4
+
+    def __init__(self):
+        self.key = None
+        self.gen = 0
+        self.fwd = self.bwd = None
+
+    def _build(self, bn, gamma, beta, rows, dev):
+        H = hip()
+        C = bn.num_features
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.arrive = torch.zeros(16, dtype=torch.int32, device=dev)
+        self.fwd, self.bwd = [], []
+        for _ in range(self.RING):
+            mean, invstd, coef = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(2 * C, **f32)
+            d = H.bn_fin_desc(1, [self.arrive, gamma, beta, mean, invstd, coef, bn.running_mean, bn.running_var,
+                                  bn.num_batches_tracked], rows, float(bn.momentum), float(bn.eps), True).to(dev)
+            self.fwd.append((d, [mean, invstd, coef]))
+            dg, db, c3 = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(3 * C, **f32)
+            d2 = H.bn_fin_desc(2, [self.arrive, gamma, mean, invstd, c3, dg, db], rows, 0.0, 0.0, True).to(dev)
+            self.bwd.append((d2, [dg, db, c3]))
+
+    def next_fwd(self, bn, gamma, beta, rows, dev):
+        key = (gamma.data_ptr(), beta.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+               bn.num_batches_tracked.data_ptr(), int(rows), float(bn.momentum), float(bn.eps))
+        if key != self.key:
+            self._build(bn, gamma, beta, rows, dev)
+            self.key = key
+        g = self.gen
+        self.gen = (g + 1) % self.RING
+        return g
 
 
-def _fin_fwd(bn, gamma, beta, dev):
-    """(conv kwargs, bn_forward pre) for a forward statistics epilogue that finalizes in-launch."""
+def _fin_state(bn) -> _BNFinState:
+    st = getattr(bn, "_kf_fin", None)
+    if st is None:
+        st = bn._kf_fin = _BNFinState()
+    return st
+
+
+def _fin_fwd(bn, gamma, beta, rows, dev):
+    """(conv kwargs, bn_forward pre, generation) for a forward statistics epilogue that finalizes
+    in its own launch; the generation selects the backward buffers (:func:`_fin_bwd`)."""
     if not _INLAUNCH_FIN:
-        return {}, None
-    C = bn.num_features
-    f32 = dict(dtype=torch.float32, device=dev)
-    mean, invstd, coef = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(2 * C, **f32)
-    t = [_arrive(bn, dev), gamma, beta, mean, invstd, coef, bn.running_mean, bn.running_var, bn.num_batches_tracked]
-    return dict(fin_mode=1, fin=t, fin_momentum=float(bn.momentum), fin_eps=float(bn.eps)), [mean, invstd, coef]
+        return {}, None, None
+    st = _fin_state(bn)
+    g = st.next_fwd(bn, gamma, beta, rows, dev)
+    d, pre = st.fwd[g]
+    return dict(fin=d), pre, g
 
 
-def _fin_bwd(bn, gamma, mean, invstd, dev):
-    """(fin tensor list, bn_backward pre) for a BN-backward-sums epilogue that finalizes in-launch."""
-    if not _INLAUNCH_FIN:
+def _fin_bwd(bn, gen):
+    """(fin descriptor, bn_backward pre) for the BN-backward-sums epilogue of the forward generation
+    ``gen`` (None: finalize separately)."""
+    if gen is None or not _INLAUNCH_FIN:
         return None, None
-    C = bn.num_features
-    f32 = dict(dtype=torch.float32, device=dev)
-    dg, db, coef = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(3 * C, **f32)
-    return [_arrive(bn, dev), gamma, mean, invstd, coef, dg, db], [dg, db, coef]
+    d, pre = _fin_state(bn).bwd[gen]
+    return d, pre
 
 
 def _wgrad(dy, x, w, stride, pad):
@@ -163,8 +199,7 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
         if bn is not None:
             ws, bx, fc, mk = bn[:4]
             fin = bn[4] if len(bn) > 4 else None
-            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even,
-                          fin_mode=2 if fin is not None else 0, fin=fin)
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even, fin=fin)
         return H.conv(dy, wt, 1, None, out, acc_mask=out_mask, acc_even=acc_even)
     assert out_mask is None and not acc_even
     ks = w.shape[2]
@@ -174,7 +209,7 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
             ws, bx, fc, mk = bn[:4]
             fin = bn[4] if len(bn) > 4 else None
             _dgrad.fused = True
-            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk, fin_mode=2 if fin is not None else 0, fin=fin)
+            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk, fin=fin)
         _dgrad.fused = False
         dx = H.conv_dgrad_s2(dy, wt, ks)
         if ks == 1:  # odd pixels get no gradient from a 1x1 stride-2 conv
@@ -249,9 +284,13 @@ class _BottleneckFn(torch.autograd.Function):
             return H.bn_forward(y, res, gam[i], bet[i], m.running_mean, m.running_var, m.momentum, m.eps, True, relu,
                                 m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply, pre=pres[i])
 
+        gens = [None] * len(spec.bns)
+
         def conv(i, inp, w_, st_):
             # the conv's statistics epilogue also finalizes BN i in its own launch (_fin_fwd)
-            kw, pres[i] = _fin_fwd(spec.bns[i], gam[i], bet[i], dev)
+            oh = (inp.shape[2] - 1) // st_ + 1
+            ow = (inp.shape[3] - 1) // st_ + 1
+            kw, pres[i], gens[i] = _fin_fwd(spec.bns[i], gam[i], bet[i], inp.shape[0] * oh * ow, dev)
             return H.conv(inp, w_, st_, _sums(spec.bns[i], dev), **kw)
 
         y1 = conv(0, x, ws_bf[0], 1)
@@ -270,8 +309,9 @@ class _BottleneckFn(torch.autograd.Function):
             out, m3, i3, c3, mask3 = bn(2, y3, x, True)
         # cross-block BN3 backward fusion: the previous block's tail (if x is its output)
         ctx.prev = getattr(x, "_kf_tail", None)
-        fin3, pre3 = _fin_bwd(spec.bns[2], gam[2], m3, i3, dev)
+        fin3, pre3 = _fin_bwd(spec.bns[2], gens[2])
         ctx.tail = _TailSlot(_sums(spec.bns[2], dev), y3, mask3, fin3, pre3)
+        ctx.gens = gens
         ctx.spec = spec
         ctx.wdtypes = [w.dtype for w in ws[0::3]]
         ctx.save_for_backward(x, y1, z1, y2, z2, y3, yd, *ws_bf, *gam, m1, i1, c1, m2, i2, c2, m3, i3, c3, mask3,
@@ -324,12 +364,12 @@ class _BottleneckFn(torch.autograd.Function):
                                             ws[2] if use3 else None, dres_x=yd if spec.ds else None,
                                             dres_sums=ws[3] if spec.ds else None, pre=pre3)
         dbn[2] = (dg3, db3)
-        fin2, pre2 = _fin_bwd(spec.bns[1], g[1], m2, i2, dout.device)
+        fin2, pre2 = _fin_bwd(spec.bns[1], ctx.gens[1])
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None, fin2))
         dw[2] = wgrad(dy3, z2, w[2], 1, 0)
         dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1], pre=pre2)
         dbn[1] = (dg2, db2)
-        fin1, pre1 = _fin_bwd(spec.bns[0], g[0], m1, i1, dout.device)
+        fin1, pre1 = _fin_bwd(spec.bns[0], ctx.gens[0])
         dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None, fin1))
         fused1 = _dgrad.fused
         dw[1] = wgrad(dy2, z1, w[1], s, 1)

@@ -714,8 +714,8 @@ def test_fused_bottleneck_inlaunch_finalize_bit_identical(cin, stride, ds, nblk,
     for i, (a, b) in enumerate(zip(*res)):
         assert torch.equal(a, b), i
     for m in other.modules():  # the in-launch finalize left its workspaces zeroed
-        if getattr(m, "_kf_arrive", None) is not None:
-            assert int(m._kf_arrive.abs().sum()) == 0
+        if getattr(m, "_kf_fin", None) is not None:
+            assert int(m._kf_fin.arrive.abs().sum()) == 0
         if getattr(m, "_kf_sums", None) is not None:
             assert float(m._kf_sums.abs().sum()) == 0.0
 
