@@ -80,9 +80,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 // those folds every channel's slots with sc1 loads (the f64 adds were performed at the memory side,
 // no L2 holds them) and re-zeroes slots and counters with sc1 stores for the next launch.  No fence:
 // the outputs are read by later kernels only.
+// `red` (the kernel's own LDS, free once the statistics are out) holds red_doubles doubles and then
+// the flag word: a separate __shared__ variable would push the 256x64 tiles' 80 KB past the
+// two-workgroups-per-CU LDS budget.
 __device__ __forceinline__ void bn_finalize_last(const BNFin *__restrict__ fp, double *sums, int C, int nwg, int orig,
                                                  int tid, int nt, double *red, int red_doubles) {
-    __shared__ int s_last;
+    int &s_last = *reinterpret_cast<int *>(red + red_doubles);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -134,6 +137,35 @@ __device__ __forceinline__ void bn_finalize_last(const BNFin *__restrict__ fp, d
     }
     if (tid < 9) __hip_atomic_store(fp->arrive + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0 && fp->mode == 1 && fp->num_batches) fp->num_batches[0] += 1;
+}
+
+// The same finalize as a launch of its own (a non-persistent statistics launch: there every
+// workgroup would hold its CU through the wait for its atomics).
+__global__ void bn_fin_desc_kernel(const BNFin *__restrict__ fp, double *sums, int C) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double v0[kStatSlots], v1[kStatSlots];
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        v0[k] = sums[k * 2 * C + c];
+        v1[k] = sums[k * 2 * C + C + c];
+    }
+    double s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        s0 += v0[k];
+        s1 += v1[k];
+        sums[k * 2 * C + c] = 0.0;
+        sums[k * 2 * C + C + c] = 0.0;
+    }
+    if (fp->mode == 1) {
+        if (c == 0 && fp->num_batches) fp->num_batches[0] += 1;
+        bn_fin_fwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
+                           fp->run_var, fp->momentum, fp->eps, fp->coef);
+    } else {
+        bn_fin_bwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta, fp->coef,
+                           fp->training != 0);
+    }
 }
 
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
@@ -550,7 +582,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         if constexpr (NSUM == 2) {
             if (ea.fin != nullptr)
                 bn_finalize_last(ea.fin, ea.stats, g.K, nwg, orig, tid, NT, reinterpret_cast<double *>(lds),
-                                 LDS_BYTES / 8);
+                                 LDS_BYTES / 8 - 2);
         }
     }
 }
@@ -668,6 +700,15 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
                 x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
             return;
         }
+    }
+    if (ea.fin) {
+        // one tile per workgroup: finalize in a launch of its own
+        EpiArgs e2 = ea;
+        e2.fin = nullptr;
+        conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+            x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, e2);
+        bn_fin_desc_kernel<<<(g.K + 255) / 256, 256, 0, s>>>(ea.fin, ea.stats, g.K);
+        return;
     }
     conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
         x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
@@ -890,10 +931,13 @@ void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g,
     g.ntiles = (g.K + BN - 1) / BN;  // a partial last N tile reads zero B rows, stores its valid columns
     const int grid = g.mtiles * g.ntiles;
     const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
-    if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
-    else if (epi == C) conv_kernel<KS, WM, WN, ST, C, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
-    else if (epi == B) conv_kernel<KS, WM, WN, ST, B, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, ea);
+    EpiArgs e2 = ea;
+    e2.fin = nullptr;  // one tile per workgroup: the finalize runs as a launch of its own
+    if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
+    else if (epi == C) conv_kernel<KS, WM, WN, ST, C, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
+    else if (epi == B) conv_kernel<KS, WM, WN, ST, B, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
     else throw std::invalid_argument("conv_dgrad_s2: unsupported epilogue");
+    if (ea.fin) bn_fin_desc_kernel<<<(g.K + 255) / 256, 256, 0, s>>>(ea.fin, ea.stats, g.K);
 }
 
 // Tile for the short-K phase GEMMs (variant >= 0 to override; tools/bench_dgrad_s2.py): 128x128

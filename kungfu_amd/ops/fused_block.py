@@ -70,9 +70,18 @@ def _sums(bn, dev) -> torch.Tensor:
     return ws
 
 
-# KUNGFU_BN_INLAUNCH_FIN=0: separate BN finalize launches (A/B); default: the statistics-producing conv
-# finalizes in its own launch (last-arriving workgroup, csrc/kernels/conv.hip bn_finalize_last)
-_INLAUNCH_FIN = os.environ.get("KUNGFU_BN_INLAUNCH_FIN", "1") != "0"
+# KUNGFU_BN_INLAUNCH_FIN=1: the statistics-producing conv finalizes its BN in its own launch
+# (last-arriving workgroup, csrc/kernels/conv.hip bn_finalize_last; bit-identical).  Off by default:
+# measured 0.55-1.25 ms/step SLOWER on ResNet-50 than the separate finalize launches (every
+# workgroup must wait for its memory-side f64 slot atomics before it may arrive, and the arrivals
+# and the last workgroup's fold sit on the launch's critical path), although dropping the finalize
+# launches altogether would save 1.0 ms (KUNGFU_BN_SKIP_FINALIZE timing experiment).
+_INLAUNCH_FIN = os.environ.get("KUNGFU_BN_INLAUNCH_FIN", "0") == "1"
+
+
+def _kw(**kw):
+    """The keyword arguments that are not None (older extension builds lack fin / pre)."""
+    return {k: v for k, v in kw.items() if v is not None}
 
 
 class _BNFinState:
@@ -199,7 +208,7 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
         if bn is not None:
             ws, bx, fc, mk = bn[:4]
             fin = bn[4] if len(bn) > 4 else None
-            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even, fin=fin)
+            return H.conv(dy, wt, 1, ws, out, -1, bx, fc, mk, acc_mask=out_mask, acc_even=acc_even, **_kw(fin=fin))
         return H.conv(dy, wt, 1, None, out, acc_mask=out_mask, acc_even=acc_even)
     assert out_mask is None and not acc_even
     ks = w.shape[2]
@@ -209,7 +218,7 @@ def _dgrad(dy, x, w, stride, pad, out: Optional[torch.Tensor] = None, flipped: O
             ws, bx, fc, mk = bn[:4]
             fin = bn[4] if len(bn) > 4 else None
             _dgrad.fused = True
-            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk, fin=fin)
+            return H.conv_dgrad_s2(dy, wt, 3, ws, bx, fc, mk, **_kw(fin=fin))
         _dgrad.fused = False
         dx = H.conv_dgrad_s2(dy, wt, ks)
         if ks == 1:  # odd pixels get no gradient from a 1x1 stride-2 conv
@@ -282,7 +291,7 @@ class _BottleneckFn(torch.autograd.Function):
         def bn(i, y, res, relu, res_coef=None, apply=True):
             m = spec.bns[i]
             return H.bn_forward(y, res, gam[i], bet[i], m.running_mean, m.running_var, m.momentum, m.eps, True, relu,
-                                m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply, pre=pres[i])
+                                m.num_batches_tracked, _sums(m, dev), res_coef=res_coef, apply=apply, **_kw(pre=pres[i]))
 
         gens = [None] * len(spec.bns)
 
@@ -362,19 +371,19 @@ class _BottleneckFn(torch.autograd.Function):
         # sums are accumulated by this same pass (that BN then skips its reduce)
         dy3, didt, dg3, db3 = H.bn_backward(dout, y3, m3, i3, g[2], c3, mask3, True, True, not in_place,
                                             ws[2] if use3 else None, dres_x=yd if spec.ds else None,
-                                            dres_sums=ws[3] if spec.ds else None, pre=pre3)
+                                            dres_sums=ws[3] if spec.ds else None, **_kw(pre=pre3))
         dbn[2] = (dg3, db3)
         fin2, pre2 = _fin_bwd(spec.bns[1], ctx.gens[1])
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None, fin2))
         dw[2] = wgrad(dy3, z2, w[2], 1, 0)
-        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1], pre=pre2)
+        dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1], **_kw(pre=pre2))
         dbn[1] = (dg2, db2)
         fin1, pre1 = _fin_bwd(spec.bns[0], ctx.gens[0])
         dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None, fin1))
         fused1 = _dgrad.fused
         dw[1] = wgrad(dy2, z1, w[1], s, 1)
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
-                                         ws[0] if fused1 else None, pre=pre1 if fused1 else None)
+                                         ws[0] if fused1 else None, **_kw(pre=pre1 if fused1 else None))
         dbn[0] = (dg1, db1)
         acc_even = False
         if spec.ds:
