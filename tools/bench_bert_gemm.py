@@ -55,3 +55,24 @@ for name, cin, cout in SHAPES:
     res.append("geluG:%.0fus" % timeit(lambda: H_.gemm(x, w, gelu_u=u, stats=st)))
     res.append("acc:%.0fus" % timeit(lambda: H_.gemm(x, w, out=u)))
     print("%-7s %4d->%4d %5.1fGF  %s" % (name, cin, cout, flop / 1e9, " ".join(res)), flush=True)
+
+# weight gradients dW[out, in] = dy^T x over T tokens: split-K MFMA kernel (ops/linear.py) vs hipBLASLt
+print("weight gradients (T=%d)" % T, flush=True)
+
+
+def as4d(t2):
+    n, c = t2.shape
+    return t2.as_strided((1, c, 1, n), (n * c, 1, n * c, c))
+
+
+for name, cin, cout in SHAPES[:4]:
+    x = torch.randn(T, cin, device="cuda").bfloat16()
+    dy = torch.randn(T, cout, device="cuda").bfloat16()
+    flop = 2.0 * T * cin * cout
+    t_blas = timeit(lambda: torch.mm(dy.t(), x))
+    t_blas2 = timeit(lambda: torch.matmul(x.t(), dy))
+    t_ours = timeit(lambda: H_.conv_wgrad(as4d(dy), as4d(x), 1, 1))
+    ref = torch.mm(dy.t().float(), x.float())
+    err = ((H_.conv_wgrad(as4d(dy), as4d(x), 1, 1).view(cout, cin).float() - ref).norm() / ref.norm()).item()
+    print("%-7s %4d->%4d  blas dy^T x %.0fus/%.0fTF  blas x^T dy %.0fus  ours %.0fus/%.0fTF (rel %.1e)" % (
+        name, cin, cout, t_blas, flop / t_blas / 1e6, t_blas2, t_ours, flop / t_ours / 1e6, err), flush=True)
