@@ -899,9 +899,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_forward(at:
 
 // Returns (ds, dgamma, dbeta, dr): dr (p > 0 only, else undefined) is the gradient of the dropped
 // residual input.
-std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at::Tensor dy, at::Tensor s,
-                                                                              at::Tensor gamma, at::Tensor mean,
-                                                                              at::Tensor rstd, double p, int64_t seed) {
+// rbias_dtype (float32 / bfloat16, optional): also return the column sums of the residual input's
+// gradient (dr, or ds without dropout) in that dtype -- the bias gradient of the linear layer that
+// produced the residual input.
+std::vector<at::Tensor> layernorm_backward(at::Tensor dy, at::Tensor s, at::Tensor gamma, at::Tensor mean,
+                                           at::Tensor rstd, double p, int64_t seed,
+                                           c10::optional<at::ScalarType> rbias_dtype) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && s.sizes() == dy.sizes() &&
                     s.scalar_type() == at::kBFloat16 && s.is_contiguous(),
                 "layernorm_backward: contiguous bf16 dy and s of equal shape");
@@ -911,7 +914,12 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at
     const int64_t rows = dy.numel() / D;
     TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_backward: stats size");
     auto ds = at::empty_like(dy);
-    auto partial = at::empty({kfk::layernorm_bwd_blocks(rows), 2, D}, dy.options().dtype(at::kFloat));
+    const bool rb = rbias_dtype.has_value();
+    TORCH_CHECK(!rb || *rbias_dtype == at::kFloat || *rbias_dtype == at::kBFloat16,
+                "layernorm_backward: rbias_dtype must be float32 or bfloat16");
+    auto partial = at::empty({kfk::layernorm_bwd_blocks(rows), rb ? 3 : 2, D}, dy.options().dtype(at::kFloat));
+    at::Tensor rbias;
+    if (rb) rbias = at::empty({D}, dy.options().dtype(*rbias_dtype));
     auto dgamma = at::empty({D}, dy.options().dtype(at::kFloat));
     auto dbeta = at::empty({D}, dy.options().dtype(at::kFloat));
     at::Tensor dr;
@@ -922,7 +930,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> layernorm_backward(at
                                    reinterpret_cast<uint16_t *>(ds.data_ptr()), partial.data_ptr<float>(),
                                    dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, stream_of(dy, 0),
                                    dr.defined() ? reinterpret_cast<uint16_t *>(dr.data_ptr()) : nullptr,
-                                   static_cast<float>(p), static_cast<uint32_t>(seed));
+                                   static_cast<float>(p), static_cast<uint32_t>(seed),
+                                   rb && *rbias_dtype == at::kFloat ? rbias.data_ptr<float>() : nullptr,
+                                   rb && *rbias_dtype == at::kBFloat16 ? reinterpret_cast<uint16_t *>(rbias.data_ptr())
+                                                                        : nullptr);
+    if (rb) return {ds, dgamma, dbeta, dr, rbias};
     return {ds, dgamma, dbeta, dr};
 }
 
@@ -1656,9 +1668,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("layernorm_forward", &layernorm_forward, "fused residual-add + LayerNorm (bf16 rows) -> (y, s, mean, rstd)",
           py::arg("x"), py::arg("r"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p") = 0.0,
           py::arg("seed") = 0);
-    m.def("layernorm_backward", &layernorm_backward, "LayerNorm backward -> (ds, dgamma, dbeta, dr or None)",
-          py::arg("dy"), py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("p") = 0.0,
-          py::arg("seed") = 0);
+    m.def("layernorm_backward", &layernorm_backward,
+          "LayerNorm backward -> (ds, dgamma, dbeta, dr or None[, residual-input bias gradient])", py::arg("dy"),
+          py::arg("s"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("p") = 0.0, py::arg("seed") = 0,
+          py::arg("rbias_dtype") = py::none());
     m.def("global_avgpool_forward", &global_avgpool_forward, "global average pool, NHWC bf16 -> [N, C]");
     m.def("global_avgpool_backward", &global_avgpool_backward, "global average pool backward -> NHWC bf16",
           py::arg("dy"), py::arg("H"), py::arg("W"));

@@ -339,7 +339,8 @@ void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float 
 void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
                                const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
                                int64_t rows, int D, hipStream_t st,
-                               uint16_t *dr = nullptr, float p = 0.f, uint32_t seed = 0);
+                               uint16_t *dr = nullptr, float p = 0.f, uint32_t seed = 0, float *rb_f32 = nullptr,
+                               uint16_t *rb_bf16 = nullptr);  // rb_*: the residual input's column sums (f32 or bf16)
 // gate_stats != nullptr: x is a ReLU output, dx = that ReLU's input gradient (window max > 0 only)
 // and the per-channel sums of dx go to gate_stats[slot][0][C] (kStatSlots x 2 x C f64, zeroed)
 void launch_maxpool2x2_backward(const uint16_t *x, const uint16_t *dy, uint16_t *dx, int64_t N, int H, int W, int C,

@@ -128,7 +128,10 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const uint2 *__re
     }
 }
 
-template <int G>
+// RB: also the column sums of the residual input's gradient (dr, or ds without dropout) as written
+// in bf16 -- the bias gradient of the linear layer that produced the residual input (its colsum
+// pass is skipped); partial rows [blocks][3][D].
+template <int G, bool RB>
 __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__restrict__ dy,
                                                                const uint2 *__restrict__ s,
                                                                const float *__restrict__ gamma,
@@ -138,13 +141,14 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
                                                                uint2 *__restrict__ dr, LnDrop drop) {
     constexpr int D = 256 * G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float gm[G][4], dg[G][4], db[G][4];
+    float gm[G][4], dg[G][4], db[G][4], rb[RB ? G : 1][4];
 #pragma unroll
     for (int j = 0; j < G; ++j)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             gm[j][k] = gamma[(j * 64 + lane) * 4 + k];
             dg[j][k] = db[j][k] = 0.f;
+            if constexpr (RB) rb[j][k] = 0.f;
         }
     const int64_t wstride = static_cast<int64_t>(gridDim.x) * kLnWaves;
     for (int64_t row = static_cast<int64_t>(blockIdx.x) * kLnWaves + wave; row < rows; row += wstride) {
@@ -173,30 +177,40 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
             float o[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) o[k] = rs * (g[j][k] - m1 - xh[j][k] * m2);
-            ds[base + j * 64 + lane] = pack4(o);
+            uint2 pk = pack4(o);
+            ds[base + j * 64 + lane] = pk;
             if (dr) {  // gradient of the dropped residual input
                 const int64_t e0 = (base + j * 64 + lane) * 4;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) o[k] = ln_keep(drop, e0 + k) ? o[k] * drop.inv_keep : 0.f;
-                dr[base + j * 64 + lane] = pack4(o);
+                pk = pack4(o);
+                dr[base + j * 64 + lane] = pk;
+            }
+            if constexpr (RB) {
+                float w[4];
+                unpack4(pk, w);  // the bf16 values the producing linear's backward consumes
+#pragma unroll
+                for (int k = 0; k < 4; ++k) rb[j][k] += w[k];
             }
         }
     }
-    // block reduction of the per-lane column sums -> partial[block][2][D]
-    __shared__ float red[kLnWaves][2][D];
+    // block reduction of the per-lane column sums -> partial[block][NS][D]
+    constexpr int NS = RB ? 3 : 2;
+    __shared__ float red[kLnWaves][NS][D];
 #pragma unroll
     for (int j = 0; j < G; ++j)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             red[wave][0][(j * 64 + lane) * 4 + k] = dg[j][k];
             red[wave][1][(j * 64 + lane) * 4 + k] = db[j][k];
+            if constexpr (RB) red[wave][2][(j * 64 + lane) * 4 + k] = rb[j][k];
         }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * D; c += 64 * kLnWaves) {
+    for (int c = threadIdx.x; c < NS * D; c += 64 * kLnWaves) {
         float t = 0.f;
 #pragma unroll
         for (int w = 0; w < kLnWaves; ++w) t += (&red[w][0][0])[c];
-        partial[static_cast<int64_t>(blockIdx.x) * 2 * D + c] = t;
+        partial[static_cast<int64_t>(blockIdx.x) * NS * D + c] = t;
     }
 }
 
@@ -206,7 +220,9 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
 constexpr int kColGroups = 16;
 __global__ __launch_bounds__(64 * kColGroups) void ln_colsum_kernel(const float *__restrict__ partial, int nblocks,
                                                                     int cols, float *__restrict__ dgamma,
-                                                                    float *__restrict__ dbeta, int D) {
+                                                                    float *__restrict__ dbeta, int D,
+                                                                    float *__restrict__ rb_f32 = nullptr,
+                                                                    uint16_t *__restrict__ rb_bf16 = nullptr) {
     __shared__ double red[kColGroups][64];
     const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + lane;
@@ -222,7 +238,9 @@ __global__ __launch_bounds__(64 * kColGroups) void ln_colsum_kernel(const float 
 #pragma unroll
         for (int g = 0; g < kColGroups; ++g) u += red[g][lane];
         if (c < D) dgamma[c] = static_cast<float>(u);
-        else dbeta[c - D] = static_cast<float>(u);
+        else if (c < 2 * D) dbeta[c - D] = static_cast<float>(u);
+        else if (rb_f32) rb_f32[c - 2 * D] = static_cast<float>(u);
+        else rb_bf16[c - 2 * D] = f32_to_bf16(static_cast<float>(u));
     }
 }
 
@@ -283,18 +301,30 @@ void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float 
 
 void launch_layernorm_backward(const uint16_t *dy, const uint16_t *s, const float *gamma, const float *mean,
                                const float *rstd, uint16_t *ds, float *partial, float *dgamma, float *dbeta,
-                               int64_t rows, int D, hipStream_t st, uint16_t *dr, float p, uint32_t seed) {
+                               int64_t rows, int D, hipStream_t st, uint16_t *dr, float p, uint32_t seed,
+                               float *rb_f32, uint16_t *rb_bf16) {
     if (rows <= 0) return;
     const LnDrop drop = make_drop(dr ? p : 0.f, seed);
     const int blocks = layernorm_bwd_blocks(rows);
+    const bool rb = rb_f32 || rb_bf16;
     dispatch_g(D, [&](auto gc) {
         constexpr int G = decltype(gc)::value;
-        ln_bwd_kernel<G><<<blocks, 64 * kLnWaves, 0, st>>>(reinterpret_cast<const uint2 *>(dy),
-                                                            reinterpret_cast<const uint2 *>(s), gamma, mean, rstd,
-                                                            reinterpret_cast<uint2 *>(ds), partial, rows,
-                                                            reinterpret_cast<uint2 *>(dr), drop);
+        if (rb) {
+            // the third partial row must fit the block's LDS reduction: D <= 2048
+            if constexpr (G <= 8)
+                ln_bwd_kernel<G, true><<<blocks, 64 * kLnWaves, 0, st>>>(
+                    reinterpret_cast<const uint2 *>(dy), reinterpret_cast<const uint2 *>(s), gamma, mean, rstd,
+                    reinterpret_cast<uint2 *>(ds), partial, rows, reinterpret_cast<uint2 *>(dr), drop);
+            else
+                throw std::invalid_argument("layernorm_backward: residual bias sums need D <= 2048");
+        } else
+            ln_bwd_kernel<G, false><<<blocks, 64 * kLnWaves, 0, st>>>(
+                reinterpret_cast<const uint2 *>(dy), reinterpret_cast<const uint2 *>(s), gamma, mean, rstd,
+                reinterpret_cast<uint2 *>(ds), partial, rows, reinterpret_cast<uint2 *>(dr), drop);
     });
-    ln_colsum_kernel<<<(2 * D + 63) / 64, 64 * kColGroups, 0, st>>>(partial, blocks, 2 * D, dgamma, dbeta, D);
+    const int cols = (rb ? 3 : 2) * D;
+    ln_colsum_kernel<<<(cols + 63) / 64, 64 * kColGroups, 0, st>>>(partial, blocks, cols, dgamma, dbeta, D, rb_f32,
+                                                                   rb_bf16);
 }
 
 }  // namespace kfk

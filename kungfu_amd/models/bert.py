@@ -40,9 +40,11 @@ class BertLayer(nn.Module):
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)
             a = a.transpose(1, 2).reshape(B, S, D)
         # residual dropout fused into the add + LayerNorm kernels (ops/layernorm.py)
-        x = self.ln1(x, self.out(a), dropout=self.dropout)
+        # the projections' outputs feed only their AddLayerNorm: its backward also produces their
+        # bias gradients (ops.linear.BiasLink), no column-sum pass of their own
+        x = self.ln1(x, self.out(a), dropout=self.dropout, bias_link=True)
         h = self.fc2(F.gelu(self.fc1(x)))
-        return self.ln2(x, h, dropout=self.dropout)
+        return self.ln2(x, h, dropout=self.dropout, bias_link=True)
 
 
 class BertForPreTraining(nn.Module):

@@ -17,10 +17,14 @@ import torch.nn.functional as F
 
 from .._lib import hip, hip_available
 
+import os
+
+_BIAS_LINK = os.environ.get("KUNGFU_LN_BIAS_LINK", "1") != "0"  # A/B switch of the linear bias-gradient link
+
 
 class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps, p=0.0, seed=0):
+    def forward(ctx, x, r, gamma, beta, eps, p=0.0, seed=0, blink=None):
         from ..parallel.mixed import direct_target
 
         y, s, mean, rstd = hip().layernorm_forward(x, r, gamma, beta, eps, p, seed)
@@ -29,12 +33,21 @@ class _AddLayerNormFn(torch.autograd.Function):
         ctx.p, ctx.seed = (p, seed) if r is not None else (0.0, 0)
         tg, tb = direct_target(gamma), direct_target(beta)
         ctx.direct = (tg, tb) if tg is not None and tb is not None else None
+        ctx.blink = blink if r is not None else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         s, gamma, mean, rstd = ctx.saved_tensors
-        ds, dg, db, dr = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd, ctx.p, ctx.seed)
+        bl = ctx.blink
+        if bl is not None:
+            # the residual input is a linear layer's output whose only consumer is this LayerNorm:
+            # the same pass also sums its gradient's columns = that layer's bias gradient
+            ds, dg, db, dr, rb = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd, ctx.p, ctx.seed,
+                                                          bl.dtype)
+            bl.value, bl.ptr = rb, (dr if dr is not None else ds).data_ptr()
+        else:
+            ds, dg, db, dr = hip().layernorm_backward(dy.contiguous(), s, gamma, mean, rstd, ctx.p, ctx.seed)
         if ctx.direct is not None:
             # gamma / beta gradients to the flat space's sink (landed with their bucket by one
             # multi-tensor kernel instead of an AccumulateGrad add each: 48 launches in BERT-base)
@@ -46,7 +59,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         # d(x + r)/dx = d(x + r)/dr = 1: both inputs receive ds (the dropped r: ds * keep / (1-p))
         if ctx.has_r and dr is None:
             dr = ds
-        return ds, (dr if ctx.has_r else None), dg, db, None, None, None
+        return ds, (dr if ctx.has_r else None), dg, db, None, None, None, None
 
 
 def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bool:
@@ -58,13 +71,20 @@ def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bo
 
 
 def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: torch.Tensor, bias: torch.Tensor,
-                   eps: float = 1e-5, dropout: float = 0.0, training: bool = False) -> torch.Tensor:
+                   eps: float = 1e-5, dropout: float = 0.0, training: bool = False,
+                   bias_link: bool = False) -> torch.Tensor:
     """``F.layer_norm(x + F.dropout(residual, dropout, training), (D,), weight, bias, eps)``; on the
-    HIP kernels the dropout is fused (hashed keep mask, recomputed in the backward)."""
+    HIP kernels the dropout is fused (hashed keep mask, recomputed in the backward).
+
+    ``bias_link``: the caller guarantees ``residual`` is the output of :func:`ops.linear.linear`
+    consumed only here -- the backward pass then also produces that layer's bias gradient
+    (:class:`~kungfu_amd.ops.linear.BiasLink`), which skips its own column-sum pass."""
     p = float(dropout) if training and residual is not None else 0.0
     if _eligible(x, residual, weight):
         seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if p > 0 else 0  # CPU generator: no device sync
-        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed)
+        bl = (getattr(residual, "_kf_blink", None) if bias_link and _BIAS_LINK and residual is not None
+              and x.shape[-1] <= 2048 else None)
+        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed, bl)
     if p > 0:
         residual = F.dropout(residual, p, True)
     s = x if residual is None else x + residual
@@ -72,8 +92,9 @@ def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: to
 
 
 class AddLayerNorm(nn.LayerNorm):
-    def forward(self, x, residual=None, dropout: float = 0.0):
-        """``layer_norm(x + dropout(residual))`` (``dropout`` active in training mode only)."""
+    def forward(self, x, residual=None, dropout: float = 0.0, bias_link: bool = False):
+        """``layer_norm(x + dropout(residual))`` (``dropout`` active in training mode only);
+        ``bias_link``: see :func:`add_layer_norm`."""
         if residual is not None and residual.dtype != x.dtype and x.is_cuda:
             residual = residual.to(x.dtype)  # e.g. an f32 dropout output beside a bf16 stream
-        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout, self.training)
+        return add_layer_norm(x, residual, self.weight, self.bias, self.eps, dropout, self.training, bias_link)

@@ -29,12 +29,24 @@ def _as_nhwc(t2: torch.Tensor) -> torch.Tensor:
     return t2.as_strided((1, C, 1, T), (T * C, 1, T * C, C))
 
 
+class BiasLink:
+    """Link from a linear layer's output to the ONE consumer that can produce the layer's bias
+    gradient in its own backward pass (an AddLayerNorm with ``bias_link=True``: the column sums of
+    the residual gradient it writes).  ``ptr`` lets the linear's backward check that the gradient it
+    receives is exactly that tensor; otherwise it sums the columns itself."""
+    __slots__ = ("dtype", "value", "ptr")
+
+    def __init__(self, dtype):
+        self.dtype, self.value, self.ptr = dtype, None, 0
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_b = b is not None
         ctx.b_dtype = b.dtype if b is not None else None
+        ctx.blink = BiasLink(b.dtype) if b is not None and b.dtype in (torch.bfloat16, torch.float32) else None
         return F.linear(x, w, b)
 
     @staticmethod
@@ -52,7 +64,11 @@ class _LinearFn(torch.autograd.Function):
             dx = torch.mm(dy2, w).view(x.shape)
         if ctx.needs_input_grad[1]:
             dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+        bl = ctx.blink
+        if bl is not None and bl.value is not None and bl.ptr == dy2.data_ptr() and ctx.needs_input_grad[2]:
+            db = bl.value  # produced by the consuming LayerNorm's backward pass
+            bl.value, bl.ptr = None, 0
+        elif ctx.has_b and ctx.needs_input_grad[2]:
             # bias gradient: deterministic two-stage column sum (norms.hip; torch's reduce took
             # 26 us per BERT-base layer product at 16 K tokens)
             if dy2.dtype == torch.bfloat16:
@@ -75,5 +91,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None) -> torch.Te
     """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible."""
     if eligible(x, w) and (b is None or b.dtype in (torch.bfloat16, torch.float32)):
         y = _LinearFn.apply(x, w, b)
+        if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
+            y._kf_blink = y.grad_fn.blink
         return y
     return F.linear(x, w, b)

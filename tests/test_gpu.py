@@ -1587,3 +1587,45 @@ def test_inception_bn_concat_matches_cat(block, monkeypatch):
         assert ((b - a).norm() / a.norm().clamp_min(1e-12)).item() < 1e-3
     for a, b in zip(b0, b1):
         assert torch.equal(a, b)
+
+
+@needs_gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bert_layer_bias_link_matches_colsum(p, monkeypatch):
+    """The out-projection / FC2 bias gradients produced by the consuming AddLayerNorm's backward
+    (column sums of the residual gradient it writes, ops.linear.BiasLink) vs the linear layer's own
+    column-sum pass: same forward, same gradients (bias gradients to bf16 rounding)."""
+    import copy
+
+    from kungfu_amd.models.bert import BertLayer
+    from kungfu_amd.ops import layernorm
+
+    torch.manual_seed(3)
+    layer = BertLayer(dropout=p).cuda()
+    for m in (layer.qkv, layer.out, layer.fc1, layer.fc2):
+        m.to(torch.bfloat16)
+        torch.nn.init.normal_(m.bias, std=0.02)
+    other = copy.deepcopy(layer)
+    x = torch.randn(4, 128, 768, device="cuda").bfloat16()
+    g = torch.randn(4, 128, 768, device="cuda").bfloat16()
+    orig = layernorm.add_layer_norm
+    res = []
+    for mod, link in ((layer, True), (other, False)):
+        if not link:
+            monkeypatch.setattr(layernorm, "add_layer_norm",
+                                lambda *a, **k: orig(*a, **{**k, "bias_link": False}) if "bias_link" in k
+                                else orig(*a[:7]))
+        torch.manual_seed(11)
+        xx = x.clone().requires_grad_(True)
+        y = mod(xx)
+        y.backward(g)
+        res.append((y.detach(), xx.grad, {n: q.grad.float() for n, q in mod.named_parameters()}))
+    (y0, gx0, gp0), (y1, gx1, gp1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1)
+    for n in gp0:
+        a, b = gp0[n], gp1[n]
+        if n in ("out.bias", "fc2.bias"):
+            assert ((a - b).norm() / b.norm()).item() < 1e-2, n
+        else:
+            assert torch.equal(a, b), n
