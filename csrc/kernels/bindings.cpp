@@ -660,6 +660,27 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
     return dw;
 }
 
+// GELU backward fused with the bias gradient: (du, colsum(du)) for bf16 dy, u [..., O] (O % 8 == 0).
+std::vector<at::Tensor> gelu_backward_colsum(at::Tensor dy, at::Tensor u, at::ScalarType dtype) {
+    TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && u.sizes() == dy.sizes() &&
+                    u.scalar_type() == at::kBFloat16 && u.is_contiguous() && u.device() == dy.device() &&
+                    dy.size(-1) % 8 == 0 && dy.numel() > 0,
+                "gelu_backward_colsum: contiguous bf16 dy and u of equal shape, last dim % 8");
+    TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "gelu_backward_colsum: dtype float32 or bfloat16");
+    c10::DeviceGuard gd(dy.device());
+    const int O = static_cast<int>(dy.size(-1));
+    const int64_t T = dy.numel() / O;
+    auto du = at::empty_like(dy);
+    auto part = at::empty({static_cast<int64_t>(kfk::colsum_chunks(T, O)) * O}, dy.options().dtype(at::kFloat));
+    auto out = at::empty({O}, dy.options().dtype(dtype));
+    kfk::launch_gelu_bwd_colsum(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
+                                reinterpret_cast<const uint16_t *>(u.data_ptr()), reinterpret_cast<uint16_t *>(du.data_ptr()),
+                                T, O, part.data_ptr<float>(), dtype == at::kFloat ? out.data_ptr<float>() : nullptr,
+                                dtype == at::kBFloat16 ? reinterpret_cast<uint16_t *>(out.data_ptr()) : nullptr,
+                                stream_of(dy, 0));
+    return {du, out};
+}
+
 // Column sums of a contiguous bf16 [T, O] (O % 8 == 0) -> [O] in `dtype` (f32 or bf16).
 at::Tensor colsum(at::Tensor x, at::ScalarType dtype) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
@@ -1645,6 +1666,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1,
           py::arg("fin") = py::none());
+    m.def("gelu_backward_colsum", &gelu_backward_colsum, "erf-GELU backward du and the column sums of du",
+          py::arg("dy"), py::arg("u"), py::arg("dtype"));
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
           py::arg("dtype"));
     m.def("conv_wgrad_rect", &conv_wgrad_rect, "weight gradient of a KH x KW padded NHWC bf16 convolution "

@@ -45,6 +45,10 @@ void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, f
 int colsum_chunks(int64_t T, int O);
 void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float *out_f32, uint16_t *out_bf16,
                         hipStream_t s);
+// du = gelu'(u) * dy (bf16 [T, O], torch's erf-GELU backward) and the column sums of du (the bias
+// gradient of the layer that produced u) in one pass + the colsum second stage.
+void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,
+                            float *out_f32, uint16_t *out_bf16, hipStream_t s);
 void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s);
 
 // K6: out[0] = sum_i | s2[i]*inv - (s1[i]*inv)^2 |  (s1 = sum g, s2 = sum g^2 over np ranks)

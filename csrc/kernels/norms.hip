@@ -276,6 +276,70 @@ __global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x
     }
 }
 
+// GELU backward fused with the column sums of its output: du = dy * (Phi(u) + u * phi(u)) (torch's
+// GeluBackward, erf form, f32 math, one bf16 rounding), and per-chunk column partial sums of the
+// bf16 du -- the bias gradient of the linear layer that produced u -- with colsum_stage1's layout
+// (fixed 8-column group per thread, 4 row lanes per block, partials [chunk][O]).
+__global__ __launch_bounds__(256) void gelu_bwd_colsum_stage1(const uint4 *__restrict__ dy, const uint4 *__restrict__ u,
+                                                              uint4 *__restrict__ du, int64_t T, int OV, int rows_per,
+                                                              float *__restrict__ part) {
+    const int v = blockIdx.y * kColVec + (threadIdx.x % kColVec);
+    const int rsub = threadIdx.x / kColVec;
+    const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per;
+    int64_t r1 = r0 + rows_per;
+    if (r1 > T) r1 = T;
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    if (v < OV) {
+        for (int64_t r = r0 + rsub; r < r1; r += 8) {
+            uint4 qd[2], qu[2];
+            bool ok[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t rr = r + 4 * h;
+                ok[h] = rr < r1;
+                if (ok[h]) {
+                    qd[h] = dy[rr * OV + v];
+                    qu[h] = u[rr * OV + v];
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (!ok[h]) continue;
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(&qd[h]);
+                const uint32_t *b = reinterpret_cast<const uint32_t *>(&qu[h]);
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float d2[2] = {__uint_as_float(a[k] << 16), __uint_as_float(a[k] & 0xffff0000u)};
+                    float x2[2] = {__uint_as_float(b[k] << 16), __uint_as_float(b[k] & 0xffff0000u)};
+                    uint16_t r2[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const float x = x2[e];
+                        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+                        const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
+                        r2[e] = f32_to_bf16(d2[e] * (cdf + x * pdf));
+                        acc[2 * k + e] += bf16_to_f32(r2[e]);
+                    }
+                    o[k] = static_cast<uint32_t>(r2[0]) | (static_cast<uint32_t>(r2[1]) << 16);
+                }
+                du[(r + 4 * h) * OV + v] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+        }
+    }
+    __shared__ float red[4][kColVec * 8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[rsub][(threadIdx.x % kColVec) * 8 + k] = acc[k];
+    __syncthreads();
+    const int O = OV * 8;
+    for (int c = threadIdx.x; c < kColVec * 8; c += 256) {
+        const int col = blockIdx.y * kColVec * 8 + c;
+        if (col < O) part[static_cast<int64_t>(blockIdx.x) * O + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    }
+}
+
 // one block per 32 columns: 8 chunk lanes per column each sum every 8th chunk partial, then the
 // 8 lane sums meet in LDS in a fixed order (deterministic)
 __global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int chunks, int O, float *out_f32,
@@ -313,6 +377,16 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
     const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(x), T, OV, rows_per, part);
+    colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+}
+
+void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,
+                            float *out_f32, uint16_t *out_bf16, hipStream_t s) {
+    const int OV = O / 8, chunks = colsum_chunks(T, O);
+    const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
+    dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
+    gelu_bwd_colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(dy), reinterpret_cast<const uint4 *>(u),
+                                              reinterpret_cast<uint4 *>(du), T, OV, rows_per, part);
     colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
 }
 

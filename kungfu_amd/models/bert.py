@@ -10,6 +10,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import self_attention
+from ..ops.linear import gelu
 
 
 class BertLayer(nn.Module):
@@ -43,7 +44,7 @@ class BertLayer(nn.Module):
         # the projections' outputs feed only their AddLayerNorm: its backward also produces their
         # bias gradients (ops.linear.BiasLink), no column-sum pass of their own
         x = self.ln1(x, self.out(a), dropout=self.dropout, bias_link=True)
-        h = self.fc2(F.gelu(self.fc1(x)))
+        h = self.fc2(gelu(self.fc1(x), bias_link=True))
         return self.ln2(x, h, dropout=self.dropout, bias_link=True)
 
 

@@ -95,3 +95,38 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None) -> torch.Te
             y._kf_blink = y.grad_fn.blink
         return y
     return F.linear(x, w, b)
+
+
+class _GeluFn(torch.autograd.Function):
+    """``F.gelu(u)`` whose backward is ONE HIP pass (norms.hip gelu_bwd_colsum): du and its column
+    sums -- the bias gradient of the linear layer that produced ``u`` (handed to that layer's
+    backward through its :class:`BiasLink`, which then skips its own column-sum pass)."""
+
+    @staticmethod
+    def forward(ctx, u, blink):
+        ctx.save_for_backward(u)
+        ctx.blink = blink
+        return F.gelu(u)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (u,) = ctx.saved_tensors
+        bl = ctx.blink
+        du, db = hip().gelu_backward_colsum(dy.contiguous(), u, bl.dtype if bl is not None else torch.float32)
+        if bl is not None:
+            bl.value, bl.ptr = db, du.data_ptr()
+        return du, None
+
+
+_GELU_LINK = os.environ.get("KUNGFU_GELU_BIAS_LINK", "1") != "0"
+
+
+def gelu(u: torch.Tensor, bias_link: bool = False) -> torch.Tensor:
+    """``F.gelu(u)``; with ``bias_link`` (the caller guarantees ``u`` is a :func:`linear` output consumed
+    only here) the backward also produces that layer's bias gradient in the same pass."""
+    bl = getattr(u, "_kf_blink", None) if bias_link and _GELU_LINK else None
+    if (u.is_cuda and u.dtype == torch.bfloat16 and u.is_contiguous() and u.shape[-1] % 8 == 0 and hip_available()
+            and (bl is not None or not bias_link)):
+        return _GeluFn.apply(u, bl)
+    return F.gelu(u)
+

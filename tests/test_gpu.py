@@ -1629,3 +1629,22 @@ def test_bert_layer_bias_link_matches_colsum(p, monkeypatch):
             assert ((a - b).norm() / b.norm()).item() < 1e-2, n
         else:
             assert torch.equal(a, b), n
+
+
+@needs_gpu
+@pytest.mark.parametrize("T,O", [(16384, 3072), (1000, 776), (37, 64)])
+def test_gelu_backward_colsum_matches_torch(T, O):
+    """Fused erf-GELU backward + column sums (norms.hip) vs torch's GELU backward on the same bf16
+    inputs and an f64 column sum of its bf16 result."""
+    from kungfu_amd._lib import hip
+
+    torch.manual_seed(9)
+    u = (torch.randn(T, O, device="cuda") * 2).bfloat16()
+    dy = torch.randn(T, O, device="cuda").bfloat16()
+    du, db = hip().gelu_backward_colsum(dy, u, torch.float32)
+    ref = torch.ops.aten.gelu_backward(dy, u)
+    assert ((du.float() - ref.float()).abs() > 0).float().mean().item() < 1e-3  # same math, ~1-ulp differences
+    assert ((du.float() - ref.float()).norm() / ref.float().norm()).item() < 1e-3
+    torch.testing.assert_close(db.double(), du.double().sum(0), rtol=1e-4, atol=1e-3)
+    _, db16 = hip().gelu_backward_colsum(dy, u, torch.bfloat16)
+    assert db16.dtype == torch.bfloat16 and ((db16.float() - db).abs() <= db.abs() * 8e-3 + 1e-3).all()
