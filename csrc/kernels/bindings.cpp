@@ -671,7 +671,7 @@ std::vector<at::Tensor> gelu_backward_colsum(at::Tensor dy, at::Tensor u, at::Sc
     const int O = static_cast<int>(dy.size(-1));
     const int64_t T = dy.numel() / O;
     auto du = at::empty_like(dy);
-    auto part = at::empty({static_cast<int64_t>(kfk::colsum_chunks(T, O)) * O}, dy.options().dtype(at::kFloat));
+    auto part = at::empty({static_cast<int64_t>(kfk::gelu_colsum_chunks(T, O)) * O}, dy.options().dtype(at::kFloat));
     auto out = at::empty({O}, dy.options().dtype(dtype));
     kfk::launch_gelu_bwd_colsum(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                                 reinterpret_cast<const uint16_t *>(u.data_ptr()), reinterpret_cast<uint16_t *>(du.data_ptr()),

@@ -276,8 +276,22 @@ __global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x
     }
 }
 
-// GELU backward fused with the column sums of its output: du = dy * (Phi(u) + u * phi(u)) (torch's
-// GeluBackward, erf form, f32 math, one bf16 rounding), and per-chunk column partial sums of the
+// gelu'(x) = Phi(x) + x phi(x) with ONE exponential: erf(x / sqrt 2) by Abramowitz-Stegun 7.1.26
+// (|error| < 1.5e-7, far below a bf16 ulp of the result) whose e^{-x^2/2} factor is phi's own.
+// ~12 vector instructions instead of erff + expf (~40): the fused pass below is memory-bound.
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float e = __expf(-0.5f * x * x);  // = e^{-z^2}
+    const float t = __frcp_rn(1.f + 0.3275911f * z);
+    const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f +
+                                                                                            t * 1.061405429f))));
+    const float erf_abs = 1.f - poly * e;
+    const float cdf = 0.5f * (1.f + (x < 0.f ? -erf_abs : erf_abs));
+    return cdf + x * (e * 0.39894228040143268f);
+}
+
+// GELU backward fused with the column sums of its output: du = dy * (Phi(u) + u * phi(u)) (the erf
+// form of torch's GeluBackward, f32 math with gelu_grad_fast, one bf16 rounding), and per-chunk column partial sums of the
 // bf16 du -- the bias gradient of the linear layer that produced u -- with colsum_stage1's layout
 // (fixed 8-column group per thread, 4 row lanes per block, partials [chunk][O]).
 __global__ __launch_bounds__(256) void gelu_bwd_colsum_stage1(const uint4 *__restrict__ dy, const uint4 *__restrict__ u,
@@ -317,10 +331,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_colsum_stage1(const uint4 *__res
                     uint16_t r2[2];
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
-                        const float x = x2[e];
-                        const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-                        const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
-                        r2[e] = f32_to_bf16(d2[e] * (cdf + x * pdf));
+                        r2[e] = f32_to_bf16(d2[e] * gelu_grad_fast(x2[e]));
                         acc[2 * k + e] += bf16_to_f32(r2[e]);
                     }
                     o[k] = static_cast<uint32_t>(r2[0]) | (static_cast<uint32_t>(r2[1]) << 16);
@@ -380,9 +391,18 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
     colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
 }
 
+int gelu_colsum_chunks(int64_t T, int O) {
+    // the erf/exp math makes this pass VALU-heavy: ~8 workgroups per CU (vs colsum's 2), >= 16 rows each
+    const int colblocks = (O / 8 + kColVec - 1) / kColVec;
+    int64_t c = 2048 / colblocks;
+    const int64_t cap = (T + 15) / 16;
+    if (c > cap) c = cap;
+    return static_cast<int>(c < 1 ? 1 : (c > 2048 ? 2048 : c));
+}
+
 void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,
                             float *out_f32, uint16_t *out_bf16, hipStream_t s) {
-    const int OV = O / 8, chunks = colsum_chunks(T, O);
+    const int OV = O / 8, chunks = gelu_colsum_chunks(T, O);
     const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     gelu_bwd_colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(dy), reinterpret_cast<const uint4 *>(u),
