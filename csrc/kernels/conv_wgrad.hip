@@ -33,6 +33,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 namespace kfk {
@@ -98,7 +99,8 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                                                              const uint16_t *__restrict__ x,
                                                              float *__restrict__ part, void *__restrict__ dw,
                                                              const uint16_t *__restrict__ zero, WGeo g,
-                                                             int out_f32, int accumulate, int atomic_out) {
+                                                             int out_f32, int accumulate, int atomic_out,
+                                                             int stagger = 0) {
     constexpr int BM = 64 * WM, BN = 16 * TN * WN, NW = WM * WN, NT = 64 * NW;
     constexpr int PAD = KS > 0 ? (KS - 1) / 2 : 0;
     constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per staged pixel row
@@ -206,11 +208,21 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     for (int p = 0; p < STAGES - 1; ++p)
         if (p < nsteps) stage(p, p);
     int buf = 0;
+    // stagger (KUNGFU_WGRAD_STAGGER): the upper half of the waves (one per SIMD with 8 waves) issues its
+    // LDS-DMA staging before its fragment reads instead of between its two MFMA clusters, so the two
+    // waves sharing a SIMD do not stall on staging issue at the same time
+    const bool early = stagger && NW >= 8 && (wave >> 2) & 1;
     for (int ks = 0; ks < nsteps; ++ks) {
         if (ks + STAGES - 1 <= nsteps) wait_vmcnt<LOADS * (STAGES - 2)>();
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (early && ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *abase = lds + buf * STAGE;
         const uint8_t *bbase = abase + A_BYTES;
@@ -225,7 +237,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         for (int j = 0; j < TN; ++j) bf1[j] = tr_frag(bbase + boff[j] + 32 * ROWB, bbase + boff[j] + 36 * ROWB);
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
-        if (ks + STAGES - 1 < nsteps) {
+        if (!early && ks + STAGES - 1 < nsteps) {
             int nb = buf + STAGES - 1;
             if (nb >= STAGES) nb -= STAGES;
             stage(ks + STAGES - 1, nb);
@@ -835,8 +847,17 @@ void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, cons
     // 2 for the 256x256 tile (64 KB per stage)
     constexpr int STAGE_BYTES = 64 * (64 * WM + 16 * TN * WN) * 2;
     constexpr int STAGES = 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
+    // staggered staging issue (KUNGFU_WGRAD_STAGGER=0/1 forces it off/on): default on for the 256x256
+    // tiles only -- BERT-base's long-K linear weight gradients +1.5 % step time, ResNet-50's 256x128
+    // tiles -0.8 % with it (tools/gpu_r3_envab.sh, same box)
+    static const int env_stagger = [] {
+        const char *e = std::getenv("KUNGFU_WGRAD_STAGGER");
+        return e ? std::atoi(e) : -1;
+    }();
+    const int stagger = env_stagger >= 0 ? env_stagger : (TN == 8 ? 1 : 0);
     wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
-        dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out);
+        dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out,
+        stagger);
     if (g.splits > 1 && !atomic_out) {
         const int64_t total = static_cast<int64_t>(g.tiles) * (64 * WM) * (16 * TN * WN) / 4;
         int sgl = 0;  // split groups: enough blocks for the chip, at most 64 groups, <= splits
