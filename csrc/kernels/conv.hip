@@ -66,6 +66,7 @@ struct Geo {
     int dh, dw;  // scat: the data-gradient image (2OH x 2OW for an even input)
     int ph, pw;  // zero padding (rows, columns)
     int stagger;  // 1: the upper half of 8 waves issues its LDS-DMA staging before its fragment reads
+    int prio;     // 1: the upper (second-dispatched) wave half runs at s_setprio 1
 };
 
 template <int N>
@@ -319,7 +320,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     for (int p = 0; p < STAGES - 1; ++p)
         if (p < ksteps) stage(p, p);
     int buf = 0;
-    const bool early = g.stagger && NW >= 8 && ((wave >> 2) & 1);
+    // g.stagger 1: the upper wave half stages before its fragment reads; 2: after its second MFMA cluster
+    const bool upper = NW >= 8 && ((wave >> 2) & 1);
+    const bool early = g.stagger == 1 && upper, late = g.stagger == 2 && upper;
+    if (g.prio && upper) __builtin_amdgcn_s_setprio(1);
     for (int ks = 0; ks < ksteps; ++ks) {
         // tile ks landed (this wave's loads); later tiles may stay in flight
         if (ks + STAGES - 1 <= ksteps) wait_vmcnt<LOADS * (STAGES - 2)>();
@@ -361,13 +365,19 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
         // next tile's staging (VALU + LDS-DMA issue) between the two MFMA clusters
-        if (!early && ks + STAGES - 1 < ksteps) {
+        if (!early && !late && ks + STAGES - 1 < ksteps) {
             int nb = buf + STAGES - 1;
             if (nb >= STAGES) nb -= STAGES;
             stage(ks + STAGES - 1, nb);  // the buffer read in iteration ks-1
         }
         __builtin_amdgcn_sched_barrier(0);
         mfma_block(af1, bf1);
+        if (late && ks + STAGES - 1 < ksteps) {
+            __builtin_amdgcn_sched_barrier(0);
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
         buf = buf + 1 == STAGES ? 0 : buf + 1;
     }
     wait_vmcnt<0>();
@@ -684,6 +694,15 @@ int conv_stagger() {
     return v;
 }
 
+// KUNGFU_CONV_PRIO=1: static s_setprio 1 for the upper wave half of the 8-wave tiles (A/B)
+int conv_prio() {
+    static const int v = [] {
+        const char *e = std::getenv("KUNGFU_CONV_PRIO");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
 // 256-byte zero page for padding rows (global_load_lds needs a real address).
 const void *zero_page() {
     static void *p = [] {
@@ -811,6 +830,7 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.mtiles = g.ntiles = 0;
     g.wtaps = ks * ks, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.dh = g.dw = 0;
     g.stagger = conv_stagger();
+    g.prio = conv_prio();
     g.ph = g.pw = pad;
     if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
     else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
@@ -890,6 +910,7 @@ void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K
     g.mtiles = g.ntiles = 0;
     g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0, g.dh = g.dw = 0;
     g.stagger = conv_stagger();
+    g.prio = conv_prio();
     if (variant < 0) {
         // enough 256x256 tiles to fill the chip twice, else 256x128, else 128x128 (or 128x64)
         const int64_t t256 = N % 256 ? 0 : ((M + 255) / 256) * (N / 256);
@@ -926,6 +947,7 @@ void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, 
     g.mtiles = g.ntiles = 0;
     g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.dh = g.dw = 0;
     g.stagger = conv_stagger();
+    g.prio = conv_prio();
     g.ph = ph, g.pw = pw;
     if (kh == 1 && kw == 1) {
         launch_ks<1>(x, w, y, g, ea, epi, s, -1);
@@ -998,6 +1020,7 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
     g.wtaps = ks * ks, g.scat = 1;
     g.dh = DH, g.dw = DW;
     g.stagger = conv_stagger();
+    g.prio = conv_prio();
     g.ph = g.pw = 0;
     if (ks == 1) {
         if (DH != 2 * OH || DW != 2 * OW || pad != 0) throw std::invalid_argument("conv_dgrad_s2: 1x1 needs an even input");

@@ -211,7 +211,10 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     // stagger (KUNGFU_WGRAD_STAGGER): the upper half of the waves (one per SIMD with 8 waves) issues its
     // LDS-DMA staging before its fragment reads instead of between its two MFMA clusters, so the two
     // waves sharing a SIMD do not stall on staging issue at the same time
-    const bool early = stagger && NW >= 8 && (wave >> 2) & 1;
+    // stagger 1: stage before the fragment reads; 2: after the second MFMA cluster (upper wave half)
+    const bool upper = NW >= 8 && ((wave >> 2) & 1);
+    const bool early = (stagger & 3) == 1 && upper, late = (stagger & 3) == 2 && upper;
+    if ((stagger & 4) && upper) __builtin_amdgcn_s_setprio(1);  // KUNGFU_WGRAD_STAGGER bit 2: static priority
     for (int ks = 0; ks < nsteps; ++ks) {
         if (ks + STAGES - 1 <= nsteps) wait_vmcnt<LOADS * (STAGES - 2)>();
         else wait_vmcnt<0>();
@@ -237,13 +240,19 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         for (int j = 0; j < TN; ++j) bf1[j] = tr_frag(bbase + boff[j] + 32 * ROWB, bbase + boff[j] + 36 * ROWB);
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
-        if (!early && ks + STAGES - 1 < nsteps) {
+        if (!early && !late && ks + STAGES - 1 < nsteps) {
             int nb = buf + STAGES - 1;
             if (nb >= STAGES) nb -= STAGES;
             stage(ks + STAGES - 1, nb);
         }
         __builtin_amdgcn_sched_barrier(0);
         mfma_block(af1, bf1);
+        if (late && ks + STAGES - 1 < nsteps) {
+            __builtin_amdgcn_sched_barrier(0);
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
         buf = buf + 1 == STAGES ? 0 : buf + 1;
     }
     wait_vmcnt<0>();
