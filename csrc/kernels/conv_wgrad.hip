@@ -330,7 +330,7 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
                                                          const uint16_t *__restrict__ x,
                                                          float *__restrict__ part, void *__restrict__ dw,
                                                          const uint16_t *__restrict__ zero, RGeo g, int out_f32,
-                                                         int accumulate, int atomic_out) {
+                                                         int accumulate, int atomic_out, int stagger = 0) {
     constexpr int ROW = 128;            // 64 channels
     constexpr int MAXP = 4;             // pieces per wave per K-step (9 * 4 >= 8 + 25)
     constexpr int STAGE = (8 + 25 + 1) * 1024;  // dy 8 KB | input image <= 25 KB | dummy 1 KB
@@ -439,11 +439,18 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
     for (int p = 0; p < STAGES - 1; ++p)
         if (p < nsteps) stage(p, p);
     int buf = 0;
+    const bool early = stagger && ((wave >> 2) & 1);  // see wgrad_kernel: staggered staging issue
     for (int ks = 0; ks < nsteps; ++ks) {
         if (ks + STAGES - 1 <= nsteps) wait_vmcnt<MAXP * (STAGES - 2)>();
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (early && ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *base = lds + buf * STAGE;
         bf16x8 af0[4], bf0[4], af1[4], bf1[4];
@@ -459,7 +466,7 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
         }
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
-        if (ks + STAGES - 1 < nsteps) {
+        if (!early && ks + STAGES - 1 < nsteps) {
             int nb = buf + STAGES - 1;
             if (nb >= STAGES) nb -= STAGES;
             stage(ks + STAGES - 1, nb);
@@ -530,7 +537,8 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
                                                                    const uint16_t *__restrict__ x,
                                                                    float *__restrict__ part, void *__restrict__ dw,
                                                                    const uint16_t *__restrict__ zero, RRGeo g,
-                                                                   int out_f32, int accumulate, int atomic_out) {
+                                                                   int out_f32, int accumulate, int atomic_out,
+                                                                   int stagger = 0) {
     constexpr int ROW = 128;                      // 64 channels
     constexpr int MAXP = (8 + 25 + NWV - 1) / NWV;  // 1 KB pieces per wave per K-step
     constexpr int STAGE = (8 + 25 + 1) * 1024;     // dy 8 KB | input image <= 25 KB | dummy 1 KB
@@ -648,11 +656,18 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     for (int p = 0; p < STAGES - 1; ++p)
         if (p < nsteps) stage(p, p);
     int buf = 0;
+    const bool early = stagger && ((wave >> 2) & 1);  // see wgrad_kernel: staggered staging issue
     for (int ks = 0; ks < nsteps; ++ks) {
         if (ks + STAGES - 1 <= nsteps) wait_vmcnt<MAXP * (STAGES - 2)>();
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if ((early || !has_tap) && ks + STAGES - 1 < nsteps) {
+            int nb = buf + STAGES - 1;
+            if (nb >= STAGES) nb -= STAGES;
+            stage(ks + STAGES - 1, nb);
+        }
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *base = lds + buf * STAGE;
         if (has_tap) {  // wave-uniform
@@ -669,17 +684,13 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
             }
             mfma_block(af0, bf0);
             __builtin_amdgcn_sched_barrier(0);
-            if (ks + STAGES - 1 < nsteps) {
+            if (!early && ks + STAGES - 1 < nsteps) {
                 int nb = buf + STAGES - 1;
                 if (nb >= STAGES) nb -= STAGES;
                 stage(ks + STAGES - 1, nb);
             }
             __builtin_amdgcn_sched_barrier(0);
             mfma_block(af1, bf1);
-        } else if (ks + STAGES - 1 < nsteps) {
-            int nb = buf + STAGES - 1;
-            if (nb >= STAGES) nb -= STAGES;
-            stage(ks + STAGES - 1, nb);
         }
         buf = buf + 1 == STAGES ? 0 : buf + 1;
     }
@@ -778,6 +789,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
             }
         }
     }
+}
+
+// Staggered staging issue in the row-image kernels (see wgrad_kernel); KUNGFU_WROWS_STAGGER=0/1 forces it.
+// Default: on for the any-window kernel (Inception-v3 21.62 -> 21.45 ms/step, same-box A/B), off for the
+// ResNet 3x3 one (neutral).
+int rows_stagger(bool rect) {
+    static const int v = [] {
+        const char *e = std::getenv("KUNGFU_WROWS_STAGGER");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v >= 0 ? v : (rect ? 1 : 0);
 }
 
 struct Tile {
@@ -974,7 +996,8 @@ void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *p
         if (!rows_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: rows variant needs 3x3/s1");
         const RGeo rg = make_rgeo(N, H, W, Cin, Cout, plan);
         wgrad_rows_kernel<2><<<rg.mtiles * rg.ntiles * rg.splits, 576, 0, s>>>(
-            dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), rg, out_f32, accumulate, atomic_out);
+            dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), rg, out_f32, accumulate, atomic_out,
+            rows_stagger(false));
         if (rg.splits > 1 && !atomic_out) {
             WGeo g{};
             g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = 9, g.tiles = rg.tiles;
@@ -1107,9 +1130,11 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
         const int grid = rg.mtiles * rg.ntiles * rg.tgroups * rg.splits;
         const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
         if (rg.taps % 7 == 0)
-            wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out);
+            wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
+                                                               rows_stagger(false));
         else
-            wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out);
+            wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
+                                                               rows_stagger(false));
         if (rg.splits > 1 && !atomic_out) {
             WGeo g{};
             g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = rg.taps, g.tiles = rg.tiles;
