@@ -1131,10 +1131,10 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
         const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
         if (rg.taps % 7 == 0)
             wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
-                                                               rows_stagger(false));
+                                                               rows_stagger(true));
         else
             wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
-                                                               rows_stagger(false));
+                                                               rows_stagger(true));
         if (rg.splits > 1 && !atomic_out) {
             WGeo g{};
             g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = rg.taps, g.tiles = rg.tiles;
