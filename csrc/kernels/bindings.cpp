@@ -582,7 +582,7 @@ at::Tensor conv_dgrad_s2(at::Tensor dy, at::Tensor wt, int64_t ks, c10::optional
 // (memory [Cout][ks][ks][Cin]).  out: bf16 or f32 destination of that shape/layout (written,
 // or added to with accumulate); otherwise a new bf16 tensor.  variant / splits: -1 = planner.
 at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c10::optional<at::Tensor> out,
-                      bool accumulate, int64_t variant, int64_t splits) {
+                      bool accumulate, int64_t variant, int64_t splits, bool atomics) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_wgrad: x must be a 4-D channels_last bf16 GPU tensor");
@@ -620,7 +620,7 @@ at::Tensor conv_wgrad(at::Tensor dy, at::Tensor x, int64_t ks, int64_t stride, c
                            reinterpret_cast<const uint16_t *>(x.data_ptr()), dw.data_ptr(),
                            plan.ws_floats > 0 ? ws.data_ptr<float>() : nullptr, N, H, W, C, K, static_cast<int>(ks),
                            static_cast<int>(stride), plan, dw.scalar_type() == at::kFloat, accumulate,
-                           stream_of(x, 0));
+                           stream_of(x, 0), atomics);
     return dw;
 }
 
@@ -1678,7 +1678,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           "covers this stride-1 window (args: N, H, W, Cin, Cout, kh, kw, ph, pw, stride)");
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",
           py::arg("dy"), py::arg("x"), py::arg("ks"), py::arg("stride") = 1, py::arg("out") = py::none(),
-          py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1);
+          py::arg("accumulate") = false, py::arg("variant") = -1, py::arg("splits") = -1,
+          py::arg("atomics") = true);
     m.def("conv_wgrad_supported", &kfk::conv_wgrad_supported);
     m.def("bias_act_supported", &kfk::bias_act_supported);
     m.def("maxpool2x2_forward", &maxpool2x2_forward, "2x2/s2 max-pool, NHWC bf16 (no argmax tensor)");

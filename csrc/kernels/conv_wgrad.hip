@@ -988,9 +988,10 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
 
 void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W, int Cin,
                        int Cout, int ks, int stride, const WgradPlan &plan, bool out_f32, bool accumulate,
-                       hipStream_t s) {
-    // split-K accumulating into an f32 destination: every split adds its tile with atomics
-    const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
+                       hipStream_t s, bool atomics) {
+    // split-K accumulating into an f32 destination: every split adds its tile with atomics (unless
+    // `atomics` is off: then partial tiles + the deterministic reduce, which adds into dw)
+    const bool atomic_out = atomics && out_f32 && accumulate && plan.splits > 1;
     if (!conv_wgrad_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: unsupported shape");
     if (plan.variant == kRowsVariant) {
         if (!rows_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: rows variant needs 3x3/s1");

@@ -218,7 +218,7 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
                           int splits = -1);
 void launch_conv_wgrad(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W, int Cin,
                        int Cout, int ks, int stride, const WgradPlan &plan, bool out_f32, bool accumulate,
-                       hipStream_t s);
+                       hipStream_t s, bool atomics = true);
 // Any KH x KW window with zero padding (ph, pw), stride 1|2, Cin / Cout multiples of 8
 // (Inception-v3's windows and channel counts): same kernel, runtime window, zero-padded tiles.
 bool conv_wgrad_rect_supported(int Cin, int Cout, int kh, int kw, int stride);

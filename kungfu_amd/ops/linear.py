@@ -40,10 +40,14 @@ class BiasLink:
         self.dtype, self.value, self.ptr = dtype, None, 0
 
 
+_DIRECT_WGRAD = os.environ.get("KUNGFU_LINEAR_DIRECT_WGRAD", "1") != "0"
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, target=None):
         ctx.save_for_backward(x, w)
+        ctx.target = target
         ctx.has_b = b is not None
         ctx.b_dtype = b.dtype if b is not None else None
         ctx.blink = BiasLink(b.dtype) if b is not None and b.dtype in (torch.bfloat16, torch.float32) else None
@@ -62,7 +66,16 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy2, w).view(x.shape)
-        if ctx.needs_input_grad[1]:
+        tgt = ctx.target
+        if ctx.needs_input_grad[1] and tgt is not None and _DIRECT_WGRAD and hasattr(tgt[0].sink, "put_direct"):
+            # the split-K partials are reduced straight into the weight's flat f32 gradient slot
+            # (deterministic, accumulating): no bf16 weight gradient, no landing pass
+            space, i = tgt
+            gv = space.grad_view(i)
+            hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1, out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
+                             accumulate=True, atomics=False)
+            space.sink.put_direct(i)
+        elif ctx.needs_input_grad[1]:
             dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
         bl = ctx.blink
         if bl is not None and bl.value is not None and bl.ptr == dy2.data_ptr() and ctx.needs_input_grad[2]:
@@ -75,7 +88,7 @@ class _LinearFn(torch.autograd.Function):
                 db = hip().colsum(dy2, ctx.b_dtype)
             else:
                 db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -87,10 +100,12 @@ def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
     return hip_available() and hip().conv_wgrad_supported(int(in_f), int(out_f), 1, 1)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None) -> torch.Tensor:
-    """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible."""
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target=None) -> torch.Tensor:
+    """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible.  ``grad_target``
+    ``(space, index)``: ``w`` is the bf16 shadow of that flat-space parameter -- its gradient is
+    reduced straight into the parameter's f32 gradient slot (``space.sink.put_direct``)."""
     if eligible(x, w) and (b is None or b.dtype in (torch.bfloat16, torch.float32)):
-        y = _LinearFn.apply(x, w, b)
+        y = _LinearFn.apply(x, w, b, grad_target)
         if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
             y._kf_blink = y.grad_fn.blink
         return y

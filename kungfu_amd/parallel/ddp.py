@@ -346,6 +346,15 @@ class GradReducer:
         if self._enabled:
             self._mark(i)
 
+    def put_direct(self, i: int):
+        """Sink for a direct gradient its producer already added into parameter ``i``'s flat f32
+        slot on the compute stream (ops/linear.py's split-K reduce): only the bucket accounting."""
+        b = self.param_bucket[i]
+        if self._enabled and b.launched:
+            self._late(i)  # (already added: with one peer nothing else to do)
+        if self._enabled:
+            self._mark(i)
+
     def _late(self, i: int):
         if self.skip:  # no collective in flight: the late gradient simply accumulates
             return

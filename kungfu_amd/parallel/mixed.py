@@ -97,8 +97,11 @@ def _conv_forward(self, x):
 def _linear_forward(self, x):
     from ..ops.linear import linear
 
-    # bf16 shadow weights: the weight gradient takes the split-K MFMA kernel (ops/linear.py)
-    return linear(x, shadow(self.weight), shadow(self.bias) if self.bias is not None else None)
+    # bf16 shadow weights: the weight gradient takes the split-K MFMA kernel (ops/linear.py), which
+    # reduces its splits straight into the weight's flat f32 gradient slot
+    w = shadow(self.weight)
+    return linear(x, w, shadow(self.bias) if self.bias is not None else None,
+                  grad_target=direct_target(self.weight) if w is not self.weight else None)
 
 
 class SideStream:
@@ -160,6 +163,10 @@ class ImmediateSink:
         SideStream.join()
         with torch.no_grad():
             self.space.grad_view(i).add_(g)
+
+    def put_direct(self, i: int) -> None:
+        """Parameter ``i``'s gradient was already added into its flat f32 slot by its producer
+        (on the current stream): nothing to land."""
 
 
 class BatchedSink(ImmediateSink):
