@@ -791,15 +791,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
     }
 }
 
-// Staggered staging issue in the row-image kernels (see wgrad_kernel); KUNGFU_WROWS_STAGGER=0/1 forces it.
-// Default: on for the any-window kernel (Inception-v3 21.62 -> 21.45 ms/step, same-box A/B), off for the
-// ResNet 3x3 one (neutral).
-int rows_stagger(bool rect) {
+// Staggered staging issue in the row-image kernels (see wgrad_kernel), default on (same-box A/Bs:
+// Inception-v3 21.62 -> 21.45 ms/step, VGG-16 34.85 -> 34.62, ResNet-50 neutral);
+// KUNGFU_WROWS_STAGGER=0 turns it off.
+int rows_stagger(bool /*rect*/) {
     static const int v = [] {
         const char *e = std::getenv("KUNGFU_WROWS_STAGGER");
-        return e ? std::atoi(e) : -1;
+        return e ? std::atoi(e) : 1;
     }();
-    return v >= 0 ? v : (rect ? 1 : 0);
+    return v;
 }
 
 struct Tile {
