@@ -682,6 +682,15 @@ bool conv_supported(int Cin, int Cout, int ks, int stride) {
     return (ks == 1 || ks == 3) && conv3x3_supported(Cin, Cout, stride);
 }
 
+// KUNGFU_CONV_TILE_RULES: 1 (default) = the round-2 tile defaults, 2 = the round-3 re-measured ones
+int conv_tile_rules() {
+    static const int v = [] {
+        const char *e = std::getenv("KUNGFU_CONV_TILE_RULES");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 // Staggered staging issue in the 8-wave tiles: the two waves sharing a SIMD issue their LDS-DMA
 // pieces in different phases of the K-step (one before its fragment reads, one between its MFMA
 // clusters) instead of stalling on staging issue together.  ResNet-50 +0.8 % (21.43-21.49 ->
@@ -792,6 +801,14 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     if (variant < 0) {
         const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);  // (K % 256 == 0 only)
         variant = g.K <= 32 ? 11 : g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
+        if (conv_tile_rules() >= 2 && g.K % 128 == 0 && g.K > 32) {
+            // re-measured with the staggered staging (tools/bench_conv1x1_variants.py, profiles/r3_conv_variants.txt):
+            // the accumulating data gradients (ResNet's conv1 dgrad into the residual gradient) run best on
+            // 128x128 / 4 waves at every ResNet size (64->256@56 303 -> 290 us, 128->512@28 174 -> 156,
+            // 256->1024@14 90 -> 82, 512->2048@7 60 -> 57), and so do the stride-1 3x3 ones with 128 or
+            // 512 outputs that are not on 256x256 tiles (128->128@28 101 -> 88, 512->512@7 76 -> 71)
+            if ((epi & kEpiAccum) != 0 || (KS == 3 && g.stride == 1 && variant != 7)) variant = 0;
+        }
     }
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
