@@ -51,10 +51,13 @@ for shp in SHAPES:
     out = cl(torch.randn(N, K, OH, OH, device="cuda")).bfloat16()
     bx = torch.empty_like(out)
     mask = torch.zeros(out.numel() // 8, dtype=torch.uint8, device="cuda")
+    fc = torch.cat([torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.2])
     modes = {"st": (lambda v: H_.conv(x, w, s, st, None, v), 0),
              "": (lambda v: H_.conv(x, w, s, None, None, v), 0),
              # dgrad-style: accumulate into `out` + BN-backward sums over bx and the ReLU mask
-             "ab": (lambda v: H_.conv(x, w, s, st, out, v, bn_x=bx, bn_mask=mask), 4.0 * M * K)}
+             "ab": (lambda v: H_.conv(x, w, s, st, out, v, bn_x=bx, bn_mask=mask), 4.0 * M * K),
+             # dgrad-style without accumulation: BN-backward sums over bx with the forward coefficients
+             "bc": (lambda v: H_.conv(x, w, s, st, None, v, bn_x=bx, bn_fcoef=fc), 2.0 * M * K)}
     for v in VARIANTS:
         for tag in MODES:
             f, extra = modes[tag]
