@@ -1,6 +1,7 @@
 """GPU tests of the S-SGD engine's data plane: the RCCL path exercised
 with one rank (``force_comm``), bf16 gradients on the wire, and elastic resize of the
 GPU optimizers (2 ranks sharing the GPU over the host-staged plane)."""
+import math
 import re
 
 import pytest
@@ -235,18 +236,25 @@ def test_resnet50_full_size_engine_matches_stock():
     stock trajectory through the deterministic phase and stay within the stock spread after.
     lr 0.01: both memorise the batch (7.16 -> 4.19) and agree within 2 % at every step.
     Measured on MI355X (r2): lr 0.1 stock 7.16/5.03/6.54/8.58/10.53/11.28, engine
-    7.17/5.04/6.63/8.82/10.61/10.79; lr 0.01 stock .../4.79/4.40/4.19, engine .../4.80/4.42/4.19."""
+    7.17/5.04/6.63/8.82/10.61/10.79; lr 0.01 stock .../4.79/4.40/4.19, engine .../4.80/4.42/4.19.
+
+    Chaotic phase (steps 5-9): the bound is against the whole window's stock envelope, not
+    step-by-step, because the peaks move in time from run to run.  r3 measured, from identical
+    seeds: stock 11.49/20.64/22.32/17.09 vs 6.76/6.54/8.45/11.59 (steps 6-9, same process), and
+    the engine under two tile-size choices for the same convolutions (default vs
+    KUNGFU_CONV_TILE_RULES=1) 14.07/17.47/16.99/11.23 vs 13.89/18.56/24.17/27.78."""
     a = _resnet50_trajectory(False)
     b = _resnet50_trajectory(False)
     e = _resnet50_trajectory(True)
     print("lr0.1 stock", a, "\nlr0.1 stock", b, "\nlr0.1 engine", e)
     assert abs(e[0] - a[0]) < 0.01 * a[0], (a, e)  # same initial model and data
+    lo, hi = min(a[5:] + b[5:]), max(a[5:] + b[5:])
     for i, (x0, x1, xe) in enumerate(zip(a, b, e)):
         if i < 5:  # the deterministic phase: within 5 % (measured <= 2.3 %; step 5 is already
             # chaotic: r3 measured engine 11.37 vs stock 10.28 / 10.44)
             assert abs(xe - x0) <= max(3 * abs(x0 - x1), 0.05 * abs(x0) + 0.05), (i, a, b, e)
-        else:  # chaotic phase: stock runs themselves differ by up to 2x (5.99 .. 16.97 seen)
-            assert 0.4 * min(x0, x1) <= xe <= 2.5 * max(x0, x1), (i, a, b, e)
+        else:  # chaotic phase: finite and within the stock window's envelope (x0.4 .. x3)
+            assert math.isfinite(xe) and 0.4 * lo <= xe <= 3.0 * hi, (i, a, b, e)
     a = _resnet50_trajectory(False, lr=0.01)
     e = _resnet50_trajectory(True, lr=0.01)
     print("lr0.01 stock", a, "\nlr0.01 engine", e)
