@@ -281,29 +281,38 @@ __global__ __launch_bounds__(kBlock) void bn_stats_finalize(const float *partial
 // Same outputs from f64 per-channel sums produced by a convolution epilogue
 // (conv.hip, EPI bit 0): kStatSlots slots of [sum x (C), sum x^2 (C)]; the sums are
 // re-zeroed for the next producer (self-cleaning workspace, no memset launch).
-__global__ void bn_sums_finalize(double *sums, int C, int64_t rows, const float *gamma, const float *beta,
-                                 float *mean, float *invstd, float *run_mean, float *run_var, float momentum,
-                                 float eps, float *coef, int64_t *num_batches) {
+__global__ __launch_bounds__(256) void bn_sums_finalize(double *__restrict__ sums, int C, int64_t rows,
+                                                        const float *__restrict__ gamma,
+                                                        const float *__restrict__ beta, float *mean, float *invstd,
+                                                        float *run_mean, float *run_var, float momentum, float eps,
+                                                        float *coef, int64_t *num_batches) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (num_batches && c == 0) num_batches[0] += 1;
     if (c >= C) return;
-    // every slot load issued before the zeroing stores (the compiler cannot prove the stores do
-    // not alias later loads, so an interleaved loop serialises 32 load latencies)
+    // every input issued before any store: the slot sums and the channel's parameters / running
+    // stats (loaded behind the zeroing and output stores, each was a serial round trip: 5.7 us)
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float rm = run_mean ? run_mean[c] : 0.f, rv = run_mean ? run_var[c] : 0.f;
+    const double *sp = sums + c;
     double vs[kStatSlots], vq[kStatSlots];
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
-        vs[k] = sums[k * 2 * C + c];
-        vq[k] = sums[k * 2 * C + C + c];
+        vs[k] = sp[k * 2 * C];
+        vq[k] = sp[k * 2 * C + C];
     }
     double s = 0, q = 0;
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
         s += vs[k];
         q += vq[k];
-        sums[k * 2 * C + c] = 0.0;
-        sums[k * 2 * C + C + c] = 0.0;
     }
-    bn_fin_fwd_channel(c, C, s, q, rows, gamma, beta, mean, invstd, run_mean, run_var, momentum, eps, coef);
+    double *zp = sums + c;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        zp[k * 2 * C] = 0.0;
+        zp[k * 2 * C + C] = 0.0;
+    }
+    bn_fin_fwd_channel(c, C, s, q, rows, g, b, rm, rv, mean, invstd, run_mean, run_var, momentum, eps, coef);
 }
 
 // Eval mode: coefficients from running stats.
@@ -716,25 +725,34 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize(const float *partial, 
 
 // Same coefficients from the f64 slotted sums of a data-gradient conv epilogue
 // (conv.hip kEpiBwd*): sum dz, sum dz*x; the slots are re-zeroed.
-__global__ void bn_bwd_finalize_sums(double *sums, int C, int64_t rows, const float *gamma, const float *mean,
-                                     const float *invstd, float *dgamma, float *dbeta, float *coef, bool training) {
+__global__ __launch_bounds__(256) void bn_bwd_finalize_sums(double *__restrict__ sums, int C, int64_t rows,
+                                                            const float *__restrict__ gamma,
+                                                            const float *__restrict__ mean,
+                                                            const float *__restrict__ invstd, float *dgamma,
+                                                            float *dbeta, float *coef, bool training) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
+    const float g = gamma ? gamma[c] : 1.f, mu = mean[c], is = invstd[c];  // issued with the slot loads
+    const double *sp = sums + c;
     double v0[kStatSlots], v1[kStatSlots];
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
-        v0[k] = sums[k * 2 * C + c];
-        v1[k] = sums[k * 2 * C + C + c];
+        v0[k] = sp[k * 2 * C];
+        v1[k] = sp[k * 2 * C + C];
     }
     double s0 = 0, s1 = 0;
 #pragma unroll
     for (int k = 0; k < kStatSlots; ++k) {
         s0 += v0[k];
         s1 += v1[k];
-        sums[k * 2 * C + c] = 0.0;
-        sums[k * 2 * C + C + c] = 0.0;
     }
-    bn_fin_bwd_channel(c, C, s0, s1, rows, gamma, mean, invstd, dgamma, dbeta, coef, training);
+    double *zp = sums + c;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        zp[k * 2 * C] = 0.0;
+        zp[k * 2 * C + C] = 0.0;
+    }
+    bn_fin_bwd_channel(c, C, s0, s1, rows, g, mu, is, dgamma, dbeta, coef, training);
 }
 
 // ---------------------------------------------------------------- backward apply

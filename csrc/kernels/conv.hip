@@ -129,10 +129,10 @@ __device__ __forceinline__ void bn_finalize_last(const BNFin *__restrict__ fp, d
             }
             const int c = c0 + cc;
             if (fp->mode == 1)
-                bn_fin_fwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
+                bn_fin_fwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
                                    fp->run_var, fp->momentum, fp->eps, fp->coef);
             else
-                bn_fin_bwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta,
+                bn_fin_bwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta,
                                    fp->coef, fp->training != 0);
         }
         __syncthreads();
@@ -162,10 +162,10 @@ __global__ void bn_fin_desc_kernel(const BNFin *__restrict__ fp, double *sums, i
     }
     if (fp->mode == 1) {
         if (c == 0 && fp->num_batches) fp->num_batches[0] += 1;
-        bn_fin_fwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
+        bn_fin_fwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
                            fp->run_var, fp->momentum, fp->eps, fp->coef);
     } else {
-        bn_fin_bwd_channel(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta, fp->coef,
+        bn_fin_bwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta, fp->coef,
                            fp->training != 0);
     }
 }
