@@ -74,6 +74,18 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Buffer-resource LDS-DMA staging in conv_kernel (KUNGFU_CONV_BUFLD): num_records = 2 GiB, so
+// the out-of-range offset kBufOOB returns zeros; dword 3 = the CDNA raw-buffer format word.
+#ifndef KUNGFU_CONV_BUFLD
+#define KUNGFU_CONV_BUFLD 1
+#endif
+constexpr uint32_t kBufOOB = 0x80000000u;
+constexpr int kBufFlags = 0x00020000;
+
+__device__ __forceinline__ __attribute__((address_space(3))) void *lds_ptr(uint8_t *p) {
+    return (__attribute__((address_space(3))) void *)(p);
+}
+
 // In-launch BN finalize (kernels.hpp BNFin): called by every workgroup after its slot atomics.
 // Completion-ordered hand-off (MI355X_MICROARCH.md, inter-workgroup visibility: "the workgroup whose
 // add came last, told by the value its add returned", sc1 loads of the handed-off words): each wave
@@ -278,6 +290,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     const int csteps = (g.C + kBK - 1) / kBK;
     const int ksteps = TAPS * csteps;
 
+#if KUNGFU_CONV_BUFLD
+    // LDS-DMA through buffer resources: 32-bit byte offsets, out-of-range lanes (padding taps,
+    // channel chunks past Cin, B rows past Cout) get offset kBufOOB >= num_records and read
+    // zeros -- no 64-bit per-lane addresses, no zero-page select (the launcher checks that x and
+    // w are below 2 GiB).
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kBufOOB), kBufFlags);
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(w), 0, static_cast<int>(kBufOOB), kBufFlags);
+#endif
     auto stage = [&](int ks, int buf) {
         const int tap = ks / csteps, cc = ks - tap * csteps;
         const int kh = tap / KW, kw = tap - kh * KW;
@@ -289,14 +311,26 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll
         for (int j = 0; j < A_INST; ++j) {
             const bool ok = ((a_ok[j] >> tap) & 1u) && cin_ok;
+#if KUNGFU_CONV_BUFLD
+            const uint32_t vo = ok ? static_cast<uint32_t>(a_off[j] + toff) * 2u : kBufOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(abase + (wave * A_INST + j) * 1024), 16, vo, 0, 0,
+                                                     0);
+#else
             const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
             __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
             const bool ok = ((b_ok >> j) & 1u) && cin_ok;
+#if KUNGFU_CONV_BUFLD
+            const uint32_t vo = ok ? static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK) * 2u : kBufOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, lds_ptr(bbase + (wave * B_INST + j) * 1024), 16, vo, 0, 0,
+                                                     0);
+#else
             const uint16_t *src = ok ? w + static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK) : zero;
             __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
+#endif
         }
     };
 
@@ -724,10 +758,18 @@ const void *zero_page() {
     return p;
 }
 
+// Buffer-resource staging addresses x and w with 32-bit byte offsets below kBufOOB.
+void check_buf_extent(const Geo &g) {
+    if (KUNGFU_CONV_BUFLD && (static_cast<int64_t>(g.N) * g.H * g.W * g.C * 2 >= kBufOOB ||
+                              static_cast<int64_t>(g.K) * (g.wtaps > 0 ? g.wtaps : 1) * g.C * 2 >= kBufOOB))
+        throw std::invalid_argument("conv: input or weight of 2 GiB or more (buffer-resource staging)");
+}
+
 template <int KS, int WM, int WN, int ST, int EPI, int TM = 4, int TN = 4>
 void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
     constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
     if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv: Cin and Cout must be multiples of 8");
+    check_buf_extent(g);
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = (g.K + BN - 1) / BN;
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
@@ -900,6 +942,7 @@ void launch_gemm_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, con
     if (g.K % BN) throw std::invalid_argument("gemm: out-features not a multiple of the tile");
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = g.K / BN;
+    check_buf_extent(g);
     const dim3 grid(g.mtiles * g.ntiles), block(64 * WM * WN);
     const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
     switch (epi) {
@@ -993,6 +1036,7 @@ void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g,
     g.mtiles = (g.M + BM - 1) / BM;
     g.ntiles = (g.K + BN - 1) / BN;  // a partial last N tile reads zero B rows, stores its valid columns
     const int grid = g.mtiles * g.ntiles;
+    check_buf_extent(g);
     const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
     EpiArgs e2 = ea;
     e2.fin = nullptr;  // one tile per workgroup: the finalize runs as a launch of its own
