@@ -66,6 +66,18 @@ struct WGeo {
 #endif
 constexpr int kWgradAux = KUNGFU_WGRAD_AUX;
 
+// Buffer-resource staging of wgrad_kernel's operands (num_records = 2 GiB; offset kWBufOOB
+// reads zeros).
+#ifndef KUNGFU_WGRAD_BUFLD
+#define KUNGFU_WGRAD_BUFLD 0
+#endif
+constexpr uint32_t kWBufOOB = 0x80000000u;
+constexpr int kWBufFlags = 0x00020000;
+
+__device__ __forceinline__ __attribute__((address_space(3))) void *wlds_ptr(uint8_t *p) {
+    return (__attribute__((address_space(3))) void *)(p);
+}
+
 __device__ __forceinline__ int fdiv(int p, uint64_t m) {
     return static_cast<int>((static_cast<uint64_t>(static_cast<uint32_t>(p)) * m) >> 40);
 }
@@ -149,6 +161,15 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         b_col[j] = n0 + lc * 8;
     }
 
+#if KUNGFU_WGRAD_BUFLD
+    // LDS-DMA through buffer resources (as conv.hip KUNGFU_CONV_BUFLD): 32-bit byte offsets, an
+    // out-of-range lane (pixel past P, channel past Cout / Cin, padding tap) reads zeros past
+    // num_records; the launcher checks that dy and x are below 2 GiB
+    const __amdgpu_buffer_rsrc_t dyr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(dy), 0, static_cast<int>(kWBufOOB), kWBufFlags);
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kWBufOOB), kWBufFlags);
+#endif
     auto stage = [&](int ks, int buf) {
         const int p0 = p_begin + ks * kBK;
         uint8_t *abase = lds + buf * STAGE;
@@ -156,15 +177,21 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int j = 0; j < A_INST; ++j) {
             const int p = p0 + a_row[j];
+#if KUNGFU_WGRAD_BUFLD
+            const uint32_t vo = p < g.P && a_col[j] < g.K ? static_cast<uint32_t>(p * g.K + a_col[j]) * 2u : kWBufOOB;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, wlds_ptr(abase + (wave * A_INST + j) * 1024), 16, vo, 0, 0,
+                                                     kWgradAux);
+#else
             const uint16_t *src = p < g.P && a_col[j] < g.K ? dy + static_cast<uint32_t>(p * g.K + a_col[j]) : zero;
             __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, kWgradAux);
+#endif
         }
 #pragma unroll
         for (int j = 0; j < B_INST; ++j) {
             const int p = p0 + b_row[j];
-            const uint16_t *src = zero;
+            uint32_t eo = 0xFFFFFFFFu;  // element offset into x, or out of range
             if constexpr (IDENT) {
-                if (p < g.P && b_col[j] < g.C) src = x + static_cast<uint32_t>(p * g.C + b_col[j]);
+                if (p < g.P && b_col[j] < g.C) eo = static_cast<uint32_t>(p * g.C + b_col[j]);
             } else {
                 const int n = fdiv(p, g.m_hw);
                 const int r = p - n * g.HW;
@@ -173,9 +200,15 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
                 const int ih = oh * S + kh - pad_h, iw = ow * S + kw - pad_w;
                 if (p < g.P && b_col[j] < g.C && static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
                     static_cast<unsigned>(iw) < static_cast<unsigned>(g.W))
-                    src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
+                    eo = static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + b_col[j]);
             }
+#if KUNGFU_WGRAD_BUFLD
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, wlds_ptr(bbase + (wave * B_INST + j) * 1024), 16,
+                                                     eo == 0xFFFFFFFFu ? kWBufOOB : eo * 2u, 0, 0, kWgradAux);
+#else
+            const uint16_t *src = eo == 0xFFFFFFFFu ? zero : x + eo;
             __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, kWgradAux);
+#endif
         }
     };
 
@@ -886,6 +919,9 @@ void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, cons
         return e ? std::atoi(e) : -1;
     }();
     const int stagger = env_stagger >= 0 ? env_stagger : (TN == 8 ? 1 : 0);
+    if (KUNGFU_WGRAD_BUFLD && (static_cast<int64_t>(g.P) * g.K * 2 >= kWBufOOB ||
+                               static_cast<int64_t>(g.N) * g.H * g.W * g.C * 2 >= kWBufOOB))
+        throw std::invalid_argument("conv_wgrad: dy or x of 2 GiB or more (buffer-resource staging)");
     wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
         dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out,
         stagger);
