@@ -254,6 +254,15 @@ def main():
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
     p.add_argument("--image-size", type=int, default=224)
+    p.add_argument("--preflight", type=int, default=1,
+                   help="N > 1: check P2P access, a 64 MiB RCCL all-reduce (values + busbw) and a HIP-IPC pull "
+                        "from the neighbouring device before warm-up; exit 5 naming the failing rank pair")
+    p.add_argument("--emulate-comm", type=int, default=0, metavar="RANKS",
+                   help="N = 1 only: replace every bucket all-reduce by comm_emu.hip, the local footprint (CTAs, "
+                        "HBM traffic, modelled xGMI time) of a RANKS-rank ring all-reduce -- a MODEL of the N-rank step")
+    p.add_argument("--emulate-ctas", type=int, default=16, help="--emulate-comm: workgroups per all-reduce")
+    p.add_argument("--emulate-busbw", type=float, default=350.0, help="--emulate-comm: modelled ring busbw, GB/s")
+    p.add_argument("--emulate-lat-us", type=float, default=25.0, help="--emulate-comm: modelled per-collective latency")
     p.add_argument("--elastic", default=None, metavar="SIZE:STEPS,...",
                    help="elastic run (config 5): resize the job along this schedule, e.g. 4:20,8:20 "
                         "(self-launches kungfu-run -w with its built-in config server)")
@@ -269,6 +278,13 @@ def main():
     if a.adam < 0:
         a.adam = 1 if bert else 0
     _setup_env()
+    if a.emulate_comm:
+        if a.gpus not in (None, 1) or world_env not in (None, 1) or a.device != "cuda":
+            print("bench.py: --emulate-comm models an N-rank job on ONE GPU", file=sys.stderr, flush=True)
+            sys.exit(2)
+        a.force_comm = 1
+        os.environ["KUNGFU_COMM_EMULATE"] = "ranks=%d,ctas=%d,busbw=%g,lat_us=%g" % (
+            a.emulate_comm, a.emulate_ctas, a.emulate_busbw, a.emulate_lat_us)
 
     import torch
     import torch.nn.functional as F
@@ -372,6 +388,20 @@ def main():
     if a.elastic:
         return _elastic_loop(a, model, opt, step, sync, bert)
 
+    preflight = None
+    if size > 1 and a.preflight:
+        # before warm-up: a broken link / IPC path is named here instead of hanging a step
+        from kungfu_amd.parallel import preflight as pf
+
+        try:
+            preflight = pf.run(dev)
+        except pf.PreflightError as e:
+            print("bench.py: rank %d: %s" % (rank, e), file=sys.stderr, flush=True)
+            if rank == 0:
+                print("bench.py: pre-flight report: %s" % json.dumps(e.report), file=sys.stderr, flush=True)
+            kf.finalize()
+            sys.exit(5)
+
     t_w0 = time.time()
     first_loss = None
     for i in range(a.warmup):
@@ -431,12 +461,18 @@ def main():
                            "max": round(a.batch * a.steps / min(dt_all), 2)},
         "replicas_consistent": consistent,
         "replica_checksum": [float(x) for x in cks[0].tolist()],
-        "rccl_watchdog": ({"ops_watched": wd["registered"], "pending": wd["pending"], "timeout_s": wd["timeout_s"]}
-                          if wd else None),
+        "rccl_watchdog": ({"ops_watched": wd["registered"], "pending": wd["pending"], "timeout_s": wd["timeout_s"],
+                           "abort_on_stall": wd.get("abort_on_stall")} if wd else None),
+        "rccl_ctas": list(getattr(getattr(reducer, "comm", None), "ctas", (0, 0)) or (0, 0)),
+        "preflight": preflight if preflight is not None else ("skipped (one rank)" if size == 1 else "disabled"),
     }
     if sync_algo and not consistent:
         print("bench.py: REPLICAS DIVERGED: per-rank checksums %s" % cks.tolist(), file=sys.stderr, flush=True)
     metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
+    if a.emulate_comm:  # a model, never the headline: say so in the metric itself
+        metric = "MODEL (1 GPU, %d-rank comm emulated): %s" % (a.emulate_comm, metric)
+        base_per_gpu = None
+        comm_info["emulated"] = reducer.comm.describe() if reducer is not None and reducer.comm is not None else None
     unit = "sequences/sec (aggregate over n_gpus)" if bert else "images/sec (aggregate over n_gpus)"
     res = {
         "metric": metric,

@@ -1493,15 +1493,84 @@ at::Tensor ipc_open(py::bytes handle, int64_t numel, int64_t device) {
     return torch::from_blob(p, {numel}, [](void *q) { (void)hipIpcCloseMemHandle(q); }, opts);
 }
 
+// gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
+at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> out,
+                   bool accumulate, int64_t bn) {
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
+                "gemm_nt: bf16 GPU tensors");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+                "gemm_nt: a [M, K], b [N, K] contiguous");
+    const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+    TORCH_CHECK(kfk::gemm_nt_supported(M, N, K), "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K);
+    int epi = 0;
+    const uint16_t *bp = nullptr;
+    if (bias && bias->defined()) {
+        TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N &&
+                        bias->is_contiguous(),
+                    "gemm_nt: bias bf16 [N]");
+        bp = reinterpret_cast<const uint16_t *>(bias->data_ptr());
+        epi |= kfk::kGemmBias;
+    }
+    at::Tensor c;
+    if (out && out->defined()) {
+        c = *out;
+        TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kBFloat16 && c.is_contiguous() && c.numel() == M * N,
+                    "gemm_nt: out bf16 [M, N] contiguous");
+        if (accumulate) epi |= kfk::kGemmAccum;
+    } else {
+        TORCH_CHECK(!accumulate, "gemm_nt: accumulate needs out");
+        c = at::empty({M, N}, a.options());
+    }
+    c10::DeviceGuard gd(a.device());
+    kfk::launch_gemm_nt(reinterpret_cast<const uint16_t *>(a.data_ptr()), reinterpret_cast<const uint16_t *>(b.data_ptr()),
+                        reinterpret_cast<uint16_t *>(c.data_ptr()), bp, static_cast<int>(M), static_cast<int>(N),
+                        static_cast<int>(K), epi, static_cast<int>(bn), c10::hip::getCurrentHIPStream().stream());
+    return c;
+}
+
+// Collective-interference emulator (comm_emu.hip): stands in for one all-reduce of `bucket`.
+void comm_emulate(at::Tensor bucket, at::Tensor scratch, int64_t traffic_bytes, int64_t ctas, double seconds,
+                  int64_t stream) {
+    check_gpu(bucket, "bucket");
+    check_gpu(scratch, "scratch");
+    const int64_t bytes = bucket.numel() * bucket.element_size();
+    TORCH_CHECK(scratch.numel() * scratch.element_size() >= bytes, "comm_emulate: scratch smaller than the bucket");
+    TORCH_CHECK(bytes >= 16 && reinterpret_cast<uintptr_t>(bucket.data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(scratch.data_ptr()) % 16 == 0,
+                "comm_emulate: 16-byte aligned buffers of >= 16 bytes");
+    c10::DeviceGuard gd(bucket.device());
+    kfk::launch_comm_emulate(bucket.data_ptr(), scratch.data_ptr(), bytes, traffic_bytes, static_cast<int>(ctas),
+                             seconds, stream_of(bucket, stream));
+}
+
+// Peer access / link of `device` to every visible device (the bench pre-flight's P2P
+// matrix): (peer, can_access_peer, link type, hop count); link type per
+// hipExtGetLinkTypeAndHopCount (HSA_AMD_LINK_INFO_TYPE_*: 4 = xGMI, 2 = PCIe).
+std::vector<std::tuple<int, int, int, int>> device_links(int64_t device) {
+    int n = 0;
+    hcheck(hipGetDeviceCount(&n), "GetDeviceCount");
+    std::vector<std::tuple<int, int, int, int>> out;
+    for (int p = 0; p < n; ++p) {
+        if (p == device) continue;
+        int can = 0;
+        uint32_t lt = 0, hops = 0;
+        if (hipDeviceCanAccessPeer(&can, static_cast<int>(device), p) != hipSuccess) can = -1;
+        if (hipExtGetLinkTypeAndHopCount(static_cast<int>(device), p, &lt, &hops) != hipSuccess) lt = hops = 0;
+        out.emplace_back(p, can, static_cast<int>(lt), static_cast<int>(hops));
+    }
+    return out;
+}
+
 // ---- RCCL --------------------------------------------------------------------------
 
 class Comm {
   public:
-    Comm(py::bytes id, int rank, int size, int device, double init_timeout_s) {
+    Comm(py::bytes id, int rank, int size, int device, double init_timeout_s, int min_ctas, int max_ctas) {
         std::string sid(id);
         py::gil_scoped_release nogil;  // init polls its deadline; other threads keep running
-        c_.reset(new kfk::RcclComm(sid, rank, size, device, init_timeout_s));
+        c_.reset(new kfk::RcclComm(sid, rank, size, device, init_timeout_s, min_ctas, max_ctas));
     }
+    py::tuple ctas() const { return py::make_tuple(c_->min_ctas(), c_->max_ctas()); }
     int rank() const { return c_->rank(); }
     int size() const { return c_->size(); }
     bool valid() const { return c_->valid(); }
@@ -1510,16 +1579,19 @@ class Comm {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(in.numel() == out.numel(), "all_reduce: size mismatch");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->all_reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
                        stream_of(in, stream), tag.c_str());
     }
     void broadcast(at::Tensor t, int64_t root, int64_t stream, const std::string &tag) {
         check_gpu(t, "t");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->broadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(root),
                       stream_of(t, stream), tag.c_str());
     }
     void reduce(at::Tensor in, at::Tensor out, int64_t op, int64_t root, int64_t stream, const std::string &tag) {
         check_gpu(in, "in");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->reduce(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), static_cast<int>(op),
                    static_cast<int>(root), stream_of(in, stream), tag.c_str());
     }
@@ -1527,6 +1599,7 @@ class Comm {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(out.numel() == in.numel() * c_->size(), "all_gather: out must hold size*numel(in)");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->all_gather(in.data_ptr(), out.data_ptr(), in.numel(), dtype_code(in), stream_of(in, stream),
                        tag.c_str());
     }
@@ -1534,19 +1607,25 @@ class Comm {
         check_gpu(in, "in");
         check_gpu(out, "out");
         TORCH_CHECK(in.numel() == out.numel() * c_->size(), "reduce_scatter: in must hold size*numel(out)");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), dtype_code(in), static_cast<int>(op),
                            stream_of(in, stream), tag.c_str());
     }
     void send(at::Tensor t, int64_t peer, int64_t stream) {
         check_gpu(t, "t");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->send(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
     }
     void recv(at::Tensor t, int64_t peer, int64_t stream) {
         check_gpu(t, "t");
+        py::gil_scoped_release nogil;  // enq may poll wait_ready (non-blocking comms)
         c_->recv(t.data_ptr(), t.numel(), dtype_code(t), static_cast<int>(peer), stream_of(t, stream));
     }
     void group_start() { c_->group_start(); }
-    void group_end() { c_->group_end(); }
+    void group_end() {
+        py::gil_scoped_release nogil;
+        c_->group_end();
+    }
     void watch(int64_t stream, const std::string &what) {
         c_->watch(reinterpret_cast<hipStream_t>(stream), what);
     }
@@ -1584,6 +1663,7 @@ class Comm {
             }
         c10::DeviceGuard gd(buf.device());
         auto s = stream_of(buf, stream);
+        py::gil_scoped_release nogil;
         for (const auto &r : rounds) {
             if (r.empty()) continue;
             c_->group_start();
@@ -1759,6 +1839,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
     m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");
     m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");
+    m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("out") = py::none(),
+          py::arg("accumulate") = false, py::arg("bn") = -1,
+          "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
+    m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
+    m.def("gemm_nt_pick_bn", &kfk::gemm_nt_pick_bn);
+    m.def("comm_emulate", &comm_emulate, py::arg("bucket"), py::arg("scratch"), py::arg("traffic_bytes"),
+          py::arg("ctas"), py::arg("seconds"), py::arg("stream") = 0,
+          "local footprint of one all-reduce: ctas workgroups stream traffic_bytes, resident for seconds");
+    m.def("device_links", &device_links, py::arg("device"),
+          "[(peer, can_access_peer, link_type, hops)] of `device` to every other visible device");
     m.def("rccl_unique_id", [] { return py::bytes(kfk::RcclComm::unique_id()); });
     m.def("rccl_version", &kfk::RcclComm::version);
     m.def("rccl_watchdog_info", [] {
@@ -1769,6 +1859,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         d["pending"] = i.pending;
         d["oldest_s"] = i.oldest_s;
         d["timeout_s"] = i.timeout_s;
+        d["abort_on_stall"] = i.abort_on_stall;
+        d["stalls_logged"] = i.stalls_logged;
         return d;
     });
     kfk::watchdog_set_freeze_hook([] {
@@ -1777,8 +1869,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rccl_watchdog_set_label", &kfk::watchdog_set_label);
     m.def("rccl_watchdog_set_timeout", &kfk::watchdog_set_timeout);
     py::class_<Comm>(m, "RcclComm")
-        .def(py::init<py::bytes, int, int, int, double>(), py::arg("uid"), py::arg("rank"), py::arg("size"),
-             py::arg("device"), py::arg("init_timeout_s") = 0.0)
+        .def(py::init<py::bytes, int, int, int, double, int, int>(), py::arg("uid"), py::arg("rank"),
+             py::arg("size"), py::arg("device"), py::arg("init_timeout_s") = 0.0, py::arg("min_ctas") = 0,
+             py::arg("max_ctas") = 0)
+        .def("ctas", &Comm::ctas, "(min, max) CTA budget of this communicator (0 = RCCL default)")
         .def("rank", &Comm::rank)
         .def("size", &Comm::size)
         .def("valid", &Comm::valid)

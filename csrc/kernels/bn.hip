@@ -85,27 +85,29 @@ __device__ __forceinline__ void st16(uint4 *p, const uint4 &v, bool nt) {
 // non-temporal stores did not pay in the full step (profiles/README.md, r3f)
 // KUNGFU_BN_SKIP_FINALIZE=1: TIMING EXPERIMENT ONLY -- the sums-finalize kernels are not launched
 // (coefficients stay stale: wrong numerics), to bound what folding them elsewhere could save.
+// Compiled in only with -DKUNGFU_DEV_EXPERIMENTS=1 (never in the release .so).
+#ifndef KUNGFU_DEV_EXPERIMENTS
+#define KUNGFU_DEV_EXPERIMENTS 0
+#endif
 bool bn_skip_finalize() {
+#if KUNGFU_DEV_EXPERIMENTS
     static const bool b = [] {
         const char *e = std::getenv("KUNGFU_BN_SKIP_FINALIZE");
         return e && std::atoi(e) != 0;
     }();
     return b;
+#else
+    return false;
+#endif
 }
 
 int bn_nt_mode() {
-    static const int m = [] {
-        const char *e = std::getenv("KUNGFU_BN_NT");
-        return e ? std::atoi(e) : 1;
-    }();
+    static const int m = dev_knob("KUNGFU_BN_NT", 1);
     return m;
 }
 
 int bn_max_grid(int def) {
-    static const int m = [] {
-        const char *e = std::getenv("KUNGFU_BN_MAXGRID");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int m = dev_knob("KUNGFU_BN_MAXGRID", 0);
     return m > 0 ? m : def;
 }
 

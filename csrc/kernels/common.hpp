@@ -12,8 +12,22 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace kfk {
+
+// Developer A/B switches (kungfu_amd/knobs.py kind "dev"): `name` is read from the environment
+// only when KUNGFU_DEV_KNOBS=1 is set too; otherwise the measured default `def` holds, so a
+// stale shell variable cannot change a production run.
+inline int dev_knob(const char *name, int def) {
+    static const bool dev = [] {
+        const char *e = std::getenv("KUNGFU_DEV_KNOBS");
+        return e && *e && std::atoi(e) != 0;
+    }();
+    if (!dev) return def;
+    const char *e = std::getenv(name);
+    return e && *e ? std::atoi(e) : def;
+}
 
 constexpr int kBlock = 256;
 constexpr int kWave = 64;

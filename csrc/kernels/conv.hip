@@ -708,6 +708,8 @@ void launch_conv_flip_multi(const FlipTable &tab_in, hipStream_t s) {
     conv_flip_tiled_kernel<<<tab.tstart[tab.n], 256, 0, s>>>(tab);
 }
 
+// Channel / stride predicates only: the caller also checks that x and w stay below 2 GiB
+// (buffer-resource staging, check_buf_extent; kungfu_amd._lib.buf_ok on the Python side).
 bool conv3x3_supported(int Cin, int Cout, int stride) {
     return Cin % 64 == 0 && Cout % 64 == 0 && (stride == 1 || stride == 2) && Cin >= 64;
 }
@@ -719,10 +721,7 @@ bool conv_supported(int Cin, int Cout, int ks, int stride) {
 // KUNGFU_CONV_TILE_RULES: 1 = the round-2 tile defaults, 2 (default) = the round-3 re-measured ones
 // (ResNet-50 21.28-21.30 -> 21.12-21.17 ms/step same-box A/B, Inception-v3 neutral)
 int conv_tile_rules() {
-    static const int v = [] {
-        const char *e = std::getenv("KUNGFU_CONV_TILE_RULES");
-        return e ? std::atoi(e) : 2;
-    }();
+    static const int v = dev_knob("KUNGFU_CONV_TILE_RULES", 2);
     return v;
 }
 
@@ -731,19 +730,13 @@ int conv_tile_rules() {
 // clusters) instead of stalling on staging issue together.  ResNet-50 +0.8 % (21.43-21.49 ->
 // 21.28-21.29 ms/step, same box), Inception-v3 neutral.  KUNGFU_CONV_STAGGER=0 turns it off.
 int conv_stagger() {
-    static const int v = [] {
-        const char *e = std::getenv("KUNGFU_CONV_STAGGER");
-        return e ? std::atoi(e) : 1;
-    }();
+    static const int v = dev_knob("KUNGFU_CONV_STAGGER", 1);
     return v;
 }
 
 // KUNGFU_CONV_PRIO=1: static s_setprio 1 for the upper wave half of the 8-wave tiles (A/B)
 int conv_prio() {
-    static const int v = [] {
-        const char *e = std::getenv("KUNGFU_CONV_PRIO");
-        return e ? std::atoi(e) : 0;
-    }();
+    static const int v = dev_knob("KUNGFU_CONV_PRIO", 0);
     return v;
 }
 
@@ -777,10 +770,7 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
         // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
         // statistics flush per block instead of per tile
         // (KUNGFU_CONV_PERSIST_BLOCKS, default 4 per CU, fewer when the tile's LDS allows less)
-        static const int env_cap = [] {
-            const char *v = std::getenv("KUNGFU_CONV_PERSIST_BLOCKS");
-            return v ? std::atoi(v) : 0;
-        }();
+        static const int env_cap = dev_knob("KUNGFU_CONV_PERSIST_BLOCKS", 0);
         constexpr int kRow = 128, STG = ST * (BM + BN) * kRow, CT = BM * (BN * 2 + 16);
         constexpr int LDS = STG > CT ? STG : CT;
         constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
@@ -958,8 +948,9 @@ void launch_gemm_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, con
 }
 
 bool gemm_supported(int M, int K, int N) {
+    // x (M x K) and the (flipped) weight are staged through buffer resources: below 2 GiB of bf16
     return M > 0 && K >= 64 && K % 64 == 0 && N % 64 == 0 && N >= 64 &&
-           static_cast<int64_t>(M) * (K > N ? K : N) < (int64_t(1) << 31);
+           static_cast<int64_t>(M) * (K > N ? K : N) < (int64_t(1) << 30);
 }
 
 void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K, int N, const EpiArgs &ea, int epi,

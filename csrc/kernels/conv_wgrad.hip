@@ -828,10 +828,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 // Inception-v3 21.62 -> 21.45 ms/step, VGG-16 34.85 -> 34.62, ResNet-50 neutral);
 // KUNGFU_WROWS_STAGGER=0 turns it off.
 int rows_stagger(bool /*rect*/) {
-    static const int v = [] {
-        const char *e = std::getenv("KUNGFU_WROWS_STAGGER");
-        return e ? std::atoi(e) : 1;
-    }();
+    static const int v = dev_knob("KUNGFU_WROWS_STAGGER", 1);
     return v;
 }
 
@@ -914,10 +911,7 @@ void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, cons
     // staggered staging issue (KUNGFU_WGRAD_STAGGER=0/1 forces it off/on): default on for the 256x256
     // tiles only -- BERT-base's long-K linear weight gradients +1.5 % step time, ResNet-50's 256x128
     // tiles -0.8 % with it (tools/gpu_r3_envab.sh, same box)
-    static const int env_stagger = [] {
-        const char *e = std::getenv("KUNGFU_WGRAD_STAGGER");
-        return e ? std::atoi(e) : -1;
-    }();
+    static const int env_stagger = dev_knob("KUNGFU_WGRAD_STAGGER", -1);
     const int stagger = env_stagger >= 0 ? env_stagger : (TN == 8 ? 1 : 0);
     if (KUNGFU_WGRAD_BUFLD && (static_cast<int64_t>(g.P) * g.K * 2 >= kWBufOOB ||
                                static_cast<int64_t>(g.N) * g.H * g.W * g.C * 2 >= kWBufOOB))

@@ -15,6 +15,20 @@ constexpr int kMaxGridHost = 2048;  // == kMaxGrid in common.hpp (partials scrat
 // K1: z = op(x, y) elementwise.  dtype/op codes as kungfu::DType / ReduceOp.
 void launch_reduce(void *z, const void *x, const void *y, size_t n, int dtype, int op, hipStream_t s);
 
+// gemm.hip: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (+ C) in bf16, f32 accumulation, on a
+// 256 x bn tile (bn 128 | 192 | 256, <= 0: by shape) with a 3-slab-deep LDS-DMA pipeline.
+constexpr int kGemmBias = 1, kGemmAccum = 2;
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
+int gemm_nt_pick_bn(int64_t M, int64_t N);
+void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
+                    int epi, int bn, hipStream_t s);
+
+// comm_emu.hip: the local footprint of one all-reduce of `bytes` (bench.py --emulate-comm):
+// `ctas` workgroups copying `traffic_bytes` of the bucket into `scratch` (>= bytes), paced over
+// and resident for `seconds`.  The bucket is only read.
+void launch_comm_emulate(const void *bucket, void *scratch, int64_t bytes, int64_t traffic_bytes, int ctas,
+                         double seconds, hipStream_t s);
+
 // K8: fused SGD step on flat f32 buffers (torch.optim.SGD semantics):
 //   d = g*gscale + wd*w ; m = first ? d : mu*m + (1-damp)*d ; d = nesterov ? d + mu*m : m ; w -= lr*d
 // lr is read from *lr_dev when lr_dev != nullptr (graph-capture friendly).

@@ -16,9 +16,14 @@
 //    with a message instead of hanging in ncclCommInitRank;
 //  * every collective registers a completion event with a process-wide watchdog
 //    thread which also polls ncclCommGetAsyncError of every live communicator;
-//    a stalled op (older than KUNGFU_RCCL_TIMEOUT_S) or an async error is
-//    reported by name and rank, every communicator is aborted and the process
-//    exits with status 3.
+//    an async error is reported by name and rank, every communicator is aborted
+//    and the process exits with status 3.  A stalled op (older than the timeout)
+//    is only LOGGED by default (600 s; like the reference's stall detector,
+//    srcs/go/utils/stalldetector.go, which never kills): a peer may legitimately
+//    spend long in an evaluation or checkpoint while the others wait in the next
+//    bucket.  Setting KUNGFU_RCCL_TIMEOUT_S explicitly (bench.py does) makes a
+//    stall fatal as well (abort + exit 3); KUNGFU_RCCL_STALL_ACTION=log|abort
+//    overrides either default.
 #include "rccl_comm.hpp"
 
 #include <rccl/rccl.h>
@@ -168,6 +173,8 @@ class Watchdog {
         double t = now_s();
         for (const auto &e : q_) i.oldest_s = std::max(i.oldest_s, t - e.t0);
         i.timeout_s = timeout_;
+        i.abort_on_stall = abort_on_stall_;
+        i.stalls_logged = stalls_logged_;
         return i;
     }
 
@@ -176,9 +183,16 @@ class Watchdog {
         hipEvent_t ev;
         std::string what;
         double t0;
+        double warned = 0;  // log-only mode: time of the last stall warning
     };
 
-    Watchdog() : timeout_(env_double("KUNGFU_RCCL_TIMEOUT_S", 600.0)) {}
+    Watchdog() : timeout_(env_double("KUNGFU_RCCL_TIMEOUT_S", 600.0)) {
+        const char *t = std::getenv("KUNGFU_RCCL_TIMEOUT_S");
+        abort_on_stall_ = t && *t;
+        const char *a = std::getenv("KUNGFU_RCCL_STALL_ACTION");
+        if (a && std::string(a) == "abort") abort_on_stall_ = true;
+        if (a && std::string(a) == "log") abort_on_stall_ = false;
+    }
 
     void start_locked() {
         if (started_) return;
@@ -210,8 +224,18 @@ class Watchdog {
                         char buf[160];
                         std::snprintf(buf, sizeof(buf), " has not completed after %.1f s (KUNGFU_RCCL_TIMEOUT_S=%g)",
                                       t - it->t0, timeout_.load());
-                        fail = "collective " + it->what + buf;
-                        break;
+                        if (abort_on_stall_) {
+                            fail = "collective " + it->what + buf;
+                            break;
+                        }
+                        if (t - it->warned > timeout_) {  // log-only: warn again every timeout period
+                            it->warned = t;
+                            ++stalls_logged_;
+                            std::fprintf(stderr, "[W] kungfu rccl watchdog (%s): collective %s%s; still waiting "
+                                         "(set KUNGFU_RCCL_TIMEOUT_S or KUNGFU_RCCL_STALL_ACTION=abort to fail)\n",
+                                         label_.empty() ? "?" : label_.c_str(), it->what.c_str(), buf);
+                            std::fflush(stderr);
+                        }
                     }
                     ++it;
                 }
@@ -277,7 +301,8 @@ class Watchdog {
     std::atomic<double> timeout_;
     void (*freeze_)() = nullptr;
     bool started_ = false;
-    long long registered_ = 0, completed_ = 0;
+    bool abort_on_stall_ = false;
+    long long registered_ = 0, completed_ = 0, stalls_logged_ = 0;
 };
 
 }  // namespace
@@ -299,7 +324,8 @@ int RcclComm::version() {
     return v;
 }
 
-RcclComm::RcclComm(const std::string &id, int rank, int size, int device, double init_timeout_s)
+RcclComm::RcclComm(const std::string &id, int rank, int size, int device, double init_timeout_s, int min_ctas,
+                   int max_ctas)
     : rank_(rank), size_(size) {
     if (id.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("rccl: bad unique id length");
     hcheck(hipSetDevice(device), "SetDevice");
@@ -307,11 +333,20 @@ RcclComm::RcclComm(const std::string &id, int rank, int size, int device, double
     std::memcpy(&uid, id.data(), sizeof(uid));
     if (init_timeout_s <= 0) init_timeout_s = env_double("KUNGFU_RCCL_INIT_TIMEOUT_S", 300.0);
     blocking_ = env_double("KUNGFU_RCCL_BLOCKING", 0) != 0;
+    if (min_ctas <= 0) min_ctas = static_cast<int>(env_double("KUNGFU_RCCL_MIN_CTAS", 0));
+    if (max_ctas <= 0) max_ctas = static_cast<int>(env_double("KUNGFU_RCCL_MAX_CTAS", 0));
+    if (min_ctas > 0 && max_ctas > 0 && min_ctas > max_ctas) min_ctas = max_ctas;
+    min_ctas_ = min_ctas > 0 ? min_ctas : 0;
+    max_ctas_ = max_ctas > 0 ? max_ctas : 0;
+    if (blocking_ && (min_ctas_ || max_ctas_))
+        throw std::invalid_argument("rccl: a CTA budget needs the config init (KUNGFU_RCCL_BLOCKING=0)");
     ncclComm_t c = nullptr;
     if (!blocking_) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
         cfg.version = static_cast<unsigned int>(version());  // the loaded library's, not the header's
         cfg.blocking = 0;
+        if (min_ctas_) cfg.minCTAs = min_ctas_;
+        if (max_ctas_) cfg.maxCTAs = max_ctas_;
         ncclResult_t r = ncclCommInitRankConfig(&c, size, uid, rank, &cfg);
         if (r != ncclSuccess && r != ncclInProgress) {
             if (c) ncclCommAbort(c);

@@ -14,7 +14,13 @@ class RcclComm {
     // Non-blocking init (ncclCommInitRankConfig, blocking=0) polled against a deadline
     // of `init_timeout_s` seconds (<= 0: KUNGFU_RCCL_INIT_TIMEOUT_S, default 300); on
     // expiry the half-built communicator is aborted and std::runtime_error is thrown.
-    RcclComm(const std::string &id, int rank, int size, int device, double init_timeout_s = 0);
+    // CTA budget (ncclConfig_t.minCTAs / maxCTAs): how many workgroups -- RCCL channels --
+    // one collective of this communicator may occupy; <= 0 = KUNGFU_RCCL_MIN_CTAS /
+    // KUNGFU_RCCL_MAX_CTAS, unset = RCCL's own choice.  Bounds the CUs the gradient
+    // all-reduces take from the overlapped backward (and lets two communicators driven
+    // concurrently -- the hierarchical local reduce / broadcast -- stay co-resident).
+    RcclComm(const std::string &id, int rank, int size, int device, double init_timeout_s = 0, int min_ctas = 0,
+             int max_ctas = 0);
     ~RcclComm();
     RcclComm(const RcclComm &) = delete;
     RcclComm &operator=(const RcclComm &) = delete;
@@ -23,6 +29,8 @@ class RcclComm {
     int size() const { return size_; }
     bool valid() const { return comm_ != nullptr; }
     bool blocking() const { return blocking_; }
+    int min_ctas() const { return min_ctas_; }  // 0 = RCCL default
+    int max_ctas() const { return max_ctas_; }
 
     // dtype / op codes follow kungfu::DType / ReduceOp (op 4 = average).  `tag` names the
     // operation for the watchdog (e.g. "bucket 3/5"); every op is registered with it.
@@ -53,6 +61,7 @@ class RcclComm {
     void *comm_ = nullptr;
     int rank_, size_;
     bool blocking_ = true;
+    int min_ctas_ = 0, max_ctas_ = 0;
     unsigned long long seq_ = 0;
 };
 
@@ -67,6 +76,8 @@ class RcclComm {
 struct WatchdogInfo {
     long long registered = 0, completed = 0, pending = 0;
     double oldest_s = 0, timeout_s = 0;
+    bool abort_on_stall = false;  // false: a stall past timeout_s is logged, not fatal
+    long long stalls_logged = 0;
 };
 WatchdogInfo watchdog_info();
 void watchdog_set_label(const std::string &label);  // e.g. "rank 3/8"

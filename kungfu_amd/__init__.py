@@ -18,7 +18,9 @@ from .python import (cluster_version, current_cluster_size, current_host_count, 
                      current_local_size, current_rank, detached, finalize, get_hip_index, init, launch_mode,
                      propose_new_size, resize_cluster, resize_cluster_from_url, run_barrier, show_hip_version,
                      show_rccl_version, uid)
-from . import checkpoint, ops, optimizers  # noqa: E402
+from . import checkpoint, knobs, ops, optimizers  # noqa: E402
 from .ops import broadcast_parameters  # noqa: E402
 
 get_cuda_index = get_hip_index
+
+knobs.check_environ_once()  # warn about misspelt / ignored KUNGFU_* settings

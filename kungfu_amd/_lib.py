@@ -47,6 +47,18 @@ def hip():
     return _hip_mod
 
 
+# The MFMA conv kernels stage operands through buffer resources with 32-bit byte offsets
+# (csrc/kernels/conv.hip kBufOOB): every operand must stay below 2 GiB; larger shapes fall back
+# to the library paths.
+BUF_LIMIT_BYTES = 1 << 31
+
+
+def buf_ok(*numels: int, esz: int = 2) -> bool:
+    """True when every operand of ``numels`` elements (``esz`` bytes each) is addressable
+    by the kernels' buffer-resource staging (below 2 GiB)."""
+    return all(int(n) * esz < BUF_LIMIT_BYTES for n in numels)
+
+
 def hip_available() -> bool:
     try:
         hip()

@@ -1,0 +1,195 @@
+"""One registry of every ``KUNGFU_*`` environment variable the framework reads.
+
+Three kinds:
+
+* ``user``     -- documented configuration (timeouts, bucket sizes, data plane, kill switches
+  that route an op back to the library path);
+* ``launcher`` -- set by ``kungfu-run`` / the elastic runtime for its workers (the worker env
+  contract, parity ``srcs/go/kungfu/env/envs.go``); users do not set these by hand;
+* ``dev``      -- A/B switches kept for re-measuring a design decision (most of them select an
+  alternative that measured slower, see profiles/README.md).  They are honoured ONLY when
+  ``KUNGFU_DEV_KNOBS=1`` is also set -- in Python (:func:`get`) and in the kernels
+  (``kfk::dev_knob``, csrc/kernels/common.hpp) -- so a stale shell variable cannot silently
+  slow a production run down.  Numerics-changing experiments are not knobs at all (e.g. the
+  BN-finalize skip is compiled in only with ``-DKUNGFU_DEV_EXPERIMENTS``).
+
+:func:`check_environ` (called once at ``import kungfu_amd``) warns about every set ``KUNGFU_*``
+variable that is not registered (a misspelt knob would otherwise be ignored silently, with a
+close-match suggestion) and about dev knobs that are set without ``KUNGFU_DEV_KNOBS=1``.
+"""
+from __future__ import annotations
+
+import difflib
+import os
+import warnings
+from typing import Dict, NamedTuple, Optional
+
+
+class Knob(NamedTuple):
+    default: Optional[str]
+    kind: str  # user | launcher | dev
+    doc: str
+
+
+class KnobWarning(UserWarning):
+    pass
+
+
+def _u(default, doc):
+    return Knob(default, "user", doc)
+
+
+def _l(doc):
+    return Knob(None, "launcher", doc)
+
+
+def _d(default, doc):
+    return Knob(default, "dev", doc)
+
+
+KNOBS: Dict[str, Knob] = {
+    # -- runtime / transport (csrc/runtime) ------------------------------------------------
+    "KUNGFU_CONFIG_LOG_LEVEL": _u("INFO", "runtime log level (DEBUG/INFO/WARN/ERROR)"),
+    "KUNGFU_CONFIG_ENABLE_MONITORING": _u("false", "net monitor + /metrics endpoint"),
+    "KUNGFU_CONFIG_MONITORING_PERIOD": _u("1s", "net monitor sampling period"),
+    "KUNGFU_CONFIG_ENABLE_STALL_DETECTION": _u("false", "log host collectives that take > 10 s"),
+    "KUNGFU_CONFIG_ENABLE_TRACE": _u("false", "print trace-scope reports at exit"),
+    "KUNGFU_CONFIG_CHUNK_SIZE_MIB": _u("1", "host all-reduce chunk size (strategies rotate per chunk)"),
+    "KUNGFU_CONFIG_STRATEGY_HASH_METHOD": _u("SIMPLE", "chunk -> strategy assignment (SIMPLE | NAME)"),
+    "KUNGFU_CONFIG_CONN_RETRY_COUNT": _u("500", "TCP dial retries"),
+    "KUNGFU_CONFIG_CONN_RETRY_PERIOD": _u("200ms", "TCP dial retry period"),
+    "KUNGFU_CONFIG_USE_UNIX_SOCK": _u("true", "same-host peers over Unix sockets"),
+    "KUNGFU_CONFIG_WAIT_RUNNER_TIMEOUT": _u("120s", "elastic: wait for a runner"),
+    "KUNGFU_CONFIG_RETRY_STDERR_PREFIX": _u(None, "runner restarts a worker whose stderr starts with this"),
+    "KUNGFU_ALLREDUCE_STRATEGY": _u("AUTO", "host all-reduce topology strategy"),
+    "KUNGFU_OP_TIMEOUT_S": _u("0", "host collective watchdog: abort (exit 3) after this many seconds; 0 = off"),
+    "KUNGFU_MNIST_DIR": _u(None, "MNIST idx files for the examples"),
+    "KUNGFU_PLATFORM": _u(None, "launcher platform hint (ModelArts discovery)"),
+    # -- device data plane (kungfu_amd/parallel, csrc/kernels/rccl_comm.hip) -------------------
+    "KUNGFU_GPU_DATAPLANE": _u("rccl", "rccl | host (stage device collectives through host memory)"),
+    "KUNGFU_GPU_ALLREDUCE": _u("rccl", "rccl | graph (bucket all-reduce along the KungFu strategy graphs)"),
+    "KUNGFU_BUCKET_MB": _u("32", "S-SGD gradient bucket size (MiB)"),
+    "KUNGFU_TAIL_BUCKET_MB": _u("4", "size cap of the buckets holding the first layers (exposed tail)"),
+    "KUNGFU_RCCL_TIMEOUT_S": _u("600", "RCCL watchdog stall timeout; setting it explicitly makes a stall fatal"),
+    "KUNGFU_RCCL_STALL_ACTION": _u("log", "log | abort: what a stalled RCCL collective does"),
+    "KUNGFU_RCCL_INIT_TIMEOUT_S": _u("300", "communicator init / finalize deadline"),
+    "KUNGFU_RCCL_BLOCKING": _u("0", "1: blocking communicator init (no deadline, no CTA budget)"),
+    "KUNGFU_RCCL_MIN_CTAS": _u("0", "ncclConfig_t.minCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
+    "KUNGFU_RCCL_MAX_CTAS": _u("0", "ncclConfig_t.maxCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
+    "KUNGFU_RCCL_COLOCATE": _u("0", "1: several RCCL ranks on one GPU (socket transport; tests)"),
+    "KUNGFU_COMM_EMULATE": _u(None, "ranks=R,ctas=C,busbw=GB/s,lat_us=L: model an R-rank all-reduce on one GPU"),
+    "KUNGFU_PREFLIGHT_TIMEOUT_S": _u("60", "bench pre-flight: deadline of each device check"),
+    "KUNGFU_PREFLIGHT_CORRUPT": _u(None, "test hook: this rank corrupts its pre-flight buffer"),
+    "KUNGFU_PREFLIGHT_CORRUPT_WHAT": _u("ipc", "test hook: ipc | allreduce"),
+    "KUNGFU_FORCE_DEVICE": _u(None, "pin every rank to this HIP device (colocated tests)"),
+    "KUNGFU_INIT_CKPT": _u(None, "elastic: initial checkpoint step"),
+    # -- kernel routing kill switches (1 = our HIP kernel, 0 = library path) --------------------
+    "KUNGFU_CONV3X3": _u("1", "3x3 convolutions on the MFMA kernel"),
+    "KUNGFU_CONV_RECT": _u("1", "rectangular-window convolutions on the MFMA kernel"),
+    "KUNGFU_WGRAD": _u("1", "weight gradients on the split-K MFMA kernel"),
+    "KUNGFU_WGRAD_RECT": _u("1", "rectangular-window weight gradients on the MFMA kernels"),
+    "KUNGFU_FUSED_BLOCK": _u("1", "ResNet bottleneck as one fused autograd node"),
+    "KUNGFU_STEM": _u("1", "ResNet stem conv on the MFMA stem kernel"),
+    "KUNGFU_LINEAR_WGRAD": _u("1", "linear-layer weight gradients on the split-K MFMA kernel"),
+    "KUNGFU_LINEAR_GEMM": _u("0", "linear forward / data gradient on gemm.hip's NT GEMM instead of hipBLASLt"),
+    "KUNGFU_DEV_KNOBS": _u("0", "1: honour the dev (A/B) knobs below"),
+    # -- launcher / worker env contract (csrc/launcher/job.cpp, csrc/runtime/peer.cpp) ---------
+    "KUNGFU_SELF_SPEC": _l("this worker's host:port"),
+    "KUNGFU_INIT_PEERS": _l("initial peer list"),
+    "KUNGFU_INIT_RUNNERS": _l("initial runner list"),
+    "KUNGFU_INIT_CLUSTER_VERSION": _l("initial cluster version"),
+    "KUNGFU_PARENT_ID": _l("runner that started this worker"),
+    "KUNGFU_CONFIG_SERVER": _l("elastic config server URL"),
+    "KUNGFU_JOB_START_TIMESTAMP": _l("job start time"),
+    "KUNGFU_PROC_START_TIMESTAMP": _l("worker start time"),
+    "KUNGFU_HIP_DEVICE_ORDINAL": _l("the worker's HIP device"),
+    "KUNGFU_HIP_VISIBLE_DEVICES": _l("devices assigned to the worker (-isolate-gpus)"),
+    "KUNGFU_ALLOW_XGMI": _l("several workers may share a GPU (-allow-xgmi)"),
+    "KUNGFU_SELF_IP": _l("this worker's IP (single mode)"),
+    # -- dev A/B knobs (need KUNGFU_DEV_KNOBS=1) ----------------------------------------------
+    "KUNGFU_CONV_PRIO": _d("0", "s_setprio 1 for the upper wave half of 8-wave conv tiles (neutral)"),
+    "KUNGFU_CONV_STAGGER": _d("1", "staggered LDS-DMA issue in 8-wave conv tiles (0 = off, -0.8 %)"),
+    "KUNGFU_CONV_TILE_RULES": _d("2", "1 = the round-2 conv tile defaults"),
+    "KUNGFU_CONV_PERSIST_BLOCKS": _d("0", "persistent conv blocks for the statistics epilogues (0 = 4/CU)"),
+    "KUNGFU_WGRAD_STAGGER": _d("-1", "wgrad staging stagger (-1 = on for 256x256 tiles only)"),
+    "KUNGFU_WROWS_STAGGER": _d("1", "row-image wgrad staging stagger"),
+    "KUNGFU_WGRAD_STREAM": _d("0", "weight gradients on a side stream (-1.2 %)"),
+    "KUNGFU_BN_NT": _d("1", "BN non-temporal policy (0 none, 1 loads, 2 stores, 3 both)"),
+    "KUNGFU_BN_MAXGRID": _d("0", "BN apply grid cap (0 = kernel default)"),
+    "KUNGFU_BN_INLAUNCH_FIN": _d("0", "BN finalize inside the statistics conv's launch (slower)"),
+    "KUNGFU_BN_CONCAT": _d("1", "Inception branch BN+ReLU stores into the concatenation"),
+    "KUNGFU_STEM_FUSED_BWD": _d("0", "one-pass fused stem backward (slower)"),
+    "KUNGFU_LN_BIAS_LINK": _d("1", "bias gradients from the consuming LayerNorm backward"),
+    "KUNGFU_GELU_BIAS_LINK": _d("1", "FC1 bias gradient from the fused GELU-backward column sum"),
+    "KUNGFU_LINEAR_DIRECT_WGRAD": _d("1", "linear weight gradients reduced straight into the flat buffer"),
+    "KUNGFU_COMM_STREAM_PRIORITY": _d("0", "HIP priority of the comm stream (-1 measured 2x slower)"),
+    "KUNGFU_BN_SKIP_FINALIZE": _d("0", "TIMING ONLY, wrong numerics: skip BN finalize (needs a -DKUNGFU_DEV_EXPERIMENTS=1 build)"),
+    "KUNGFU_BERT_GEMM": _d("0", "BERT linear layers on the hand-written GEMM"),
+}
+
+# compile-time switches (-D...), not environment variables; listed so the source lint knows them
+MACROS = ("KUNGFU_CONV_BUFLD", "KUNGFU_WGRAD_BUFLD", "KUNGFU_WGRAD_AUX", "KUNGFU_DISABLE_TRACE",
+          "KUNGFU_ENABLE_TRACE", "KUNGFU_DEV_EXPERIMENTS", "KUNGFU_AMD_CAPI_H", "KUNGFU_ENABLE_HIP")
+
+# prefixes with a free suffix (per-scope overrides)
+PREFIXES = ("KUNGFU_RCCL_MIN_CTAS_", "KUNGFU_RCCL_MAX_CTAS_")
+
+
+def dev_enabled() -> bool:
+    return os.environ.get("KUNGFU_DEV_KNOBS", "0") not in ("", "0")
+
+
+def get(name: str, default: Optional[str] = None) -> Optional[str]:
+    """The value of a registered knob (its registered default when unset; ``default``
+    overrides that).  Dev knobs read as their default unless ``KUNGFU_DEV_KNOBS=1``."""
+    k = KNOBS.get(name)
+    if k is None:
+        raise KeyError("unregistered knob %s (add it to kungfu_amd/knobs.py)" % name)
+    dflt = default if default is not None else k.default
+    if k.kind == "dev" and not dev_enabled():
+        return dflt
+    return os.environ.get(name, dflt)
+
+
+def get_int(name: str, default: Optional[int] = None) -> int:
+    v = get(name, None if default is None else str(default))
+    return int(v) if v not in (None, "") else 0
+
+
+_checked = [False]
+
+
+def check_environ(environ=None) -> list:
+    """Warn (once per process) about unknown ``KUNGFU_*`` variables and ignored dev knobs.
+    Returns the warning messages."""
+    env = os.environ if environ is None else environ
+    msgs = []
+    for name in sorted(env):
+        if not name.startswith("KUNGFU_"):
+            continue
+        if name in KNOBS:
+            if KNOBS[name].kind == "dev" and not (env.get("KUNGFU_DEV_KNOBS", "0") not in ("", "0")):
+                msgs.append("%s is a developer A/B knob and is IGNORED without KUNGFU_DEV_KNOBS=1" % name)
+            continue
+        if name.startswith(PREFIXES):
+            continue
+        close = difflib.get_close_matches(name, list(KNOBS), n=1, cutoff=0.75)
+        msgs.append("unknown setting %s%s (see kungfu_amd/knobs.py)" % (
+            name, " -- did you mean %s?" % close[0] if close else ""))
+    for m in msgs:
+        warnings.warn("kungfu_amd: " + m, KnobWarning, stacklevel=3)
+    return msgs
+
+
+def check_environ_once() -> None:
+    if not _checked[0]:
+        _checked[0] = True
+        check_environ()
+
+
+def table() -> str:
+    """Markdown table of every knob (docs/KNOBS.md is generated from this)."""
+    rows = ["| variable | kind | default | meaning |", "|---|---|---|---|"]
+    for n, k in KNOBS.items():
+        rows.append("| `%s` | %s | %s | %s |" % (n, k.kind, "" if k.default is None else "`%s`" % k.default, k.doc))
+    return "\n".join(rows) + "\n"

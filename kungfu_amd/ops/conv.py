@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .._lib import hip, hip_available
+from .._lib import buf_ok, hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_CONV3X3", "1") != "0"
 _WGRAD = os.environ.get("KUNGFU_WGRAD", "1") != "0"
@@ -90,7 +90,7 @@ def eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, groups
         return False
     if not w.is_contiguous(memory_format=torch.channels_last):
         return False
-    if not hip_available():
+    if not hip_available() or not buf_ok(x.numel(), w.numel()):
         return False
     return hip().conv3x3_supported(int(x.shape[1]), int(w.shape[0]), int(st))
 
@@ -167,6 +167,8 @@ def rect_eligible(x: torch.Tensor, w: torch.Tensor, stride, padding, dilation, g
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not hip_available():
         return False
     if not x.is_contiguous(memory_format=torch.channels_last) or not w.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if not buf_ok(x.numel(), w.numel()):
         return False
     return hip().conv_rect_supported(int(x.shape[1]), int(w.shape[0]), int(w.shape[2]), int(w.shape[3]), st[0])
 

@@ -45,7 +45,8 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
-from .._lib import hip, hip_available
+from .. import knobs
+from .._lib import buf_ok, hip, hip_available
 from ..parallel.mixed import SideStream, deliver, direct_target, shadow
 
 _ENABLED = os.environ.get("KUNGFU_FUSED_BLOCK", "1") != "0"
@@ -76,7 +77,7 @@ def _sums(bn, dev) -> torch.Tensor:
 # workgroup must wait for its memory-side f64 slot atomics before it may arrive, and the arrivals
 # and the last workgroup's fold sit on the launch's critical path), although dropping the finalize
 # launches altogether would save 1.0 ms (KUNGFU_BN_SKIP_FINALIZE timing experiment).
-_INLAUNCH_FIN = os.environ.get("KUNGFU_BN_INLAUNCH_FIN", "0") == "1"
+_INLAUNCH_FIN = knobs.get("KUNGFU_BN_INLAUNCH_FIN") == "1"
 
 
 def _kw(**kw):
@@ -176,7 +177,10 @@ class _FlipCache:
     def get(self, i: int) -> torch.Tensor:
         if self.gen != self.space.shadow_gen:
             idx = sorted(self.index)
-            hip().conv_flip_weights([self.space.shadow_view(j) for j in idx], [self.index[j] for j in idx])
+            # linear weights [out, in] are 1x1 convolutions [out, in, 1, 1]: their flip is W^T
+            ws = [self.space.shadow_view(j) for j in idx]
+            ws = [w if w.dim() == 4 else w.view(w.shape[0], w.shape[1], 1, 1) for w in ws]
+            hip().conv_flip_weights(ws, [self.index[j] for j in idx])
             self.gen = self.space.shadow_gen
         return self.index[i]
 
@@ -430,6 +434,11 @@ def eligible(block, x: torch.Tensor) -> bool:
     if not (_ENABLED and block.training and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4):
         return False
     if not x.is_contiguous(memory_format=torch.channels_last) or not hip_available():
+        return False
+    # every activation of the block (at most N*H*W * its widest channel count) must stay below
+    # the conv kernels' 2 GiB buffer-resource range; larger batches take the layered path
+    widest = max(block.conv1.in_channels, block.conv3.out_channels, block.conv1.out_channels)
+    if not buf_ok(x.numel() // x.shape[1] * widest):
         return False
     H = hip()
     convs = [block.conv1, block.conv2, block.conv3] + ([block.downsample[0]] if block.downsample is not None else [])

@@ -23,13 +23,14 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import knobs
 from .._lib import hip, hip_available
 from ..parallel.mixed import deliver, direct_target
 
 import os
 
 # KUNGFU_BN_CONCAT=0: apply deferred branch BNs and concatenate with torch.cat (A/B, tests)
-CONCAT_ENABLED = os.environ.get("KUNGFU_BN_CONCAT", "1") != "0"
+CONCAT_ENABLED = knobs.get("KUNGFU_BN_CONCAT") != "0"
 
 
 def available() -> bool:

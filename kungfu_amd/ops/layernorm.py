@@ -15,11 +15,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import knobs
 from .._lib import hip, hip_available
 
 import os
 
-_BIAS_LINK = os.environ.get("KUNGFU_LN_BIAS_LINK", "1") != "0"  # A/B switch of the linear bias-gradient link
+_BIAS_LINK = knobs.get("KUNGFU_LN_BIAS_LINK") != "0"  # A/B switch of the linear bias-gradient link
 
 
 class _AddLayerNormFn(torch.autograd.Function):

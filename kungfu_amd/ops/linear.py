@@ -17,6 +17,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from .. import knobs
 from .._lib import hip, hip_available
 
 _MAX_TOKENS = 1 << 23
@@ -40,7 +41,32 @@ class BiasLink:
         self.dtype, self.value, self.ptr = dtype, None, 0
 
 
-_DIRECT_WGRAD = os.environ.get("KUNGFU_LINEAR_DIRECT_WGRAD", "1") != "0"
+_DIRECT_WGRAD = knobs.get("KUNGFU_LINEAR_DIRECT_WGRAD") != "0"
+# KUNGFU_LINEAR_GEMM=1: forward (x W^T + b) and data gradient (dy W, with W^T from the flat
+# space's per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt
+_GEMM = knobs.get("KUNGFU_LINEAR_GEMM") == "1"
+
+
+def set_gemm_enabled(on: bool) -> bool:
+    global _GEMM
+    old, _GEMM = _GEMM, bool(on)
+    return old
+
+
+def _gemm_ok(M: int, K: int, N: int) -> bool:
+    return _GEMM and hip().gemm_nt_supported(M, N, K)
+
+
+def _wt_cache(target, w):
+    """(flip cache, index) giving W^T [in, out] for the shadow weight ``w`` of flat-space parameter
+    ``target`` -- the 1x1-conv "flip" of [out, in, 1, 1] is exactly the transpose -- refreshed by ONE
+    multi-tensor kernel per optimizer step (ops.fused_block._FlipCache)."""
+    from .fused_block import _flip_cache
+
+    fc = _flip_cache(target[0])
+    out_f, in_f = w.shape
+    fc.register(target[1], w.view(out_f, in_f, 1, 1))
+    return fc, target[1]
 
 
 class _LinearFn(torch.autograd.Function):
@@ -51,6 +77,13 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_b = b is not None
         ctx.b_dtype = b.dtype if b is not None else None
         ctx.blink = BiasLink(b.dtype) if b is not None and b.dtype in (torch.bfloat16, torch.float32) else None
+        out_f, in_f = w.shape
+        M = x.numel() // in_f
+        ctx.wt = None
+        if _gemm_ok(M, in_f, out_f) and x.is_contiguous() and (b is None or b.dtype == torch.bfloat16):
+            if target is not None and _gemm_ok(M, out_f, in_f):
+                ctx.wt = _wt_cache(target, w)
+            return hip().gemm_nt(x.view(M, in_f), w, b).view(*x.shape[:-1], out_f)
         return F.linear(x, w, b)
 
     @staticmethod
@@ -65,7 +98,11 @@ class _LinearFn(torch.autograd.Function):
             x2 = x2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.mm(dy2, w).view(x.shape)
+            if ctx.wt is not None:  # dx = dy . W = dy . (W^T)^T on the NT GEMM
+                fc, i = ctx.wt
+                dx = hip().gemm_nt(dy2, fc.get(i).view(in_f, out_f)).view(x.shape)
+            else:
+                dx = torch.mm(dy2, w).view(x.shape)
         tgt = ctx.target
         if ctx.needs_input_grad[1] and tgt is not None and _DIRECT_WGRAD and hasattr(tgt[0].sink, "put_direct"):
             # the split-K partials are reduced straight into the weight's flat f32 gradient slot
@@ -133,7 +170,7 @@ class _GeluFn(torch.autograd.Function):
         return du, None
 
 
-_GELU_LINK = os.environ.get("KUNGFU_GELU_BIAS_LINK", "1") != "0"
+_GELU_LINK = knobs.get("KUNGFU_GELU_BIAS_LINK") != "0"
 
 
 def gelu(u: torch.Tensor, bias_link: bool = False) -> torch.Tensor:

@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .._lib import hip, hip_available
+from .._lib import buf_ok, hip, hip_available
 
 _CL = torch.channels_last
 
@@ -130,6 +130,10 @@ class FusedVGGFeatures(nn.Sequential):
         if not convs or not x.is_cuda or not hip_available() or x.dim() != 4:
             return False
         if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+            return False
+        # the stack's activations (N*H*W * widest channel count at its input resolution) must stay
+        # below the conv kernels' 2 GiB buffer-resource range
+        if not buf_ok(x.numel() // x.shape[1] * max(c.out_channels for c in convs)):
             return False
         H = hip()
         for i, c in enumerate(convs):

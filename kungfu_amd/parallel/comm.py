@@ -34,6 +34,7 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
+from .. import knobs
 from .._lib import dtype_code, hip, op_code, runtime
 
 _U8 = 0
@@ -164,10 +165,11 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         # non-blocking init against a deadline (KUNGFU_RCCL_INIT_TIMEOUT_S): a peer that
         # never arrives raises here instead of hanging; collectives are then watched by
         # the native watchdog (KUNGFU_RCCL_TIMEOUT_S), see rccl_comm.hip
-        self.comm = H.RcclComm(uid, self.rank, self.size, self.device)
+        self.comm = H.RcclComm(uid, self.rank, self.size, self.device, 0.0, *_cta_budget(scope))
+        self.ctas = tuple(self.comm.ctas())  # (min, max); 0 = RCCL's default
         # Normal priority: a high-priority HIP stream measured 2x SLOWER for the
         # whole ResNet-50 step on MI355X (63 vs 32 ms, 1 GPU, profiles/README.md).
-        prio = int(os.environ.get("KUNGFU_COMM_STREAM_PRIORITY", "0"))
+        prio = knobs.get_int("KUNGFU_COMM_STREAM_PRIORITY")
         self.stream = torch.cuda.Stream(device=self.device, priority=prio)
 
     # -- collectives on an explicit stream (default: the comm stream) ---------
@@ -469,6 +471,86 @@ class HostComm(_StreamOrdered):
 HostStagedComm = HostComm
 
 
+class EmulatedComm(_StreamOrdered):
+    """One-GPU stand-in for the all-reduces of an ``ranks``-rank job (``bench.py --emulate-comm``,
+    ``KUNGFU_COMM_EMULATE="ranks=8,ctas=16,busbw=350,lat_us=25"``): every all-reduce of B bytes
+    launches ``comm_emu.hip`` on the comm stream -- ``ctas`` workgroups, resident for the
+    modelled ring time 2(r-1)/r * B / busbw + lat, streaming the ~4(r-1)/r * B bytes of local HBM
+    traffic such an all-reduce makes -- so its cost to the overlapped backward (CUs, HBM,
+    stream ordering) shows up in a 1-GPU step time.  The data is NOT reduced (one rank: the
+    gradient already is the average).  A model: no inter-rank skew, no link congestion."""
+
+    plane = "emulate"
+
+    def __init__(self, spec: str):
+        kv = dict(p.split("=", 1) for p in spec.split(",") if "=" in p)
+        self.ranks = int(kv.get("ranks", 8))
+        self.ctas_n = int(kv.get("ctas", 16))
+        self.busbw = float(kv.get("busbw", 350.0)) * 1e9  # bytes/s
+        self.lat = float(kv.get("lat_us", 25.0)) * 1e-6
+        self.scope = "global"
+        self.version = runtime.cluster_version()
+        self.rank, self.size = 0, 1
+        self.device = torch.cuda.current_device()
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.comm = self
+        self.ctas = (self.ctas_n, self.ctas_n)
+        self._scratch = None
+        self.calls = 0
+        self.modelled_s = 0.0
+
+    def model_seconds(self, nbytes: int) -> float:
+        r = self.ranks
+        return 2.0 * (r - 1) / r * nbytes / self.busbw + self.lat
+
+    def all_reduce(self, inp, out=None, op="sum", stream=None, tag=""):
+        out = inp if out is None else out
+        if out is not inp:
+            out.copy_(inp)
+        nb = inp.numel() * inp.element_size()
+        nb16 = max(16, (nb + 15) // 16 * 16)
+        if self._scratch is None or self._scratch.numel() < 2 * nb16:
+            self._scratch = torch.empty(2 * nb16, dtype=torch.uint8, device=inp.device)
+        src, dst = self._scratch[:nb16], self._scratch[nb16:2 * nb16]
+        s = stream if stream is not None else self.stream
+        sp = s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
+        r = self.ranks
+        t = self.model_seconds(nb)
+        hip().comm_emulate(src, dst, int(4 * (r - 1) / r * nb), self.ctas_n, t, sp)
+        self.calls += 1
+        self.modelled_s += t
+        return out
+
+    monitored_all_reduce = all_reduce
+
+    def broadcast(self, t, root: int = 0, stream=None, tag=""):
+        return t
+
+    def watch(self, what: str, stream=None):
+        pass
+
+    def destroy(self):
+        self.comm = None
+
+    def describe(self) -> dict:
+        return {"ranks": self.ranks, "ctas": self.ctas_n, "busbw_gbs": self.busbw / 1e9, "lat_us": self.lat * 1e6,
+                "calls": self.calls, "modelled_comm_ms_total": round(self.modelled_s * 1e3, 3)}
+
+
+def _cta_budget(scope: str):
+    """(min, max) RCCL CTAs for a communicator of ``scope``: KUNGFU_RCCL_{MIN,MAX}_CTAS, with
+    per-scope overrides KUNGFU_RCCL_{MIN,MAX}_CTAS_<SCOPE> (``local``, ``local_bcast``); 0 = RCCL
+    default.  The hierarchical mode's two local communicators run concurrently from two
+    threads: giving each at most half the chip keeps their kernels co-resident."""
+    key = scope.upper().replace(":", "_")
+
+    def get(kind):
+        v = os.environ.get("KUNGFU_RCCL_%s_CTAS_%s" % (kind, key), os.environ.get("KUNGFU_RCCL_%s_CTAS" % kind, "0"))
+        return int(v or 0)
+
+    return get("MIN"), get("MAX")
+
+
 def _colocate_env() -> None:
     """``KUNGFU_RCCL_COLOCATE=1``: several RCCL ranks on ONE GPU (tests on a one-GPU box).
     RCCL rejects two ranks of one communicator on the same device of the same host
@@ -485,6 +567,10 @@ def _colocate_env() -> None:
 
 def _use_host_staging() -> bool:
     return os.environ.get("KUNGFU_GPU_DATAPLANE", "rccl") == "host"
+
+
+def _emulate_spec() -> str:
+    return os.environ.get("KUNGFU_COMM_EMULATE", "")
 
 
 def flush_strategy_stats() -> None:
@@ -513,7 +599,10 @@ def get_device_comm(scope: str = "global", device=None):
 
     _ensure()
     cpu = device is not None and torch.device(device).type == "cpu"
-    kind = "cpu" if cpu else ("staged" if _use_host_staging() else "rccl")
+    emu = _emulate_spec()
+    if emu and runtime.size() != 1:
+        raise RuntimeError("KUNGFU_COMM_EMULATE models an N-rank job on ONE rank; this job has %d" % runtime.size())
+    kind = "cpu" if cpu else ("emulate" if emu and scope == "global" else "staged" if _use_host_staging() else "rccl")
     with _lock:
         ver = runtime.cluster_version()
         cur = _comms.get((scope, kind))
@@ -524,6 +613,8 @@ def get_device_comm(scope: str = "global", device=None):
                 cur = HostComm(scope, device="cpu")
             elif kind == "staged":
                 cur = HostComm(scope)
+            elif kind == "emulate":
+                cur = EmulatedComm(emu)
             else:
                 cur = DeviceComm(scope)
             _comms[(scope, kind)] = cur

@@ -104,13 +104,16 @@ class _CrossHostStage:
         self.th = threading.Thread(target=self._loop, name="kungfu-cross-host", daemon=True)
         self.th.start()
 
-    def submit(self, g: torch.Tensor, tag: str):
+    def submit(self, g: torch.Tensor, tag: str, post=None):
+        """``post()``: issued on the stage stream after the local broadcast (e.g. the cast of
+        a bf16 wire buffer back into the f32 gradient) -- it must not run on the comm stream,
+        which is not ordered after this stage's work."""
         ev = None
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(self.r.comm.stream)
         self.seq += 1
-        self.q.put((g, ev, tag, self.seq))
+        self.q.put((g, ev, tag, self.seq, post))
 
     def _loop(self):
         from .._lib import dtype_code, op_code, runtime
@@ -122,7 +125,7 @@ class _CrossHostStage:
             if item is None:
                 self.q.task_done()
                 return
-            g, ev, tag, seq = item
+            g, ev, tag, seq, post = item
             try:
                 ctx = torch.cuda.stream(self.stream) if self.cuda else contextlib.nullcontext()
                 with ctx:
@@ -141,6 +144,8 @@ class _CrossHostStage:
                         if self.cuda:
                             g.copy_(h)
                     self.bcast.broadcast(g, root=0, stream=self.stream, tag=tag + " (local broadcast)")
+                    if post is not None:
+                        post()
             except BaseException as e:  # noqa: BLE001 -- re-raised by drain()
                 self.err = e
             self.q.task_done()
@@ -413,15 +418,27 @@ class GradReducer:
             c = self._cbuf[b.start:b.end]
             with comm.on_stream():
                 hip().cast_copy(c, g, 1.0)
-            self._reduce(comm, c)
-            with comm.on_stream():
+
+            def cast_back():  # on whichever stream the reduction of ``c`` ends
                 hip().cast_copy(g, c, 1.0)
+
+            self._reduce(comm, c, post=cast_back)
         else:
             self._reduce(comm, g)
 
-    def _reduce(self, comm, g):
+    def _reduce(self, comm, g, post=None):
+        """Reduce ``g`` in place; ``post()`` is then issued on the stream the reduction ends
+        on (the comm stream, or the cross-host stage's stream)."""
         if self.hierarchical:
-            return self._reduce_hierarchical(comm, g)
+            if self._reduce_hierarchical(comm, g, post):
+                return
+        else:
+            self._reduce_flat(comm, g)
+        if post is not None:
+            with comm.on_stream():
+                post()
+
+    def _reduce_flat(self, comm, g):
         if not self.graph:
             # one rank: the average IS the sum, and RCCL's in-place one-rank sum is free while
             # its one-rank average is a scaled copy of the bucket (oneRankReduce<PreMulSum>:
@@ -437,21 +454,23 @@ class GradReducer:
             with comm.on_stream():
                 g.mul_(1.0 / comm.size)
 
-    def _reduce_hierarchical(self, comm, g):
+    def _reduce_hierarchical(self, comm, g, post=None) -> bool:
         """Local reduce to the host's root on the comm stream; then either (one host) the
         local broadcast right behind it -- all stream-ordered, no host sync -- or (several
         hosts) hand the bucket to the cross-host stage, which runs the host all-reduce among
-        the local roots and the local broadcast on its own thread and stream."""
+        the local roots, the local broadcast and ``post`` on its own thread and stream.
+        Returns True when ``post`` was handed over (the caller must not issue it)."""
         from .._lib import runtime
 
         comm.reduce(g, op="sum", root=0, tag=self._tag + " (local reduce)")
         if self._hier is not None:
-            self._hier.submit(g, self._tag)
-            return
+            self._hier.submit(g, self._tag, post)
+            return True
         if self.op == "avg" and comm.rank == 0:
             with comm.on_stream():
                 g.mul_(1.0 / runtime.size())
         comm.broadcast(g, root=0, tag=self._tag + " (local broadcast)")
+        return False
 
     def _finish(self):
         from .mixed import SideStream

@@ -38,6 +38,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import knobs
 from .flat import FlatParamSpace
 
 # id(param) -> (space, index) for parameters whose gradients go to space.sink
@@ -114,7 +115,7 @@ class SideStream:
     event recorded so far (:meth:`join`) -- the join is deferred to the bucket launch / the
     end of backward instead of the end of each layer."""
 
-    enabled = os.environ.get("KUNGFU_WGRAD_STREAM", "0") == "1"
+    enabled = knobs.get("KUNGFU_WGRAD_STREAM") == "1"
     _streams: Dict[int, torch.cuda.Stream] = {}
     _pending: list = []
 

@@ -43,6 +43,21 @@ def test_bench_self_launches_and_verifies_replicas():
     assert v["world_size"] == 2 and v["comm_ranks"] == 2 and v["launch"] == "torchrun"
     assert v["replicas_consistent"] is True
     assert v["per_rank_img_s"]["min"] <= v["per_rank_img_s"]["max"]
+    pf = v["preflight"]
+    assert pf["ok"] is True and pf["ranks"] == 2 and pf["errors"] == [], pf
+
+
+def test_bench_preflight_names_the_failing_rank():
+    """VERDICT r3 #1a: a corrupted contribution fails the pre-flight on every rank, before any
+    training step, with exit status 5 and the failing rank named."""
+    t0 = time.time()
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--model", "resnet18",
+                "--batch", "2", "--image-size", "32"],
+               env={"KUNGFU_PREFLIGHT_CORRUPT": "1", "KUNGFU_PREFLIGHT_CORRUPT_WHAT": "allreduce"})
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert "pre-flight failed" in r.stderr and "all-reduce check failed" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")], r.stdout
+    assert time.time() - t0 < 120
 
 
 def test_bench_refuses_mislabelled_world():

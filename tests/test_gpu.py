@@ -300,6 +300,29 @@ def test_conv3x3_mfma_matches_torch(shape):
 
 
 @needs_gpu
+def test_conv_over_2gib_falls_back():
+    """the conv kernels' buffer-resource staging addresses < 2 GiB per operand; larger
+    inputs must not be routed to them (they used to raise inside forward) but fall back."""
+    import torch.nn.functional as F
+
+    from kungfu_amd.ops.conv import conv3x3, eligible, rect_eligible
+
+    x = torch.zeros(1, 64, 4096, 4100, device="cuda", dtype=torch.bfloat16).to(memory_format=torch.channels_last)
+    assert x.numel() * 2 >= 1 << 31
+    w = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).bfloat16().to(memory_format=torch.channels_last)
+    assert not eligible(x, w, 1, 1, 1, 1) and not rect_eligible(x, w, 1, 1, 1, 1)
+    xs = x[:, :, :64, :64]
+    assert eligible(xs.contiguous(memory_format=torch.channels_last), w, 1, 1, 1, 1)
+    x[:, :, 5:9, 7:11] = 1.0
+    y = conv3x3(x, w, 1)
+    ref = F.conv2d(x[:, :, :16, :16].float(), w.float(), padding=1)
+    assert y.shape == (1, 64, 4096, 4100)
+    assert ((y[:, :, 1:15, 1:15].float() - ref[:, :, 1:15, 1:15]).norm() / ref.norm()).item() < 1e-2
+    del x, y
+    torch.cuda.empty_cache()
+
+
+@needs_gpu
 @pytest.mark.parametrize("shape", [(3, 64, 9, 11, 256, 1, 1), (2, 256, 14, 14, 64, 1, 1), (2, 128, 15, 13, 512, 1, 2),
                                    (2, 64, 10, 12, 64, 3, 1), (3, 128, 9, 9, 256, 3, 2), (1, 512, 7, 7, 512, 3, 1),
                                    (2, 192, 6, 5, 128, 3, 1), (1, 64, 4, 130, 128, 3, 1), (2, 128, 5, 64, 64, 3, 1),
@@ -1648,3 +1671,41 @@ def test_gelu_backward_colsum_matches_torch(T, O):
     torch.testing.assert_close(db.double(), du.double().sum(0), rtol=1e-4, atol=1e-3)
     _, db16 = hip().gelu_backward_colsum(dy, u, torch.bfloat16)
     assert db16.dtype == torch.bfloat16 and ((db16.float() - db).abs() <= db.abs() * 8e-3 + 1e-3).all()
+
+
+@needs_gpu
+def test_comm_emulate_kernel_paces_and_keeps_bucket(H):
+    """comm_emu.hip (bench.py --emulate-comm): resident for the modelled time, copies the
+    requested traffic into the scratch half, never writes the bucket."""
+    b = torch.randn(4 << 20, device="cuda")  # 16 MiB
+    keep = b.clone()
+    scratch = torch.zeros_like(b)
+    s = torch.cuda.current_stream()
+    for secs in (0.0005, 0.004):
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        H.comm_emulate(b, scratch, int(b.numel() * 4 * 1.75), 16, secs, s.cuda_stream)
+        en.record()
+        en.synchronize()
+        ms = st.elapsed_time(en)
+        assert secs * 1e3 * 0.95 < ms < secs * 1e3 * 1.5 + 0.3, (secs, ms)
+    assert torch.equal(b, keep)
+    assert torch.equal(scratch, b)  # 1.75 passes cover every element at least once
+
+
+@needs_gpu
+def test_bench_emulate_comm_model():
+    """bench.py --emulate-comm 8: every bucket all-reduce becomes the emulator on the comm
+    stream; the JSON labels the number a MODEL and reports the emulator's parameters."""
+    import json
+
+    e = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "2", "--batch", "32",
+                        "--emulate-comm", "8", "--emulate-ctas", "8"], cwd=ROOT, env=e, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["metric"].startswith("MODEL") and res["vs_baseline"] is None, res["metric"]
+    em = res["config"]["comm"]["emulated"]
+    assert em["ranks"] == 8 and em["ctas"] == 8 and em["calls"] >= 5 * res["config"]["comm"]["buckets"], em
+    assert res["config"]["comm"]["comm_plane"] == "emulate"

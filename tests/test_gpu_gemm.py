@@ -68,3 +68,90 @@ def test_gemm_accumulate():
     ref = out.float() + x.float() @ w.float().t()
     y = H.gemm(x, w, out=out)[0]
     assert y.data_ptr() == out.data_ptr() and _rel(out, ref) < 1e-2
+
+
+# ---- gemm.hip: the pipelined NT GEMM (BERT's forward / data-gradient products) ----
+@pytest.mark.parametrize("M,K,N", [(16384, 768, 2304), (4096, 3072, 768), (1000, 768, 768), (300, 64, 384),
+                                   (257, 3072, 3072), (5000, 2304, 768)])
+@pytest.mark.parametrize("bn", [-1, 128, 192, 256])
+def test_gemm_nt_matches_fp32(M, K, N, bn):
+    """a[M,K] . b[N,K]^T (+ bias) (+ accumulate into out) vs the fp32 torch product: every tile
+    width, M tails (rows past M read zeros and are not stored), K from one slab up."""
+    H = _hip()
+    if bn > 0 and N % bn:
+        pytest.skip("tile width does not divide N")
+    torch.manual_seed(11)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda").bfloat16()
+    ref = a.float() @ b.float().t()
+    y = H.gemm_nt(a, b, bn=bn)
+    assert y.shape == (M, N) and _rel(y, ref) < 8e-3
+    # asymmetric check of the output map: a one-hot row picks exactly one row of b
+    e = torch.zeros(M, K, device="cuda").bfloat16()
+    e[torch.arange(M), torch.arange(M) % K] = 1
+    pick = H.gemm_nt(e, b, bn=bn)
+    assert torch.equal(pick, b[:, torch.arange(M, device="cuda") % K].t().contiguous())
+    yb = H.gemm_nt(a, b, bias, bn=bn)
+    assert _rel(yb, ref + bias.float()) < 8e-3
+    old = torch.randn(M, N, device="cuda").bfloat16()
+    out = old.clone()
+    H.gemm_nt(a, b, bias, out=out, accumulate=True, bn=bn)
+    assert _rel(out, ref + bias.float() + old.float()) < 8e-3
+
+
+def test_gemm_nt_rejects_bad_shapes():
+    H = _hip()
+    a = torch.randn(64, 100, device="cuda").bfloat16()
+    with pytest.raises(Exception):
+        H.gemm_nt(a, torch.randn(128, 100, device="cuda").bfloat16())  # K % 32
+    a = torch.randn(64, 128, device="cuda").bfloat16()
+    with pytest.raises(Exception):
+        H.gemm_nt(a, torch.randn(100, 128, device="cuda").bfloat16())  # N % 128
+    assert H.gemm_nt_pick_bn(16384, 768) == 192 and H.gemm_nt_pick_bn(16384, 3072) == 256
+
+
+def test_linear_gemm_path_matches_library_path():
+    """ops.linear with KUNGFU_LINEAR_GEMM (forward + data gradient on gemm_nt, W^T from the
+    per-step multi-tensor flip of the bf16 shadow weights) vs the hipBLASLt path: same loss and
+    flat gradients up to bf16 rounding, over two optimizer steps (the W^T cache must refresh)."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
+    from kungfu_amd.ops import linear as lin
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(on):
+        old = lin.set_gemm_enabled(on)
+        try:
+            torch.manual_seed(0)
+            m = BertForPreTraining(layers=2).cuda()
+            for l in m.layers:
+                l.dropout = 0.0
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
+                                                        named_parameters=m.named_parameters())
+            enable_bf16_shadow(m, opt)
+            g = torch.Generator(device="cuda").manual_seed(1)
+            batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
+            losses, grads = [], []
+            for _ in range(2):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = pretraining_loss(m, batch)
+                loss.backward()
+                opt.reducer.synchronize()
+                grads.append(opt.space.flat_grad.clone())
+                losses.append(loss.item())
+                opt.step()
+            torch.cuda.synchronize()
+            return losses, grads
+        finally:
+            lin.set_gemm_enabled(old)
+
+    la, ga = run(False)
+    lb, gb = run(True)
+    for x, y in zip(la, lb):
+        assert abs(x - y) < 2e-3 * abs(x), (la, lb)
+    for x, y in zip(ga, gb):
+        assert _rel(y, x) < 3e-2, _rel(y, x)

@@ -48,13 +48,16 @@ def test_rccl_watchdog_names_stalled_bucket():
     assert "kungfu rccl watchdog" in out and "bucket" in out and "has not completed" in out, out[-4000:]
 
 
-def _bench(env, extra=()):
+def _bench(env, extra=(), expect_rc=0):
     e = dict(os.environ, PYTHONPATH=ROOT, **env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KUNGFU_SELF_SPEC"):
         e.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
                         "--batch", "16"] + list(extra), cwd=ROOT, env=e, stdout=subprocess.PIPE,
                        stderr=subprocess.STDOUT, text=True, timeout=600)
+    if expect_rc != 0:
+        assert r.returncode != 0, r.stdout[-5000:]
+        return r.stdout
     assert r.returncode == 0, r.stdout[-5000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-5000:]
@@ -74,6 +77,24 @@ def test_bench_self_launch_two_ranks(plane):
     assert v["replicas_consistent"] is True, v
     if plane == "rccl":
         assert v["rccl_watchdog"]["ops_watched"] > 0 and v["rccl_watchdog"]["pending"] == 0, v
+    pf = v["preflight"]
+    assert pf["ok"] is True and pf["errors"] == [], pf
+    # one device shared by both ranks: the P2P matrix says so; the value / IPC checks ran
+    assert all(str(x).startswith("n/a") for row in pf["p2p"].values() for x in row.values()), pf["p2p"]
+    assert all(b and b > 0 for b in pf["allreduce_busbw_gbs"].values()), pf
+    assert all(b and b > 0 for b in pf["ipc_pull_gbs"].values()), pf
+
+
+@needs_gpu
+def test_bench_preflight_detects_corrupt_ipc_slot():
+    """VERDICT r3 #1a: rank 1 corrupts its exported IPC buffer; rank 0's pull of it fails the
+    pre-flight on every rank, exit non-zero within seconds, naming the pair 0 <- 1."""
+    import time
+
+    t0 = time.time()
+    out = _bench(dict(COLO, KUNGFU_PREFLIGHT_CORRUPT="1"), expect_rc=1)
+    assert "pre-flight failed" in out and "IPC pull 0 <- 1 failed" in out, out[-4000:]
+    assert time.time() - t0 < 240
 
 
 @needs_gpu
@@ -137,13 +158,15 @@ def test_bench_elastic_bert_gns(plane):
 
 
 @needs_gpu
-def test_hierarchical_bucket_engine_two_fake_hosts_rccl():
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_hierarchical_bucket_engine_two_fake_hosts_rccl(dtype):
     """Hierarchical S-SGD on the GPU with 2 "hosts" x 2 ranks (conftest.run_fake_hosts):
     per bucket a local RCCL reduce, the host all-reduce among the local roots on the
     cross-host thread, a local RCCL broadcast on the second local communicator -- equal to
-    one process on the global batch."""
+    one process on the global batch.  bf16: the wire buffer is cast back into the f32
+    gradient on the cross-host stage's stream, after the broadcast."""
     from conftest import run_fake_hosts
 
-    rcs, text = run_fake_hosts([worker("ssgd_exact.py"), "f32", "cuda", "hier"], env=COLO, timeout=300)
+    rcs, text = run_fake_hosts([worker("ssgd_exact.py"), dtype, "cuda", "hier"], env=COLO, timeout=300)
     assert all(rc == 0 for rc in rcs), text[-5000:]
     assert text.count("SSGD_EXACT_OK") == 4 and "hier=True" in text, text[-5000:]

@@ -65,8 +65,12 @@ if rccl:
     assert slowed.sum() >= 1, (slowed, ad.throughputs)
 else:
     assert ad.changed and ad.switched_at is not None and ad.switched_at > 3, (ad.switched_at, ad.throughputs)
-    if kind == "cpu":  # the host plane on CPU is quiet enough to pin the cause: the injected slowdown
-        assert ad.switched_at >= 8, (ad.switched_at, ad.throughputs)
+    if kind == "cpu" and ad.switched_at < 8:
+        # switched before the injected slowdown: only acceptable when the statistics really showed
+        # a slowdown then (a loaded CI machine stalls the host transport too); the vote must have
+        # had the evidence it acted on
+        early = [t for t in ad.throughputs[3:ad.switched_at] if t]
+        assert early and min(early) < 0.5 * max(tps[:6]), (ad.switched_at, ad.throughputs)
     assert tps[-1] < 0.5 * max(tps[2:6]), ad.throughputs  # the slowdown is visible in the statistics
     after = runtime.global_strategy_pairs()
     assert after != before, (before, after)

@@ -2,6 +2,7 @@
 # A/B of two builds of the HIP extension on the ResNet-50 bench (box-local swap of the .so):
 #   tools/gpu_ab_so.sh <alt.so> <tag> [bench args...]
 set -o pipefail
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 ALT=$1; TAG=$2; shift 2

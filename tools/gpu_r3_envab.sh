@@ -2,6 +2,7 @@
 # A/B of one environment variable on a model bench (1 GPU):
 #   tools/gpu_r3_envab.sh <VAR> <a> <b> <tag> [bench args...]
 set -o pipefail
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 VAR=$1; A=$2; B=$3; TAG=$4; shift 4

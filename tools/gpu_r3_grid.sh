@@ -1,6 +1,7 @@
 #!/bin/bash
 # BN apply grid cap (KUNGFU_BN_MAXGRID) x non-temporal mode (KUNGFU_BN_NT) on the ResNet-50 bench.
 set -o pipefail
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 for cfg in "1 2048" "1 1024" "1 4096" "3 1024" "1 2048" "0 2048"; do

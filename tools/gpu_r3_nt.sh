@@ -2,6 +2,7 @@
 # BN apply passes with non-temporal loads/stores (KUNGFU_BN_NT bit 0 loads, bit 1 stores):
 # streaming micro-benchmark + ResNet-50 bench A/B.
 set -o pipefail
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 hipcc -O3 --offload-arch=gfx950 tools/stream_bw.hip -o /tmp/stream_bw || exit 1

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Weight gradients on a side stream (KUNGFU_WGRAD_STREAM): numerics test + ResNet-50 A/B.
 set -o pipefail
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 cd "$GRAFT_REPO_ROOT"
 OUT=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p "$OUT"
 timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_gpu_engine.py -k side_stream > "$OUT/r3k_side_test.log" 2>&1

@@ -1,5 +1,6 @@
 #!/bin/bash
 cd "$GRAFT_REPO_ROOT"
+export KUNGFU_DEV_KNOBS=1  # A/B of developer knobs (kungfu_amd/knobs.py)
 OUT=gpurun_out; mkdir -p $OUT
 run() {  # tag, env...
   tag=$1; shift
