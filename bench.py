@@ -69,6 +69,11 @@ def _setup_env():
     # message naming the op and rank (exit 3) instead of hanging until an outer timeout
     os.environ.setdefault("KUNGFU_RCCL_TIMEOUT_S", "300")
     os.environ.setdefault("KUNGFU_OP_TIMEOUT_S", "900")
+    if world > 1:
+        # >= 16 workgroups per gradient all-reduce: with fewer, the emulated 8-rank collectives
+        # could not keep up with backward (profiles/r4_comm_emulation.md: 4 CTAs +1.9-3.4 ms/step,
+        # 16-32 CTAs +0.3 ms); a floor only -- RCCL may use more
+        os.environ.setdefault("KUNGFU_RCCL_MIN_CTAS", "16")
 
 
 def _launcher_env() -> bool:
@@ -250,6 +255,9 @@ def main():
     p.add_argument("--bf16-shadow", type=int, default=1,
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
     p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--graph", type=int, default=0,
+                   help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
+                        "(kungfu_amd.parallel.graphs.GraphedStep)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -387,6 +395,13 @@ def main():
 
     if a.elastic:
         return _elastic_loop(a, model, opt, step, sync, bert)
+    graphed = None
+    if a.graph and cuda:
+        from kungfu_amd.parallel.graphs import GraphedStep
+
+        graphed = GraphedStep(step, opt, warmup=3)
+        step = graphed
+        a.warmup = max(a.warmup, 4)  # the capture happens inside warm-up
 
     preflight = None
     if size > 1 and a.preflight:
@@ -448,7 +463,13 @@ def main():
     from kungfu_amd._lib import hip as _hip_mod
 
     try:
+        # every collective has completed (synchronised above); give the watchdog thread (50 ms
+        # poll period) a moment to retire their events before reading its counters
+        t_wd = time.time() + 2.0
         wd = dict(_hip_mod().rccl_watchdog_info())
+        while wd["pending"] and time.time() < t_wd:
+            time.sleep(0.02)
+            wd = dict(_hip_mod().rccl_watchdog_info())
     except Exception:
         wd = None
     verify = {
@@ -499,6 +520,8 @@ def main():
             "optimizer": "%s(%s)" % (a.optimizer, opt_desc),
             "fused_bn_hip": bool(fused_bn),
             "bf16_shadow_weights": bool(a.bf16_shadow),
+            "hip_graph": ({"replays": graphed.replays, "captured": graphed.graph is not None}
+                          if graphed is not None else False),
             "per_gpu_img_s": round(value / size, 2),
             "tokens_per_s": round(value * a.seq_len, 1) if bert else None,
             "gradient_noise_scale": (opt.noise_scale if a.optimizer == "gns" else None),

@@ -138,7 +138,13 @@ struct AttnArgs {
     float scale;
     uint32_t seed, thresh;
     float inv_keep;
+    const uint32_t *seed_base;  // device word mixed into the seed (graph replays advance it), or null
 };
+
+// the per-call seed mixed with the device seed base (dropout_seed_base)
+__device__ __forceinline__ uint32_t call_seed(const AttnArgs &a) {
+    return a.seed_base ? a.seed ^ (a.seed_base[0] * 0x85EBCA6Bu) : a.seed;
+}
 
 template <int S>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
@@ -148,6 +154,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     __shared__ __attribute__((aligned(1024))) uint8_t lds[3 * S * 128 + S * PROW];
     uint8_t *Qi = lds, *Ki = lds + S * 128, *Vi = lds + 2 * S * 128, *Pi = lds + 3 * S * 128;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t seed = call_seed(a);
     const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
     const int D = a.H * DH, RS = 3 * D;  // qkv row stride (elements)
     const uint16_t *base = a.qkv + static_cast<int64_t>(b) * S * RS + h * DH;
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
             for (int j = 0; j < TK; ++j) {
                 const int key = 16 * j + lc;
                 float p = acc[i][j][r] * inv;
-                p = keep_elem(a.seed, bh, row, key, a.thresh) ? p * a.inv_keep : 0.f;
+                p = keep_elem(seed, bh, row, key, a.thresh) ? p * a.inv_keep : 0.f;
                 *reinterpret_cast<uint16_t *>(Pi + off<PROW>(row, key)) = bf16_bits(p);
             }
         }
@@ -243,6 +250,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
     uint8_t *Qi = lds, *Ki = lds + S * 128, *Vi = lds + 2 * S * 128, *Oi = lds + 3 * S * 128;  // Oi: dO
     uint8_t *Pi = lds + 4 * S * 128, *Si = Pi + S * PROW;                                      // P_drop, dS
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t seed = call_seed(a);
     const int bh = blockIdx.x, b = bh / a.H, h = bh - b * a.H;
     const int D = a.H * DH, RS = 3 * D;
     const uint16_t *base = a.qkv + static_cast<int64_t>(b) * S * RS + h * DH;
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
             for (int j = 0; j < TK; ++j) {
                 const int key = 16 * j + lc;
                 const float p = __expf(sc[i][j][r] * a.scale - l);
-                const bool kp = keep_elem(a.seed, bh, row, key, a.thresh);
+                const bool kp = keep_elem(seed, bh, row, key, a.thresh);
                 const float pd = kp ? p * a.inv_keep : 0.f;
                 const float dpd = kp ? dp[i][j][r] * a.inv_keep : 0.f;
                 *reinterpret_cast<uint16_t *>(Pi + off<PROW>(row, key)) = bf16_bits(pd);
@@ -396,6 +404,7 @@ AttnArgs make_args(const uint16_t *qkv, uint16_t *out, float *lse, const uint16_
                    float scale, uint32_t seed, float p_drop) {
     AttnArgs a;
     a.qkv = qkv, a.out = out, a.lse = lse, a.dout = dout, a.dqkv = dqkv, a.H = H, a.scale = scale, a.seed = seed;
+    a.seed_base = dropout_seed_base();
     const double t = static_cast<double>(p_drop) * 4294967296.0;
     a.thresh = p_drop <= 0.f ? 0u : (t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t));
     a.inv_keep = p_drop < 1.f ? 1.f / (1.f - p_drop) : 0.f;

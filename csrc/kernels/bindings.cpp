@@ -1843,6 +1843,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("bn") = -1,
           "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
     m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
+    m.def(
+        "set_dropout_seed_base",
+        [](c10::optional<at::Tensor> t) {
+            if (!t || !t->defined()) {
+                kfk::set_dropout_seed_base(nullptr);
+                return;
+            }
+            TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1 && t->is_contiguous(),
+                        "set_dropout_seed_base: a contiguous int32 GPU tensor (kept alive by the caller)");
+            kfk::set_dropout_seed_base(reinterpret_cast<const uint32_t *>(t->data_ptr()));
+        },
+        py::arg("base"), "device word mixed into every hashed dropout seed (None: host seeds only)");
     m.def("gemm_nt_pick_bn", &kfk::gemm_nt_pick_bn);
     m.def("comm_emulate", &comm_emulate, py::arg("bucket"), py::arg("scratch"), py::arg("traffic_bytes"),
           py::arg("ctas"), py::arg("seconds"), py::arg("stream") = 0,

@@ -106,7 +106,10 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint8_t *p0, const uint8_t *p1) 
 // KS = 1 | 3 (pad (KS-1)/2), or 0: a KH x KW window with padding (g.kwin, g.ph, g.pw) at run
 // time (Inception-v3's 1x7 / 7x1 / 1x3 / 3x1 / 5x5 / 3x3-pad-0).  Channel counts that are not
 // multiples of the tile: channels past Cout / Cin read the zero page, their outputs are dropped.
-template <int KS, int S, int WM, int WN, int STAGES, int TN = 4>
+// KB: pixels per staged K-step (64, or 32 with a deeper ring: the 256x256 tile holds only two
+// 64-deep stages -- every K-step then waits for ALL its LDS-DMA -- but four 32-deep ones, which
+// keep two K-steps in flight across the barrier; gemm.hip uses the same structure).
+template <int KS, int S, int WM, int WN, int STAGES, int TN = 4, int KB = 64>
 __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__restrict__ dy,
                                                              const uint16_t *__restrict__ x,
                                                              float *__restrict__ part, void *__restrict__ dw,
@@ -118,10 +121,11 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     constexpr int ROWA = BM * 2, ROWB = BN * 2;  // bytes per staged pixel row
     constexpr int CPRA = ROWA / 16, CPRB = ROWB / 16;
     constexpr int RPIA = 64 / CPRA, RPIB = 64 / CPRB;  // rows per 1 KB glds instruction
-    constexpr int A_BYTES = kBK * ROWA, B_BYTES = kBK * ROWB, STAGE = A_BYTES + B_BYTES;
-    constexpr int A_INST = kBK / RPIA / NW, B_INST = kBK / RPIB / NW;
+    constexpr int A_BYTES = KB * ROWA, B_BYTES = KB * ROWB, STAGE = A_BYTES + B_BYTES;
+    constexpr int A_INST = KB / RPIA / NW, B_INST = KB / RPIB / NW;
     constexpr int LOADS = A_INST + B_INST;
-    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * RPIA == kBK && B_INST * NW * RPIB == kBK, "split");
+    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * RPIA == KB && B_INST * NW * RPIB == KB, "split");
+    static_assert(KB == 32 || KB == 64, "K-step of 32 or 64 pixels");
     constexpr bool IDENT = KS == 1 && S == 1;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
 
@@ -137,9 +141,9 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     const int kh = tap / kwin, kw = tap - kh * kwin;
     const int pad_h = KS > 0 ? PAD : g.ph, pad_w = KS > 0 ? PAD : g.pw;
     const int m0 = mt * BM, n0 = nt * BN;
-    const int p_begin = split * g.kps * kBK;
-    int nsteps = (g.P - p_begin + kBK - 1) / kBK;
-    if (nsteps > g.kps) nsteps = g.kps;
+    const int p_begin = split * g.kps * kBK;  // the plan's splits are in 64-pixel steps
+    int nsteps = (g.P - p_begin + KB - 1) / KB;
+    if (nsteps > g.kps * (kBK / KB)) nsteps = g.kps * (kBK / KB);
 
     // ---- staging descriptors: lane l of an instruction writes image bytes [16l, 16l+16)
     int a_row[A_INST], a_col[A_INST];
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kWBufOOB), kWBufFlags);
 #endif
     auto stage = [&](int ks, int buf) {
-        const int p0 = p_begin + ks * kBK;
+        const int p0 = p_begin + ks * KB;
         uint8_t *abase = lds + buf * STAGE;
         uint8_t *bbase = abase + A_BYTES;
 #pragma unroll
@@ -262,24 +266,36 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *abase = lds + buf * STAGE;
         const uint8_t *bbase = abase + A_BYTES;
-        bf16x8 af0[4], bf0[TN], af1[4], bf1[TN];
+        bf16x8 af0[4], bf0[TN];
 #pragma unroll
         for (int i = 0; i < 4; ++i) af0[i] = tr_frag(abase + aoff[i], abase + aoff[i] + 4 * ROWA);
 #pragma unroll
         for (int j = 0; j < TN; ++j) bf0[j] = tr_frag(bbase + boff[j], bbase + boff[j] + 4 * ROWB);
+        if constexpr (KB == 64) {
+            bf16x8 af1[4], bf1[TN];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af1[i] = tr_frag(abase + aoff[i] + 32 * ROWA, abase + aoff[i] + 36 * ROWA);
+            for (int i = 0; i < 4; ++i) af1[i] = tr_frag(abase + aoff[i] + 32 * ROWA, abase + aoff[i] + 36 * ROWA);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) bf1[j] = tr_frag(bbase + boff[j] + 32 * ROWB, bbase + boff[j] + 36 * ROWB);
-        mfma_block(af0, bf0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (!early && !late && ks + STAGES - 1 < nsteps) {
-            int nb = buf + STAGES - 1;
-            if (nb >= STAGES) nb -= STAGES;
-            stage(ks + STAGES - 1, nb);
+            for (int j = 0; j < TN; ++j) bf1[j] = tr_frag(bbase + boff[j] + 32 * ROWB, bbase + boff[j] + 36 * ROWB);
+            mfma_block(af0, bf0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!early && !late && ks + STAGES - 1 < nsteps) {
+                int nb = buf + STAGES - 1;
+                if (nb >= STAGES) nb -= STAGES;
+                stage(ks + STAGES - 1, nb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_block(af1, bf1);
+        } else {
+            // one 32-deep sub-step: stage the slot read at ks-1 first, then compute
+            if (!early && !late && ks + STAGES - 1 < nsteps) {
+                int nb = buf + STAGES - 1;
+                if (nb >= STAGES) nb -= STAGES;
+                stage(ks + STAGES - 1, nb);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_block(af0, bf0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_block(af1, bf1);
         if (late && ks + STAGES - 1 < nsteps) {
             __builtin_amdgcn_sched_barrier(0);
             int nb = buf + STAGES - 1;
@@ -916,9 +932,24 @@ void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, cons
     if (KUNGFU_WGRAD_BUFLD && (static_cast<int64_t>(g.P) * g.K * 2 >= kWBufOOB ||
                                static_cast<int64_t>(g.N) * g.H * g.W * g.C * 2 >= kWBufOOB))
         throw std::invalid_argument("conv_wgrad: dy or x of 2 GiB or more (buffer-resource staging)");
-    wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
-        dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out,
-        stagger);
+    // 256x256 tiles: four 32-pixel stages (two K-steps in flight across each barrier) instead of two
+    // 64-pixel ones (KUNGFU_WGRAD_KB32, A/B)
+    static const int kb32 = dev_knob("KUNGFU_WGRAD_KB32", 0);
+    if constexpr (TN == 8) {
+        if (kb32) {
+            wgrad_kernel<KS, S, WM, WN, 4, TN, 32><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
+                dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out,
+                stagger);
+        } else {
+            wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
+                dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate,
+                atomic_out, stagger);
+        }
+    } else {
+        wgrad_kernel<KS, S, WM, WN, STAGES, TN><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(
+            dy, x, part, dw, reinterpret_cast<const uint16_t *>(zero_page()), g, out_f32, accumulate, atomic_out,
+            stagger);
+    }
     if (g.splits > 1 && !atomic_out) {
         const int64_t total = static_cast<int64_t>(g.tiles) * (64 * WM) * (16 * TN * WN) / 4;
         int sgl = 0;  // split groups: enough blocks for the chip, at most 64 groups, <= splits

@@ -495,4 +495,10 @@ void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, f
     }
 }
 
+namespace {
+const uint32_t *g_dropout_seed_base = nullptr;
+}
+void set_dropout_seed_base(const uint32_t *p) { g_dropout_seed_base = p; }
+const uint32_t *dropout_seed_base() { return g_dropout_seed_base; }
+
 }  // namespace kfk

@@ -15,6 +15,12 @@ constexpr int kMaxGridHost = 2048;  // == kMaxGrid in common.hpp (partials scrat
 // K1: z = op(x, y) elementwise.  dtype/op codes as kungfu::DType / ReduceOp.
 void launch_reduce(void *z, const void *x, const void *y, size_t n, int dtype, int op, hipStream_t s);
 
+// Device word mixed into every hashed dropout seed (attention, add+LayerNorm): a graph replay
+// re-uses the host seeds recorded at capture, so kungfu_amd.ops.dropout_seed advances this word
+// before each replay instead (null: host seeds only).  Defined in flat_ops.hip.
+void set_dropout_seed_base(const uint32_t *p);
+const uint32_t *dropout_seed_base();
+
 // gemm.hip: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (+ C) in bf16, f32 accumulation, on a
 // 256 x bn tile (bn 128 | 192 | 256, <= 0: by shape) with a 3-slab-deep LDS-DMA pipeline.
 constexpr int kGemmBias = 1, kGemmAccum = 2;

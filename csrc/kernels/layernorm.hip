@@ -48,7 +48,13 @@ struct LnDrop {
     uint32_t seed = 0, thresh = 0;  // keep(e) <=> hash(seed, e) >= thresh (thresh = p * 2^32)
     float inv_keep = 1.f;
     bool on = false;
+    const uint32_t *base = nullptr;  // device seed base (dropout_seed_base), mixed in at kernel entry
 };
+
+// the kernel-entry seed: the call's host seed mixed with the device seed base
+__device__ __forceinline__ void ln_seed(LnDrop &d) {
+    if (d.on && d.base) d.seed ^= d.base[0] * 0x85EBCA6Bu;
+}
 
 __device__ __forceinline__ bool ln_keep(const LnDrop &d, int64_t e) {
     uint32_t h = static_cast<uint32_t>(e) * 0x9E3779B1u ^ static_cast<uint32_t>(e >> 32) * 0x7FEB352Du ^ d.seed;
@@ -68,6 +74,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_fwd_kernel(const uint2 *__re
                                                                uint2 *__restrict__ s_out, float *__restrict__ mean,
                                                                float *__restrict__ rstd, int64_t rows, float eps,
                                                                LnDrop drop) {
+    ln_seed(drop);
     constexpr int D = 256 * G;
     const int lane = threadIdx.x & 63;
     float gm[G][4], bt[G][4];
@@ -139,6 +146,7 @@ __global__ __launch_bounds__(64 * kLnWaves) void ln_bwd_kernel(const uint2 *__re
                                                                const float *__restrict__ rstd, uint2 *__restrict__ ds,
                                                                float *__restrict__ partial, int64_t rows,
                                                                uint2 *__restrict__ dr, LnDrop drop) {
+    ln_seed(drop);
     constexpr int D = 256 * G;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float gm[G][4], dg[G][4], db[G][4], rb[RB ? G : 1][4];
@@ -278,6 +286,7 @@ static LnDrop make_drop(float p, uint32_t seed) {
         if (p >= 1.f) throw std::invalid_argument("layernorm: dropout p must be < 1");
         d.on = true;
         d.seed = seed;
+        d.base = dropout_seed_base();
         d.thresh = static_cast<uint32_t>(static_cast<double>(p) * 4294967296.0);
         d.inv_keep = 1.f / (1.f - p);
     }

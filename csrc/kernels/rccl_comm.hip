@@ -400,6 +400,11 @@ void RcclComm::enq(int r, const char *what) {
 }
 
 void RcclComm::watch(hipStream_t s, const std::string &what) {
+    // inside a hipGraph capture the collective is a graph node, not work in flight: an event
+    // recorded now would never complete as such (and querying it from the watchdog thread is
+    // not allowed during capture) -- graph replays are not watched
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return;
     char buf[64];
     std::snprintf(buf, sizeof(buf), " #%llu on rank %d/%d", ++seq_, rank_, size_);
     Watchdog::get().add(s, what + buf);

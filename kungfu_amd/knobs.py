@@ -113,6 +113,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_CONV_PERSIST_BLOCKS": _d("0", "persistent conv blocks for the statistics epilogues (0 = 4/CU)"),
     "KUNGFU_WGRAD_STAGGER": _d("-1", "wgrad staging stagger (-1 = on for 256x256 tiles only)"),
     "KUNGFU_WROWS_STAGGER": _d("1", "row-image wgrad staging stagger"),
+    "KUNGFU_WGRAD_KB32": _d("0", "256x256 weight-gradient tiles with four 32-pixel LDS stages"),
     "KUNGFU_WGRAD_STREAM": _d("0", "weight gradients on a side stream (-1.2 %)"),
     "KUNGFU_BN_NT": _d("1", "BN non-temporal policy (0 none, 1 loads, 2 stores, 3 both)"),
     "KUNGFU_BN_MAXGRID": _d("0", "BN apply grid cap (0 = kernel default)"),

@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from .._lib import hip, hip_available
+from . import dropout_seed
 
 
 class _AttnFn(torch.autograd.Function):
@@ -48,6 +49,7 @@ def self_attention(qkv: torch.Tensor, heads: int, p: float = 0.0) -> torch.Tenso
     B, S, D3 = qkv.shape
     if eligible(qkv, heads):
         seed = int(torch.randint(0, 2**31 - 1, (1,)).item())  # CPU generator: no device sync
+        dropout_seed.base(qkv.device)  # registers the device seed word (graph replays advance it)
         return _AttnFn.apply(qkv, heads, float(p), seed)
     dh = D3 // (3 * heads)
     q, k, v = qkv.view(B, S, 3, heads, dh).permute(2, 0, 3, 1, 4)

@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from .. import knobs
 from .._lib import hip, hip_available
+from . import dropout_seed
 
 import os
 
@@ -83,6 +84,8 @@ def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: to
     p = float(dropout) if training and residual is not None else 0.0
     if _eligible(x, residual, weight):
         seed = int(torch.randint(0, 2**31 - 1, (1,)).item()) if p > 0 else 0  # CPU generator: no device sync
+        if p > 0:
+            dropout_seed.base(x.device)  # registers the device seed word (graph replays advance it)
         bl = (getattr(residual, "_kf_blink", None) if bias_link and _BIAS_LINK and residual is not None
               and x.shape[-1] <= 2048 else None)
         return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed, bl)

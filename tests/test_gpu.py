@@ -1266,7 +1266,9 @@ def test_fused_attention_matches_fp32(S, p):
     x = qkv.detach().float().requires_grad_(True)
     q, k, v = x.view(B, S, 3, H, 64).permute(2, 0, 3, 1, 4)
     P = torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1)
-    keep = dropout_keep(seed, B, H, S, p, device="cuda")
+    from kungfu_amd.ops import dropout_seed
+
+    keep = dropout_keep(dropout_seed.effective(seed), B, H, S, p, device="cuda")
     if p > 0:
         frac = keep.float().mean().item()
         assert abs(frac - (1 - p)) < 0.01, frac

@@ -17,6 +17,8 @@ ROUNDS = int(os.environ.get("ROUNDS", "5"))
 # (name, K = in-features of the product, N = out-features); forward then data-gradient products
 SHAPES = [("qkv", 768, 2304), ("out", 768, 768), ("fc1", 768, 3072), ("fc2", 3072, 768),
           ("qkv.dg", 2304, 768), ("fc1.dg", 3072, 768), ("fc2.dg", 768, 3072)]
+# square reference shapes (steady-state throughput without BERT's short K): (name, M, K, N)
+SQUARE = [("sq4k", 4096, 4096, 4096), ("sq8k", 8192, 8192, 8192)]
 
 
 def timeit(f, n=20):
@@ -31,11 +33,12 @@ def timeit(f, n=20):
 
 
 tot = {"blas": 0.0, "ours": 0.0}
-for name, K, N in SHAPES:
-    x = (torch.rand(T, K, device="cuda") * 2 - 1).bfloat16()
+for name, M, K, N in [(n, T, k, nn) for n, k, nn in SHAPES] + SQUARE:
+    T_ = M
+    x = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
     w = ((torch.rand(N, K, device="cuda") * 2 - 1) / K ** 0.5).bfloat16()
     b = (torch.rand(N, device="cuda") * 2 - 1).bfloat16()
-    flop = 2.0 * T * K * N
+    flop = 2.0 * M * K * N
     ref = F.linear(x, w, b).float()
     cands = {"blas": lambda: F.linear(x, w, b)}
     for bn in (128, 192, 256):
@@ -49,9 +52,10 @@ for name, K, N in SHAPES:
         for k, f in cands.items():
             res[k].append(timeit(f))
     med = {k: statistics.median(v) for k, v in res.items()}
-    auto = "bn%d" % H.gemm_nt_pick_bn(T, N)
-    tot["blas"] += med["blas"]
-    tot["ours"] += med[auto]
+    auto = "bn%d" % H.gemm_nt_pick_bn(M, N)
+    if not name.startswith("sq"):
+        tot["blas"] += med["blas"]
+        tot["ours"] += med[auto]
     print("%-7s K %4d N %4d %5.1f GF  " % (name, K, N, flop / 1e9) +
           "  ".join("%s %.1fus %.0fTF" % (k, v, flop / v / 1e6) for k, v in med.items()) + "  (auto %s)" % auto,
           flush=True)

@@ -19,16 +19,34 @@ from kungfu_amd.parallel.mixed import enable_bf16_shadow
 
 
 def main():
+    """argv[1]: resnet50 | inception_v3 | vgg16 | bert_base; GRAPH=1: replay a captured step."""
     model_name = sys.argv[1] if len(sys.argv) > 1 else "resnet50"
     kf.init()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    model = get_model(model_name, fused_bn=True).to(dev).to(memory_format=torch.channels_last)
-    base = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    bert = model_name.startswith("bert")
+    model = get_model(model_name, fused_bn=True) if not bert else get_model(model_name)
+    model = model.to(dev)
+    if not bert:
+        model = model.to(memory_format=torch.channels_last)
+        base = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        base = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.01)
     opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(), force_comm=True)
     enable_bf16_shadow(model, opt)
-    x = torch.randn(256, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (256,), device=dev)
+    if bert:
+        from kungfu_amd.models.bert import pretraining_loss, synthetic_pretraining_batch
+
+        data = synthetic_pretraining_batch(128, 128, device=dev)
+
+        def compute_loss():
+            return pretraining_loss(model, data)
+    else:
+        x = torch.randn(256, 3, 224, 224, device=dev).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (256,), device=dev)
+
+        def compute_loss():
+            return F.cross_entropy(model(x).float(), y)
     ph = {"zero": 0.0, "fwd": 0.0, "bwd": 0.0, "step": 0.0}
 
     def step():
@@ -36,7 +54,7 @@ def main():
         opt.zero_grad()
         t1 = time.perf_counter()
         with torch.autocast("cuda", dtype=torch.bfloat16):
-            loss = F.cross_entropy(model(x).float(), y)
+            loss = compute_loss()
         t2 = time.perf_counter()
         loss.backward()
         t3 = time.perf_counter()
@@ -45,8 +63,13 @@ def main():
         for k, a, b in (("zero", t0, t1), ("fwd", t1, t2), ("bwd", t2, t3), ("step", t3, t4)):
             ph[k] += b - a
 
+    run = step
+    if os.environ.get("GRAPH") == "1":  # whole-step hipGraph: host cost of a replay
+        from kungfu_amd.parallel.graphs import GraphedStep
+
+        run = GraphedStep(step, opt, warmup=3)
     for _ in range(5):
-        step()
+        run()
     torch.cuda.synchronize()
     for k in ph:
         ph[k] = 0.0
@@ -55,7 +78,7 @@ def main():
     e0.record()
     h0 = time.perf_counter()
     for _ in range(n):
-        step()
+        run()
     h1 = time.perf_counter()
     e1.record()
     torch.cuda.synchronize()
