@@ -3,11 +3,17 @@ as stock PyTorch does, not just match it for a few steps on one random batch.
 
 * ResNet-50: 1,024 synthetic 96x96 images in 10 classes -- each class a fixed low-frequency
   pattern (sums of 2-D sinusoids per channel) under heavy Gaussian noise -- trained for 150
-  steps (batch 64, SGD momentum 0.9, linear warm-up then cosine decay) by (a) the bench's fused
-  engine (HIP BN / MFMA convs / bf16 shadow weights / bucketed S-SGD / fused SGD) and (b) the
-  stock modules with torch.optim.SGD, from the same initial weights and the same batches.
-  Both must reach >= 90 % accuracy over the whole set in eval mode (this also checks the fused
-  BN's running statistics) and agree on the mean loss of the last 50 steps within 10 %.
+  steps (batch 64, SGD momentum 0.9, linear warm-up to lr 0.05 then cosine decay) by (a) the
+  bench's fused engine (HIP BN / MFMA convs / bf16 shadow weights / bucketed S-SGD / fused SGD)
+  and (b) the stock modules with torch.optim.SGD, from the same initial weights and batches, for
+  two seeds each.  Every engine run must reach >= 95 % accuracy over the whole set in eval mode
+  (this also checks the fused BN's running statistics), its mean accuracy must be within 2 points
+  of stock's and its mean last-50-step loss no worse than 1.5x stock's + 0.05.
+  Why not "losses within 10 %": measured over 3 seeds (r4t6, profiles/r4_convergence.md) the
+  last-50 loss of ONE configuration spans 0.0004 .. 0.91 across seeds -- at peak lr 0.2 even
+  stock PyTorch diverges on some seeds -- so a per-step loss match between two implementations
+  (different bf16 rounding: the gradients at initialisation already have cosine ~0.1-0.3
+  between stock f32 and stock bf16, tools/diag/grad_compare.py) is not a property either has.
 * BERT (4 encoder layers of BERT-base width: the same fused attention / add+LayerNorm / MFMA
   weight-gradient kernels): masked-LM on a synthetic first-order Markov corpus over 512 tokens
   (each token has 4 successors), 20 masked positions per 128-token sequence.  The fused model
@@ -55,7 +61,7 @@ def _lr(step, steps, peak=0.2, warm=20):
     return peak * 0.5 * (1 + math.cos(math.pi * (step - warm) / (steps - warm)))
 
 
-def _train_resnet(engine: bool, steps=150, batch=64):
+def _train_resnet(engine: bool, steps=150, batch=64, seed=1):
     import kungfu_amd as kf
     from kungfu_amd.models import resnet50
 
@@ -64,7 +70,7 @@ def _train_resnet(engine: bool, steps=150, batch=64):
     x_all, y_all = _pattern_dataset()
     x_all = x_all.to(dev).to(memory_format=torch.channels_last)
     y_all = y_all.to(dev)
-    torch.manual_seed(1234)
+    torch.manual_seed(seed)
     model = resnet50(fused_bn=engine).to(dev).to(memory_format=torch.channels_last)
     base = torch.optim.SGD(model.parameters(), lr=0.0, momentum=0.9, weight_decay=5e-5)
     if engine:
@@ -74,12 +80,12 @@ def _train_resnet(engine: bool, steps=150, batch=64):
         enable_bf16_shadow(model, opt)
     else:
         opt = base
-    order = torch.randperm(len(y_all), generator=torch.Generator().manual_seed(77)).to(dev)
+    order = torch.randperm(len(y_all), generator=torch.Generator().manual_seed(77 + seed)).to(dev)
     losses = []
     nb = len(y_all) // batch
     for s in range(steps):
         for gr in opt.param_groups:
-            gr["lr"] = _lr(s, steps)
+            gr["lr"] = _lr(s, steps, peak=0.05)
         idx = order[(s % nb) * batch:(s % nb + 1) * batch]
         opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16):
@@ -97,14 +103,20 @@ def _train_resnet(engine: bool, steps=150, batch=64):
 
 @needs_gpu
 def test_resnet50_engine_learns_like_stock():
-    ls, acc_s = _train_resnet(False)
-    le, acc_e = _train_resnet(True)
-    ms, me = sum(ls[-50:]) / 50, sum(le[-50:]) / 50
-    print("stock acc %.3f last-50 loss %.4f | engine acc %.3f last-50 loss %.4f" % (acc_s, ms, acc_e, me))
-    print("stock", [round(v, 3) for v in ls[::10]], "\nengine", [round(v, 3) for v in le[::10]])
-    assert all(math.isfinite(v) for v in ls + le)
-    assert acc_s >= 0.9 and acc_e >= 0.9, (acc_s, acc_e)
-    assert abs(me - ms) <= 0.1 * max(me, ms) + 0.02, (ms, me)
+    st, en = [], []
+    for seed in (1, 2):
+        ls, acc_s = _train_resnet(False, seed=seed)
+        le, acc_e = _train_resnet(True, seed=seed)
+        st.append((sum(ls[-50:]) / 50, acc_s))
+        en.append((sum(le[-50:]) / 50, acc_e))
+        print("seed %d stock acc %.3f last-50 loss %.4f | engine acc %.3f last-50 loss %.4f" % (
+            seed, acc_s, st[-1][0], acc_e, en[-1][0]))
+        print("stock", [round(v, 3) for v in ls[::10]], "\nengine", [round(v, 3) for v in le[::10]])
+        assert all(math.isfinite(v) for v in ls + le)
+    assert all(a >= 0.95 for _, a in en), en
+    mean = lambda rows, k: sum(r[k] for r in rows) / len(rows)  # noqa: E731
+    assert mean(en, 1) >= mean(st, 1) - 0.02, (st, en)
+    assert mean(en, 0) <= 1.5 * mean(st, 0) + 0.05, (st, en)
 
 
 # ------------------------------------------------------------------ BERT

@@ -17,7 +17,7 @@ from kungfu_amd.models import resnet50  # noqa: E402
 from kungfu_amd.parallel.mixed import enable_bf16_shadow  # noqa: E402
 
 
-def grads(engine, x, y, steps=1, lr=0.0):
+def grads(engine, x, y, steps=1, lr=0.0, amp=True):
     torch.manual_seed(1234)
     m = resnet50(fused_bn=engine).cuda().to(memory_format=torch.channels_last)
     names = [n for n, _ in m.named_parameters()]
@@ -30,7 +30,7 @@ def grads(engine, x, y, steps=1, lr=0.0):
     losses = []
     for _ in range(steps):
         opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             loss = F.cross_entropy(m(x).float(), y)
         loss.backward()
         if engine:
@@ -43,10 +43,27 @@ def grads(engine, x, y, steps=1, lr=0.0):
     return losses, g, names
 
 
+def cos_all(ga, gb, names):
+    a = torch.cat([ga[n].flatten() for n in names])
+    b = torch.cat([gb[n].flatten() for n in names])
+    return F.cosine_similarity(a, b, 0).item(), ((b - a).norm() / a.norm()).item()
+
+
 def compare(tag, x, y):
+    lf, gf, names = grads(False, x, y, amp=False)
     ls, gs, names = grads(False, x, y)
+    ls2, gs2, _ = grads(False, x, y)
     le, ge, _ = grads(True, x, y)
-    print("== %s: loss stock %.5f engine %.5f" % (tag, ls[0], le[0]))
+    print("== %s: loss stock-f32 %.5f stock-bf16 %.5f engine %.5f" % (tag, lf[0], ls[0], le[0]))
+    for na, ga, nb, gb in (("stock-f32", gf, "stock-bf16", gs), ("stock-bf16", gs, "stock-bf16 again", gs2),
+                           ("stock-f32", gf, "engine", ge), ("stock-bf16", gs, "engine", ge)):
+        c, r = cos_all(ga, gb, names)
+        print("  %-12s vs %-16s: cos %.5f rel %.4f" % (na, nb, c, r))
+    # per-layer view against the f32 reference, the first 12 parameters in model order
+    for n in names[:12]:
+        a, b, c = gf[n].flatten(), gs[n].flatten(), ge[n].flatten()
+        print("  %-32s cos(f32, bf16) %.4f  cos(f32, engine) %.4f" % (
+            n, F.cosine_similarity(a, b, 0).item(), F.cosine_similarity(a, c, 0).item()))
     rows = []
     for n in names:
         a, b = gs[n], ge.get(n)
