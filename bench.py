@@ -69,11 +69,10 @@ def _setup_env():
     # message naming the op and rank (exit 3) instead of hanging until an outer timeout
     os.environ.setdefault("KUNGFU_RCCL_TIMEOUT_S", "300")
     os.environ.setdefault("KUNGFU_OP_TIMEOUT_S", "900")
-    if world > 1:
-        # >= 16 workgroups per gradient all-reduce: with fewer, the emulated 8-rank collectives
-        # could not keep up with backward (profiles/r4_comm_emulation.md: 4 CTAs +1.9-3.4 ms/step,
-        # 16-32 CTAs +0.3 ms); a floor only -- RCCL may use more
-        os.environ.setdefault("KUNGFU_RCCL_MIN_CTAS", "16")
+    # RCCL's own CTA choice is kept (no KUNGFU_RCCL_{MIN,MAX}_CTAS default): the comm emulation
+    # (profiles/r4_comm_emulation.md) wants >= 16 CTAs per gradient all-reduce, and RCCL sizes its
+    # channels for the 8-GPU xGMI ring itself (unmeasured here); a floor set alone is rejected by
+    # ncclCommInitRankConfig (minCTAs needs maxCTAs), measured on the colocated 2-rank run
 
 
 def _launcher_env() -> bool:
@@ -255,9 +254,11 @@ def main():
     p.add_argument("--bf16-shadow", type=int, default=1,
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
     p.add_argument("--lr", type=float, default=0.1)
-    p.add_argument("--graph", type=int, default=0,
+    p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
-                        "(kungfu_amd.parallel.graphs.GraphedStep)")
+                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for single-rank runs of the conv "
+                        "models (every op of their step is capturable; replay measured bit-identical to eager); "
+                        "multi-rank capture and BERT are opt-in")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -396,6 +397,11 @@ def main():
     if a.elastic:
         return _elastic_loop(a, model, opt, step, sync, bert)
     graphed = None
+    if a.graph < 0:
+        # multi-rank capture (RCCL collectives inside the graph) stays opt-in until it is validated on
+        # real multi-GPU nodes: with 2 colocated ranks hipStreamEndCapture recursed without end inside
+        # the HIP runtime (gpurun_out/r4t10_g1.log), see profiles/r4_host_overhead.md
+        a.graph = 0 if bert or a.optimizer not in ("ssgd", "local") or size > 1 else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 
@@ -420,9 +426,9 @@ def main():
     t_w0 = time.time()
     first_loss = None
     for i in range(a.warmup):
-        l0 = step()
+        l0 = step().detach()  # no reference to the step's autograd graph outlives the step
         if i == 0:
-            first_loss = float(l0.detach())
+            first_loss = float(l0)
     sync()
     warm_s = time.time() - t_w0
 
@@ -430,7 +436,7 @@ def main():
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = step()
+        loss = step().detach()
     sync()
     kf.run_barrier()
     dt = time.perf_counter() - t0
@@ -520,7 +526,7 @@ def main():
             "optimizer": "%s(%s)" % (a.optimizer, opt_desc),
             "fused_bn_hip": bool(fused_bn),
             "bf16_shadow_weights": bool(a.bf16_shadow),
-            "hip_graph": ({"replays": graphed.replays, "captured": graphed.graph is not None}
+            "hip_graph": ({"replays": graphed.replays, "captured": graphed.graph is not None, "disabled": graphed.disabled}
                           if graphed is not None else False),
             "per_gpu_img_s": round(value / size, 2),
             "tokens_per_s": round(value * a.seq_len, 1) if bert else None,

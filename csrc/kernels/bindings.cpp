@@ -13,6 +13,9 @@
 #include <tuple>
 #include <vector>
 #include <cstring>
+#include <csignal>
+#include <execinfo.h>
+#include <unistd.h>
 
 namespace {
 
@@ -1493,6 +1496,22 @@ at::Tensor ipc_open(py::bytes handle, int64_t numel, int64_t device) {
     return torch::from_blob(p, {numel}, [](void *q) { (void)hipIpcCloseMemHandle(q); }, opts);
 }
 
+// grad[V, D] (f32, accumulated into) += scatter of dy[T, D] (f32 / bf16) by ids[T] (int64)
+void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy) {
+    check_gpu(grad, "grad");
+    check_gpu(ids, "ids");
+    check_gpu(dy, "dy");
+    TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.dim() == 2, "embedding_backward: grad f32 [V, D]");
+    TORCH_CHECK(ids.scalar_type() == at::kLong, "embedding_backward: ids int64");
+    const int64_t V = grad.size(0), D = grad.size(1), T = ids.numel();
+    TORCH_CHECK(dy.numel() == T * D && (dy.scalar_type() == at::kFloat || dy.scalar_type() == at::kBFloat16),
+                "embedding_backward: dy f32/bf16 [T, D]");
+    TORCH_CHECK(D % 4 == 0, "embedding_backward: D % 4");
+    c10::DeviceGuard gd(grad.device());
+    kfk::launch_embedding_backward(grad.data_ptr<float>(), ids.data_ptr<int64_t>(), dy.data_ptr(),
+                                   dy.scalar_type() == at::kBFloat16, T, static_cast<int>(D), V, stream_of(grad, 0));
+}
+
 // gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
 at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> out,
                    bool accumulate, int64_t bn) {
@@ -1699,7 +1718,41 @@ class Comm {
 
 }  // namespace
 
+// Native backtrace on SIGSEGV / SIGBUS / SIGABRT (KUNGFU_NATIVE_BACKTRACE=1, a debugging aid: Python's
+// faulthandler shows only the Python frames of a crash inside RCCL / HIP).  Chains to the previous
+// handler so faulthandler still prints its part.
+namespace {
+struct sigaction g_prev_segv, g_prev_bus, g_prev_abrt;
+void native_bt_handler(int sig, siginfo_t *info, void *uc) {
+    static const char hdr[] = "\n[F] kungfu: native backtrace (signal):\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    void *frames[64];
+    const int n = backtrace(frames, 64);
+    backtrace_symbols_fd(frames, n, 2);
+    struct sigaction *prev = sig == SIGSEGV ? &g_prev_segv : sig == SIGBUS ? &g_prev_bus : &g_prev_abrt;
+    sigaction(sig, prev, nullptr);
+    if (prev->sa_flags & SA_SIGINFO) {
+        if (prev->sa_sigaction) prev->sa_sigaction(sig, info, uc);
+    } else if (prev->sa_handler != SIG_DFL && prev->sa_handler != SIG_IGN && prev->sa_handler) {
+        prev->sa_handler(sig);
+    }
+    raise(sig);
+}
+void install_native_backtrace() {
+    struct sigaction sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = native_bt_handler;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
+}
+}  // namespace
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.def("install_native_backtrace", &install_native_backtrace,
+          "print a native backtrace to stderr on SIGSEGV/SIGBUS/SIGABRT (chains to the previous handler)");
     m.doc() = "kungfu-amd CDNA4 kernels (gfx950) and RCCL controller";
     m.def("reduce", &reduce_op, "K1: z = op(x, y)");
     m.def("sgd_step", &sgd_step, "K8: fused SGD/momentum/nesterov/wd step on flat f32 buffers", py::arg("w"),
@@ -1843,6 +1896,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("bn") = -1,
           "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
     m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
+    m.def("embedding_backward", &embedding_backward, py::arg("grad"), py::arg("ids"), py::arg("dy"),
+          "grad[ids[t]] += dy[t] by f32 atomics (graph-replayable embedding gradient)");
     m.def(
         "set_dropout_seed_base",
         [](c10::optional<at::Tensor> t) {

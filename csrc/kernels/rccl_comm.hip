@@ -216,6 +216,13 @@ class Watchdog {
                         ++completed_;
                         continue;
                     }
+                    if (r == hipErrorCapturedEvent || r == hipErrorStreamCaptureUnsupported ||
+                        r == hipErrorStreamCaptureImplicit || r == hipErrorStreamCaptureWrongThread) {
+                        // the op's stream joined a hipGraph capture after the op was enqueued: its
+                        // event cannot be queried until the capture ends -- look again later
+                        ++it;
+                        continue;
+                    }
                     if (r != hipErrorNotReady) {
                         fail = "device error while waiting for " + it->what + ": " + hipGetErrorString(r);
                         break;
@@ -336,6 +343,8 @@ RcclComm::RcclComm(const std::string &id, int rank, int size, int device, double
     if (min_ctas <= 0) min_ctas = static_cast<int>(env_double("KUNGFU_RCCL_MIN_CTAS", 0));
     if (max_ctas <= 0) max_ctas = static_cast<int>(env_double("KUNGFU_RCCL_MAX_CTAS", 0));
     if (min_ctas > 0 && max_ctas > 0 && min_ctas > max_ctas) min_ctas = max_ctas;
+    if (min_ctas > 0 && max_ctas <= 0)  // RCCL rejects a minCTAs without a maxCTAs ("invalid argument")
+        throw std::invalid_argument("rccl: KUNGFU_RCCL_MIN_CTAS needs KUNGFU_RCCL_MAX_CTAS as well");
     min_ctas_ = min_ctas > 0 ? min_ctas : 0;
     max_ctas_ = max_ctas > 0 ? max_ctas : 0;
     if (blocking_ && (min_ctas_ || max_ctas_))

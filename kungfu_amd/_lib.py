@@ -44,6 +44,10 @@ def hip():
             "kungfu_amd._hip (HIP kernels) is not built or failed to load: %s; "
             "run `make hip` (hipcc --offload-arch=gfx950)" % e
         ) from e
+    from . import knobs
+
+    if knobs.get("KUNGFU_NATIVE_BACKTRACE") == "1":
+        _hip_mod.install_native_backtrace()
     return _hip_mod
 
 

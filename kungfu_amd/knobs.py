@@ -76,6 +76,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_RCCL_BLOCKING": _u("0", "1: blocking communicator init (no deadline, no CTA budget)"),
     "KUNGFU_RCCL_MIN_CTAS": _u("0", "ncclConfig_t.minCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
     "KUNGFU_RCCL_MAX_CTAS": _u("0", "ncclConfig_t.maxCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
+    "KUNGFU_NATIVE_BACKTRACE": _u("0", "1: print a native backtrace on SIGSEGV/SIGBUS/SIGABRT (debugging)"),
     "KUNGFU_RCCL_COLOCATE": _u("0", "1: several RCCL ranks on one GPU (socket transport; tests)"),
     "KUNGFU_COMM_EMULATE": _u(None, "ranks=R,ctas=C,busbw=GB/s,lat_us=L: model an R-rank all-reduce on one GPU"),
     "KUNGFU_PREFLIGHT_TIMEOUT_S": _u("60", "bench pre-flight: deadline of each device check"),

@@ -10,6 +10,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.attention import self_attention
+from ..ops.embedding import embedding
 from ..ops.linear import gelu
 
 
@@ -77,7 +78,9 @@ class BertForPreTraining(nn.Module):
         B, S = ids.shape
         pos = torch.arange(S, device=ids.device)
         types = torch.zeros_like(ids) if types is None else types
-        x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ(types))
+        # scatter-add embedding gradients (ops/embedding.py): fixed-shape, graph-replayable
+        x = self.ln(embedding(ids, self.tok.weight) + embedding(pos, self.pos.weight)[None]
+                    + embedding(types, self.typ.weight))
         if torch.is_autocast_enabled(x.device.type) and x.is_cuda:
             x = x.to(torch.get_autocast_dtype(x.device.type))  # bf16 residual stream from here on
         for layer in self.layers:

@@ -28,9 +28,37 @@ graphs are its equivalent); MI355X-first replacement for a tracing compiler.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Callable, List, Optional
 
 import torch
+
+# Every captured graph that may hold RCCL collectives: RCCL keeps per-graph resources alive until the
+# graph is destroyed, and finalizing the communicator first waits for them (a hang at exit, measured
+# with 2 colocated ranks) -- kungfu_amd.finalize() releases these graphs before the communicators.
+_live = weakref.WeakSet()
+
+
+def track(graph: torch.cuda.CUDAGraph) -> torch.cuda.CUDAGraph:
+    """Register a captured graph for :func:`release_all` (called by ``kungfu_amd.finalize``)."""
+    _live.add(graph)
+    return graph
+
+
+def release_all() -> None:
+    """Destroy every tracked graph (device-synchronised first)."""
+    if not _live:
+        return
+    try:
+        torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 -- shutting down
+        pass
+    for g in list(_live):
+        try:
+            g.reset()
+        except Exception:  # noqa: BLE001
+            pass
+    _live.clear()
 
 
 def _lr_holders(opt) -> List[object]:
@@ -49,6 +77,21 @@ def _lr_holders(opt) -> List[object]:
     return out
 
 
+def _drain_watchdog(timeout_s: float = 2.0) -> None:
+    """Wait (after a device synchronize) until the native RCCL watchdog has retired every event:
+    its thread polls every 50 ms, and an event recorded before the capture on a stream that then
+    joins the capture cannot be queried during it."""
+    import time
+
+    from .._lib import hip, hip_available
+
+    if not hip_available():
+        return
+    t_end = time.time() + timeout_s
+    while hip().rccl_watchdog_info()["pending"] and time.time() < t_end:
+        time.sleep(0.01)
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, optimizer)``; ``loss = step()`` runs ``fn`` eagerly for ``warmup``
     calls, then captures it and replays the graph on every later call (returning the captured
@@ -64,7 +107,12 @@ class GraphedStep:
         self.out = None
         self.calls = 0
         self.replays = 0
+        self.disabled = False
         self._lr = _lr_holders(optimizer) if optimizer is not None else []
+        # warm-up AND capture run on this one side stream: autograd's AccumulateGrad nodes remember
+        # the stream they were created on, and a node created on the default stream by a warm-up step
+        # whose graph is still alive (a kept loss tensor) makes the capture wait across streams
+        self.stream = torch.cuda.Stream()
 
     def pre_replay(self):
         from ..ops import dropout_seed
@@ -73,20 +121,64 @@ class GraphedStep:
             o._lr_t.fill_(o.param_groups[0]["lr"])
         dropout_seed.advance()  # fresh hashed dropout masks for this replay
 
-    def capture(self):
+    def capture(self) -> bool:
+        """Record one step.  Every rank must agree: a capture that failed anywhere (an op that
+        cannot be captured) is dropped on ALL ranks, which then stay eager -- nothing ran during
+        any rank's capture, so the ranks' collective sequences stay aligned."""
+        from .._lib import runtime
+
         torch.cuda.synchronize()
+        _drain_watchdog()  # no RCCL completion event left to query while streams are capturing
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode=self.mode):
-            self.out = self.fn()
+        err = None
+        reducer = getattr(self.opt, "reducer", None)
+        plane = getattr(getattr(reducer, "comm", None), "plane", "rccl") if reducer is not None else "rccl"
+        if plane not in ("rccl", "emulate", "skip"):
+            # the host-staged plane synchronises and copies through host memory inside every
+            # collective: not capturable (decided identically on every rank, nothing attempted)
+            err = RuntimeError("the %s data plane cannot be captured" % plane)
+        try:
+            if err is not None:
+                raise err
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode=self.mode):
+                self.out = self.fn()
+        except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
+            err = e
         torch.cuda.synchronize()
-        self.graph = g
+        ok = err is None
+        if runtime.size() > 1:
+            flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+            from .. import ops
+
+            ok = bool(ops.all_reduce(flag, op="min", name="kf:graph:capture_ok:%d" % self.calls).item())
+        if not ok:
+            import sys
+
+            print("kungfu_amd: whole-step hipGraph capture %s; training continues eagerly" % (
+                "failed: %s" % err if err is not None else "failed on another rank"), file=sys.stderr, flush=True)
+            self.out, self.disabled = None, True
+            reducer = getattr(self.opt, "reducer", None)
+            if reducer is not None:  # the aborted step left its bucket bookkeeping half done
+                reducer._reset_buckets()
+            return False
+        self.graph = track(g)
+        return True
+
+    def _eager(self):
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            out = self.fn()
+        cur.wait_stream(self.stream)
+        return out
 
     def __call__(self):
         self.calls += 1
         if self.graph is None:
-            if self.calls <= self.warmup:
-                return self.fn()
-            self.capture()  # records without executing: replay now so this call did a step
+            if self.calls <= self.warmup or self.disabled:
+                return self._eager()
+            if not self.capture():  # records without executing: replay now so this call did a step
+                return self._eager()
         self.pre_replay()
         self.graph.replay()
         self.replays += 1

@@ -93,7 +93,9 @@ def init(strategy: str = "") -> None:
 
 def finalize() -> None:
     from ..parallel import comm as _comm
+    from ..parallel import graphs as _graphs
 
+    _graphs.release_all()  # graphs holding RCCL work go before their communicators
     _comm.destroy_device_comm()
     if runtime.initialized():
         runtime.finalize()

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out; mkdir -p $O
 j() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["config"].get("hip_graph"))'; }
-for M in resnet50 bert_base inception_v3; do
+for M in bert_base resnet50 inception_v3; do
   OPT=ssgd; [ $M = bert_base ] && OPT=gns
   for G in 0 1; do
     timeout -k 10 300 python bench.py --model $M --optimizer $OPT --steps 30 --warmup 6 --graph $G > $O/r4t5_${M}_g$G.log 2>&1 || { tail -20 $O/r4t5_${M}_g$G.log; exit 1; }
