@@ -1497,7 +1497,7 @@ at::Tensor ipc_open(py::bytes handle, int64_t numel, int64_t device) {
 }
 
 // grad[V, D] (f32, accumulated into) += scatter of dy[T, D] (f32 / bf16) by ids[T] (int64)
-void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy) {
+void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy, int64_t ch) {
     check_gpu(grad, "grad");
     check_gpu(ids, "ids");
     check_gpu(dy, "dy");
@@ -1509,7 +1509,8 @@ void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy) {
     TORCH_CHECK(D % 4 == 0, "embedding_backward: D % 4");
     c10::DeviceGuard gd(grad.device());
     kfk::launch_embedding_backward(grad.data_ptr<float>(), ids.data_ptr<int64_t>(), dy.data_ptr(),
-                                   dy.scalar_type() == at::kBFloat16, T, static_cast<int>(D), V, stream_of(grad, 0));
+                                   dy.scalar_type() == at::kBFloat16, T, static_cast<int>(D), V, stream_of(grad, 0),
+                                   static_cast<int>(ch));
 }
 
 // gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
@@ -1896,7 +1897,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("bn") = -1,
           "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
     m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
-    m.def("embedding_backward", &embedding_backward, py::arg("grad"), py::arg("ids"), py::arg("dy"),
+    m.def("embedding_backward", &embedding_backward, py::arg("grad"), py::arg("ids"), py::arg("dy"), py::arg("ch") = 0,
           "grad[ids[t]] += dy[t] by f32 atomics (graph-replayable embedding gradient)");
     m.def(
         "set_dropout_seed_base",

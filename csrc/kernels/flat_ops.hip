@@ -496,49 +496,93 @@ void launch_cast(void *dst, const void *src, size_t n, int src_dt, int dst_dt, f
 }
 
 // Embedding gradient: grad[ids[t], :] += dy[t, :] (grad f32 [V, D], zeroed by the caller; dy f32
-// or bf16 [T, D]).  One f32 atomic per element (hardware global_atomic_add_f32, -munsafe-fp-atomics):
-// a fixed launch shape -- unlike a sort + unique-by-key segment reduction, whose work size comes
-// from the data, so a hipGraph can replay it.  The summation order is not deterministic.
+// or bf16 [T, D]).  A thread owns 4 columns of a run of `ch` consecutive tokens and sums them in
+// registers while the id repeats, issuing one f32 atomic per column at every id change
+// (hardware global_atomic_add_f32, -munsafe-fp-atomics).  Long runs for small vocabularies (the
+// segment ids: 2 rows; per-address atomic chains of T/ch instead of T), short ones for large
+// ones (random token ids: nothing to merge, many threads).  A fixed launch shape -- unlike a sort
+// + unique-by-key segment reduction, whose work size comes from the data -- so a hipGraph can
+// replay it.  The summation order is not deterministic.
 namespace {
 template <bool BF16>
+__device__ __forceinline__ void emb_load4(const void *dy, int64_t e, float v[4]) {
+    if constexpr (BF16) {
+        const uint2 r = reinterpret_cast<const uint2 *>(dy)[e];
+        v[0] = bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
+        v[1] = bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
+        v[2] = bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
+        v[3] = bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
+    } else {
+        const float4 r = reinterpret_cast<const float4 *>(dy)[e];
+        v[0] = r.x, v[1] = r.y, v[2] = r.z, v[3] = r.w;
+    }
+}
+
+template <bool BF16>
 __global__ __launch_bounds__(kBlock) void embedding_bwd_kernel(float *__restrict__ grad, const int64_t *__restrict__ ids,
-                                                              const void *__restrict__ dy, int64_t T, int D4, int64_t V) {
-    const int64_t total = T * D4;
+                                                              const void *__restrict__ dy, int64_t T, int D4, int64_t V,
+                                                              int ch) {
+    const int64_t chunks = (T + ch - 1) / ch;
+    const int64_t total = chunks * D4;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t t = i / D4;
-        const int c4 = static_cast<int>(i - t * D4);
-        const int64_t id = ids[t];
-        if (id < 0 || id >= V) continue;  // padding / out-of-range ids contribute nothing
-        float v[4];
-        if constexpr (BF16) {
-            const uint2 r = reinterpret_cast<const uint2 *>(dy)[i];
-            v[0] = bf16_to_f32(static_cast<uint16_t>(r.x & 0xffff));
-            v[1] = bf16_to_f32(static_cast<uint16_t>(r.x >> 16));
-            v[2] = bf16_to_f32(static_cast<uint16_t>(r.y & 0xffff));
-            v[3] = bf16_to_f32(static_cast<uint16_t>(r.y >> 16));
-        } else {
-            const float4 r = reinterpret_cast<const float4 *>(dy)[i];
-            v[0] = r.x, v[1] = r.y, v[2] = r.z, v[3] = r.w;
-        }
-        float *g = grad + id * (static_cast<int64_t>(D4) * 4) + c4 * 4;
+        const int64_t q = i / D4;
+        const int c4 = static_cast<int>(i - q * D4);
+        const int64_t t0 = q * ch, t1 = t0 + ch < T ? t0 + ch : T;
+        int64_t cur = ids[t0];
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        constexpr int U = 4;  // tokens whose id and gradient loads are in flight together
+        for (int64_t tb = t0; tb < t1; tb += U) {
+            int64_t idu[U];
+            float v[U][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) atomicAdd(g + k, v[k]);
+            for (int u = 0; u < U; ++u) {
+                if (tb + u < t1) {
+                    idu[u] = ids[tb + u];
+                    emb_load4<BF16>(dy, (tb + u) * D4 + c4, v[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (tb + u >= t1) break;
+                if (idu[u] != cur) {
+                    if (cur >= 0 && cur < V) {  // padding / out-of-range ids contribute nothing
+                        float *g = grad + cur * (static_cast<int64_t>(D4) * 4) + c4 * 4;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) atomicAdd(g + k, acc[k]);
+                    }
+                    cur = idu[u];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) acc[k] = 0.f;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] += v[u][k];
+            }
+        }
+        if (cur >= 0 && cur < V) {
+            float *g = grad + cur * (static_cast<int64_t>(D4) * 4) + c4 * 4;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicAdd(g + k, acc[k]);
+        }
     }
 }
 }  // namespace
 
 void launch_embedding_backward(float *grad, const int64_t *ids, const void *dy, bool dy_bf16, int64_t T, int D,
-                               int64_t V, hipStream_t s) {
+                               int64_t V, hipStream_t s, int ch) {
     if (T <= 0) return;
     if (D % 4) throw std::invalid_argument("embedding_backward: D must be a multiple of 4");
-    const int64_t total = T * (D / 4);
+    if (ch <= 0) {  // long runs only where rows repeat a lot and there are tokens to spare
+        const int64_t per_row = T / (V > 0 ? V : 1);
+        ch = per_row >= 512 ? 64 : 4;  // segment ids (V = 2, T = 16 K): 64 -> 25 us, 128 -> 42, 4 -> 212
+    }
+    const int64_t total = (T + ch - 1) / ch * (D / 4);
     int64_t g = (total + kBlock - 1) / kBlock;
     if (g > 8192) g = 8192;
     if (dy_bf16)
-        embedding_bwd_kernel<true><<<static_cast<int>(g), kBlock, 0, s>>>(grad, ids, dy, T, D / 4, V);
+        embedding_bwd_kernel<true><<<static_cast<int>(g), kBlock, 0, s>>>(grad, ids, dy, T, D / 4, V, ch);
     else
-        embedding_bwd_kernel<false><<<static_cast<int>(g), kBlock, 0, s>>>(grad, ids, dy, T, D / 4, V);
+        embedding_bwd_kernel<false><<<static_cast<int>(g), kBlock, 0, s>>>(grad, ids, dy, T, D / 4, V, ch);
 }
 
 namespace {

@@ -16,8 +16,9 @@ constexpr int kMaxGridHost = 2048;  // == kMaxGrid in common.hpp (partials scrat
 void launch_reduce(void *z, const void *x, const void *y, size_t n, int dtype, int op, hipStream_t s);
 
 // Embedding gradient by f32 atomics (flat_ops.hip): grad[ids[t], :] += dy[t, :], D % 4 == 0.
+// ch: tokens per thread run (<= 0: by T / V).
 void launch_embedding_backward(float *grad, const int64_t *ids, const void *dy, bool dy_bf16, int64_t T, int D,
-                               int64_t V, hipStream_t s);
+                               int64_t V, hipStream_t s, int ch = 0);
 
 // Device word mixed into every hashed dropout seed (attention, add+LayerNorm): a graph replay
 // re-uses the host seeds recorded at capture, so kungfu_amd.ops.dropout_seed advances this word

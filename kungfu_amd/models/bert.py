@@ -11,7 +11,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import self_attention
 from ..ops.embedding import embedding
-from ..ops.linear import gelu
+from ..ops.linear import gelu, residual_link
 
 
 class BertLayer(nn.Module):
@@ -33,6 +33,9 @@ class BertLayer(nn.Module):
     def forward(self, x, mask=None):
         B, S, D = x.shape
         p = self.dropout if self.training else 0.0
+        # x feeds exactly two consumers, the QKV projection and ln1's skip input: ln1's backward hands
+        # its gradient of x to the projection's data-gradient GEMM (ops.linear.ResidualLink)
+        residual_link(x)
         qkv = self.qkv(x)
         if mask is None:
             # fused HIP attention straight from / into the projections' layouts (SDPA off that path)
@@ -45,6 +48,7 @@ class BertLayer(nn.Module):
         # the projections' outputs feed only their AddLayerNorm: its backward also produces their
         # bias gradients (ops.linear.BiasLink), no column-sum pass of their own
         x = self.ln1(x, self.out(a), dropout=self.dropout, bias_link=True)
+        residual_link(x)  # likewise FC1 and ln2's skip input
         h = self.fc2(gelu(self.fc1(x), bias_link=True))
         return self.ln2(x, h, dropout=self.dropout, bias_link=True)
 

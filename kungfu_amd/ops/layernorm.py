@@ -26,7 +26,7 @@ _BIAS_LINK = knobs.get("KUNGFU_LN_BIAS_LINK") != "0"  # A/B switch of the linear
 
 class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, r, gamma, beta, eps, p=0.0, seed=0, blink=None):
+    def forward(ctx, x, r, gamma, beta, eps, p=0.0, seed=0, blink=None, rlink=None):
         from ..parallel.mixed import direct_target
 
         y, s, mean, rstd = hip().layernorm_forward(x, r, gamma, beta, eps, p, seed)
@@ -36,6 +36,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         tg, tb = direct_target(gamma), direct_target(beta)
         ctx.direct = (tg, tb) if tg is not None and tb is not None else None
         ctx.blink = blink if r is not None else None
+        ctx.rlink = rlink
         return y
 
     @staticmethod
@@ -61,7 +62,12 @@ class _AddLayerNormFn(torch.autograd.Function):
         # d(x + r)/dx = d(x + r)/dr = 1: both inputs receive ds (the dropped r: ds * keep / (1-p))
         if ctx.has_r and dr is None:
             dr = ds
-        return ds, (dr if ctx.has_r else None), dg, db, None, None, None, None
+        dx = ds
+        if ctx.rlink is not None and ctx.needs_input_grad[0]:
+            # the skip input's other consumer (a linear layer, ops.linear.ResidualLink) adds this
+            # gradient inside its data-gradient GEMM
+            ctx.rlink.value, dx = ds, None
+        return dx, (dr if ctx.has_r else None), dg, db, None, None, None, None, None
 
 
 def _eligible(x: torch.Tensor, r: Optional[torch.Tensor], w: torch.Tensor) -> bool:
@@ -88,7 +94,10 @@ def add_layer_norm(x: torch.Tensor, residual: Optional[torch.Tensor], weight: to
             dropout_seed.base(x.device)  # registers the device seed word (graph replays advance it)
         bl = (getattr(residual, "_kf_blink", None) if bias_link and _BIAS_LINK and residual is not None
               and x.shape[-1] <= 2048 else None)
-        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed, bl)
+        rl = getattr(x, "_kf_rlink", None) if residual is not None else None
+        if rl is not None and not rl.armed:
+            rl = None  # the linear consumer did not take the linking path: plain gradient return
+        return _AddLayerNormFn.apply(x, residual, weight.contiguous(), bias.contiguous(), float(eps), p, seed, bl, rl)
     if p > 0:
         residual = F.dropout(residual, p, True)
     s = x if residual is None else x + residual

@@ -41,6 +41,32 @@ class BiasLink:
         self.dtype, self.value, self.ptr = dtype, None, 0
 
 
+class ResidualLink:
+    """Link between the two consumers of a residual-stream tensor ``x`` in a transformer layer: a
+    linear layer ``linear(x)`` and the AddLayerNorm that adds ``x`` back as its skip input.  The
+    LayerNorm's backward runs first (it consumes the linear's descendants) and hands its gradient of
+    ``x`` over instead of returning it; the linear's backward then forms the whole gradient of ``x``
+    in ONE GEMM, ``g_skip.addmm_(dy, W)`` (hipBLASLt beta = 1 epilogue, in place) -- no separate residual add
+    pass over the [tokens, d] gradient (25 launches per BERT-base step).  ``armed``: the linear's
+    forward took the path that consumes the link (set before the LayerNorm's forward checks it)."""
+    __slots__ = ("armed", "value")
+
+    def __init__(self):
+        self.armed, self.value = False, None
+
+
+_RES_LINK = knobs.get("KUNGFU_RESIDUAL_LINK") != "0"
+
+
+def residual_link(x: torch.Tensor):
+    """Attach a fresh :class:`ResidualLink` to ``x`` (its two consumers pick it up) and return it."""
+    if not (_RES_LINK and x.is_cuda and x.requires_grad and torch.is_grad_enabled()):
+        return None
+    rl = ResidualLink()
+    x._kf_rlink = rl
+    return rl
+
+
 _DIRECT_WGRAD = knobs.get("KUNGFU_LINEAR_DIRECT_WGRAD") != "0"
 # KUNGFU_LINEAR_GEMM=1: forward (x W^T + b) and data gradient (dy W, with W^T from the flat
 # space's per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt
@@ -71,9 +97,12 @@ def _wt_cache(target, w):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, target=None):
+    def forward(ctx, x, w, b, target=None, rlink=None):
         ctx.save_for_backward(x, w)
         ctx.target = target
+        ctx.rlink = rlink
+        if rlink is not None:
+            rlink.armed = True
         ctx.has_b = b is not None
         ctx.b_dtype = b.dtype if b is not None else None
         ctx.blink = BiasLink(b.dtype) if b is not None and b.dtype in (torch.bfloat16, torch.float32) else None
@@ -98,9 +127,22 @@ class _LinearFn(torch.autograd.Function):
             x2 = x2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
+            rl, g = ctx.rlink, None
+            if rl is not None and rl.value is not None:  # the consuming AddLayerNorm's skip gradient
+                g, rl.value = rl.value.reshape(-1, in_f), None
             if ctx.wt is not None:  # dx = dy . W = dy . (W^T)^T on the NT GEMM
                 fc, i = ctx.wt
-                dx = hip().gemm_nt(dy2, fc.get(i).view(in_f, out_f)).view(x.shape)
+                dx = hip().gemm_nt(dy2, fc.get(i).view(in_f, out_f))
+                if g is not None:
+                    dx += g
+                dx = dx.view(x.shape)
+            elif g is not None:
+                # added by the GEMM itself (beta = 1), IN PLACE: torch.addmm into a new tensor copies
+                # g first (a 25 MB D2D copy per BERT-base product, measured slower than the add it
+                # replaces).  g is the AddLayerNorm's own backward output; when it also went out as
+                # the residual branch's gradient (no dropout) that branch's backward consumed it
+                # earlier on this stream
+                dx = g.addmm_(dy2, w).view(x.shape)
             else:
                 dx = torch.mm(dy2, w).view(x.shape)
         tgt = ctx.target
@@ -125,7 +167,7 @@ class _LinearFn(torch.autograd.Function):
                 db = hip().colsum(dy2, ctx.b_dtype)
             else:
                 db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -142,7 +184,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target
     ``(space, index)``: ``w`` is the bf16 shadow of that flat-space parameter -- its gradient is
     reduced straight into the parameter's f32 gradient slot (``space.sink.put_direct``)."""
     if eligible(x, w) and (b is None or b.dtype in (torch.bfloat16, torch.float32)):
-        y = _LinearFn.apply(x, w, b, grad_target)
+        rl = getattr(x, "_kf_rlink", None)
+        if rl is not None and (rl.armed or x.dtype != torch.bfloat16):
+            rl = None  # one linear consumer per link
+        y = _LinearFn.apply(x, w, b, grad_target, rl)
         if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
             y._kf_blink = y.grad_fn.blink
         return y

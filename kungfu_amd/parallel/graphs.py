@@ -33,6 +33,8 @@ from typing import Callable, List, Optional
 
 import torch
 
+from .. import knobs
+
 # Every captured graph that may hold RCCL collectives: RCCL keeps per-graph resources alive until the
 # graph is destroyed, and finalizing the communicator first waits for them (a hang at exit, measured
 # with 2 colocated ranks) -- kungfu_amd.finalize() releases these graphs before the communicators.
@@ -137,6 +139,12 @@ class GraphedStep:
             # the host-staged plane synchronises and copies through host memory inside every
             # collective: not capturable (decided identically on every rank, nothing attempted)
             err = RuntimeError("the %s data plane cannot be captured" % plane)
+        elif plane == "rccl" and getattr(reducer.comm, "size", 1) > 1 and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
+            # RCCL collectives on a stream that joined the capture from another stream (the
+            # engine's comm stream) crash hipStreamEndCapture: the HIP runtime recurses without end
+            # over the captured graph (tests/workers/rccl_graph.py phase "fork", r4t10); the same
+            # collectives on the capture's origin stream are fine but would serialise with backward
+            err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=1 to try it)")
         try:
             if err is not None:
                 raise err

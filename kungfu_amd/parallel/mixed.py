@@ -68,11 +68,16 @@ class _ShadowWeight(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, space, i):
         ctx.target = (space, i)
+        # a consumer that reduced the weight gradient straight into the flat slot (ops/linear.py
+        # put_direct) returns None: no zero-filled gradient to materialise and land (49 weight-sized
+        # fills + landing adds per BERT-base step)
+        ctx.set_materialize_grads(False)
         return space.shadow_view(i)
 
     @staticmethod
     def backward(ctx, g):
-        deliver(ctx.target, g)
+        if g is not None:
+            deliver(ctx.target, g)
         return None, None, None
 
 

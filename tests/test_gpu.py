@@ -1657,6 +1657,46 @@ def test_bert_layer_bias_link_matches_colsum(p, monkeypatch):
 
 
 @needs_gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_bert_layer_residual_link_matches_autograd_add(p, monkeypatch):
+    """The skip-input gradient handed from each AddLayerNorm's backward to the consuming linear's
+    data-gradient GEMM (``addmm``, ops.linear.ResidualLink) vs autograd's separate add: same forward,
+    gradients equal to bf16 rounding (one rounding of dx instead of two), and the link is consumed."""
+    import copy
+
+    from kungfu_amd.models.bert import BertLayer
+    from kungfu_amd.ops import linear as lin
+
+    torch.manual_seed(3)
+    layer = BertLayer(dropout=p).cuda()
+    for m in (layer.qkv, layer.out, layer.fc1, layer.fc2):
+        m.to(torch.bfloat16)
+    other = copy.deepcopy(layer)
+    for mod in (layer, other):  # the engine's linear (what the bf16-shadow models run)
+        for m in (mod.qkv, mod.out, mod.fc1, mod.fc2):
+            m.forward = (lambda mm: (lambda t: lin.linear(t, mm.weight, mm.bias)))(m)
+    x = torch.randn(4, 128, 768, device="cuda").bfloat16()
+    g = torch.randn(4, 128, 768, device="cuda").bfloat16()
+    res = []
+    for mod, link in ((layer, True), (other, False)):
+        monkeypatch.setattr(lin, "_RES_LINK", link)
+        torch.manual_seed(11)
+        xx = x.clone().requires_grad_(True)
+        y = mod(xx)
+        rl = getattr(xx, "_kf_rlink", None)
+        assert (rl is not None and rl.armed) == link
+        y.backward(g)
+        assert rl is None or rl.value is None  # handed over and consumed
+        res.append((y.detach(), xx.grad.float(), {n: q.grad.float() for n, q in mod.named_parameters()}))
+    (y0, gx0, gp0), (y1, gx1, gp1) = res
+    assert torch.equal(y0, y1)
+    assert ((gx0 - gx1).norm() / gx1.norm()).item() < 1e-2
+    for n in gp0:
+        a, b = gp0[n], gp1[n]
+        assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-2, n
+
+
+@needs_gpu
 @pytest.mark.parametrize("T,O", [(16384, 3072), (1000, 776), (37, 64)])
 def test_gelu_backward_colsum_matches_torch(T, O):
     """Fused erf-GELU backward + column sums (norms.hip) vs torch's GELU backward on the same bf16

@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("dy_dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("V,D,shape", [(30522, 768, (32, 128)), (512, 768, (128,)), (2, 64, (4, 16)), (97, 4, (3, 5))])
+@pytest.mark.parametrize("V,D,shape", [(30522, 768, (32, 128)), (512, 768, (128,)), (2, 64, (4, 16)), (2, 768, (128, 128)),
+                                   (97, 4, (3, 5)), (30522, 768, (7, 33))])
 def test_embedding_backward_matches_torch(V, D, shape, dy_dtype):
     from kungfu_amd._lib import hip
 
@@ -16,6 +17,8 @@ def test_embedding_backward_matches_torch(V, D, shape, dy_dtype):
     ids = torch.randint(0, V, shape, device="cuda", generator=g)
     if V > 1000:
         ids[0, :64] = 7  # heavy repeats: many atomics on one row
+    if V == 2:  # BERT segment ids: long runs of one row
+        ids = (torch.arange(shape[-1], device="cuda") >= shape[-1] // 2).long().expand(*shape).contiguous()
     dy = torch.randn(*shape, D, device="cuda", generator=g).to(dy_dtype)
     grad = torch.zeros(V, D, device="cuda")
     hip().embedding_backward(grad, ids.reshape(-1), dy)
