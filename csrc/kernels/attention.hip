@@ -98,16 +98,16 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // Stage NIMG images of S rows x 64 bf16 (128-byte rows) with 16-byte global_load_lds: image t
-// row r comes from src[t] + r * stride[t]; the 4 waves split the 1 KB (8-row) pieces.
-template <int S, int NIMG>
+// row r comes from src[t] + r * stride[t]; the NW waves split the 1 KB (8-row) pieces.
+template <int S, int NIMG, int NW = 4>
 __device__ __forceinline__ void stage_images(uint8_t *lds, const uint16_t *const (&src)[NIMG],
                                              const int (&stride)[NIMG], int wave, int lane) {
     constexpr int PIECES = S / 8;
-    static_assert((NIMG * PIECES) % 4 == 0, "pieces per wave");
+    static_assert((NIMG * PIECES) % NW == 0, "pieces per wave");
     const int pch = lane & 7;
 #pragma unroll
-    for (int u = 0; u < NIMG * PIECES / 4; ++u) {
-        const int gp = wave + 4 * u;
+    for (int u = 0; u < NIMG * PIECES / NW; ++u) {
+        const int gp = wave + NW * u;
         const int t = gp / PIECES, pc = gp - t * PIECES;
         const int r = pc * 8 + (lane >> 3);
         const int col = ((((pch >> 1) ^ hsw<128>(r)) << 1) | (pch & 1)) * 8;
@@ -240,10 +240,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         }
 }
 
-template <int S>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
+// NW waves: 8 at S = 128 -- the 128 KB of LDS allow one workgroup per CU, so 4 waves would leave
+// one wave per SIMD with nothing to overlap its exp / dropout-hash VALU work or LDS waits against
+template <int S, int NW>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
     constexpr int PROW = 2 * S;
-    constexpr int QW = S / 4;
+    constexpr int QW = S / NW;
+    static_assert(QW % 16 == 0, "query rows per wave");
     constexpr int TQ = QW / 16, TK = S / 16;
     __shared__ __attribute__((aligned(1024))) uint8_t lds[4 * S * 128 + 2 * S * PROW];
     __shared__ float dsum[S];
@@ -257,16 +260,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
     const uint16_t *dob = a.dout + static_cast<int64_t>(b) * S * D + h * DH;
     const uint16_t *src[4] = {base, base + D, base + 2 * D, dob};
     const int strd[4] = {RS, RS, RS, D};
-    stage_images<S, 4>(lds, src, strd, wave, lane);
-    // D[q] = sum_d dO[q][d] * O[q][d]: lane pair per row (32 dims each), from global
+    stage_images<S, 4, NW>(lds, src, strd, wave, lane);
+    // D[q] = sum_d dO[q][d] * O[q][d]: TPR lanes per row (64 / TPR dims each), from global
     {
-        const int q = (threadIdx.x >> 1), half = threadIdx.x & 1;  // 256 threads -> 128 rows
+        constexpr int TPR = NW * 64 / 128 < 1 ? 1 : NW * 64 / 128;  // 2 (256 threads) or 4 (512)
+        constexpr int NV = 8 / TPR;                                   // 16-byte vectors per lane
+        const int q = threadIdx.x / TPR, part = threadIdx.x % TPR;
         if (q < S) {
-            const uint4 *po = reinterpret_cast<const uint4 *>(a.out + (static_cast<int64_t>(b) * S + q) * D + h * DH + 32 * half);
-            const uint4 *pd = reinterpret_cast<const uint4 *>(dob + static_cast<int64_t>(q) * D + 32 * half);
+            const uint4 *po = reinterpret_cast<const uint4 *>(a.out + (static_cast<int64_t>(b) * S + q) * D + h * DH + 8 * NV * part);
+            const uint4 *pd = reinterpret_cast<const uint4 *>(dob + static_cast<int64_t>(q) * D + 8 * NV * part);
             float t = 0.f;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < NV; ++k) {
                 const uint4 ov = po[k], dv = pd[k];
                 const uint32_t *ow = reinterpret_cast<const uint32_t *>(&ov);
                 const uint32_t *dw = reinterpret_cast<const uint32_t *>(&dv);
@@ -275,8 +280,9 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
                     t += __uint_as_float(ow[e] << 16) * __uint_as_float(dw[e] << 16) +
                          __uint_as_float(ow[e] & 0xffff0000u) * __uint_as_float(dw[e] & 0xffff0000u);
             }
-            t += __shfl_xor(t, 1);
-            if (half == 0) dsum[q] = t;
+#pragma unroll
+            for (int o = 1; o < TPR; o <<= 1) t += __shfl_xor(t, o);
+            if (part == 0) dsum[q] = t;
         }
     }
     wait_vmcnt<0>();
@@ -400,6 +406,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
         }
 }
 
+// KUNGFU_ATTN_BWD_WAVES (dev knob, A/B): 8 (default) or 4 waves per S = 128 backward workgroup
+int attn_bwd_waves() {
+    static const int w = dev_knob("KUNGFU_ATTN_BWD_WAVES", 8) == 4 ? 4 : 8;
+    return w;
+}
+
 AttnArgs make_args(const uint16_t *qkv, uint16_t *out, float *lse, const uint16_t *dout, uint16_t *dqkv, int H,
                    float scale, uint32_t seed, float p_drop) {
     AttnArgs a;
@@ -429,8 +441,12 @@ void launch_attention_backward(const uint16_t *qkv, const uint16_t *out, const f
     if (!attention_supported(S, DH)) throw std::invalid_argument("attention: S must be 64 or 128");
     const AttnArgs a = make_args(qkv, const_cast<uint16_t *>(out), const_cast<float *>(lse), dout, dqkv, H, scale,
                                  seed, p_drop);
-    if (S == 128) attn_bwd_kernel<128><<<B * H, 256, 0, s>>>(a);
-    else attn_bwd_kernel<64><<<B * H, 256, 0, s>>>(a);
+    if (S == 128) {
+        if (attn_bwd_waves() == 8) attn_bwd_kernel<128, 8><<<B * H, 512, 0, s>>>(a);
+        else attn_bwd_kernel<128, 4><<<B * H, 256, 0, s>>>(a);
+    } else {
+        attn_bwd_kernel<64, 4><<<B * H, 256, 0, s>>>(a);
+    }
 }
 
 }  // namespace kfk
