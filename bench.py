@@ -256,9 +256,9 @@ def main():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
-                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for single-rank runs of the conv "
-                        "models (every op of their step is capturable; replay measured bit-identical to eager); "
-                        "multi-rank capture and BERT are opt-in")
+                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for the conv models with S-SGD "
+                        "(every op of their step is capturable; replay measured bit-identical to eager; multi-rank "
+                        "steps capture their RCCL all-reduces too), off for BERT")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -398,10 +398,9 @@ def main():
         return _elastic_loop(a, model, opt, step, sync, bert)
     graphed = None
     if a.graph < 0:
-        # multi-rank capture (RCCL collectives inside the graph) stays opt-in until it is validated on
-        # real multi-GPU nodes: with 2 colocated ranks hipStreamEndCapture recursed without end inside
-        # the HIP runtime (gpurun_out/r4t10_g1.log), see profiles/r4_host_overhead.md
-        a.graph = 0 if bert or a.optimizer not in ("ssgd", "local") or size > 1 else 1
+        # multi-rank: the bucket all-reduces are captured with the comm stream as the capture's origin
+        # (GraphedStep; RCCL on a joined stream crashed the HIP runtime, profiles/r4_host_overhead.md)
+        a.graph = 0 if bert or a.optimizer not in ("ssgd", "local") else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 

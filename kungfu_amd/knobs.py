@@ -127,7 +127,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_RESIDUAL_LINK": _d("1", "transformer skip-input gradient added inside the consumer linear's dgrad GEMM"),
     "KUNGFU_LINEAR_DIRECT_WGRAD": _d("1", "linear weight gradients reduced straight into the flat buffer"),
     "KUNGFU_COMM_STREAM_PRIORITY": _d("0", "HIP priority of the comm stream (-1 measured 2x slower)"),
-    "KUNGFU_GRAPH_MULTIRANK": _d("0", "1: let GraphedStep capture multi-rank RCCL steps (crashed the HIP runtime, r4t10)"),
+    "KUNGFU_GRAPH_MULTIRANK": _u("1", "0: GraphedStep keeps multi-rank RCCL steps eager (capture uses the comm stream as origin)"),
     "KUNGFU_BN_SKIP_FINALIZE": _d("0", "TIMING ONLY, wrong numerics: skip BN finalize (needs a -DKUNGFU_DEV_EXPERIMENTS=1 build)"),
     "KUNGFU_BERT_GEMM": _d("0", "BERT linear layers on the hand-written GEMM"),
 }

@@ -139,17 +139,28 @@ class GraphedStep:
             # the host-staged plane synchronises and copies through host memory inside every
             # collective: not capturable (decided identically on every rank, nothing attempted)
             err = RuntimeError("the %s data plane cannot be captured" % plane)
-        elif plane == "rccl" and getattr(reducer.comm, "size", 1) > 1 and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
-            # RCCL collectives on a stream that joined the capture from another stream (the
-            # engine's comm stream) crash hipStreamEndCapture: the HIP runtime recurses without end
-            # over the captured graph (tests/workers/rccl_graph.py phase "fork", r4t10); the same
-            # collectives on the capture's origin stream are fine but would serialise with backward
-            err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=1 to try it)")
+        multi = plane == "rccl" and getattr(reducer.comm, "size", 1) > 1
+        if multi and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
+            err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=0)")
         try:
             if err is not None:
                 raise err
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode=self.mode):
-                self.out = self.fn()
+            if multi:
+                # RCCL collectives on a stream that JOINED the capture (the engine's comm stream,
+                # forked from the compute stream) crash hipStreamEndCapture -- the HIP runtime
+                # recurses without end over the captured graph (tests/workers/rccl_graph.py phase
+                # "fork", r4t10) -- while collectives on the capture's ORIGIN stream replay fine.  So
+                # the capture starts on the comm stream and the step's compute runs on a stream
+                # forked from it: the same overlap, the collectives on the origin.
+                origin = reducer.comm.stream
+                with torch.cuda.graph(g, stream=origin, capture_error_mode=self.mode):
+                    self.stream.wait_stream(origin)
+                    with torch.cuda.stream(self.stream):
+                        self.out = self.fn()
+                    origin.wait_stream(self.stream)
+            else:
+                with torch.cuda.graph(g, stream=self.stream, capture_error_mode=self.mode):
+                    self.out = self.fn()
         except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
             err = e
         torch.cuda.synchronize()

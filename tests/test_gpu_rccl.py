@@ -173,11 +173,22 @@ def test_hierarchical_bucket_engine_two_fake_hosts_rccl(dtype):
 
 
 @needs_gpu
-def test_bench_two_ranks_whole_step_graph_falls_back_to_eager():
-    """bench.py --graph 1 with 2 colocated RCCL ranks: multi-rank capture is refused on every rank
-    (comm-stream RCCL collectives crash hipStreamEndCapture, see test below), all ranks agree and
-    train eagerly, and the replicas end identical."""
-    res = _bench(dict(COLO), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
+def test_bench_two_ranks_whole_step_graph():
+    """bench.py with 2 colocated RCCL ranks (graph on by default): each rank captures its whole step
+    with the comm stream as the capture's origin (bucket all-reduces inside the graph), the ranks
+    agree on the capture, replays exchange gradients (every rank draws its own batch, yet the
+    replicas end identical)."""
+    res = _bench(dict(COLO), extra=["--steps", "4", "--warmup", "4"])
+    v = res["verify"]
+    hg = res["config"]["hip_graph"]
+    assert hg["captured"] is True and hg["replays"] >= 4 and not hg["disabled"], hg
+    assert v["comm_ranks"] == 2 and v["replicas_consistent"] is True, v
+
+
+@needs_gpu
+def test_bench_two_ranks_graph_disabled_falls_back_to_eager():
+    """KUNGFU_GRAPH_MULTIRANK=0: capture refused identically on every rank, eager training."""
+    res = _bench(dict(COLO, KUNGFU_GRAPH_MULTIRANK="0"), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
     v = res["verify"]
     hg = res["config"]["hip_graph"]
     assert hg["captured"] is False and hg["disabled"] is True and hg["replays"] == 0, hg
@@ -186,11 +197,11 @@ def test_bench_two_ranks_whole_step_graph_falls_back_to_eager():
 
 @needs_gpu
 def test_rccl_collectives_replay_inside_hipgraph():
-    """RCCL collectives captured on the capture's own stream (sum, two in a row, ncclAvg) replay
-    with correct values, and the process exits cleanly with the graphs alive at shutdown
+    """RCCL collectives captured on the capture's own stream (sum, two in a row, ncclAvg, and with
+    the compute on a stream forked from it -- GraphedStep's multi-rank layout) replay with correct values, and the process exits cleanly with the graphs alive at shutdown
     (kungfu_amd.finalize releases tracked graphs before destroying the communicator -- without
     that, the communicator's finalize waited on the graph's RCCL resources until the deadline)."""
-    r = kungfu_run(2, [worker("rccl_graph.py"), "one,two,avg"], timeout=180, extra=["-allow-xgmi"], env=COLO)
+    r = kungfu_run(2, [worker("rccl_graph.py"), "one,two,avg,ofork"], timeout=180, extra=["-allow-xgmi"], env=COLO)
     assert r.returncode == 0, r.stdout[-5000:]
     assert r.stdout.count("RCCL_GRAPH_OK") == 2, r.stdout[-5000:]
 

@@ -1,6 +1,7 @@
 """Worker: RCCL all-reduces captured in hipGraphs (torch.cuda.graph) and replayed, values
 checked after every replay.  Phases: ``one`` (one all-reduce on the capture stream), ``two``
-(two all-reduces on the capture stream), ``avg`` (ncclAvg), ``fork`` (two all-reduces on a side comm stream forked
+(two all-reduces on the capture stream), ``avg`` (ncclAvg), ``ofork`` (compute on a forked stream, the all-reduces on the capture's
+origin stream), ``fork`` (two all-reduces on a side comm stream forked
 from and joined back into the capture, the S-SGD engine's pattern), ``hook`` (all-reduces issued
 from autograd hooks during a captured backward).  Ranks colocated on one GPU
 (KUNGFU_RCCL_COLOCATE).  Measured (r4t10, ROCm 7.0 runtime in torch 2.10, RCCL 2.26.6): one / two /
@@ -48,6 +49,19 @@ def body(phase):
             comm.all_reduce(x, op="sum", stream=side)
             comm.all_reduce(y, op="sum", stream=side)
         s.wait_stream(side)
+    elif phase == "ofork":
+        # the collectives on the capture's ORIGIN stream, the compute on a forked stream: the
+        # layout GraphedStep uses for multi-rank steps
+        side.wait_stream(s)
+        with torch.cuda.stream(side):
+            x.mul_(2)
+        s.wait_stream(side)
+        comm.all_reduce(x, op="sum", stream=s)
+        side.wait_stream(s)
+        with torch.cuda.stream(side):
+            y.mul_(1)
+        comm.all_reduce(y, op="sum", stream=s)
+        s.wait_stream(side)
     elif phase == "avg":
         x.mul_(2)
         comm.all_reduce(x, op="avg", stream=s)
@@ -73,7 +87,7 @@ def check(phase, i):
     assert torch.all(x == want), (phase, i, x[:4], want)
     if phase == "two":
         assert torch.all(y == 2 * tri), (phase, y[:4])
-    if phase == "fork":
+    if phase in ("fork", "ofork"):
         assert torch.all(y == 2 * tri), (phase, y[:4])
 
 
