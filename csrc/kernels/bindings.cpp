@@ -663,6 +663,18 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
     return dw;
 }
 
+// erf-GELU forward of a contiguous bf16 tensor (numel % 8 == 0)
+at::Tensor gelu_forward(at::Tensor u) {
+    TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kBFloat16 && u.is_contiguous() && u.numel() % 8 == 0,
+                "gelu_forward: contiguous bf16, numel % 8");
+    c10::DeviceGuard gd(u.device());
+    auto y = at::empty_like(u);
+    if (u.numel() > 0)
+        kfk::launch_gelu_forward(reinterpret_cast<const uint16_t *>(u.data_ptr()), reinterpret_cast<uint16_t *>(y.data_ptr()),
+                                 u.numel(), stream_of(u, 0));
+    return y;
+}
+
 // GELU backward fused with the bias gradient: (du, colsum(du)) for bf16 dy, u [..., O] (O % 8 == 0).
 std::vector<at::Tensor> gelu_backward_colsum(at::Tensor dy, at::Tensor u, at::ScalarType dtype) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && u.sizes() == dy.sizes() &&
@@ -1800,6 +1812,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1,
           py::arg("fin") = py::none());
+    m.def("gelu_forward", &gelu_forward, "erf-GELU forward (bf16, one-exponential erf)");
     m.def("gelu_backward_colsum", &gelu_backward_colsum, "erf-GELU backward du and the column sums of du",
           py::arg("dy"), py::arg("u"), py::arg("dtype"));
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),

@@ -73,6 +73,8 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
 // du = gelu'(u) * dy (bf16 [T, O], torch's erf-GELU backward) and the column sums of du (the bias
 // gradient of the layer that produced u) in one pass + the colsum second stage.
 int gelu_colsum_chunks(int64_t T, int O);  // partial rows of its scratch (part: f32 [chunks * O])
+// y = gelu(u) (erf form, bf16, n % 8 == 0; norms.hip)
+void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s);
 void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,
                             float *out_f32, uint16_t *out_bf16, hipStream_t s);
 void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s);

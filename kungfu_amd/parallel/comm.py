@@ -157,6 +157,11 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         leader = self.rank == 0
         self.device = torch.cuda.current_device()
         _colocate_env()
+        # collectives captured into a hipGraph (parallel/graphs.py) take the same data path as eager
+        # ones: no user-buffer registration at capture (RCCL's NCCL_GRAPH_REGISTER, default on,
+        # registers the captured buffers for zero-copy P2P -- an IPC path this pool only supports
+        # through dmabuf).  Read once, at the process's first communicator.
+        os.environ.setdefault("NCCL_GRAPH_REGISTER", "0")
         H.rccl_watchdog_set_label("rank %d/%d (cluster v%d, %s)" % (runtime.rank(), runtime.size(), self.version,
                                                                     runtime.self_spec()))
         uid = H.rccl_unique_id() if leader else bytes(128)
