@@ -663,6 +663,42 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
     return dw;
 }
 
+// fused softmax cross-entropy over bf16 logits [R, V]: (lse [R] f32, per-row loss [R] f32)
+std::vector<at::Tensor> xent_forward(at::Tensor x, at::Tensor labels) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
+                    x.size(1) % 2 == 0,
+                "xent_forward: contiguous bf16 [R, V] logits, V even");
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
+                    labels.numel() == x.size(0) && labels.device() == x.device(),
+                "xent_forward: int64 labels [R] on the logits' device");
+    TORCH_CHECK(x.size(1) < (int64_t(1) << 30) && x.size(0) < (int64_t(1) << 31), "xent_forward: shape too large");
+    c10::DeviceGuard gd(x.device());
+    auto lse = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+    auto loss = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+    kfk::launch_xent_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), labels.data_ptr<int64_t>(), x.size(0),
+                             static_cast<int>(x.size(1)), lse.data_ptr<float>(), loss.data_ptr<float>(),
+                             stream_of(x, 0));
+    return {lse, loss};
+}
+
+// its backward: d logits (bf16 [R, V]) = (softmax - onehot(label)) * scale[0]
+at::Tensor xent_backward(at::Tensor x, at::Tensor labels, at::Tensor lse, at::Tensor scale) {
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
+                    x.size(1) % 2 == 0,
+                "xent_backward: contiguous bf16 [R, V] logits, V even");
+    TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == x.size(0) &&
+                    lse.scalar_type() == at::kFloat && lse.numel() == x.size(0) && scale.scalar_type() == at::kFloat &&
+                    scale.numel() >= 1 && labels.device() == x.device() && lse.device() == x.device() &&
+                    scale.device() == x.device(),
+                "xent_backward: labels int64 [R], lse f32 [R], scale f32 [1] on the logits' device");
+    c10::DeviceGuard gd(x.device());
+    auto dx = at::empty_like(x);
+    kfk::launch_xent_backward(reinterpret_cast<const uint16_t *>(x.data_ptr()), labels.data_ptr<int64_t>(),
+                              lse.data_ptr<float>(), scale.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)),
+                              reinterpret_cast<uint16_t *>(dx.data_ptr()), stream_of(x, 0));
+    return dx;
+}
+
 // erf-GELU forward of a contiguous bf16 tensor (numel % 8 == 0)
 at::Tensor gelu_forward(at::Tensor u) {
     TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kBFloat16 && u.is_contiguous() && u.numel() % 8 == 0,
@@ -1812,6 +1848,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(),
           py::arg("variant") = -1, py::arg("dh") = 0, py::arg("dw") = 0, py::arg("pad") = 1,
           py::arg("fin") = py::none());
+    m.def("xent_forward", &xent_forward, "fused softmax cross-entropy over bf16 logits: (lse, per-row loss)");
+    m.def("xent_backward", &xent_backward, "its bf16 logit gradient, scaled by scale[0]");
     m.def("gelu_forward", &gelu_forward, "erf-GELU forward (bf16, one-exponential erf)");
     m.def("gelu_backward_colsum", &gelu_backward_colsum, "erf-GELU backward du and the column sums of du",
           py::arg("dy"), py::arg("u"), py::arg("dtype"));
@@ -1949,6 +1987,39 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     });
     m.def("rccl_watchdog_set_label", &kfk::watchdog_set_label);
     m.def("rccl_watchdog_set_timeout", &kfk::watchdog_set_timeout);
+    py::class_<kfk::PairPrefetcher>(m, "PairPrefetcher",
+                                    "native prefetch thread of the pair-averaging peer model (pair_prefetch.hip)")
+        .def(py::init<const std::string &, int, int, const std::string &, const std::string &, int64_t, int>(),
+             py::arg("libpath"), py::arg("device"), py::arg("self_rank"), py::arg("rec_name"), py::arg("model_name"),
+             py::arg("nbytes"), py::arg("slots") = 3)
+        .def(
+            "start",
+            [](kfk::PairPrefetcher &p, uintptr_t pending_ev, int64_t pending_ver, uintptr_t host_copy, int target,
+               std::vector<uintptr_t> src_slots, int64_t own_ver, uintptr_t dst, uintptr_t after_ev,
+               uintptr_t host_stage) {
+                kfk::PairPrefetcher::Job j;
+                j.pending_ev = pending_ev, j.pending_ver = pending_ver, j.host_copy = host_copy, j.target = target;
+                j.src_slots = std::move(src_slots), j.own_ver = own_ver, j.dst = dst, j.after_ev = after_ev;
+                j.host_stage = host_stage;
+                py::gil_scoped_release nogil;  // waits for the previous job
+                p.start(j);
+            },
+            py::arg("pending_ev"), py::arg("pending_ver"), py::arg("host_copy"), py::arg("target"),
+            py::arg("src_slots"), py::arg("own_ver"), py::arg("dst"), py::arg("after_ev"), py::arg("host_stage"))
+        .def("busy", &kfk::PairPrefetcher::busy)
+        .def(
+            "finish",
+            [](kfk::PairPrefetcher &p, uintptr_t wait_stream) {
+                kfk::PairPrefetcher::Result r;
+                {
+                    py::gil_scoped_release nogil;
+                    r = p.finish(wait_stream);
+                }
+                if (!r.error.empty()) throw std::runtime_error(r.error);
+                return py::make_tuple(r.status, r.version, r.own_ver);
+            },
+            py::arg("wait_stream"), "join the job: (status 0 none / 1 pulled / 2 dropped, version, own advertised version)");
+
     py::class_<Comm>(m, "RcclComm")
         .def(py::init<py::bytes, int, int, int, double, int, int>(), py::arg("uid"), py::arg("rank"),
              py::arg("size"), py::arg("device"), py::arg("init_timeout_s") = 0.0, py::arg("min_ctas") = 0,

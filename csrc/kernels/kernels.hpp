@@ -7,6 +7,8 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <string>
+#include <vector>
 
 namespace kfk {
 
@@ -73,6 +75,46 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
 // du = gelu'(u) * dy (bf16 [T, O], torch's erf-GELU backward) and the column sums of du (the bias
 // gradient of the layer that produced u) in one pass + the colsum second stage.
 int gelu_colsum_chunks(int64_t T, int O);  // partial rows of its scratch (part: f32 [chunks * O])
+// Native prefetch thread of the pair-averaging peer model (pair_prefetch.hip).
+class PairPrefetcher {
+  public:
+    struct Job {
+        uintptr_t pending_ev = 0;  // snapshot event to host-wait before advertising (0: nothing to advertise)
+        int64_t pending_ver = 0;   // its version
+        uintptr_t host_copy = 0;   // host copy of the snapshot to save too (peers on other hosts), or 0
+        int target = 0;            // peer to pull from
+        std::vector<uintptr_t> src_slots;  // the target's ring slots (device pointers); empty: via host store
+        int64_t own_ver = 0;       // own advertised version before this job (self-pull record)
+        uintptr_t dst = 0;         // device destination
+        uintptr_t after_ev = 0;    // event the copy waits for (the previous pull's consumer), or 0
+        uintptr_t host_stage = 0;  // pinned host staging buffer for host-store pulls
+    };
+    struct Result {
+        int status = 0;  // 0: nothing pulled, 1: pulled, 2: dropped (possibly torn)
+        int64_t version = 0, own_ver = 0;
+        std::string error;
+    };
+    PairPrefetcher(const std::string &libpath, int device, int self_rank, const std::string &rec_name,
+                   const std::string &model_name, int64_t nbytes, int slots);
+    ~PairPrefetcher();
+    PairPrefetcher(const PairPrefetcher &) = delete;
+    PairPrefetcher &operator=(const PairPrefetcher &) = delete;
+    void start(const Job &job);
+    bool busy();
+    Result finish(uintptr_t wait_stream);  // joins the job; on success `wait_stream` waits on the copy
+
+  private:
+    struct Impl;
+    Impl *d_;
+};
+
+// Softmax cross-entropy over bf16 logits [R, V] (V even; xent.hip): per-row log-sum-exp and loss
+// (0 where the label is outside [0, V)); backward writes the bf16 gradient scaled by *scale.
+void launch_xent_forward(const uint16_t *x, const int64_t *labels, int64_t R, int V, float *lse, float *loss,
+                         hipStream_t s);
+void launch_xent_backward(const uint16_t *x, const int64_t *labels, const float *lse, const float *scale, int64_t R,
+                          int V, uint16_t *dx, hipStream_t s);
+
 // y = gelu(u) (erf form, bf16, n % 8 == 0; norms.hip)
 void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s);
 void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,

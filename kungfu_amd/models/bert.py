@@ -11,6 +11,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import self_attention
 from ..ops.embedding import embedding
+from ..ops.xent import cross_entropy
 from ..ops.linear import gelu, residual_link
 
 
@@ -118,5 +119,5 @@ def synthetic_pretraining_batch(batch: int, seq_len: int = 128, vocab: int = 305
 def pretraining_loss(model, batch):
     ids, types, pos, mlm_labels, nsp_labels = batch
     mlm, nsp = model(ids, types, pos)
-    return (F.cross_entropy(mlm.float().reshape(-1, mlm.shape[-1]), mlm_labels.reshape(-1))
-            + F.cross_entropy(nsp.float(), nsp_labels))
+    # MLM loss straight from the bf16 logits (ops/xent.py: no f32 copies of the 2560 x 30522 logits)
+    return cross_entropy(mlm, mlm_labels) + F.cross_entropy(nsp.float(), nsp_labels)

@@ -200,6 +200,59 @@ class _Prefetcher:
         return self.result
 
 
+class _NativePrefetcher:
+    """The same prefetch on a C++ thread (csrc/kernels/pair_prefetch.hip): advertise + pull without
+    Python or the GIL off the training thread; ``finish`` makes the compute stream wait on the
+    copy natively (returns True), so the training loop only enqueues the averaging kernel."""
+
+    def __init__(self, store: DeviceModelStore, out: torch.Tensor):
+        import os
+
+        from .. import _lib
+
+        lib = os.path.join(os.path.dirname(os.path.abspath(_lib.__file__)), "lib", "libkungfu_amd.so")
+        self.store, self.out = store, out
+        self.p = hip().PairPrefetcher(lib, store.device.index, store.rank, _REC + store.name,
+                                      "kf:pair:model:" + store.name, store.numel * 4, store.SLOTS)
+        self.stage = (torch.empty(store.numel, dtype=torch.float32, pin_memory=True) if store.cross_host else None)
+        self.thread = None  # truthy while a job is in flight (synchronize() checks it)
+        self._keep = ()
+        self._target = -1
+
+    def start(self, target: int, consumed: Optional[torch.cuda.Event]):
+        st = self.store
+        pend, host = st._pending, st._host_copy
+        own = st.version
+        if pend is not None:  # advertised by the native thread: the store's state moves on now
+            st.version, st._pending = st._pending_ver, None
+        if target == st.rank:
+            src = [b.data_ptr() for b in st.bufs]
+        elif st.local.get(target, False):
+            src = [b.data_ptr() for b in st.peer_bufs[target]]
+        else:
+            src = []
+        self._keep = (pend, host, consumed)  # alive until the native thread is done with them
+        self._target = target
+        self.p.start(pend.cuda_event if pend is not None else 0, st.version if pend is not None else 0,
+                     host.data_ptr() if (pend is not None and host is not None) else 0, target, src, own,
+                     self.out.data_ptr(), consumed.cuda_event if consumed is not None else 0,
+                     self.stage.data_ptr() if self.stage is not None else 0)
+        self.thread = True
+
+    def finish(self):
+        if not self.thread:
+            return None
+        status, ver, _ = self.p.finish(torch.cuda.current_stream(self.store.device).cuda_stream)
+        self.thread, self._keep = None, ()
+        if status == 2:
+            self.store.dropped += 1
+            return None
+        if status != 1:
+            return None
+        self.store.last_pulled = (self._target, ver)
+        return True  # the current stream already waits on the copy
+
+
 class _PairAveraging(KungFuOptimizer):
     def __init__(self, optimizer, named_parameters=None, fuse_requests: bool = True,
                  fused_model_name: str = "model", fused: bool = True, seed: Optional[int] = None,
@@ -223,7 +276,10 @@ class _PairAveraging(KungFuOptimizer):
             self.store = DeviceModelStore(self.space.numel, self.space.device, fused_model_name)
             self._other = torch.empty_like(self.space.flat_param)
             if prefetch:
-                self.prefetcher = _Prefetcher(self.store, self._other)
+                from .. import knobs
+
+                native = knobs.get("KUNGFU_PAIR_NATIVE") != "0" and hasattr(hip(), "PairPrefetcher")
+                self.prefetcher = (_NativePrefetcher if native else _Prefetcher)(self.store, self._other)
         self._consumed: Optional[torch.cuda.Event] = None
 
     def random_peer(self) -> int:
@@ -271,11 +327,14 @@ class _PairAveraging(KungFuOptimizer):
                     v.add_(o.to(v.device)).mul_(0.5)
 
     # -- algorithm ----------------------------------------------------------------
-    def _average(self, done: Optional[torch.cuda.Event]):
+    def _average(self, done):
+        """``done``: the pull's completion event, True (the native prefetcher already made the
+        current stream wait on it) or None (nothing pulled)."""
         if done is None:
             return
         cur = torch.cuda.current_stream(self.space.device)
-        cur.wait_event(done)  # normally complete already: no stall
+        if done is not True:
+            cur.wait_event(done)  # normally complete already: no stall
         hip().axpby(self.space.flat_param, self._other, None, 0.5, 0.5)
         self.pulls += 1
         ev = torch.cuda.Event()
