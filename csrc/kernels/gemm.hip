@@ -133,6 +133,66 @@ __device__ __forceinline__ void gemm_mfma(f32x4 (&acc)[TM][TN], const bf16x8 (&a
     __builtin_amdgcn_s_setprio(0);
 }
 
+// ---- 4-wave layout (NW4): 2 x 2 waves, each 128 x BN/2 of the 256 x BN tile -------------------------
+// Per K = 32 slab a wave reads 8 A + BN/32 B fragments for 8 * BN/32 MFMAs: at BN = 256 twice the MFMAs per
+// LDS byte of the 8-wave layout, whose 12 reads per 32 MFMAs (plus the LDS-DMA writes) kept the LDS
+// port as busy as the matrix cores (profiles/r4_gemm_nt.md).  The 256 accumulators live in AGPRs:
+// the MFMAs are inline asm with tied "+a" accumulators -- through the builtin, hipcc kept them in
+// AGPRs too but re-coalesced the chains with ~216 v_accvgpr_mov per 128 MFMAs.
+template <int BN>
+__device__ __forceinline__ void gemm_stage4(uint8_t *lds, __amdgpu_buffer_rsrc_t ar, __amdgpu_buffer_rsrc_t br,
+                                            const uint32_t *a_off, const uint32_t *b_off, int wave, int s,
+                                            int slot, bool ghost) {
+    // ghost: a slab past K -- the loads still issue (every step then waits for the same vmcnt, no
+    // branch in the main loop) but read nothing (offset past num_records: zeros, no memory access)
+    constexpr int SLOT = kABytes + BN * kRowB;
+    constexpr int B_PER = BN / 16 / 4;
+    uint8_t *abase = lds + slot * SLOT;
+    uint8_t *bbase = abase + kABytes;
+    const uint32_t kb = static_cast<uint32_t>(s * kSlabK * 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t vo = (ghost || a_off[i] == kOOB) ? kOOB : a_off[i] + kb;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ar, lds3(abase + (i * 4 + wave) * 1024), 16, vo, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(br, lds3(bbase + (i * 4 + wave) * 1024), 16,
+                                                 ghost ? kOOB : b_off[i] + kb, 0, 0, 0);
+}
+
+// one row block's TN MFMAs, acc[j] += B_j^T A (transposed product, as gemm_mfma).  `s_nop 1` first:
+// the A fragment may have just landed (a just-written operand before an MFMA, cdna_hip_programming.md
+// inline-asm item 2); the accumulate chains need no wait.
+template <int TN>
+__device__ __forceinline__ void mfma_row(f32x4 (&acc)[TN], const bf16x8 (&b)[TN], const bf16x8 &a) {
+    static_assert(TN == 8 || TN == 4, "TN");
+    if constexpr (TN == 8) {
+        asm volatile(
+            "s_nop 1\n"
+            "v_mfma_f32_16x16x32_bf16 %0, %8, %16, %0\n"
+            "v_mfma_f32_16x16x32_bf16 %1, %9, %16, %1\n"
+            "v_mfma_f32_16x16x32_bf16 %2, %10, %16, %2\n"
+            "v_mfma_f32_16x16x32_bf16 %3, %11, %16, %3\n"
+            "v_mfma_f32_16x16x32_bf16 %4, %12, %16, %4\n"
+            "v_mfma_f32_16x16x32_bf16 %5, %13, %16, %5\n"
+            "v_mfma_f32_16x16x32_bf16 %6, %14, %16, %6\n"
+            "v_mfma_f32_16x16x32_bf16 %7, %15, %16, %7"
+            : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3]), "+a"(acc[4]), "+a"(acc[5]), "+a"(acc[6]),
+              "+a"(acc[7])
+            : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(b[4]), "v"(b[5]), "v"(b[6]), "v"(b[7]), "v"(a));
+    } else {
+        asm volatile(
+            "s_nop 1\n"
+            "v_mfma_f32_16x16x32_bf16 %0, %4, %8, %0\n"
+            "v_mfma_f32_16x16x32_bf16 %1, %5, %8, %1\n"
+            "v_mfma_f32_16x16x32_bf16 %2, %6, %8, %2\n"
+            "v_mfma_f32_16x16x32_bf16 %3, %7, %8, %3"
+            : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3])
+            : "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(b[3]), "v"(a));
+    }
+}
+
 }  // namespace
 
 // (outside the anonymous namespace: hipcc leaves the host stubs of kernel templates declared
@@ -336,7 +396,188 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
     }
 }
 
+// 4-wave variant: 256 x BN tile (BN 256 / 128), waves 2 (M) x 2 (N) of 128 x BN/2, same ring, swizzle,
+// XCD remap and epilogue as gemm_nt_kernel.
+template <int BN, int EPI>
+__global__ __launch_bounds__(256) void gemm_nt4_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
+                                                       uint16_t *__restrict__ C, const uint16_t *__restrict__ bias,
+                                                       int M, int N, int K, int mtiles, int ntiles) {
+    constexpr int TN = BN / 32;           // 16-column blocks per wave (2 waves along N)
+    constexpr int TM = 8;                 // 16-row blocks per wave (2 waves along M)
+    constexpr int SLOT = kABytes + BN * kRowB;
+    constexpr int B_PER = BN / 64;        // 16-row glds instructions of the B slab per wave
+    constexpr int PER = 4 + B_PER;        // glds per wave per slab
+    constexpr int WCOLS = BN / 2;         // output columns per wave
+    constexpr int EROW = WCOLS * 2;       // epilogue LDS row pitch (bytes)
+    constexpr int LDS_RING = kSlots * SLOT;
+    constexpr int LDS_EPI = 4 * 128 * EROW;
+    constexpr int LDS = LDS_RING > LDS_EPI ? LDS_RING : LDS_EPI;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1;
+    const int nwg = mtiles * ntiles;
+    const int orig = blockIdx.x;
+    const int q = nwg >> 3, r8 = nwg & 7, xcd = orig & 7;
+    const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+    const int mt = wgid / ntiles, nt = wgid - mt * ntiles;
+    const int m0 = mt * kGM, n0 = nt * BN;
+
+    const __amdgpu_buffer_rsrc_t ar =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(A), 0, static_cast<int>(kOOB), kRsrcFlags);
+    const __amdgpu_buffer_rsrc_t br =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(B), 0, static_cast<int>(kOOB), kRsrcFlags);
+    const int srow = lane >> 2;
+    const int schk = (lane & 3) ^ slab_swz(srow);
+    uint32_t a_off[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = (i * 4 + wave) * 16 + srow;
+        a_off[i] = m0 + row < M ? static_cast<uint32_t>(((m0 + row) * K + schk * 8) * 2) : kOOB;
+    }
+    uint32_t b_off[B_PER];
+#pragma unroll
+    for (int i = 0; i < B_PER; ++i) {
+        const int row = (i * 4 + wave) * 16 + srow;
+        b_off[i] = static_cast<uint32_t>(((n0 + row) * K + schk * 8) * 2);
+    }
+    const int slabs = K / kSlabK;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fchk = lane >> 4;
+    const int arow0 = wm * 128, bcol0 = wn * WCOLS;
+    // slabs is even (K % 64 == 0, launch_gemm_nt): every step below runs both halves, no branch
+#pragma unroll
+    for (int p = 0; p < kSlots - 1; ++p) gemm_stage4<BN>(lds, ar, br, a_off, b_off, wave, p, p, p >= slabs);
+    vm_wait<3 * PER>();
+    __builtin_amdgcn_s_barrier();
+    bf16x8 af[TM], b0[TN], b1[TN];
+    gemm_frags<TM, TN>(lds, arow0, bcol0, frow, fchk, af, b0);
+
+    int slot_next = 1, slot_stage = 4;
+    auto pre = [&](int s) {
+        vm_wait<2 * PER>();  // slab s + 1 landed (ghost slabs keep the count uniform at the tail)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        gemm_stage4<BN>(lds, ar, br, a_off, b_off, wave, s + 4, slot_stage, s + 4 >= slabs);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // per slab: the next slab's B fragments into the other B set, then row block i's MFMAs and the
+    // next slab's A fragment i read in place behind them; before row block i the reads newer than
+    // this slab's A fragment i are its 7 - i successors, the TN next-B reads and i next-A reads
+    auto half = [&](bf16x8 (&bc)[TN], bf16x8 (&bn)[TN]) {
+        const uint8_t *nslot = lds + slot_next * SLOT;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bn[j] = ds_read16(nslot + kABytes + slab_off(bcol0 + j * 16 + frow, fchk));
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            gemm_wait_frags<TN + 7>();
+            mfma_row<TN>(acc[i], bc, af[i]);
+            __builtin_amdgcn_sched_barrier(0);
+            af[i] = ds_read16(nslot + slab_off(arow0 + i * 16 + frow, fchk));
+        }
+    };
+    for (int s = 0; s < slabs; s += 2) {
+        pre(s);
+        half(b0, b1);
+        slot_next = slot_next == kSlots - 1 ? 0 : slot_next + 1;
+        slot_stage = slot_stage == kSlots - 1 ? 0 : slot_stage + 1;
+        pre(s + 1);
+        half(b1, b0);
+        slot_next = slot_next == kSlots - 1 ? 0 : slot_next + 1;
+        slot_stage = slot_stage == kSlots - 1 ? 0 : slot_stage + 1;
+    }
+    vm_wait<0>();  // the ghost slabs' loads
+    // the last (unused) prefetch reads, and 16 wait states before the accumulators are read (an
+    // MFMA's result -> a non-MFMA reader: 12 states for the 8-pass XDL ops)
+    asm volatile("s_waitcnt lgkmcnt(0)\n s_nop 7\n s_nop 7" ::: "memory");
+    __syncthreads();
+
+    uint8_t *ew = lds + wave * (128 * EROW);
+    const int em = lane & 15, en = (lane >> 4) * 4;
+    constexpr int CH = EROW / 16;  // 16-byte chunks per epilogue row
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int row = i * 16 + em;
+            const int col = j * 16 + en;
+            uint32_t lo = static_cast<uint32_t>(f32_to_bf16(acc[i][j][0])) |
+                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][1])) << 16);
+            uint32_t hi = static_cast<uint32_t>(f32_to_bf16(acc[i][j][2])) |
+                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][3])) << 16);
+            const int chunk = ((col >> 3) ^ (row & 7)) & (CH - 1);
+            *reinterpret_cast<uint2 *>(ew + row * EROW + chunk * 16 + (col & 7) * 2) = make_uint2(lo, hi);
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int CPR = WCOLS / 8;
+    constexpr int RPI = 64 / CPR;
+    const int ch = lane % CPR, rsub = lane / CPR;
+    const int gcol = n0 + wn * WCOLS + ch * 8;
+    float bv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) bv[k] = 0.f;
+    if constexpr ((EPI & kGemmBias) != 0) {
+        const uint4 braw = *reinterpret_cast<const uint4 *>(bias + gcol);
+        const uint32_t bw[4] = {braw.x, braw.y, braw.z, braw.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            bv[2 * k] = bf16_to_f32(static_cast<uint16_t>(bw[k] & 0xffff));
+            bv[2 * k + 1] = bf16_to_f32(static_cast<uint16_t>(bw[k] >> 16));
+        }
+    }
+#pragma unroll 4
+    for (int r0 = 0; r0 < 128; r0 += RPI) {
+        const int row = r0 + rsub;
+        const int grow = m0 + wm * 128 + row;
+        if (grow >= M) continue;
+        uint4 v = *reinterpret_cast<const uint4 *>(ew + row * EROW + (((ch ^ (row & 7)) & (CH - 1)) << 4));
+        uint16_t *dst = C + static_cast<int64_t>(grow) * N + gcol;
+        if constexpr (EPI != 0) {
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            uint32_t o[4] = {0u, 0u, 0u, 0u};
+            if constexpr ((EPI & kGemmAccum) != 0) {
+                const uint4 ov = *reinterpret_cast<const uint4 *>(dst);
+                o[0] = ov.x, o[1] = ov.y, o[2] = ov.z, o[3] = ov.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float x0 = bf16_to_f32(static_cast<uint16_t>(w[k] & 0xffff)) + bv[2 * k];
+                float x1 = bf16_to_f32(static_cast<uint16_t>(w[k] >> 16)) + bv[2 * k + 1];
+                if constexpr ((EPI & kGemmAccum) != 0) {
+                    x0 += bf16_to_f32(static_cast<uint16_t>(o[k] & 0xffff));
+                    x1 += bf16_to_f32(static_cast<uint16_t>(o[k] >> 16));
+                }
+                w[k] = static_cast<uint32_t>(f32_to_bf16(x0)) | (static_cast<uint32_t>(f32_to_bf16(x1)) << 16);
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4 *>(dst) = v;
+    }
+}
+
 namespace {
+
+template <int BN>
+void launch_bn4(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K, int epi,
+                hipStream_t s) {
+    const int mtiles = (M + kGM - 1) / kGM, ntiles = N / BN;
+    const dim3 grid(mtiles * ntiles), block(256);
+    switch (epi) {
+    case 0: gemm_nt4_kernel<BN, 0><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
+    case kGemmBias: gemm_nt4_kernel<BN, kGemmBias><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
+    case kGemmAccum: gemm_nt4_kernel<BN, kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
+    case kGemmBias | kGemmAccum:
+        gemm_nt4_kernel<BN, kGemmBias | kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles);
+        break;
+    default: throw std::invalid_argument("gemm_nt: unsupported epilogue");
+    }
+}
 
 template <int BN>
 void launch_bn(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K, int epi,
@@ -379,7 +620,16 @@ void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uin
     if (!gemm_nt_supported(M, N, K)) throw std::invalid_argument("gemm_nt: unsupported shape");
     if ((epi & kGemmBias) && !bias) throw std::invalid_argument("gemm_nt: bias epilogue without bias");
     if (bn <= 0) bn = gemm_nt_pick_bn(M, N);
-    if (N % bn) throw std::invalid_argument("gemm_nt: N not a multiple of the tile width");
+    if (bn < 1000 && N % bn) throw std::invalid_argument("gemm_nt: N not a multiple of the tile width");
+    // bn 1256 / 1128: the 4-wave layout of the 256 / 128-wide tiles
+    if (bn > 1000) {
+        if (N % (bn - 1000)) throw std::invalid_argument("gemm_nt: N not a multiple of the tile width");
+        if (K % 64) throw std::invalid_argument("gemm_nt: the 4-wave tiles need K % 64 == 0");
+        if (bn == 1256) launch_bn4<256>(a, b, c, bias, M, N, K, epi, s);
+        else if (bn == 1128) launch_bn4<128>(a, b, c, bias, M, N, K, epi, s);
+        else throw std::invalid_argument("gemm_nt: 4-wave tile width must be 1128 or 1256");
+        return;
+    }
     switch (bn) {
     case 256: launch_bn<256>(a, b, c, bias, M, N, K, epi, s); break;
     case 192: launch_bn<192>(a, b, c, bias, M, N, K, epi, s); break;

@@ -63,7 +63,9 @@ class BertForPreTraining(nn.Module):
         self.ln = nn.LayerNorm(d, eps=1e-12)
         self.layers = nn.ModuleList([BertLayer(d, heads, ffn) for _ in range(layers)])
         self.mlm_dense = nn.Linear(d, d)
-        self.mlm_ln = nn.LayerNorm(d, eps=1e-12)
+        from ..ops.layernorm import AddLayerNorm
+
+        self.mlm_ln = AddLayerNorm(d, eps=1e-12)  # HIP LayerNorm on the bf16 head (torch's off the GPU path)
         self.mlm_bias = nn.Parameter(torch.zeros(vocab))
         self.nsp = nn.Linear(d, 2)
         self.apply(self._init)

@@ -73,13 +73,16 @@ def test_gemm_accumulate():
 # ---- gemm.hip: the pipelined NT GEMM (BERT's forward / data-gradient products) ----
 @pytest.mark.parametrize("M,K,N", [(16384, 768, 2304), (4096, 3072, 768), (1000, 768, 768), (300, 64, 384),
                                    (257, 3072, 3072), (5000, 2304, 768)])
-@pytest.mark.parametrize("bn", [-1, 128, 192, 256])
+@pytest.mark.parametrize("bn", [-1, 128, 192, 256, 1128, 1256])
 def test_gemm_nt_matches_fp32(M, K, N, bn):
     """a[M,K] . b[N,K]^T (+ bias) (+ accumulate into out) vs the fp32 torch product: every tile
-    width, M tails (rows past M read zeros and are not stored), K from one slab up."""
+    width (1128 / 1256: the 4-wave layout, K % 64), M tails (rows past M read zeros and are not
+    stored), K from one slab up."""
     H = _hip()
-    if bn > 0 and N % bn:
+    if bn > 0 and N % (bn % 1000):
         pytest.skip("tile width does not divide N")
+    if bn > 1000 and K % 64:
+        pytest.skip("the 4-wave tiles need K % 64")
     torch.manual_seed(11)
     a = torch.randn(M, K, device="cuda").bfloat16()
     b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
