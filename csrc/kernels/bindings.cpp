@@ -1171,6 +1171,47 @@ BNCommon bn_common(int C, const at::Tensor &weight, const at::Tensor &bias,
     return b;
 }
 
+// Batched sums-finalize of several training-mode BNs (each with its producing conv's f64 slotted
+// sums): ONE launch; returns [mean, invstd, coef] per BN for bn_forward(..., pre=...).
+std::vector<std::vector<at::Tensor>> bn_finalize_multi(std::vector<at::Tensor> xs, std::vector<at::Tensor> sums,
+                                                       std::vector<at::Tensor> weights, std::vector<at::Tensor> biases,
+                                                       std::vector<c10::optional<at::Tensor>> running_means,
+                                                       std::vector<c10::optional<at::Tensor>> running_vars,
+                                                       std::vector<c10::optional<at::Tensor>> num_batches,
+                                                       std::vector<double> momentum, std::vector<double> eps) {
+    const size_t n = xs.size();
+    TORCH_CHECK(n >= 1 && n <= static_cast<size_t>(kfk::kBnFinMax) && sums.size() == n && weights.size() == n &&
+                    biases.size() == n && running_means.size() == n && running_vars.size() == n &&
+                    num_batches.size() == n && momentum.size() == n && eps.size() == n,
+                "bn_finalize_multi: 1..8 BNs, every list of the same length");
+    kfk::BnFinBatch b{};
+    b.n = static_cast<int>(n);
+    std::vector<std::vector<at::Tensor>> out;
+    for (size_t i = 0; i < n; ++i) {
+        auto sh = bn_shape(xs[i]);
+        const int C = sh.channels;
+        TORCH_CHECK(xs[i].device() == xs[0].device(), "bn_finalize_multi: one device");
+        auto c = bn_common(C, weights[i], biases[i], running_means[i], running_vars[i], num_batches[i], true);
+        const at::Tensor &s = sums[i];
+        TORCH_CHECK(s.is_cuda() && s.scalar_type() == at::kDouble && s.numel() == 2 * C * kfk::kStatSlots &&
+                        s.is_contiguous() && s.device() == xs[i].device(),
+                    "bn_finalize_multi: sums must be the conv epilogue's f64 slotted workspace");
+        auto fopt = xs[i].options().dtype(at::kFloat);
+        at::Tensor mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt), coef = at::empty({2 * C}, fopt);
+        kfk::BnFinDesc &d = b.d[i];
+        d.sums = s.data_ptr<double>();
+        d.gamma = weights[i].data_ptr<float>(), d.beta = biases[i].data_ptr<float>();
+        d.mean = mean.data_ptr<float>(), d.invstd = invstd.data_ptr<float>(), d.coef = coef.data_ptr<float>();
+        d.run_mean = c.rm, d.run_var = c.rv, d.nbt = c.nbt;
+        d.rows = sh.rows, d.C = C;
+        d.momentum = static_cast<float>(momentum[i]), d.eps = static_cast<float>(eps[i]);
+        out.push_back({mean, invstd, coef});
+    }
+    c10::DeviceGuard gd(xs[0].device());
+    kfk::launch_bn_sums_finalize_multi(b, stream_of(xs[0], 0));
+    return out;
+}
+
 // Returns (y, mean, invstd, coef, mask-or-undefined).
 std::vector<at::Tensor> bn_forward(at::Tensor x, c10::optional<at::Tensor> res, at::Tensor weight, at::Tensor bias,
                                    c10::optional<at::Tensor> running_mean, c10::optional<at::Tensor> running_var,
@@ -1916,6 +1957,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
           py::arg("num_batches") = py::none(), py::arg("sums") = py::none(), py::arg("res_coef") = py::none(),
           py::arg("apply") = true, py::arg("out") = py::none(), py::arg("pre") = py::none());
+    m.def("bn_finalize_multi", &bn_finalize_multi,
+          "batched sums-finalize of several training BNs in one launch -> [[mean, invstd, coef], ...]");
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",
           py::arg("dy"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"), py::arg("fcoef"),
           py::arg("mask"), py::arg("relu"), py::arg("training"), py::arg("want_dres"), py::arg("sums") = py::none(),

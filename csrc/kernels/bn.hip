@@ -317,6 +317,40 @@ __global__ __launch_bounds__(256) void bn_sums_finalize(double *__restrict__ sum
     bn_fin_fwd_channel(c, C, s, q, rows, g, b, rm, rv, mean, invstd, run_mean, run_var, momentum, eps, coef);
 }
 
+// Several BNs' sums-finalizes in ONE launch (blockIdx.y = which BN): the deferred branch BNs of an
+// Inception block's concatenation are all finalized before any of their applies (ops/fused_bn.py
+// _BNConcatFn), 2-6 launches of ~5 us each that were back-to-back anyway.
+__global__ __launch_bounds__(256) void bn_sums_finalize_multi(BnFinBatch b) {
+    const BnFinDesc &d = b.d[blockIdx.y];
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d.nbt && c == 0) d.nbt[0] += 1;
+    if (c >= d.C) return;
+    const int C = d.C;
+    const float g = d.gamma ? d.gamma[c] : 1.f, bb = d.beta ? d.beta[c] : 0.f;
+    const float rm = d.run_mean ? d.run_mean[c] : 0.f, rv = d.run_mean ? d.run_var[c] : 0.f;
+    const double *sp = d.sums + c;
+    double vs[kStatSlots], vq[kStatSlots];
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        vs[k] = sp[k * 2 * C];
+        vq[k] = sp[k * 2 * C + C];
+    }
+    double s = 0, q = 0;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        s += vs[k];
+        q += vq[k];
+    }
+    double *zp = d.sums + c;
+#pragma unroll
+    for (int k = 0; k < kStatSlots; ++k) {
+        zp[k * 2 * C] = 0.0;
+        zp[k * 2 * C + C] = 0.0;
+    }
+    bn_fin_fwd_channel(c, C, s, q, d.rows, g, bb, rm, rv, d.mean, d.invstd, d.run_mean, d.run_var, d.momentum, d.eps,
+                       d.coef);
+}
+
 // Eval mode: coefficients from running stats.
 __global__ void bn_eval_coef(int C, const float *gamma, const float *beta, const float *run_mean,
                              const float *run_var, float eps, float *mean, float *invstd, float *coef) {
@@ -957,6 +991,15 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
 }
 
 }  // namespace
+
+void launch_bn_sums_finalize_multi(const BnFinBatch &b, hipStream_t s) {
+    if (b.n <= 0) return;
+    if (b.n > kBnFinMax) throw std::invalid_argument("bn_sums_finalize_multi: too many BNs");
+    int cmax = 0;
+    for (int i = 0; i < b.n; ++i) cmax = b.d[i].C > cmax ? b.d[i].C : cmax;
+    if (bn_skip_finalize()) return;
+    bn_sums_finalize_multi<<<dim3((cmax + 255) / 256, b.n), 256, 0, s>>>(b);
+}
 
 bool bn_supported_channels(int C) {
     if (C % 8) return false;

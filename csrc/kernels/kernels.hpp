@@ -338,6 +338,24 @@ int bn_num_chunks(BNShape sh);  // partial scratch = 2 * nchunks * C floats
 // (2C floats), y = act(x*scale + shift [+ res]).  Eval: running stats.
 // With res && relu, mask (rows*C/8 bytes) receives the ReLU bits for the backward.
 // num_batches (optional, int64 on device) is incremented in training mode.
+// Batched sums-finalize of up to kBnFinMax BNs (the f64 slotted sums of their producing convs): mean,
+// invstd, running stats, coef = [scale; shift], num_batches += 1, slots re-zeroed -- one launch.
+struct BnFinDesc {
+    double *sums;
+    const float *gamma, *beta;
+    float *mean, *invstd, *run_mean, *run_var, *coef;
+    int64_t *nbt;
+    int64_t rows;
+    int C;
+    float momentum, eps;
+};
+constexpr int kBnFinMax = 8;
+struct BnFinBatch {
+    BnFinDesc d[kBnFinMax];
+    int n;
+};
+void launch_bn_sums_finalize_multi(const BnFinBatch &b, hipStream_t s);
+
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
                        float momentum, float eps, float *partial, float *mean, float *invstd, float *coef,

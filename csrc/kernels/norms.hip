@@ -389,22 +389,31 @@ __global__ __launch_bounds__(256) void gelu_bwd_colsum_stage1(const uint4 *__res
     }
 }
 
-// one block per 32 columns: 8 chunk lanes per column each sum every 8th chunk partial, then the
-// 8 lane sums meet in LDS in a fixed order (deterministic)
-__global__ __launch_bounds__(256) void colsum_stage2(const float *__restrict__ part, int chunks, int O, float *out_f32,
-                                                     uint16_t *out_bf16) {
-    __shared__ float red[8][33];
+// one block per 32 columns: kC2Lanes chunk lanes per column each sum every kC2Lanes-th chunk partial
+// (coalesced: the 32 columns of a row are adjacent), then the lane sums meet in LDS in a fixed order
+// (deterministic).  32 lanes (1024 threads): ~11 loads per lane for GELU's 341 chunks -- with 8 lanes the
+// 43-load chains made this ~10 us launch latency-bound (25 launches per BERT-base step).
+constexpr int kC2Lanes = 32;
+__global__ __launch_bounds__(32 * kC2Lanes) void colsum_stage2(const float *__restrict__ part, int chunks, int O,
+                                                               float *out_f32, uint16_t *out_bf16) {
+    __shared__ float red[kC2Lanes][33];
     const int cl = threadIdx.x & 31, lane = threadIdx.x >> 5;
     const int c = blockIdx.x * 32 + cl;
-    float s = 0.f;
-    if (c < O)
-        for (int k = lane; k < chunks; k += 8) s += part[static_cast<int64_t>(k) * O + c];
-    red[lane][cl] = s;
+    float s0 = 0.f, s1 = 0.f;
+    if (c < O) {
+        int k = lane;
+        for (; k + kC2Lanes < chunks; k += 2 * kC2Lanes) {  // two independent chains
+            s0 += part[static_cast<int64_t>(k) * O + c];
+            s1 += part[static_cast<int64_t>(k + kC2Lanes) * O + c];
+        }
+        if (k < chunks) s0 += part[static_cast<int64_t>(k) * O + c];
+    }
+    red[lane][cl] = s0 + s1;
     __syncthreads();
     if (lane == 0 && c < O) {
         float t = 0.f;
 #pragma unroll
-        for (int l = 0; l < 8; ++l) t += red[l][cl];
+        for (int l = 0; l < kC2Lanes; ++l) t += red[l][cl];
         if (out_f32) out_f32[c] = t;
         else out_bf16[c] = f32_to_bf16(t);
     }
@@ -426,7 +435,7 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
     const int rows_per = static_cast<int>((T + chunks - 1) / chunks);
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(x), T, OV, rows_per, part);
-    colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+    colsum_stage2<<<(O + 31) / 32, 32 * kC2Lanes, 0, s>>>(part, chunks, O, out_f32, out_bf16);
 }
 
 void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s) {
@@ -455,7 +464,7 @@ void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du,
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     gelu_bwd_colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(dy), reinterpret_cast<const uint4 *>(u),
                                               reinterpret_cast<uint4 *>(du), T, OV, rows_per, part);
-    colsum_stage2<<<(O + 31) / 32, 256, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+    colsum_stage2<<<(O + 31) / 32, 32 * kC2Lanes, 0, s>>>(part, chunks, O, out_f32, out_bf16);
 }
 
 }  // namespace kfk

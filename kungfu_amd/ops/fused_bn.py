@@ -192,6 +192,10 @@ class _ConcatSpec:
         self.items, self.ctot = items, ctot  # items: (bn module, sums) or None for a plain tensor
 
 
+# KUNGFU_BN_BATCH_FIN=0 (A/B): finalize the concatenation's BNs one launch each
+_BATCH_FIN = knobs.get("KUNGFU_BN_BATCH_FIN") != "0"
+
+
 class _BNConcatFn(torch.autograd.Function):
     """``torch.cat([relu(bn_i(y_i)) ..., t_j ...], 1)`` without the copy: each BN+ReLU apply pass
     writes straight into its channel slice of the concatenation (a strided HIP store), the plain
@@ -206,7 +210,27 @@ class _BNConcatFn(torch.autograd.Function):
         out = torch.empty((N, spec.ctot, Hh, W), dtype=torch.bfloat16, device=first.device,
                           memory_format=torch.channels_last)
         saved, direct, k, c0 = [], [], 0, 0
-        for item in spec.items:
+        # the conv-statistics BNs of the block: finalized together in ONE launch (bn_finalize_multi),
+        # then each applies straight into its slice with those coefficients
+        pre = {}
+        if _BATCH_FIN:
+            fin, kk = [], 0
+            for idx, item in enumerate(spec.items):
+                if item is not None:
+                    if item[1] is not None:
+                        fin.append((idx, args[kk], args[kk + 1], args[kk + 2], item))
+                    kk += 3
+                else:
+                    kk += 1
+            if 2 <= len(fin) <= 8:
+                cols = [[], [], [], [], [], [], [], [], []]
+                for _, y, g, b, (m, sums) in fin:
+                    a, nbt = m._args()
+                    for lst, v in zip(cols, (y, sums, g, b, a[2], a[3], nbt, float(a[5]), float(a[6]))):
+                        lst.append(v)
+                for (idx, *_), r in zip(fin, H.bn_finalize_multi(*cols)):
+                    pre[idx] = r
+        for idx, item in enumerate(spec.items):
             if item is not None:
                 y, g, b = args[k:k + 3]
                 k += 3
@@ -214,7 +238,7 @@ class _BNConcatFn(torch.autograd.Function):
                 a, nbt = m._args()
                 C = int(y.shape[1])
                 _, mean, invstd, coef, _ = H.bn_forward(y, None, g, b, a[2], a[3], a[5], a[6], True, True, nbt, sums,
-                                                        None, True, out[:, c0:c0 + C])
+                                                        None, True, out[:, c0:c0 + C], pre.get(idx))
                 saved += [y, mean, invstd, g, coef]
                 direct.append(_direct(g, b))
             else:
