@@ -1357,6 +1357,75 @@ std::vector<at::Tensor> bn_backward(at::Tensor dy, at::Tensor x, at::Tensor mean
     return {dx, dres, dw, db};
 }
 
+// Backward of several training BN+ReLUs (no residual, no sums) whose output gradients may be channel
+// slices of one concatenation's gradient: every reduce pass, ONE batched finalize, every apply pass.
+// Returns [dx, dgamma, dbeta] per BN.
+std::vector<std::vector<at::Tensor>> bn_backward_multi(std::vector<at::Tensor> dys, std::vector<at::Tensor> xs,
+                                                       std::vector<at::Tensor> means, std::vector<at::Tensor> invstds,
+                                                       std::vector<at::Tensor> weights, std::vector<at::Tensor> fcoefs) {
+    const size_t n = xs.size();
+    TORCH_CHECK(n >= 1 && n <= static_cast<size_t>(kfk::kBnFinMax) && dys.size() == n && means.size() == n &&
+                    invstds.size() == n && weights.size() == n && fcoefs.size() == n,
+                "bn_backward_multi: 1..8 BNs, every list of the same length");
+    c10::DeviceGuard gd(xs[0].device());
+    kfk::BnBwdFinBatch fb{};
+    fb.n = static_cast<int>(n);
+    struct Piece {
+        at::Tensor dy, dx, dw, db, coef, partial;
+        int64_t ld;
+        kfk::BNShape sh;
+    };
+    std::vector<Piece> ps(n);
+    for (size_t i = 0; i < n; ++i) {
+        Piece &p = ps[i];
+        p.sh = bn_shape(xs[i]);
+        const int C = p.sh.channels;
+        at::Tensor dy = dys[i];
+        p.ld = 0;
+        if (!dy.is_contiguous(at::MemoryFormat::ChannelsLast)) {
+            const int64_t ld = dy.dim() == 4 ? dy.stride(3) : 0;
+            const bool slice = dy.dim() == 4 && dy.stride(1) == 1 && ld >= C && ld % 8 == 0 &&
+                               dy.stride(2) == dy.size(3) * ld && dy.stride(0) == dy.size(2) * dy.size(3) * ld &&
+                               reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0;
+            if (slice) p.ld = ld;
+            else dy = dy.contiguous(at::MemoryFormat::ChannelsLast);
+        }
+        TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.sizes() == xs[i].sizes() && dy.device() == xs[0].device(),
+                    "bn_backward_multi: dy must match x");
+        TORCH_CHECK(fcoefs[i].scalar_type() == at::kFloat && fcoefs[i].numel() == 2 * C &&
+                        means[i].numel() == C && invstds[i].numel() == C && weights[i].numel() == C &&
+                        weights[i].scalar_type() == at::kFloat,
+                    "bn_backward_multi: f32 fcoef [2C], mean / invstd / weight [C]");
+        p.dy = dy;
+        auto fopt = xs[i].options().dtype(at::kFloat);
+        p.dx = at::empty_like(xs[i], at::MemoryFormat::ChannelsLast);
+        p.dw = at::empty({C}, fopt), p.db = at::empty({C}, fopt), p.coef = at::empty({3 * C}, fopt);
+        p.partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(p.sh)) * C}, fopt);
+        kfk::BnBwdFinDesc &d = fb.d[i];
+        d.partial = p.partial.data_ptr<float>();
+        d.nchunks = kfk::bn_num_chunks(p.sh), d.C = C, d.rows = p.sh.rows;
+        d.gamma = weights[i].data_ptr<float>(), d.mean = means[i].data_ptr<float>(), d.invstd = invstds[i].data_ptr<float>();
+        d.dgamma = p.dw.data_ptr<float>(), d.dbeta = p.db.data_ptr<float>(), d.coef = p.coef.data_ptr<float>();
+    }
+    const hipStream_t st = stream_of(xs[0], 0);
+    for (int phase : {1, 2}) {
+        if (phase == 2) kfk::launch_bn_bwd_finalize_multi(fb, st);
+        for (size_t i = 0; i < n; ++i) {
+            Piece &p = ps[i];
+            kfk::launch_bn_backward(reinterpret_cast<const uint16_t *>(p.dy.data_ptr()),
+                                    reinterpret_cast<const uint16_t *>(xs[i].data_ptr()), fcoefs[i].data_ptr<float>(),
+                                    nullptr, means[i].data_ptr<float>(), invstds[i].data_ptr<float>(),
+                                    weights[i].data_ptr<float>(), p.sh, true, true, p.partial.data_ptr<float>(),
+                                    p.dw.data_ptr<float>(), p.db.data_ptr<float>(), p.coef.data_ptr<float>(),
+                                    reinterpret_cast<uint16_t *>(p.dx.data_ptr()), nullptr, st, nullptr, nullptr,
+                                    nullptr, p.ld, false, phase);
+        }
+    }
+    std::vector<std::vector<at::Tensor>> out;
+    for (auto &p : ps) out.push_back({p.dx, p.dw, p.db});
+    return out;
+}
+
 // Stem BN+ReLU+MaxPool(3,2,1).  Returns (y_pool, mean, invstd, coef, argmax bytes).
 std::vector<at::Tensor> bn_pool_forward(at::Tensor x, at::Tensor weight, at::Tensor bias,
                                         c10::optional<at::Tensor> running_mean,
@@ -1957,6 +2026,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("momentum"), py::arg("eps"), py::arg("training"), py::arg("relu"),
           py::arg("num_batches") = py::none(), py::arg("sums") = py::none(), py::arg("res_coef") = py::none(),
           py::arg("apply") = true, py::arg("out") = py::none(), py::arg("pre") = py::none());
+    m.def("bn_backward_multi", &bn_backward_multi,
+          "backward of several BN+ReLUs (slices of one concatenation's gradient): one batched finalize");
     m.def("bn_finalize_multi", &bn_finalize_multi,
           "batched sums-finalize of several training BNs in one launch -> [[mean, invstd, coef], ...]");
     m.def("bn_backward", &bn_backward, "fused NHWC BN(+residual)(+ReLU) backward -> (dx, dres, dweight, dbias)",

@@ -759,6 +759,28 @@ __global__ __launch_bounds__(kBlock) void bn_bwd_finalize(const float *partial, 
     }
 }
 
+// Several BNs' backward finalizes in ONE launch (blockIdx.y = which BN): the branch BNs of an
+// Inception block's concatenation (ops/fused_bn.py _BNConcatFn.backward).
+__global__ __launch_bounds__(kBlock) void bn_bwd_finalize_multi(BnBwdFinBatch b) {
+    const BnBwdFinDesc &d = b.d[blockIdx.y];
+    const int C = d.C;
+    if (static_cast<int>(blockIdx.x) * kFoldCh >= C) return;  // a narrower BN of the batch: uniform exit
+    const int c = blockIdx.x * kFoldCh + threadIdx.x % kFoldCh, kl = threadIdx.x / kFoldCh;
+    double sums[2];
+    fold_partials<2>(d.partial, d.nchunks, C, c, kl, sums);
+    if (kl != 0 || c >= C) return;
+    double db = sums[0], dg = static_cast<double>(d.invstd[c]) * (sums[1] - static_cast<double>(d.mean[c]) * db);
+    d.dgamma[c] = static_cast<float>(dg);
+    d.dbeta[c] = static_cast<float>(db);
+    float g = d.gamma ? d.gamma[c] : 1.f;
+    float a = g * d.invstd[c];
+    const float inv_m = 1.f / static_cast<float>(d.rows);
+    const float k2 = -a * static_cast<float>(dg) * d.invstd[c] * inv_m;
+    d.coef[c] = a;
+    d.coef[C + c] = k2;
+    d.coef[2 * C + c] = -a * static_cast<float>(db) * inv_m - k2 * d.mean[c];
+}
+
 // Same coefficients from the f64 slotted sums of a data-gradient conv epilogue
 // (conv.hip kEpiBwd*): sum dz, sum dz*x; the slots are re-zeroed.
 __global__ __launch_bounds__(256) void bn_bwd_finalize_sums(double *__restrict__ sums, int C, int64_t rows,
@@ -939,12 +961,15 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
                           const float *invstd, const float *gamma, BNShape sh, int rm, bool training, float *partial,
                           float *dgamma, float *dbeta, float *coef, uint16_t *dx, uint16_t *dres, hipStream_t s,
                           double *sums = nullptr, const uint16_t *dres_x = nullptr, double *dres_sums = nullptr,
-                          bool prefinalized = false) {
+                          bool prefinalized = false, int phase = 0) {
+    // phase 0: everything; 1: the reduce pass only (statistics path, no sums); 2: the apply pass only
+    // (coef already finalized -- bn_bwd_finalize_multi)
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     Chunking ch = chunking(sh);
     const uint4 *xx = reinterpret_cast<const uint4 *>(x);
-    if (sums) {
+    if (phase == 2) {
+    } else if (sums) {
         if (!prefinalized && !bn_skip_finalize())
         bn_bwd_finalize_sums<<<(C + 255) / 256, 256, 0, s>>>(sums, C, sh.rows, gamma, mean, invstd, dgamma, dbeta,
                                                              coef, training);
@@ -961,6 +986,7 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
         else if (rm == RM_BITS) go(std::integral_constant<int, RM_BITS>());
         else go(std::integral_constant<int, RM_NONE>());
     });
+    if (phase == 1) return;
     bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
                                                                    invstd, dgamma, dbeta, coef, training);
     }
@@ -991,6 +1017,14 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
 }
 
 }  // namespace
+
+void launch_bn_bwd_finalize_multi(const BnBwdFinBatch &b, hipStream_t s) {
+    if (b.n <= 0) return;
+    if (b.n > kBnFinMax) throw std::invalid_argument("bn_bwd_finalize_multi: too many BNs");
+    int cmax = 0;
+    for (int i = 0; i < b.n; ++i) cmax = b.d[i].C > cmax ? b.d[i].C : cmax;
+    bn_bwd_finalize_multi<<<dim3((cmax + kFoldCh - 1) / kFoldCh, b.n), kBlock, 0, s>>>(b);
+}
 
 void launch_bn_sums_finalize_multi(const BnFinBatch &b, hipStream_t s) {
     if (b.n <= 0) return;
@@ -1062,17 +1096,17 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                         const float *mean, const float *invstd, const float *gamma, BNShape sh, bool relu,
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                         uint16_t *dres, hipStream_t s, double *sums, const uint16_t *dres_x, double *dres_sums,
-                        int64_t dy_ld, bool prefinalized) {
+                        int64_t dy_ld, bool prefinalized, int phase) {
     const int rm = !relu ? RM_NONE : (mask ? RM_BITS : RM_COEF);
     if (dy_ld > 0 && dy_ld != sh.channels) {
         if (dy_ld % 8) throw std::invalid_argument("bn_backward: dy row stride must be a multiple of 8");
         launch_backward_impl(StridedGrad{reinterpret_cast<const uint4 *>(dy), dy_ld / 8}, x, fcoef, mask, mean, invstd,
                              gamma, sh, rm, training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x,
-                             dres_sums, prefinalized);
+                             dres_sums, prefinalized, phase);
         return;
     }
     launch_backward_impl(DirectGrad{reinterpret_cast<const uint4 *>(dy), (bn_nt_mode() & 1) != 0}, x, fcoef, mask, mean, invstd, gamma, sh, rm,
-                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums, prefinalized);
+                         training, partial, dgamma, dbeta, coef, dx, dres, s, sums, dres_x, dres_sums, prefinalized, phase);
 }
 
 bool bn_pool_supported(BNShape sh, int H, int W) {

@@ -355,6 +355,19 @@ struct BnFinBatch {
     int n;
 };
 void launch_bn_sums_finalize_multi(const BnFinBatch &b, hipStream_t s);
+// Batched backward finalize (statistics path: the reduce pass's partials) of up to kBnFinMax training BNs.
+struct BnBwdFinDesc {
+    const float *partial;
+    int nchunks, C;
+    int64_t rows;
+    const float *gamma, *mean, *invstd;
+    float *dgamma, *dbeta, *coef;
+};
+struct BnBwdFinBatch {
+    BnBwdFinDesc d[kBnFinMax];
+    int n;
+};
+void launch_bn_bwd_finalize_multi(const BnBwdFinBatch &b, hipStream_t s);
 
 void launch_bn_forward(const uint16_t *x, const uint16_t *res, const float *gamma, const float *beta, uint16_t *y,
                        uint8_t *mask, BNShape sh, bool relu, bool training, float *run_mean, float *run_var,
@@ -375,7 +388,7 @@ void launch_bn_backward(const uint16_t *dy, const uint16_t *x, const float *fcoe
                         bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
                         uint16_t *dres, hipStream_t s, double *sums = nullptr, const uint16_t *dres_x = nullptr,
                         double *dres_sums = nullptr,
-                        int64_t dy_ld = 0, bool prefinalized = false);
+                        int64_t dy_ld = 0, bool prefinalized = false, int phase = 0);
 // (dres_x / dres_sums: dres also feeds a second, ReLU-free BN with input dres_x -- its backward
 //  sums go to dres_sums, zeroed f64 [slots][2][C])
 // (sums: f64 kStatSlots x [sum dz; sum dz*x] from a conv epilogue -> no reduce pass; re-zeroed.)

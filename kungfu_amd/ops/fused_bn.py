@@ -192,8 +192,8 @@ class _ConcatSpec:
         self.items, self.ctot = items, ctot  # items: (bn module, sums) or None for a plain tensor
 
 
-# KUNGFU_BN_BATCH_FIN=0 (A/B): finalize the concatenation's BNs one launch each
-_BATCH_FIN = knobs.get("KUNGFU_BN_BATCH_FIN") != "0"
+# KUNGFU_BN_BATCH_FIN=1 (A/B): the concatenation's BN finalizes batched, one launch per direction
+_BATCH_FIN = knobs.get("KUNGFU_BN_BATCH_FIN") == "1"
 
 
 class _BNConcatFn(torch.autograd.Function):
@@ -259,13 +259,33 @@ class _BNConcatFn(torch.autograd.Function):
             dout = dout.contiguous(memory_format=torch.channels_last)
         saved = list(ctx.saved_tensors)
         grads, c0, si, pi, bi = [], 0, 0, 0, 0
+        multi = None
+        nbn = sum(1 for it in ctx.spec.items if it is not None)
+        if _BATCH_FIN and 2 <= nbn <= 8:
+            # every branch BN's reduce pass, ONE batched finalize, every apply (bn_backward_multi)
+            cols, cc, ss, pp = [[], [], [], [], [], []], 0, 0, 0
+            for item in ctx.spec.items:
+                if item is not None:
+                    y, mean, invstd, g, coef = saved[ss:ss + 5]
+                    ss += 5
+                    C = int(y.shape[1])
+                    for lst, v in zip(cols, (dout[:, cc:cc + C], y, mean, invstd, g, coef)):
+                        lst.append(v)
+                    cc += C
+                else:
+                    cc += ctx.plain[pp]
+                    pp += 1
+            multi = iter(H.bn_backward_multi(*cols))
         for item in ctx.spec.items:
             if item is not None:
                 y, mean, invstd, g, coef = saved[si:si + 5]
                 si += 5
                 C = int(y.shape[1])
-                dx, _, dw, db = H.bn_backward(dout[:, c0:c0 + C], y, mean, invstd, g, coef, None, True, True, False,
-                                              None)
+                if multi is not None:
+                    dx, dw, db = next(multi)
+                else:
+                    dx, _, dw, db = H.bn_backward(dout[:, c0:c0 + C], y, mean, invstd, g, coef, None, True, True,
+                                                  False, None)
                 d = ctx.direct[bi]
                 bi += 1
                 if d is not None:

@@ -1568,16 +1568,20 @@ def test_colsum_matches_torch(H, T, O):
 
 
 @needs_gpu
+@pytest.mark.parametrize("batch_fin", [False, True])
 @pytest.mark.parametrize("block", ["A", "B", "C", "D", "E"])
-def test_inception_bn_concat_matches_cat(block, monkeypatch):
+def test_inception_bn_concat_matches_cat(block, batch_fin, monkeypatch):
     """Inception blocks whose branch BN+ReLUs write straight into their slice of the
     concatenation (ops.fused_bn.bn_relu_concat) against the same blocks with the BNs applied
-    separately and torch.cat: outputs, block-input and parameter gradients, running stats."""
+    separately and torch.cat: outputs, block-input and parameter gradients, running stats
+    (including num_batches_tracked).  ``batch_fin``: the concatenation's BN finalizes (forward
+    and backward) batched into one launch each (bn_finalize_multi / bn_backward_multi)."""
     import copy
 
     from kungfu_amd.models import inception as inc
     from kungfu_amd.ops import fused_bn
 
+    monkeypatch.setattr(fused_bn, "_BATCH_FIN", batch_fin)
     torch.manual_seed(5)
     inc._FUSED_BN[0] = True
     try:
