@@ -140,7 +140,11 @@ class GraphedStep:
             # collective: not capturable (decided identically on every rank, nothing attempted)
             err = RuntimeError("the %s data plane cannot be captured" % plane)
         multi = plane == "rccl" and getattr(reducer.comm, "size", 1) > 1
-        if multi and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
+        if err is None and getattr(reducer, "_hier", None) is not None:
+            # hierarchical across hosts: a host thread all-reduces between the local reduce and the
+            # local broadcast -- host work inside the step, not capturable
+            err = RuntimeError("the cross-host hierarchical all-reduce cannot be captured")
+        elif multi and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
             err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=0)")
         try:
             if err is not None:
