@@ -139,7 +139,7 @@ class GraphedStep:
             # the host-staged plane synchronises and copies through host memory inside every
             # collective: not capturable (decided identically on every rank, nothing attempted)
             err = RuntimeError("the %s data plane cannot be captured" % plane)
-        multi = plane == "rccl" and getattr(reducer.comm, "size", 1) > 1
+        multi = reducer is not None and plane == "rccl" and getattr(getattr(reducer, "comm", None), "size", 1) > 1
         if err is None and getattr(reducer, "_hier", None) is not None:
             # hierarchical across hosts: a host thread all-reduces between the local reduce and the
             # local broadcast -- host work inside the step, not capturable
