@@ -256,9 +256,9 @@ def main():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
-                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for the conv models with S-SGD "
-                        "(every op of their step is capturable; replay measured bit-identical to eager; multi-rank "
-                        "steps capture their RCCL all-reduces too), off for BERT")
+                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for ResNet-50 / Inception-v3 with "
+                        "S-SGD (replay measured bit-identical to eager; multi-rank steps capture their RCCL "
+                        "all-reduces too), off for BERT and VGG-16 (its fused stack's replay diverged)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -400,7 +400,8 @@ def main():
     if a.graph < 0:
         # multi-rank: the bucket all-reduces are captured with the comm stream as the capture's origin
         # (GraphedStep; RCCL on a joined stream crashed the HIP runtime, profiles/r4_host_overhead.md)
-        a.graph = 0 if bert or a.optimizer not in ("ssgd", "local") else 1
+        # VGG-16's fused conv stack is not replay-safe yet: its captured step diverged to NaN (r4final)
+        a.graph = 0 if bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local") else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 
