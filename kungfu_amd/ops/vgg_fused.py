@@ -126,15 +126,19 @@ class FusedVGGFeatures(nn.Sequential):
                 return [], ()
         return convs, tuple(pool_after)
 
-    def _eligible(self, x: torch.Tensor, convs: Sequence[nn.Conv2d]) -> bool:
+    def _eligible(self, x: torch.Tensor, convs: Sequence[nn.Conv2d], pool_after: Sequence[bool] = ()) -> bool:
         if not convs or not x.is_cuda or not hip_available() or x.dim() != 4:
             return False
         if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             return False
-        # the stack's activations (N*H*W * widest channel count at its input resolution) must stay
-        # below the conv kernels' 2 GiB buffer-resource range
-        if not buf_ok(x.numel() // x.shape[1] * max(c.out_channels for c in convs)):
-            return False
+        # every layer's activations (N * H_l * W_l * its widest channel count, at ITS resolution: the
+        # max-pools halve it) must stay below the conv kernels' 2 GiB buffer-resource range
+        n, h, w = x.shape[0], x.shape[2], x.shape[3]
+        for i, c in enumerate(convs):
+            if not buf_ok(n * h * w * max(c.in_channels, c.out_channels)):
+                return False
+            if i < len(pool_after) and pool_after[i]:
+                h, w = h // 2, w // 2
         H = hip()
         for i, c in enumerate(convs):
             if c.kernel_size != (3, 3) or c.stride != (1, 1) or c.padding != (1, 1) or c.groups != 1 or c.bias is None:
@@ -147,7 +151,7 @@ class FusedVGGFeatures(nn.Sequential):
 
     def forward(self, x):
         convs, pool_after = self._plan()
-        if not self._eligible(x, convs):
+        if not self._eligible(x, convs, pool_after):
             return super().forward(x)
         from ..parallel.mixed import shadow
 
