@@ -33,6 +33,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._lib import buf_ok, hip, hip_available
+from .. import knobs
+
+_ENABLED = knobs.get("KUNGFU_VGG_FUSED") != "0"
 
 _CL = torch.channels_last
 
@@ -127,7 +130,7 @@ class FusedVGGFeatures(nn.Sequential):
         return convs, tuple(pool_after)
 
     def _eligible(self, x: torch.Tensor, convs: Sequence[nn.Conv2d], pool_after: Sequence[bool] = ()) -> bool:
-        if not convs or not x.is_cuda or not hip_available() or x.dim() != 4:
+        if not convs or not x.is_cuda or not hip_available() or x.dim() != 4 or not _ENABLED:
             return False
         if not (torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
             return False
