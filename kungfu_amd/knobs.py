@@ -125,6 +125,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_GELU_BIAS_LINK": _d("1", "FC1 bias gradient from the fused GELU-backward column sum"),
     "KUNGFU_ATTN_BWD_WAVES": _d("8", "waves per S = 128 attention-backward workgroup (8 or 4)"),
     "KUNGFU_BN_BATCH_FIN": _d("1", "Inception concatenation: its BNs' finalizes in one launch each way (0: one per BN)"),
+    "KUNGFU_LINEAR_WGRAD_ATOMICS": _d("0", "1: linear weight-gradient split-K tiles added into the f32 slot by atomics (not reproducible)"),
     "KUNGFU_VGG_FUSED": _d("1", "VGG-16 conv/ReLU/pool stack as one autograd node (0: the per-layer modules)"),
     "KUNGFU_PAIR_NATIVE": _d("1", "pair-averaging prefetch on the native C++ thread (0: the Python thread)"),
     "KUNGFU_FUSED_XENT": _d("1", "BERT MLM loss on xent.hip straight from the bf16 logits (0: torch f32 path)"),

@@ -68,6 +68,9 @@ def residual_link(x: torch.Tensor):
 
 
 _DIRECT_WGRAD = knobs.get("KUNGFU_LINEAR_DIRECT_WGRAD") != "0"
+# split-K weight-gradient tiles added into the f32 slot with atomics (no partials, no reduce pass;
+# not bitwise reproducible) instead of the deterministic two-pass reduce
+_WGRAD_ATOMICS = knobs.get("KUNGFU_LINEAR_WGRAD_ATOMICS") == "1"  # A/B r4t29: 3 % slower on BERT-base
 # KUNGFU_LINEAR_GEMM=1: forward (x W^T + b) and data gradient (dy W, with W^T from the flat
 # space's per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt
 _GEMM = knobs.get("KUNGFU_LINEAR_GEMM") == "1"
@@ -152,7 +155,7 @@ class _LinearFn(torch.autograd.Function):
             space, i = tgt
             gv = space.grad_view(i)
             hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1, out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
-                             accumulate=True, atomics=False)
+                             accumulate=True, atomics=_WGRAD_ATOMICS)
             space.sink.put_direct(i)
         elif ctx.needs_input_grad[1]:
             dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
