@@ -256,9 +256,9 @@ def main():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
-                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for ResNet-50 / Inception-v3 with "
-                        "S-SGD (replay measured bit-identical to eager; multi-rank steps capture their RCCL "
-                        "all-reduces too), off for BERT and VGG-16 (its fused stack's replay diverged)")
+                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for single-rank ResNet-50 / "
+                        "Inception-v3 with S-SGD (replay measured bit-identical to eager); off for multi-rank steps "
+                        "(the replay overlaps the all-reduces with backward less), BERT and VGG-16 (measured no gain)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -398,10 +398,13 @@ def main():
         return _elastic_loop(a, model, opt, step, sync, bert)
     graphed = None
     if a.graph < 0:
-        # multi-rank: the bucket all-reduces are captured with the comm stream as the capture's origin
-        # (GraphedStep; RCCL on a joined stream crashed the HIP runtime, profiles/r4_host_overhead.md)
-        # VGG-16's fused conv stack is not replay-safe yet: its captured step diverged to NaN (r4final)
-        a.graph = 0 if bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local") else 1
+        # single-rank ResNet-50 / Inception-v3 only.  Multi-rank steps stay eager: with the all-reduces
+        # in flight (1-GPU model of an 8-rank ring, --emulate-comm 8) the replay overlaps them with
+        # backward less than eager streams do -- 21.52-21.86 vs 21.41-21.55 ms/step, r4t33 -- which
+        # outweighs the host time it saves (multi-rank capture itself works: --graph 1).  BERT: replay
+        # measured 2.4 % slower (r4t31); VGG-16: +0.4 % only (r4_host_overhead.md)
+        a.graph = 0 if (bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local") or size > 1
+                        or a.emulate_comm) else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 

@@ -174,11 +174,11 @@ def test_hierarchical_bucket_engine_two_fake_hosts_rccl(dtype):
 
 @needs_gpu
 def test_bench_two_ranks_whole_step_graph():
-    """bench.py with 2 colocated RCCL ranks (graph on by default): each rank captures its whole step
+    """bench.py --graph 1 with 2 colocated RCCL ranks (multi-rank steps default to eager): each rank captures its whole step
     with the comm stream as the capture's origin (bucket all-reduces inside the graph), the ranks
     agree on the capture, replays exchange gradients (every rank draws its own batch, yet the
     replicas end identical)."""
-    res = _bench(dict(COLO), extra=["--steps", "4", "--warmup", "4"])
+    res = _bench(dict(COLO), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
     v = res["verify"]
     hg = res["config"]["hip_graph"]
     assert hg["captured"] is True and hg["replays"] >= 4 and not hg["disabled"], hg
