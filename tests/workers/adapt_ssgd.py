@@ -68,10 +68,14 @@ else:
     if kind == "cpu" and ad.switched_at < 8:
         # switched before the injected slowdown: only acceptable when the statistics really showed
         # a slowdown then (a loaded CI machine stalls the host transport too); the vote must have
-        # had the evidence it acted on
+        # had the evidence it acted on (the vote's own rule: a window below 0.8 x the reference,
+        # adaptiveStrategies.go)
         early = [t for t in ad.throughputs[3:ad.switched_at] if t]
-        assert early and min(early) < 0.5 * max(tps[:6]), (ad.switched_at, ad.throughputs)
-    assert tps[-1] < 0.5 * max(tps[2:6]), ad.throughputs  # the slowdown is visible in the statistics
+        assert early and min(early) < 0.8 * max(tps[:6]), (ad.switched_at, ad.throughputs)
+    # the slowdown is visible in the statistics (in some window after it starts: on a loaded CI
+    # machine single windows of the slowed phase can be as fast as the noisy warm-up ones)
+    late = [t for t in ad.throughputs[7:] if t]
+    assert late and min(late) < 0.5 * max(tps[2:6]), ad.throughputs
     after = runtime.global_strategy_pairs()
     assert after != before, (before, after)
 print("ADAPT_OK rank=%d switched_at=%s tp_before=%.3g tp_after=%.3g" % (r, ad.switched_at, tps[4], tps[-1]), flush=True)
