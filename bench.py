@@ -69,10 +69,12 @@ def _setup_env():
     # message naming the op and rank (exit 3) instead of hanging until an outer timeout
     os.environ.setdefault("KUNGFU_RCCL_TIMEOUT_S", "300")
     os.environ.setdefault("KUNGFU_OP_TIMEOUT_S", "900")
-    # RCCL's own CTA choice is kept (no KUNGFU_RCCL_{MIN,MAX}_CTAS default): the comm emulation
-    # (profiles/r4_comm_emulation.md) wants >= 16 CTAs per gradient all-reduce, and RCCL sizes its
-    # channels for the 8-GPU xGMI ring itself (unmeasured here); a floor set alone is rejected by
-    # ncclCommInitRankConfig (minCTAs needs maxCTAs), measured on the colocated 2-rank run
+    # RCCL CTA budget of the gradient all-reduces: >= 16 CTAs per collective (the comm emulation,
+    # profiles/r4_comm_emulation.md: fewer cost +0.3 .. +3.4 ms/step at N = 8), at most 64 (a quarter
+    # of the 256 CUs' wave slots of one SIMD each, leaving the backward its CUs).  RCCL needs the pair
+    # (a floor alone is rejected by ncclCommInitRankConfig).  Reported in verify.rccl_ctas.
+    os.environ.setdefault("KUNGFU_RCCL_MIN_CTAS", "16")
+    os.environ.setdefault("KUNGFU_RCCL_MAX_CTAS", "64")
 
 
 def _launcher_env() -> bool:
@@ -256,9 +258,9 @@ def main():
     p.add_argument("--lr", type=float, default=0.1)
     p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
-                        "(kungfu_amd.parallel.graphs.GraphedStep); -1 (default): on for single-rank ResNet-50 / "
-                        "Inception-v3 with S-SGD (replay measured bit-identical to eager); off for multi-rank steps "
-                        "(the replay overlaps the all-reduces with backward less), BERT and VGG-16 (measured no gain)")
+                        "(kungfu_amd.parallel.graphs.GraphedStep; N > 1: graph segments with eager collectives); "
+                        "-1 (default): on for ResNet-50 / Inception-v3 with S-SGD (replay measured bit-identical "
+                        "to eager); off for BERT and VGG-16 (measured no gain)")
     p.add_argument("--json-out", default=None)
     p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                    help="cpu: f32 on CPU peers over the host transport (tests of the launch / verify path only)")
@@ -272,6 +274,9 @@ def main():
     p.add_argument("--emulate-ctas", type=int, default=16, help="--emulate-comm: workgroups per all-reduce")
     p.add_argument("--emulate-busbw", type=float, default=350.0, help="--emulate-comm: modelled ring busbw, GB/s")
     p.add_argument("--emulate-lat-us", type=float, default=25.0, help="--emulate-comm: modelled per-collective latency")
+    p.add_argument("--comm-probe", type=int, default=3, metavar="STEPS",
+                   help="after the timed steps: this many extra (untimed, eager) steps with HIP events around every "
+                        "bucket collective -> verify.comm_per_bucket_ms / exposed_comm_ms (0 = off)")
     p.add_argument("--elastic", default=None, metavar="SIZE:STEPS,...",
                    help="elastic run (config 5): resize the job along this schedule, e.g. 4:20,8:20 "
                         "(self-launches kungfu-run -w with its built-in config server)")
@@ -398,13 +403,14 @@ def main():
         return _elastic_loop(a, model, opt, step, sync, bert)
     graphed = None
     if a.graph < 0:
-        # single-rank ResNet-50 / Inception-v3 only.  Multi-rank steps stay eager: with the all-reduces
-        # in flight (1-GPU model of an 8-rank ring, --emulate-comm 8) the replay overlaps them with
-        # backward less than eager streams do -- 21.52-21.86 vs 21.41-21.55 ms/step, r4t33 -- which
-        # outweighs the host time it saves (multi-rank capture itself works: --graph 1).  BERT: replay
-        # measured 2.4 % slower (r4t31); VGG-16: +0.4 % only (r4_host_overhead.md)
-        a.graph = 0 if (bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local") or size > 1
-                        or a.emulate_comm) else 1
+        # ResNet-50 / Inception-v3 with S-SGD.  N = 1: one whole-step graph.  N > 1 (and the 1-GPU
+        # model of it, --emulate-comm): graph SEGMENTS cut at every bucket launch with the collectives
+        # issued eagerly between replays (parallel/graphs.py; KUNGFU_GRAPH_SEGMENTED) -- emulated 8-rank
+        # ResNet-50 21.15-21.18 vs eager 21.19-21.22 ms/step (r5t6; one graph with the collectives
+        # inside: 21.55-21.59), and the host no longer enqueues ~460-900 kernels per rank per step
+        # (Inception-v3: 17.4 ms of host time per 20.9 ms step eagerly, r5t5).  BERT: replay measured
+        # 2.4 % slower (r4t31); VGG-16: +0.4 % only (r4_host_overhead.md)
+        a.graph = 0 if (bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local")) else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 
@@ -448,6 +454,15 @@ def main():
     dt_max = max(dt_all)
     value = a.batch * size * a.steps / dt_max
     reducer = getattr(opt, "reducer", None)
+    comm_probe = None
+    if a.comm_probe > 0 and cuda and reducer is not None and not reducer.skip:
+        # untimed: where an N-rank step's communication goes, per bucket (HIP events, eager steps)
+        reducer.probe = []
+        for _ in range(a.comm_probe):
+            (graphed._eager() if graphed is not None else step()).detach()
+        comm_probe = reducer.probe_summary()
+        reducer.probe = None
+        sync()
     if reducer is not None:
         comm_info = reducer.describe()
     elif getattr(opt, "averager", None) is not None:  # SMA / AdaSGD: model all-reduce per step
@@ -494,6 +509,9 @@ def main():
         "rccl_watchdog": ({"ops_watched": wd["registered"], "pending": wd["pending"], "timeout_s": wd["timeout_s"],
                            "abort_on_stall": wd.get("abort_on_stall")} if wd else None),
         "rccl_ctas": list(getattr(getattr(reducer, "comm", None), "ctas", (0, 0)) or (0, 0)),
+        "comm_per_bucket_ms": comm_probe["comm_per_bucket_ms"] if comm_probe else None,
+        "exposed_comm_ms": comm_probe["exposed_comm_ms"] if comm_probe else None,
+        "comm_probe": comm_probe,
         "preflight": preflight if preflight is not None else ("skipped (one rank)" if size == 1 else "disabled"),
     }
     if sync_algo and not consistent:
@@ -529,7 +547,8 @@ def main():
             "optimizer": "%s(%s)" % (a.optimizer, opt_desc),
             "fused_bn_hip": bool(fused_bn),
             "bf16_shadow_weights": bool(a.bf16_shadow),
-            "hip_graph": ({"replays": graphed.replays, "captured": graphed.graph is not None, "disabled": graphed.disabled}
+            "hip_graph": ({"replays": graphed.replays, "captured": graphed.graph is not None, "disabled": graphed.disabled,
+                           "segments": len(graphed.segs) if graphed.segs else (1 if graphed.graph is not None else 0)}
                           if graphed is not None else False),
             "per_gpu_img_s": round(value / size, 2),
             "tokens_per_s": round(value * a.seq_len, 1) if bert else None,

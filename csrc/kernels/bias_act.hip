@@ -14,8 +14,17 @@
 // Layout: rows = N*H*W, C contiguous, one lane = one 16-byte vector of 8 channels,
 // CVEC = C/8 divides the 256-thread block, so every grid stride is a multiple of CVEC and
 // a lane's channel group is fixed: per-channel bias / gradient accumulators stay in
-// registers.  The bias-gradient block partials are reduced through LDS and added with one
-// f32 global atomic per channel per block (vector memory atomics).
+// registers.  The bias gradient is deterministic and needs no zeroed output: each block
+// folds its rows through LDS and WRITES its [C] partial (plain vector stores, no atomics),
+// then colsum_rows_kernel sums the <= 4096 block partials per channel in a fixed order
+// (two levels: 64 rows per workgroup, then the <= 64 level sums).
+//
+// Round 5: the previous form zeroed the f32 gradient with
+// hipMemsetAsync and added block partials with f32 atomics.  It was the only in-step
+// hipMemsetAsync of the engine and the only piece of VGG-16's per-layer path that the
+// fused stack does not share; under whole-step capture that path gave a different loss
+// in every run and went NaN in ~1 of 4 runs, while eager was bit-stable.  The memset
+// node is not needed any more and the sum no longer depends on atomic arrival order.
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -66,7 +75,7 @@ __global__ __launch_bounds__(kBlock) void bias_act_fwd_kernel(uint4 *__restrict_
 template <int CVEC, bool RELU>
 __global__ __launch_bounds__(kBlock) void bias_act_bwd_kernel(const uint4 *__restrict__ dy,
                                                               const uint4 *__restrict__ y, uint4 *__restrict__ dz,
-                                                              float *__restrict__ dbias, int64_t nvec) {
+                                                              float *__restrict__ partial, int64_t nvec) {
     constexpr int C = CVEC * 8, RPI = kBlock / CVEC;
     __shared__ float lds[kBlock * 8];
     const int64_t tid = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
@@ -93,12 +102,63 @@ __global__ __launch_bounds__(kBlock) void bias_act_bwd_kernel(const uint4 *__res
 #pragma unroll
     for (int k = 0; k < 8; ++k) lds[r0 * C + cv * 8 + k] = acc[k];
     __syncthreads();
+    float *part = partial + static_cast<int64_t>(blockIdx.x) * C;
     for (int c = threadIdx.x; c < C; c += kBlock) {
         float s = 0.f;
         for (int r = 0; r < RPI; ++r) s += lds[r * C + c];
-        atomicAdd(dbias + c, s);
+        part[c] = s;
     }
 }
+
+// Deterministic column sums of an f32 [R, C] partial matrix (C % 4 == 0), in a fixed order:
+// workgroup w sums rows [w * rpw, (w + 1) * rpw) into out[w][:].  Lanes are (row group, channel
+// quad): CQ = C / 4 quads, RG = 256 / CQ row groups when CQ < 256, each lane adding every RG-th row
+// of its range with 16-byte loads (adjacent lanes = adjacent quads: coalesced), the RG lane partials
+// then folded through LDS in row-group order.  Two launches (R -> R / 64 -> 1) replace one lane per
+// channel walking all <= 4096 block partials (latency-bound: ~4 ms per VGG-16 step, r5t6).
+__global__ __launch_bounds__(kBlock) void colsum_rows_kernel(const float *__restrict__ in, float *__restrict__ out,
+                                                             int R, int C, int rpw) {
+    __shared__ float4 lds[kBlock];
+    const int CQ = C >> 2;
+    const int RG = CQ >= kBlock ? 1 : kBlock / CQ;
+    const int r0 = blockIdx.x * rpw;
+    const int r1 = min(R, r0 + rpw);
+    const int rg = threadIdx.x / min(CQ, kBlock);
+    for (int cq0 = 0; cq0 < CQ; cq0 += kBlock) {
+        const int cq = cq0 + threadIdx.x % min(CQ, kBlock);
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (cq < CQ) {
+            const float4 *col = reinterpret_cast<const float4 *>(in) + cq;
+#pragma unroll 4
+            for (int r = r0 + rg; r < r1; r += RG) {
+                const float4 v = col[static_cast<int64_t>(r) * CQ];
+                a.x += v.x;
+                a.y += v.y;
+                a.z += v.z;
+                a.w += v.w;
+            }
+        }
+        if (RG == 1) {
+            if (cq < CQ) reinterpret_cast<float4 *>(out)[static_cast<int64_t>(blockIdx.x) * CQ + cq] = a;
+            continue;
+        }
+        lds[threadIdx.x] = a;
+        __syncthreads();
+        if (rg == 0) {
+            for (int g = 1; g < RG; ++g) {
+                const float4 v = lds[g * CQ + threadIdx.x];
+                a.x += v.x;
+                a.y += v.y;
+                a.z += v.z;
+                a.w += v.w;
+            }
+            reinterpret_cast<float4 *>(out)[static_cast<int64_t>(blockIdx.x) * CQ + cq] = a;
+        }
+        __syncthreads();
+    }
+}
+
+constexpr int kColsumRows = 64;  // rows per workgroup of the first column-sum level
 
 template <class F>
 void dispatch_bias_cvec(int cvec, F &&f) {
@@ -143,18 +203,34 @@ void launch_bias_act_forward(uint16_t *y, const float *bias, int64_t rows, int C
     });
 }
 
-void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, int64_t rows, int C,
-                              bool relu, hipStream_t s) {
+int bias_act_backward_blocks(int64_t rows, int C) {
+    const int blocks = bias_grid(rows * (C / 8));
+    return blocks + (blocks + kColsumRows - 1) / kColsumRows;  // block partials + the first sum level
+}
+
+void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, float *partial,
+                              int64_t rows, int C, bool relu, hipStream_t s) {
     const int64_t nvec = rows * (C / 8);
-    (void)hipMemsetAsync(dbias, 0, sizeof(float) * C, s);
-    if (nvec == 0) return;
-    dispatch_bias_cvec(C / 8, [&](auto cvc) {
-        constexpr int CV = decltype(cvc)::value;
-        const uint4 *dv = reinterpret_cast<const uint4 *>(dy), *yv = reinterpret_cast<const uint4 *>(y);
-        uint4 *zv = reinterpret_cast<uint4 *>(dz);
-        if (relu) bias_act_bwd_kernel<CV, true><<<bias_grid(nvec), kBlock, 0, s>>>(dv, yv, zv, dbias, nvec);
-        else bias_act_bwd_kernel<CV, false><<<bias_grid(nvec), kBlock, 0, s>>>(dv, yv, zv, dbias, nvec);
-    });
+    const int blocks = bias_grid(nvec);
+    if (nvec > 0) {
+        dispatch_bias_cvec(C / 8, [&](auto cvc) {
+            constexpr int CV = decltype(cvc)::value;
+            const uint4 *dv = reinterpret_cast<const uint4 *>(dy), *yv = reinterpret_cast<const uint4 *>(y);
+            uint4 *zv = reinterpret_cast<uint4 *>(dz);
+            if (relu) bias_act_bwd_kernel<CV, true><<<blocks, kBlock, 0, s>>>(dv, yv, zv, partial, nvec);
+            else bias_act_bwd_kernel<CV, false><<<blocks, kBlock, 0, s>>>(dv, yv, zv, partial, nvec);
+        });
+    }
+    // nvec == 0: zero partial rows are summed (the column sum writes dbias = 0 then)
+    const int R = nvec > 0 ? blocks : 0;
+    if (R > kColsumRows) {
+        const int R2 = (R + kColsumRows - 1) / kColsumRows;
+        float *mid = partial + static_cast<int64_t>(blocks) * C;
+        colsum_rows_kernel<<<R2, kBlock, 0, s>>>(partial, mid, R, C, kColsumRows);
+        colsum_rows_kernel<<<1, kBlock, 0, s>>>(mid, dbias, R2, C, R2);
+    } else {
+        colsum_rows_kernel<<<1, kBlock, 0, s>>>(partial, dbias, R, C, kColsumRows);
+    }
 }
 
 }  // namespace kfk

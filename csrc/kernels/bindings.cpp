@@ -817,10 +817,11 @@ std::vector<at::Tensor> bias_act_backward(at::Tensor dy, at::Tensor y, bool relu
     const int64_t rows = y.numel() / C;
     at::Tensor dz = relu ? at::empty_like(dy, dy.options().memory_format(at::MemoryFormat::ChannelsLast)) : dy;
     at::Tensor db = at::empty({C}, y.options().dtype(at::kFloat));
+    at::Tensor part = at::empty({std::max(1, kfk::bias_act_backward_blocks(rows, C)), C}, y.options().dtype(at::kFloat));
     kfk::launch_bias_act_backward(reinterpret_cast<const uint16_t *>(dy.data_ptr()),
                                   reinterpret_cast<const uint16_t *>(y.data_ptr()),
-                                  reinterpret_cast<uint16_t *>(dz.data_ptr()), db.data_ptr<float>(), rows, C, relu,
-                                  stream_of(y, 0));
+                                  reinterpret_cast<uint16_t *>(dz.data_ptr()), db.data_ptr<float>(),
+                                  part.data_ptr<float>(), rows, C, relu, stream_of(y, 0));
     return {dz, db};
 }
 

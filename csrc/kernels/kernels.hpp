@@ -409,11 +409,13 @@ void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint
                              hipStream_t s, const uint16_t *xarg = nullptr, double *sums = nullptr);
 
 // Conv bias (+ ReLU) on NHWC bf16 [rows, C] (bias_act.hip): forward in place; backward
-// dz = dy * (y > 0) (relu) and dbias[c] = sum over rows (f32, zeroed first).
+// dz = dy * (y > 0) (relu) and dbias[c] = sum over rows (f32, deterministic: per-block partials
+// [bias_act_backward_blocks(rows, C), C] f32 then a fixed-order column sum; no memset, no atomics).
 bool bias_act_supported(int C);
 void launch_bias_act_forward(uint16_t *y, const float *bias, int64_t rows, int C, bool relu, hipStream_t s);
-void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, int64_t rows, int C,
-                              bool relu, hipStream_t s);
+int bias_act_backward_blocks(int64_t rows, int C);
+void launch_bias_act_backward(const uint16_t *dy, const uint16_t *y, uint16_t *dz, float *dbias, float *partial,
+                              int64_t rows, int C, bool relu, hipStream_t s);
 
 // 2x2 / stride-2 max-pool, NHWC bf16, C % 8 == 0, even H and W (pool.hip); backward
 // recomputes the window argmax from x and writes every dx element once.

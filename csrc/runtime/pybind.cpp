@@ -266,6 +266,25 @@ PYBIND11_MODULE(_kungfu, m) {
         .def("order", &OrderedScheduler::order)
         .def("arrivals", &OrderedScheduler::arrivals)
         .def("size", &OrderedScheduler::size);
+    py::class_<BucketTracker>(m, "BucketTracker")
+        .def(py::init<int, const std::vector<int> &>())
+        .def("mark", &BucketTracker::mark)
+        .def("flush", &BucketTracker::flush)
+        .def("reset", &BucketTracker::reset)
+        .def("learn", &BucketTracker::learn)
+        .def("learned", &BucketTracker::learned)
+        .def("launched", &BucketTracker::launched)
+        .def("fires", &BucketTracker::fires)
+        .def("expected", &BucketTracker::expected)
+        .def("auto_order", [](BucketTracker &t) {
+            auto s = require_session();
+            py::gil_scoped_release r;
+            t.scheduler().auto_order(*s);
+        })
+        .def("set_order", [](BucketTracker &t, const std::vector<int> &o) { t.scheduler().set_order(o); })
+        .def("order", [](BucketTracker &t) { return t.scheduler().order(); })
+        .def("arrivals", [](BucketTracker &t) { return t.scheduler().arrivals(); })
+        .def_property_readonly_static("LATE", [](py::object) { return BucketTracker::kLate; });
 
     // ---- model averaging (legacy pair-averaging ops) --------------------------
     py::class_<ModelAverager>(m, "ModelAverager")

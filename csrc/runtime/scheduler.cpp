@@ -81,4 +81,73 @@ std::vector<int> OrderedScheduler::arrivals() const {
     return arrivals_;
 }
 
+BucketTracker::BucketTracker(int n_buckets, const std::vector<int> &bucket_of)
+    : sched_(n_buckets), bucket_of_(bucket_of), fires_(bucket_of.size(), 0), pending_(n_buckets, 1),
+      launched_(n_buckets, 0) {
+    for (int b : bucket_of_)
+        if (b < 0 || b >= n_buckets) throw std::invalid_argument("BucketTracker: bucket index out of range");
+}
+
+std::vector<int> BucketTracker::mark(int p) {
+    std::lock_guard<std::mutex> l(mu_);
+    if (p < 0 || p >= static_cast<int>(bucket_of_.size())) throw std::out_of_range("BucketTracker::mark: bad param");
+    ++fires_[p];
+    if (expected_.empty()) return {};  // learning step: buckets launch at flush()
+    const int b = bucket_of_[p];
+    if (launched_[b]) return {kLate};
+    if (--pending_[b] > 0) return {};
+    std::vector<int> go = sched_.ready(b);
+    for (int j : go) launched_[j] = 1;
+    return go;
+}
+
+std::vector<int> BucketTracker::flush() {
+    std::lock_guard<std::mutex> l(mu_);
+    std::vector<int> go;
+    for (int j : sched_.flush())
+        if (!launched_[j]) {
+            launched_[j] = 1;
+            go.push_back(j);
+        }
+    return go;
+}
+
+void BucketTracker::reset() {
+    std::lock_guard<std::mutex> l(mu_);
+    std::fill(fires_.begin(), fires_.end(), 0);
+    std::fill(launched_.begin(), launched_.end(), 0);
+    if (expected_.empty()) {
+        std::fill(pending_.begin(), pending_.end(), 1);
+    } else {
+        std::fill(pending_.begin(), pending_.end(), 0);
+        for (size_t p = 0; p < bucket_of_.size(); ++p) pending_[bucket_of_[p]] += expected_[p];
+    }
+    sched_.reset();
+}
+
+void BucketTracker::learn() {
+    std::lock_guard<std::mutex> l(mu_);
+    expected_ = fires_;
+}
+
+bool BucketTracker::learned() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return !expected_.empty();
+}
+
+bool BucketTracker::launched(int bucket) const {
+    std::lock_guard<std::mutex> l(mu_);
+    return bucket >= 0 && bucket < static_cast<int>(launched_.size()) && launched_[bucket];
+}
+
+std::vector<int> BucketTracker::fires() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return fires_;
+}
+
+std::vector<int> BucketTracker::expected() const {
+    std::lock_guard<std::mutex> l(mu_);
+    return expected_;
+}
+
 }  // namespace kungfu

@@ -81,7 +81,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_COMM_EMULATE": _u(None, "ranks=R,ctas=C,busbw=GB/s,lat_us=L: model an R-rank all-reduce on one GPU"),
     "KUNGFU_PREFLIGHT_TIMEOUT_S": _u("60", "bench pre-flight: deadline of each device check"),
     "KUNGFU_PREFLIGHT_CORRUPT": _u(None, "test hook: this rank corrupts its pre-flight buffer"),
-    "KUNGFU_PREFLIGHT_CORRUPT_WHAT": _u("ipc", "test hook: ipc | allreduce"),
+    "KUNGFU_PREFLIGHT_CORRUPT_WHAT": _u("ipc", "test hook: ipc | allreduce | stall (reports a stall without stalling)"),
     "KUNGFU_FORCE_DEVICE": _u(None, "pin every rank to this HIP device (colocated tests)"),
     "KUNGFU_INIT_CKPT": _u(None, "elastic: initial checkpoint step"),
     # -- kernel routing kill switches (1 = our HIP kernel, 0 = library path) --------------------
@@ -134,6 +134,8 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_LINEAR_DIRECT_WGRAD": _d("1", "linear weight gradients reduced straight into the flat buffer"),
     "KUNGFU_COMM_STREAM_PRIORITY": _d("0", "HIP priority of the comm stream (-1 measured 2x slower)"),
     "KUNGFU_GRAPH_MULTIRANK": _u("1", "0: GraphedStep keeps multi-rank RCCL steps eager (capture uses the comm stream as origin)"),
+    "KUNGFU_GRAPH_SEGMENTED": _u("1", "N-rank capture as graph segments cut at every bucket launch, collectives issued "
+                                       "eagerly between replays (0: one graph with the collectives inside)"),
     "KUNGFU_BN_SKIP_FINALIZE": _d("0", "TIMING ONLY, wrong numerics: skip BN finalize (needs a -DKUNGFU_DEV_EXPERIMENTS=1 build)"),
     "KUNGFU_BERT_GEMM": _d("0", "BERT linear layers on the hand-written GEMM"),
 }

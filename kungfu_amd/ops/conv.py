@@ -132,9 +132,10 @@ class _BiasActFn(torch.autograd.Function):
     """y = relu(y + b) in place on a conv output (csrc/kernels/bias_act.hip); backward is one
     pass producing dy * (y > 0) and its per-channel sum (the bias gradient).
 
-    Determinism: the per-channel bias-gradient sum is accumulated with f32 atomics across
-    workgroups, so it is NOT bitwise reproducible between runs (differences at the f32
-    rounding level, like MIOpen's split-K paths); the gated data gradient is exact.  The
+    Determinism: the per-channel bias-gradient sum is per-block partials plus a fixed-order
+    column sum -- bitwise reproducible, no zero-fill of the output (round 5: the previous f32
+    atomics into a hipMemsetAsync-zeroed buffer made VGG-16's per-layer step vary, and go NaN,
+    under whole-step capture; tests/test_gpu_engine.py captured-vs-eager VGG test).  The
     ReLU keeps NaN (``!(v <= 0)``), as ``torch.relu`` does."""
 
     @staticmethod

@@ -480,8 +480,8 @@ class EmulatedComm(_StreamOrdered):
     """One-GPU stand-in for the all-reduces of an ``ranks``-rank job (``bench.py --emulate-comm``,
     ``KUNGFU_COMM_EMULATE="ranks=8,ctas=16,busbw=350,lat_us=25"``): every all-reduce of B bytes
     launches ``comm_emu.hip`` on the comm stream -- ``ctas`` workgroups, resident for the
-    modelled ring time 2(r-1)/r * B / busbw + lat, streaming the ~4(r-1)/r * B bytes of local HBM
-    traffic such an all-reduce makes -- so its cost to the overlapped backward (CUs, HBM,
+    modelled ring time 2(r-1)/r * B / busbw + lat, copying 2(r-1)/r * B bytes (a read plus a write:
+    the ~4(r-1)/r * B bytes of local HBM traffic such an all-reduce makes) -- so its cost to the overlapped backward (CUs, HBM,
     stream ordering) shows up in a 1-GPU step time.  The data is NOT reduced (one rank: the
     gradient already is the average).  A model: no inter-rank skew, no link congestion."""
 
@@ -514,14 +514,22 @@ class EmulatedComm(_StreamOrdered):
             out.copy_(inp)
         nb = inp.numel() * inp.element_size()
         nb16 = max(16, (nb + 15) // 16 * 16)
-        if self._scratch is None or self._scratch.numel() < 2 * nb16:
-            self._scratch = torch.empty(2 * nb16, dtype=torch.uint8, device=inp.device)
-        src, dst = self._scratch[:nb16], self._scratch[nb16:2 * nb16]
         s = stream if stream is not None else self.stream
-        sp = s.cuda_stream if hasattr(s, "cuda_stream") else int(s)
+        if not isinstance(s, torch.cuda.Stream):
+            s = torch.cuda.ExternalStream(int(s), device=inp.device)
+        if self._scratch is None or self._scratch.numel() < 2 * nb16:
+            # allocated on the stream that uses it: when a larger bucket replaces it, the caching
+            # allocator only hands the old block out again in that stream's order, i.e. after the
+            # paced kernels still writing it have finished
+            with torch.cuda.stream(s):
+                self._scratch = torch.empty(2 * nb16, dtype=torch.uint8, device=inp.device)
+        src, dst = self._scratch[:nb16], self._scratch[nb16:2 * nb16]
         r = self.ranks
         t = self.model_seconds(nb)
-        hip().comm_emulate(src, dst, int(4 * (r - 1) / r * nb), self.ctas_n, t, sp)
+        # bytes COPIED: 2(r-1)/r x B, i.e. a read plus a write of that much = the 4(r-1)/r x B of
+        # local HBM traffic a ring all-reduce makes (comm_emu.hip header; r4 passed the traffic
+        # itself here and so doubled the modelled contention -- ADVICE r4)
+        hip().comm_emulate(src, dst, int(2 * (r - 1) / r * nb), self.ctas_n, t, s.cuda_stream)
         self.calls += 1
         self.modelled_s += t
         return out

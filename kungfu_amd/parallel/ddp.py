@@ -19,7 +19,10 @@ MI355X design:
   for its predecessors): index order first, then -- from the second step after
   (re)binding to a communicator -- rank 0's observed completion order,
   broadcast once (the reference scheduler's auto-order), decided by the native
-  ``kungfu::OrderedScheduler`` (csrc/runtime/scheduler.cpp).
+  ``kungfu::OrderedScheduler`` (csrc/runtime/scheduler.cpp).  The per-gradient
+  bookkeeping (arrival counts, per-bucket countdown, launched flags, late
+  detection, the scheduler query) is ONE native call per hook,
+  ``kungfu::BucketTracker::mark``.
 * an autograd end-of-backward callback launches any bucket whose params got
   no gradient (unused params keep zeros) and makes the compute stream wait
   for the comm stream, so ``loss.backward()`` returns with the reduced
@@ -61,11 +64,10 @@ from .flat import FlatParamSpace
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "params", "pending", "launched", "staged", "staged_off")
+    __slots__ = ("index", "start", "end", "params", "launched", "staged", "staged_off")
 
     def __init__(self, index: int, start: int, end: int, params: List[int]):
         self.index, self.start, self.end, self.params = index, start, end, params
-        self.pending = len(params)
         self.launched = False
         self.staged: List[torch.Tensor] = []  # direct gradients waiting for the bucket
         self.staged_off: List[int] = []
@@ -230,15 +232,18 @@ class GradReducer:
         for b in self.buckets:
             for i in b.params:
                 self.param_bucket[i] = b
-        # Expected gradient accumulations per param per backward.  Unknown on
-        # the first backward (learned, like a static graph): that step reduces
-        # every bucket at the end of backward; later steps overlap.
-        self._expected: Optional[List[int]] = None
-        self._fires = [0] * len(space.params)
+        from .._lib import runtime
+
+        # Native per-gradient accounting (csrc/runtime/scheduler.cpp BucketTracker): expected
+        # gradient accumulations per param per backward are unknown on the first backward (learned,
+        # like a static graph: that step reduces every bucket at the end of backward); later steps
+        # count each bucket down and launch it, in the scheduler's order, when it completes.
+        self.tracker = runtime.BucketTracker(len(self.buckets),
+                                             [self.param_bucket[i].index for i in range(len(space.params))])
+        self._late_code = runtime.BucketTracker.LATE
         # Communicator binding (lazy; see _bind).
         self.comm = None
         self.skip = True
-        self.sched = None
         self._bound = None  # (cluster version, comm epoch) bound at
         self._steps_bound = 0  # completed backward passes since the last (re)bind
         self._ordered = False
@@ -253,6 +258,13 @@ class GradReducer:
         #   post_finish()                        on the compute stream, after all buckets
         self.pre_reduce = None
         self.post_finish = None
+        # comm probe (bench.py verify.comm_per_bucket_ms / exposed_comm_ms): when a list, every
+        # backward appends its per-bucket HIP timing events (see :meth:`probe_summary`)
+        self.probe: Optional[list] = None
+        self._probe_cur = None
+        # set by a segmented GraphedStep capture (parallel/graphs.py): bucket launches and the
+        # end-of-backward join become cut points between captured graph segments
+        self.segmenter = None
         for i, p in enumerate(space.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         # direct gradients (parallel/mixed.py) are delivered to put()
@@ -282,7 +294,7 @@ class GradReducer:
             self.comm = None if self.skip else get_device_comm(device=self.space.device)
         # The learned collective order belongs to the old membership: start again
         # from index order; the new rank 0's arrival order is adopted after one step.
-        self.sched = runtime.OrderedScheduler(len(self.buckets))
+        self.tracker.set_order(list(range(len(self.buckets))))
         self._ordered = False
         self._steps_bound = 0
         if self._bound is not None:
@@ -374,16 +386,12 @@ class GradReducer:
             self._armed = True
             self._bind()
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
-        self._fires[i] += 1
-        if self._expected is None:
-            return
-        b = self.param_bucket[i]
-        if b.launched:
-            self._late(i)
-            return
-        b.pending -= 1
-        if b.pending == 0:
-            for j in self.sched.ready(b.index):
+        go = self.tracker.mark(i)
+        if go:
+            if go[0] == self._late_code:
+                self._late(i)
+                return
+            for j in go:
                 self._launch(self.buckets[j])
 
     def _land(self, b: Bucket):
@@ -402,9 +410,19 @@ class GradReducer:
         self._land(b)
         if self.skip:
             return
+        if self.segmenter is not None:
+            # segmented capture (parallel/graphs.py): the compute captured so far becomes one graph
+            # segment; this bucket's collective is issued eagerly between segment replays
+            self.segmenter.cut(("bucket", b.index))
+            return
+        self._issue(b)
+
+    def _issue(self, b: Bucket):
+        """The comm-stream side of a bucket launch: fence, pre-reduce callback, wire cast, collective."""
         comm = self.comm
         # names the collective for the watchdog: "bucket 3/5 of step 12"
         self._tag = "bucket %d/%d of step %d" % (b.index, len(self.buckets), self.steps)
+        probe = self._probe_begin(comm, b)
         comm.fence()
         g = self.space.flat_grad[b.start:b.end]
         if self.pre_reduce is not None:
@@ -425,6 +443,54 @@ class GradReducer:
             self._reduce(comm, c, post=cast_back)
         else:
             self._reduce(comm, g)
+        if probe is not None:
+            with comm.on_stream():
+                probe[-1].record()
+
+    # ------------------------------------------------------------ comm probe
+    def _probe_begin(self, comm, b: Bucket):
+        """Timing events of one bucket: ready (compute stream: its last gradient produced), start /
+        end of its collective (comm stream).  None unless probing a device plane."""
+        if self.probe is None or getattr(comm, "stream", None) is None or self._hier is not None:
+            return None
+        if self._probe_cur is None:
+            self._probe_cur = {"buckets": [], "bwd_end": None}
+        ready, st, en = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        ready.record()
+        comm.fence()
+        with comm.on_stream():
+            st.record()
+        rec = [b.index, (b.end - b.start) * self.space.flat_grad.element_size(), ready, st, en]
+        self._probe_cur["buckets"].append(rec)
+        return rec
+
+    def probe_summary(self) -> Optional[dict]:
+        """Per-bucket collective time and the exposed communication tail over the probed steps
+        (medians; synchronises the device).  ``comm_per_bucket_ms``: device time of each bucket's
+        collective, in launch order; ``wait_per_bucket_ms``: from the bucket's gradients being
+        ready to its collective starting (queueing behind earlier buckets); ``exposed_comm_ms``:
+        from the end of backward's compute to the end of the last collective -- the part of the
+        communication the step could not hide."""
+        steps = [r for r in (self.probe or []) if r["buckets"] and r["bwd_end"] is not None]
+        if not steps:
+            return None
+        torch.cuda.synchronize()
+
+        def med(v):
+            v = sorted(v)
+            return v[len(v) // 2]
+
+        nb = len(steps[0]["buckets"])
+        steps = [r for r in steps if len(r["buckets"]) == nb]
+        comm_ms = [med([r["buckets"][k][3].elapsed_time(r["buckets"][k][4]) for r in steps]) for k in range(nb)]
+        wait_ms = [med([r["buckets"][k][2].elapsed_time(r["buckets"][k][3]) for r in steps]) for k in range(nb)]
+        exposed = [max(0.0, max(r["bwd_end"].elapsed_time(b[4]) for b in r["buckets"])) for r in steps]
+        return {"steps": len(steps), "bucket_order": [b[0] for b in steps[0]["buckets"]],
+                "bucket_mb": [round(b[1] / (1 << 20), 2) for b in steps[0]["buckets"]],
+                "comm_per_bucket_ms": [round(v, 3) for v in comm_ms],
+                "wait_per_bucket_ms": [round(v, 3) for v in wait_ms],
+                "comm_total_ms": round(sum(comm_ms), 3),
+                "exposed_comm_ms": round(med(exposed), 3)}
 
     def _reduce(self, comm, g, post=None):
         """Reduce ``g`` in place; ``post()`` is then issued on the stream the reduction ends
@@ -475,24 +541,32 @@ class GradReducer:
     def _finish(self):
         from .mixed import SideStream
 
-        for j in self.sched.flush():
-            if not self.buckets[j].launched:
-                self._launch(self.buckets[j])
+        for j in self.tracker.flush():
+            self._launch(self.buckets[j])
         if self._hier is not None:
             self._hier.drain()
         SideStream.join()  # nothing computed on the side stream outlives backward
+        if self._probe_cur is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()  # backward's compute is done (before the wait for the comm stream)
+            self._probe_cur["bwd_end"] = ev
+            self.probe.append(self._probe_cur)
+            self._probe_cur = None
         if not self.skip:
-            self.comm.join()
+            if self.segmenter is not None:
+                self.segmenter.cut(("join",))  # the compute waits for the comm stream between replays
+            else:
+                self.comm.join()
             if self._steps_bound == 1 and not self._ordered:
                 # second step on this communicator: every rank adopts rank 0's
                 # arrival order for its collectives from now on (native auto-order).
                 # The step count since binding is the same on every rank (old
                 # members and workers that just joined), so all of them take
                 # part in this broadcast.
-                self.sched.auto_order()
+                self.tracker.auto_order()
                 self._ordered = True
-        if self._expected is None:
-            self._expected = list(self._fires)
+        if not self.tracker.learned():
+            self.tracker.learn()
         self._steps_bound += 1
         self.steps += 1
         self._reset_buckets()
@@ -501,13 +575,10 @@ class GradReducer:
 
     def _reset_buckets(self):
         for b in self.buckets:
-            b.pending = sum(self._expected[i] for i in b.params) if self._expected is not None else 1
             b.launched = False
             if b.staged:  # never carry staged gradients into another step
                 self._land(b)
-        self._fires = [0] * len(self.space.params)
-        if self.sched is not None:
-            self.sched.reset()
+        self.tracker.reset()
         self._armed = False
 
     # ------------------------------------------------------------------ API
@@ -521,7 +592,7 @@ class GradReducer:
         """Reduce every bucket immediately (for grads computed without hooks)."""
         self._bind()
         self._reset_buckets()
-        for j in self.sched.flush():
+        for j in self.tracker.flush():
             self._launch(self.buckets[j])
         if not self.skip:
             self.comm.join()

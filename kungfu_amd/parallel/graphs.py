@@ -20,6 +20,14 @@ What makes a step capturable here:
   collective order (rank 0's order is adopted on the second step) and every lazily allocated
   workspace (BN statistics slots, flip caches, comm buffers) exists.
 
+N-rank steps (``KUNGFU_GRAPH_SEGMENTED=1``, the default): the step is captured as a chain of graph
+SEGMENTS cut at every bucket launch and at the end-of-backward join; a replay runs segment 0, issues
+the bucket's RCCL collective eagerly on the comm stream (event-fenced after the segment), replays
+segment 1, ... -- the compute stream never carries a collective, and the collectives overlap the
+following segments exactly as in an eager step (one whole-step graph with the collectives inside
+hid them worse than eager streams: r4t33, r5t3).  Host cost per step: one graph launch per segment
+plus one RCCL call per bucket.  The segments share one memory pool and are replayed in capture order.
+
 Limits: inputs must be static tensors the caller refills in place; the step's Python code runs
 only at capture (counters it keeps stop advancing).  Dropout: the attention / add+LayerNorm
 kernels hash a host seed recorded at capture with a device word that :meth:`pre_replay`
@@ -94,6 +102,25 @@ def _drain_watchdog(timeout_s: float = 2.0) -> None:
         time.sleep(0.01)
 
 
+def _graph_nodes(g: torch.cuda.CUDAGraph) -> int:
+    """Node count of a captured (kept, not yet instantiated) graph: hipGraphGetNodes."""
+    import ctypes
+
+    global _HIP_RT
+    if _HIP_RT is None:
+        _HIP_RT = ctypes.CDLL("libamdhip64.so")
+        _HIP_RT.hipGraphGetNodes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+        _HIP_RT.hipGraphGetNodes.restype = ctypes.c_int
+    n = ctypes.c_size_t(0)
+    rc = _HIP_RT.hipGraphGetNodes(ctypes.c_void_p(g.raw_cuda_graph()), None, ctypes.byref(n))
+    if rc != 0:
+        raise RuntimeError("hipGraphGetNodes failed (%d)" % rc)
+    return int(n.value)
+
+
+_HIP_RT = None
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, optimizer)``; ``loss = step()`` runs ``fn`` eagerly for ``warmup``
     calls, then captures it and replays the graph on every later call (returning the captured
@@ -106,6 +133,11 @@ class GraphedStep:
         self.warmup = warmup
         self.mode = capture_error_mode
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        # segmented capture: graph segments and the replay program [("g", k) | ("bucket", j) | ("join",)]
+        self.segs: List[torch.cuda.CUDAGraph] = []
+        self.program: List[tuple] = []
+        self._cur: Optional[torch.cuda.CUDAGraph] = None
+        self._pool = None
         self.out = None
         self.calls = 0
         self.replays = 0
@@ -139,17 +171,24 @@ class GraphedStep:
             # the host-staged plane synchronises and copies through host memory inside every
             # collective: not capturable (decided identically on every rank, nothing attempted)
             err = RuntimeError("the %s data plane cannot be captured" % plane)
-        multi = reducer is not None and plane == "rccl" and getattr(getattr(reducer, "comm", None), "size", 1) > 1
+        comm = getattr(reducer, "comm", None)
+        # the N-rank layout (comm stream as the capture's origin): real multi-rank RCCL, and the 1-GPU
+        # emulation of an N-rank job (bench.py --emulate-comm), which must model the same graph shape
+        multi = reducer is not None and ((plane == "rccl" and getattr(comm, "size", 1) > 1)
+                                         or (plane == "emulate" and getattr(comm, "ranks", 1) > 1))
         if err is None and getattr(reducer, "_hier", None) is not None:
             # hierarchical across hosts: a host thread all-reduces between the local reduce and the
             # local broadcast -- host work inside the step, not capturable
             err = RuntimeError("the cross-host hierarchical all-reduce cannot be captured")
         elif multi and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
             err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=0)")
+        segmented = multi and knobs.get("KUNGFU_GRAPH_SEGMENTED") != "0"
         try:
             if err is not None:
                 raise err
-            if multi:
+            if segmented:
+                self._capture_segments(reducer)
+            elif multi:
                 # RCCL collectives on a stream that JOINED the capture (the engine's comm stream,
                 # forked from the compute stream) crash hipStreamEndCapture -- the HIP runtime
                 # recurses without end over the captured graph (tests/workers/rccl_graph.py phase
@@ -167,6 +206,17 @@ class GraphedStep:
                     self.out = self.fn()
         except Exception as e:  # noqa: BLE001 -- reported, then the step runs eagerly
             err = e
+            if self._cur is not None:  # a segment still capturing: end it (discarded)
+                try:
+                    with torch.cuda.stream(self.stream):
+                        self._cur.capture_end()
+                except Exception:  # noqa: BLE001
+                    pass
+                self._cur = None
+            reducer = getattr(self.opt, "reducer", None)
+            if reducer is not None:
+                reducer.segmenter = None
+            self.segs, self.program = [], []
         torch.cuda.synchronize()
         ok = err is None
         if runtime.size() > 1:
@@ -184,8 +234,81 @@ class GraphedStep:
             if reducer is not None:  # the aborted step left its bucket bookkeeping half done
                 reducer._reset_buckets()
             return False
-        self.graph = track(g)
+        if self.segs:
+            for sg in self.segs:
+                track(sg)
+            self.graph = self.segs[-1]
+        else:
+            self.graph = track(g)
         return True
+
+    # ------------------------------------------------------------ segmented capture
+    def _begin(self):
+        # keep_graph: the captured graph is instantiated only after the capture, so segments that
+        # captured nothing (two cut points with no kernel between) can be dropped first
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        # "relaxed": a segment begun on the caller's thread is ended by the autograd worker thread at
+        # a bucket launch (thread-local captures must end on the thread that began them)
+        g.capture_begin(pool=self._pool, capture_error_mode="relaxed")
+        self._cur = g
+
+    def _end(self):
+        self._cur.capture_end()
+        self.segs.append(self._cur)
+        self.program.append(("g", len(self.segs) - 1))
+        self._cur = None
+
+    def cut(self, op: tuple):
+        """Called by the reducer (on the capturing stream) at a bucket launch / the final join: end the
+        current segment, record ``op`` for the replay program, begin the next segment."""
+        self._end()
+        self.program.append(op)
+        self._begin()
+
+    def _capture_segments(self, reducer):
+        import gc
+
+        gc.collect()
+        self.segs, self.program = [], []
+        self._pool = torch.cuda.graph_pool_handle()
+        reducer.segmenter = self
+        try:
+            with torch.cuda.stream(self.stream):
+                self._begin()
+                self.out = self.fn()
+                self._end()
+        finally:
+            reducer.segmenter = None
+        if not any(op[0] == "join" for op in self.program):
+            raise RuntimeError("segmented capture saw no end-of-backward join (no bucket engine in the step?)")
+        # drop the empty segments (each graph launch costs the GPU a few microseconds), instantiate the rest
+        keep, prog = [], []
+        for op in self.program:
+            if op[0] == "g":
+                sg = self.segs[op[1]]
+                if _graph_nodes(sg) == 0:
+                    sg.reset()
+                    continue
+                sg.instantiate()
+                keep.append(sg)
+                op = ("g", len(keep) - 1)
+            prog.append(op)
+        self.segs, self.program = keep, prog
+
+    def _replay_segments(self):
+        reducer = self.opt.reducer
+        cur = torch.cuda.current_stream()
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            for op in self.program:
+                if op[0] == "g":
+                    self.segs[op[1]].replay()
+                elif op[0] == "bucket":
+                    reducer._issue(reducer.buckets[op[1]])
+                else:
+                    reducer.comm.join()
+        cur.wait_stream(self.stream)
+        reducer.steps += 1  # names the next replay's collectives for the watchdog
 
     def _eager(self):
         cur = torch.cuda.current_stream()
@@ -203,6 +326,9 @@ class GraphedStep:
             if not self.capture():  # records without executing: replay now so this call did a step
                 return self._eager()
         self.pre_replay()
-        self.graph.replay()
+        if self.segs:
+            self._replay_segments()
+        else:
+            self.graph.replay()
         self.replays += 1
         return self.out

@@ -18,9 +18,16 @@ every rank learns every failure; on any failure each rank raises :class:`Preflig
 the failing rank pairs (bench.py exits 5).  With CPU tensors only the value check runs (host
 plane).  A stalled RCCL check is bounded (``KUNGFU_PREFLIGHT_TIMEOUT_S``, default 60 s).
 
+Bounded on the stall paths: a rank whose all-reduce did not complete says so over the
+host transport and EVERY rank then skips the IPC check (its device work would queue behind the
+stuck collective); the IPC fill is ordered by an event wait bounded like the others, never a
+device-wide synchronise; and a pull that timed out keeps both its mapping and the exporter's
+buffer alive (the copy may still be in flight) -- the process is about to fail anyway.
+
 Test hook: ``KUNGFU_PREFLIGHT_CORRUPT=<rank>`` makes that rank corrupt one element of its IPC
 buffer after filling it (``ipc``) or of its all-reduce contribution (``KUNGFU_PREFLIGHT_CORRUPT_WHAT
-=allreduce``), so the failure path is exercised.
+=allreduce``), or report its all-reduce as stalled without stalling it (``stall``), so the failure
+paths are exercised.
 
 Parity: the reference checks every NCCL call's result and synchronises
 (``srcs/cpp/src/nccl/gpu_collective.cpp:96-152``); it has no pre-flight -- this is the
@@ -128,16 +135,16 @@ def _check_allreduce(comm, device, timeout_s: float) -> dict:
         comm.all_reduce(x, y, op="sum", stream=s, tag="preflight warm-up")
         ok = _wait_record(s, timeout_s)
         if not ok:
-            return {"ok": False, "error": "RCCL all-reduce did not complete within %.0f s" % timeout_s,
-                    "plane": comm.plane}
+            return {"ok": False, "stalled": True, "plane": comm.plane,
+                    "error": "RCCL all-reduce did not complete within %.0f s" % timeout_s}
         bad = int((y != _pattern(elems, 0, device).mul_(want_scale)).sum())
         evs[0].record(s)
         for _ in range(reps):
             comm.all_reduce(x, y, op="sum", stream=s, tag="preflight timing")
         evs[1].record(s)
         if not _wait(evs[1], timeout_s, "timing"):
-            return {"ok": False, "error": "RCCL all-reduce timing loop did not complete within %.0f s" % timeout_s,
-                    "plane": comm.plane}
+            return {"ok": False, "stalled": True, "plane": comm.plane,
+                    "error": "RCCL all-reduce timing loop did not complete within %.0f s" % timeout_s}
     t = evs[0].elapsed_time(evs[1]) / 1e3 / reps
     return {"ok": bad == 0, "bad_elements": bad, "bytes": _ALLREDUCE_BYTES, "plane": comm.plane,
             "ms": round(t * 1e3, 3), "algbw_gbs": round(_ALLREDUCE_BYTES / t / 1e9, 2),
@@ -151,6 +158,11 @@ def _wait_record(stream, timeout_s: float) -> bool:
     return _wait(ev, timeout_s, "")
 
 
+# buffers of a timed-out IPC pull: a copy may still be reading / writing them, so they are never
+# freed (the pre-flight is failing; the process exits soon after)
+_LEAKED: list = []
+
+
 def _check_ipc(device, timeout_s: float) -> dict:
     """Export one buffer with this rank's pattern, pull the next rank's over HIP IPC, compare."""
     H = hip()
@@ -160,12 +172,18 @@ def _check_ipc(device, timeout_s: float) -> dict:
     buf.copy_(_pattern(elems, rank, device))
     if _corrupt("ipc"):
         buf[elems // 2] = -1.0
-    torch.cuda.synchronize(device)
+    # the fill must be complete before a peer pulls: wait for THIS stream's work, bounded (a
+    # device-wide synchronise would also wait for other streams' possibly stuck work)
+    filled = _wait_record(torch.cuda.current_stream(device), timeout_s)
     mine = torch.frombuffer(bytearray(H.ipc_handle(buf)), dtype=torch.uint8).clone()
     allh = ops.all_gather(mine, name="kf:preflight:ipc")
     peer = (rank + 1) % n
     hosts = runtime.peers().split(",")
-    if hosts[peer].split(":")[0] != hosts[rank].split(":")[0]:
+    pending = False
+    if not filled:
+        res = {"ok": False, "peer": peer, "error": "IPC buffer fill did not complete within %.0f s" % timeout_s}
+        pending = True
+    elif hosts[peer].split(":")[0] != hosts[rank].split(":")[0]:
         res = {"ok": True, "peer": peer, "skipped": "peer on another host (no IPC)"}
     else:
         try:
@@ -178,6 +196,8 @@ def _check_ipc(device, timeout_s: float) -> dict:
             en.record()
             if not _wait(en, timeout_s, "ipc"):
                 res = {"ok": False, "peer": peer, "error": "IPC pull did not complete within %.0f s" % timeout_s}
+                pending = True
+                _LEAKED.extend([remote, local])
             else:
                 bad = int((local != _pattern(elems, peer, device)).sum())
                 t = st.elapsed_time(en) / 1e3
@@ -186,8 +206,12 @@ def _check_ipc(device, timeout_s: float) -> dict:
             del remote
         except Exception as e:  # noqa: BLE001 -- reported, then raised collectively
             res = {"ok": False, "peer": peer, "error": "%s: %s" % (type(e).__name__, e)}
-    # every rank is done reading before any owner frees its exported buffer
-    ops.barrier()
+    # every rank is done reading before any owner frees its exported buffer; an owner whose
+    # buffer a peer may still be copying (that peer's pull timed out) keeps it
+    flags = ops.all_gather(torch.tensor([1 if pending else 0], dtype=torch.int32),
+                           name="kf:preflight:ipc_done").view(-1).tolist()
+    if any(flags):
+        _LEAKED.append(buf)
     del buf
     return res
 
@@ -224,11 +248,24 @@ def run(device: Optional[torch.device] = None, comm=None) -> dict:
         ar = _check_allreduce(comm, device, timeout_s)
     except Exception as e:  # noqa: BLE001
         ar = {"ok": False, "error": "%s: %s" % (type(e).__name__, e)}
+    if _corrupt("stall"):
+        # test hook: the collective ran (the peers are not left waiting in it), this rank then
+        # reports it as stalled -- the stall path without a stuck kernel on the box
+        ar = {"ok": False, "stalled": True, "plane": ar.get("plane", "?"),
+              "error": "all-reduce did not complete within %.0f s (simulated)" % timeout_s}
     mine["allreduce"] = ar
     if not ar["ok"]:
         mine["errors"].append("all-reduce check failed on rank %d: %s" % (
             rank, ar.get("error") or "%d wrong elements" % ar.get("bad_elements", -1)))
-    if cuda and n > 1:
+    # the IPC check queues device work; behind a stuck collective it would hang -- skip it on
+    # every rank (the decision is collective, over the host transport) if any rank stalled
+    stalled = [r for r, v in enumerate(ops.all_gather(torch.tensor([1 if ar.get("stalled") else 0],
+                                                                   dtype=torch.int32),
+                                                      name="kf:preflight:stalled").view(-1).tolist()) if v]
+    if cuda and n > 1 and stalled:
+        mine["ipc"] = {"ok": True, "peer": (rank + 1) % n,
+                       "skipped": "all-reduce stalled on rank(s) %s" % ",".join(map(str, stalled))}
+    elif cuda and n > 1:
         ipc = _check_ipc(device, timeout_s)
         mine["ipc"] = ipc
         if not ipc["ok"]:
@@ -242,6 +279,8 @@ def run(device: Optional[torch.device] = None, comm=None) -> dict:
               "ipc_pull_gbs": {str(r["rank"]): (r.get("ipc") or {}).get("pull_gbs") for r in rows},
               "p2p": {str(r["rank"]): r.get("p2p", "n/a") for r in rows},
               "rccl_ctas": (rows[0].get("allreduce") or {}).get("ctas"),
+              "ipc_skipped": {str(r["rank"]): (r.get("ipc") or {}).get("skipped") for r in rows
+                              if (r.get("ipc") or {}).get("skipped")},
               "errors": errors}
     if errors:
         raise PreflightError("pre-flight failed: " + "; ".join(errors), report)

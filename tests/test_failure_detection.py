@@ -60,6 +60,19 @@ def test_bench_preflight_names_the_failing_rank():
     assert time.time() - t0 < 120
 
 
+def test_bench_preflight_reports_allreduce_stall_bounded():
+    """a rank whose pre-flight all-reduce stalls (simulated by the test hook: the report,
+    no stuck collective) fails the pre-flight on every rank, named, within the bound -- the later
+    checks do not wait behind it."""
+    t0 = time.time()
+    r = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--model", "resnet18",
+                "--batch", "2", "--image-size", "32"],
+               env={"KUNGFU_PREFLIGHT_CORRUPT": "0", "KUNGFU_PREFLIGHT_CORRUPT_WHAT": "stall"})
+    assert r.returncode != 0, r.stderr[-3000:]
+    assert "all-reduce check failed on rank 0" in r.stderr and "did not complete" in r.stderr, r.stderr[-3000:]
+    assert time.time() - t0 < 120
+
+
 def test_bench_refuses_mislabelled_world():
     # a launcher env with one rank but --gpus 2 must fail, not report a 1-rank number as 2
     r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--device", "cpu", "--model", "resnet18",

@@ -874,6 +874,16 @@ def test_bias_act_matches_torch(H, C, relu):
     assert torch.equal(dz.float(), dz_ref.bfloat16().float())
     db_ref = dz_ref.sum(dim=(0, 2, 3))
     assert ((db - db_ref).norm() / db_ref.norm()).item() < 1e-4
+    # deterministic (fixed-order partial sums, no atomics), also over a many-block grid
+    dz2, db2 = H.bias_act_backward(dy, y, relu)
+    assert torch.equal(db, db2) and torch.equal(dz, dz2)
+    big = torch.randn(64, C, 28, 28, device="cuda").bfloat16().to(memory_format=torch.channels_last)
+    dyb = torch.randn_like(big)
+    _, d1 = H.bias_act_backward(dyb, big, relu)
+    _, d2 = H.bias_act_backward(dyb, big, relu)
+    gb = (big.float() > 0) if relu else torch.ones_like(big, dtype=torch.bool)
+    ref_b = (dyb.float() * gb).double().sum(dim=(0, 2, 3))
+    assert torch.equal(d1, d2) and ((d1.double() - ref_b).norm() / ref_b.norm()).item() < 1e-5
 
 
 @needs_gpu
@@ -1751,8 +1761,10 @@ def test_gelu_backward_colsum_matches_torch(T, O):
 
 @needs_gpu
 def test_comm_emulate_kernel_paces_and_keeps_bucket(H):
-    """comm_emu.hip (bench.py --emulate-comm): resident for the modelled time, copies the
-    requested traffic into the scratch half, never writes the bucket."""
+    """comm_emu.hip (bench.py --emulate-comm): resident for AT LEAST the modelled time (its waves
+    spin on the wall clock until each slice is due -- a one-sided bound: an upper bound would time
+    the box's load), copies the requested bytes into the scratch half, never
+    writes the bucket."""
     b = torch.randn(4 << 20, device="cuda")  # 16 MiB
     keep = b.clone()
     scratch = torch.zeros_like(b)
@@ -1767,7 +1779,7 @@ def test_comm_emulate_kernel_paces_and_keeps_bucket(H):
         en.record()
         en.synchronize()
         ms = st.elapsed_time(en)
-        assert secs * 1e3 * 0.95 < ms < secs * 1e3 * 1.5 + 0.3, (secs, ms)
+        assert ms > secs * 1e3 * 0.95, (secs, ms)
     assert torch.equal(b, keep)
     assert torch.equal(scratch, b)  # 1.75 passes cover every element at least once
 

@@ -1,7 +1,6 @@
 """GPU tests of the S-SGD engine's data plane: the RCCL path exercised
 with one rank (``force_comm``), bf16 gradients on the wire, and elastic resize of the
 GPU optimizers (2 ranks sharing the GPU over the host-staged plane)."""
-import math
 import re
 
 import pytest
@@ -224,43 +223,97 @@ def _resnet50_trajectory(engine: bool, steps=10, batch=64, lr=0.1):
     return out
 
 
+def _stock_resnet50(state):
+    from kungfu_amd.models import resnet50
+
+    m = resnet50(fused_bn=False).cuda().to(memory_format=torch.channels_last)
+    m.load_state_dict(state)
+    return m
+
+
+def _layer_rel(ref, got):
+    return {n: ((got[n].reshape(a.shape) - a).norm() / a.norm().clamp_min(1e-30)).item() for n, a in ref.items()}
+
+
 @needs_gpu
-def test_resnet50_full_size_engine_matches_stock():
-    """Full-size numerics of the bench path: 224x224, batch 64, SGD momentum
-    0.9, 10 steps on one fixed batch, fused engine vs two stock runs from the same seed.
+def test_resnet50_engine_gradients_within_stock_bf16_envelope():
+    """Full-size numerics of the bench path (VERDICT r4 next #1a; replaces the lr-0.1 trajectory-spread
+    comparison, whose outcome depended on run-to-run chaos): ResNet-50 at 224x224, batch 64, from ONE
+    shared state at step 0 and after 3 stock lr-0.1 steps, the engine's (fused BN, MFMA convs, bf16
+    shadow weights, bucketed S-SGD) per-parameter gradient vs a stock f32 reference.  Every one of the
+    161 parameters' relative L2 error must stay within 2x the stock-bf16-vs-f32 error of the same
+    parameter (max over two stock bf16 runs) + 1e-3; the loss within 3x the stock-bf16 loss error.
+    Measured r5 (profiles/r5_engine_numerics.md): worst layer 1.14x the envelope, over 9 component
+    variants and both states; BN gamma/beta gradients at random init are rounding-dominated in bf16
+    for stock and engine alike (relative error ~1.2-1.4 vs f32), conv weights agree to ~1e-2."""
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet50
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
 
-    lr 0.1 (the bench's): the STOCK model itself climbs from 7.16 to ~10-11 by step 4 and
-    then oscillates chaotically (two stock runs measured 16.97 vs 9.75 at step 7, MIOpen's
-    split-K kernels not being bitwise deterministic) -- no warm-up at that LR from random
-    init.  This is why the bench's final_loss sits above ln(1000).  The engine must follow the
-    stock trajectory through the deterministic phase and stay within the stock spread after.
-    lr 0.01: both memorise the batch (7.16 -> 4.19) and agree within 2 % at every step.
-    Measured on MI355X (r2): lr 0.1 stock 7.16/5.03/6.54/8.58/10.53/11.28, engine
-    7.17/5.04/6.63/8.82/10.61/10.79; lr 0.01 stock .../4.79/4.40/4.19, engine .../4.80/4.42/4.19.
+    kf.init()
+    g = torch.Generator(device="cuda").manual_seed(99)
+    x = torch.randn(64, 3, 224, 224, device="cuda", generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (64,), device="cuda", generator=g)
+    torch.manual_seed(1234)
+    m = resnet50(fused_bn=False).cuda().to(memory_format=torch.channels_last)
+    s0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    sgd = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for _ in range(3):
+        sgd.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            F.cross_entropy(m(x).float(), y).backward()
+        sgd.step()
+    s3 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    del m, sgd
 
-    Chaotic phase (steps 5-9): the bound is against the whole window's stock envelope, not
-    step-by-step, because the peaks move in time from run to run.  r3 measured, from identical
-    seeds: stock 11.49/20.64/22.32/17.09 vs 6.76/6.54/8.45/11.59 (steps 6-9, same process), and
-    the engine under two tile-size choices for the same convolutions (default vs
-    KUNGFU_CONV_TILE_RULES=1) 14.07/17.47/16.99/11.23 vs 13.89/18.56/24.17/27.78."""
-    a = _resnet50_trajectory(False)
-    b = _resnet50_trajectory(False)
-    e = _resnet50_trajectory(True)
-    print("lr0.1 stock", a, "\nlr0.1 stock", b, "\nlr0.1 engine", e)
-    assert abs(e[0] - a[0]) < 0.01 * a[0], (a, e)  # same initial model and data
-    lo, hi = min(a[5:] + b[5:]), max(a[5:] + b[5:])
-    for i, (x0, x1, xe) in enumerate(zip(a, b, e)):
-        if i < 5:  # the deterministic phase: within 5 % (measured <= 2.3 %; step 5 is already
-            # chaotic: r3 measured engine 11.37 vs stock 10.28 / 10.44)
-            assert abs(xe - x0) <= max(3 * abs(x0 - x1), 0.05 * abs(x0) + 0.05), (i, a, b, e)
-        else:  # chaotic phase: finite and within the stock window's envelope (x0.4 .. x3)
-            assert math.isfinite(xe) and 0.4 * lo <= xe <= 3.0 * hi, (i, a, b, e)
+    def stock(state, amp):
+        mm = _stock_resnet50(state)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            loss = F.cross_entropy(mm(x).float(), y)
+        loss.backward()
+        return loss.item(), {n: p.grad.detach().float().clone() for n, p in mm.named_parameters()}
+
+    def engine(state):
+        mm = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+        mm.load_state_dict(state)
+        opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(mm.parameters(), lr=0.0, momentum=0.9),
+                                                    named_parameters=mm.named_parameters())
+        enable_bf16_shadow(mm, opt)
+        opt.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(mm(x).float(), y)
+        loss.backward()
+        opt.reducer.synchronize()
+        return loss.item(), {n: opt.space.grad_view(i).detach().float().clone() for i, n in enumerate(opt.space.names)}
+
+    for tag, st in (("S0", s0), ("S3", s3)):
+        lf, gf = stock(st, False)
+        la, ga = stock(st, True)
+        lb, gb = stock(st, True)
+        le, ge = engine(st)
+        assert set(ge) == set(gf), set(gf) ^ set(ge)
+        ea, eb, ee = _layer_rel(gf, ga), _layer_rel(gf, gb), _layer_rel(gf, ge)
+        worst = max(gf, key=lambda n: ee[n] / max(ea[n], eb[n], 1e-12))
+        print("%s loss f32 %.5f bf16 %.5f %.5f engine %.5f; worst %s rel %.4f env %.4f" % (
+            tag, lf, la, lb, le, worst, ee[worst], max(ea[worst], eb[worst])))
+        bad = [(n, ee[n], max(ea[n], eb[n])) for n in gf if ee[n] > 2 * max(ea[n], eb[n]) + 1e-3]
+        assert not bad, (tag, bad[:10])
+        assert abs(le - lf) <= 3 * max(abs(la - lf), abs(lb - lf)) + 5e-3, (tag, lf, la, lb, le)
+        assert all(torch.isfinite(v).all() for v in ge.values())
+
+
+@needs_gpu
+def test_resnet50_full_size_engine_memorises_batch_like_stock():
+    """lr 0.01 (no chaotic phase): stock and engine both memorise one fixed 224x224 batch of 64
+    (7.16 -> ~4.2 in 10 steps) and agree within 2 % at every step (measured within 0.5 %).  The
+    lr-0.1 trajectory is not compared: it amplifies a single bf16 ulp of 1 % of the weights into a
+    several-% loss difference by step 3 (profiles/r5_engine_numerics.md)."""
     a = _resnet50_trajectory(False, lr=0.01)
     e = _resnet50_trajectory(True, lr=0.01)
     print("lr0.01 stock", a, "\nlr0.01 engine", e)
     for t in (a, e):  # memorising the batch: a steady decrease, then a plateau near 4.19
         assert all(y < x for x, y in zip(t[:7], t[1:7])) and t[-1] < 0.65 * t[0], t
-    for x0, xe in zip(a, e):  # measured within 0.5 % at every step
+    for x0, xe in zip(a, e):
         assert abs(xe - x0) <= 0.02 * x0, (a, e)
 
 
@@ -526,3 +579,146 @@ def test_graphed_bert_step_matches_eager_without_dropout_and_redraws_masks():
     lg, pg = run(True, 0.0, freeze=False)
     torch.testing.assert_close(torch.tensor(lg), torch.tensor(le), rtol=1e-3, atol=1e-3)
     torch.testing.assert_close(pg, pe, rtol=0, atol=2e-3)
+
+
+def _captured_vs_eager(build, batch, size, steps=8, lr=0.01, seed=7):
+    """Losses and flat parameters of ``steps`` S-SGD steps (bf16 shadow engine, RCCL 1-rank buckets),
+    eager vs GraphedStep (3 eager warm-up steps, capture, replays), for the model ``build()`` returns."""
+    import kungfu_amd as kf
+    from kungfu_amd.parallel.graphs import GraphedStep
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(graph):
+        torch.manual_seed(1234)
+        m = build().cuda().to(memory_format=torch.channels_last)
+        opt = kf.optimizers.SynchronousSGDOptimizer(
+            torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4),
+            named_parameters=m.named_parameters(), force_comm=True)
+        enable_bf16_shadow(m, opt)
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        x = torch.randn(batch, 3, size, size, device="cuda", generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (batch,), device="cuda", generator=g)
+
+        def step():
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        fn = GraphedStep(step, opt, warmup=3) if graph else step
+        losses = [float(fn().detach()) for _ in range(steps)]
+        torch.cuda.synchronize()
+        if graph:
+            assert fn.graph is not None and fn.replays == steps - 3, (fn.graph, fn.replays)
+        return losses, opt.space.flat_param.clone()
+
+    return run(False), run(True), run(True)
+
+
+@needs_gpu
+def test_graphed_vgg16_per_layer_step_matches_eager(monkeypatch):
+    """VGG-16's per-layer path (the fallback of the fused stack,
+    KUNGFU_VGG_FUSED=0) under whole-step capture.  Before round 5 the captured step gave a different
+    loss in every run and went NaN in ~1 of 4 runs while eager was bit-stable; the cause was the
+    bias+ReLU backward (_BiasActFn), the only in-step hipMemsetAsync plus f32 atomics (now fixed-order
+    partial sums, bias_act.hip).  Dropout off (a replay draws other masks than eager): two captured
+    runs and the eager run must agree bitwise -- losses and weights."""
+    from kungfu_amd.models.vgg import vgg16
+    from kungfu_amd.ops import vgg_fused
+
+    monkeypatch.setattr(vgg_fused, "_ENABLED", False)
+
+    def build():
+        m = vgg16(fused_bn=True)
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = 0.0
+        assert isinstance(m.features, vgg_fused.FusedVGGFeatures)
+        return m
+
+    (le, pe), (lg, pg), (lg2, pg2) = _captured_vs_eager(build, 32, 224)
+    print("eager", le, "\ngraph", lg, "\ngraph", lg2)
+    assert all(v == v for v in le + lg + lg2), (le, lg, lg2)
+    assert lg == lg2 and torch.equal(pg, pg2), "captured VGG-16 step not reproducible run to run"
+    assert le == lg and torch.equal(pe, pg), (le, lg)
+
+
+@needs_gpu
+def test_graphed_inception_v3_step_matches_eager():
+    """every model the bench captures by default has a captured-vs-eager bitwise test.
+    Inception-v3 (fused BN, sibling MFMA convs, batched BN finalizes) at 224x224 (the bench input), batch 16: two
+    captured runs and the eager run agree bitwise over 8 steps.  MIOpen's deterministic solvers for the
+    layers still on MIOpen: with its defaults even two EAGER runs differ from step 4 on (r5t4,
+    tools/diag/capture_repro.py), and with them eager, eager and two captures are bit-identical -- the
+    run-to-run variation is MIOpen's, not a capture race."""
+    from kungfu_amd.models.inception import inception_v3
+
+    old = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        (le, pe), (lg, pg), (lg2, pg2) = _captured_vs_eager(lambda: inception_v3(fused_bn=True), 16, 224)
+    finally:
+        torch.backends.cudnn.deterministic = old
+    print("eager", le, "\ngraph", lg, "\ngraph", lg2)
+    assert all(v == v for v in le + lg), (le, lg)
+    assert lg == lg2 and torch.equal(pg, pg2), "captured Inception-v3 step not reproducible run to run"
+    assert le == lg and torch.equal(pe, pg), (le, lg)
+
+
+@needs_gpu
+def test_segmented_capture_with_emulated_comm_matches_eager(monkeypatch):
+    """the N-rank capture layout -- graph segments cut at every bucket launch, the
+    bucket collectives issued eagerly on the comm stream between segment replays -- exercised on one
+    GPU through the comm emulator (an 8-rank all-reduce's footprint per bucket; it leaves the gradient
+    as it is).  The replay program must hold every bucket and one join, and the losses / weights must
+    match the eager step bitwise (ResNet-50, batch 16)."""
+    from kungfu_amd.models import resnet50
+
+    monkeypatch.setenv("KUNGFU_COMM_EMULATE", "ranks=8,ctas=16,busbw=350,lat_us=25")
+    import kungfu_amd as kf
+    from kungfu_amd.parallel.graphs import GraphedStep
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(graph):
+        torch.manual_seed(1234)
+        m = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+        opt = kf.optimizers.SynchronousSGDOptimizer(
+            torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4),
+            named_parameters=m.named_parameters(), force_comm=True)
+        enable_bf16_shadow(m, opt)
+        g = torch.Generator(device="cuda").manual_seed(5)
+        x = torch.randn(16, 3, 224, 224, device="cuda", generator=g).to(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (16,), device="cuda", generator=g)
+
+        def step():
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        fn = GraphedStep(step, opt, warmup=3) if graph else step
+        losses = [float(fn().detach()) for _ in range(8)]
+        torch.cuda.synchronize()
+        assert opt.reducer.describe()["comm_plane"] == "emulate"
+        if graph:
+            nb = len(opt.reducer.buckets)
+            kinds = [op[0] for op in fn.program]
+            assert fn.replays == 5 and not fn.disabled, (fn.replays, fn.disabled)
+            assert kinds.count("bucket") == nb and kinds.count("join") == 1, fn.program
+            assert sorted(op[1] for op in fn.program if op[0] == "bucket") == list(range(nb)), fn.program
+            # one segment before each cut point and one after the join, minus those that captured nothing
+            assert len(fn.segs) == kinds.count("g") and 2 <= len(fn.segs) <= nb + 2, (len(fn.segs), fn.program)
+        return losses, opt.space.flat_param.clone()
+
+    le, pe = run(False)
+    lg, pg = run(True)
+    print("eager", le, "\ngraph", lg)
+    assert le == lg and torch.equal(pe, pg), (le, lg)

@@ -48,13 +48,13 @@ def test_rccl_watchdog_names_stalled_bucket():
     assert "kungfu rccl watchdog" in out and "bucket" in out and "has not completed" in out, out[-4000:]
 
 
-def _bench(env, extra=(), expect_rc=0):
+def _bench(env, extra=(), expect_rc=0, gpus=2, batch=16, timeout=600):
     e = dict(os.environ, PYTHONPATH=ROOT, **env)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KUNGFU_SELF_SPEC"):
         e.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "2",
-                        "--batch", "16"] + list(extra), cwd=ROOT, env=e, stdout=subprocess.PIPE,
-                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "3", "--warmup",
+                        "2", "--batch", str(batch)] + list(extra), cwd=ROOT, env=e, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=timeout)
     if expect_rc != 0:
         assert r.returncode != 0, r.stdout[-5000:]
         return r.stdout
@@ -95,6 +95,16 @@ def test_bench_preflight_detects_corrupt_ipc_slot():
     out = _bench(dict(COLO, KUNGFU_PREFLIGHT_CORRUPT="1"), expect_rc=1)
     assert "pre-flight failed" in out and "IPC pull 0 <- 1 failed" in out, out[-4000:]
     assert time.time() - t0 < 240
+
+
+@needs_gpu
+def test_bench_preflight_stall_skips_ipc_on_every_rank():
+    """ADVICE r4: rank 1 reports its pre-flight all-reduce as stalled (test hook: no stuck kernel);
+    every rank then skips the IPC check (its device work would queue behind a real stuck
+    collective) and the pre-flight fails, naming rank 1, instead of hanging."""
+    out = _bench(dict(COLO, KUNGFU_PREFLIGHT_CORRUPT="1", KUNGFU_PREFLIGHT_CORRUPT_WHAT="stall"), expect_rc=1)
+    assert "pre-flight failed" in out and "all-reduce check failed on rank 1" in out, out[-4000:]
+    assert "IPC pull" not in out, out[-4000:]
 
 
 @needs_gpu
@@ -182,6 +192,18 @@ def test_bench_two_ranks_whole_step_graph():
     v = res["verify"]
     hg = res["config"]["hip_graph"]
     assert hg["captured"] is True and hg["replays"] >= 4 and not hg["disabled"], hg
+    assert hg["segments"] > 2, hg  # segmented N-rank capture (KUNGFU_GRAPH_SEGMENTED=1, default)
+    assert v["comm_ranks"] == 2 and v["replicas_consistent"] is True, v
+
+
+@needs_gpu
+def test_bench_two_ranks_single_graph_layout():
+    """KUNGFU_GRAPH_SEGMENTED=0: the N-rank step as ONE graph with the collectives inside (comm stream as
+    the capture's origin, compute forked from it) -- the round-4 layout, kept selectable."""
+    res = _bench(dict(COLO, KUNGFU_GRAPH_SEGMENTED="0"), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
+    v = res["verify"]
+    hg = res["config"]["hip_graph"]
+    assert hg["captured"] is True and hg["replays"] >= 4 and hg.get("segments", 1) == 1, hg
     assert v["comm_ranks"] == 2 and v["replicas_consistent"] is True, v
 
 
@@ -213,3 +235,50 @@ def test_bench_two_ranks_cta_budget():
     res = _bench(dict(COLO, KUNGFU_RCCL_MIN_CTAS="2", KUNGFU_RCCL_MAX_CTAS="8"))
     v = res["verify"]
     assert v["rccl_ctas"] == [2, 8] and v["replicas_consistent"] is True, v
+
+
+@needs_gpu
+def test_bench_eight_colocated_ranks():
+    """the N = 8 code path of bench.py before the first real 8-GPU run -- 8 RCCL
+    ranks colocated on one device (socket transport): torchrun self-launch, uid bootstrap, the 8-rank
+    pre-flight (P2P "n/a", 64 MiB all-reduce value check, IPC pull ring), bucket order learned from
+    rank 0, the watchdog, the default N-rank capture (graph segments with eager collectives), the
+    per-bucket comm probe and replica checksums; ResNet-50, batch 8 per rank."""
+    res = _bench(dict(COLO), gpus=8, batch=8, timeout=900, extra=["--warmup", "4"])
+    v = res["verify"]
+    assert res["n_gpus"] == 8 and res["config"]["parallelism"] == "dp8", res
+    assert v["comm_ranks"] == 8 and v["comm_plane"] == "rccl" and v["replicas_consistent"] is True, v
+    pf = v["preflight"]
+    assert pf["ok"] is True and pf["ranks"] == 8 and len(pf["devices"]) == 8, pf
+    assert all(str(x).startswith("n/a") for row in pf["p2p"].values() for x in row.values()), pf["p2p"]
+    assert all(b and b > 0 for b in pf["ipc_pull_gbs"].values()), pf
+    assert v["rccl_watchdog"]["ops_watched"] > 0 and v["rccl_watchdog"]["pending"] == 0, v
+    assert v["rccl_ctas"] == [16, 64], v["rccl_ctas"]
+    hg = res["config"]["hip_graph"]
+    assert hg["captured"] is True and hg["segments"] > 2 and hg["replays"] >= 3, hg
+    nb = res["config"]["comm"]["buckets"]
+    assert len(v["comm_per_bucket_ms"]) == nb and all(t > 0 for t in v["comm_per_bucket_ms"]), v
+    assert v["exposed_comm_ms"] is not None and v["exposed_comm_ms"] >= 0, v
+
+
+@needs_gpu
+def test_bench_elastic_bert_gns_four_to_eight_ranks():
+    """config 5 at its real sizes -- BERT-base + gradient noise scale, elastic
+    4 -> 8 ranks (kungfu-run -w, config server), every rank colocated on one device over RCCL's
+    socket transport; both phases keep identical replicas and the 8-rank phase reports a finite
+    noise scale."""
+    e = dict(os.environ, PYTHONPATH=ROOT, **COLO)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "KUNGFU_SELF_SPEC"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "bert_base", "--optimizer", "gns",
+                        "--elastic", "4:3,8:3", "--batch", "4", "--seq-len", "64"], cwd=ROOT, env=e,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-5000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stderr[-5000:]
+    res = json.loads(lines[0])
+    assert [p["np"] for p in res["phases"]] == [4, 8], res["phases"]
+    assert res["all_phases_consistent"] is True, res["phases"]
+    gns = res["phases"][1]["gradient_noise_scale"]
+    assert gns is not None and gns == gns and abs(gns) != float("inf"), res["phases"]
+    assert [(z["from"], z["to"]) for z in res["resizes"]] == [(4, 8)], res["resizes"]

@@ -33,5 +33,5 @@ assert opt.reducer._ordered, "auto-order did not run"
 w = opt.space.flat_param.double().sum().reshape(1)
 ws = kf.ops.all_gather(w.cpu())
 assert torch.all(ws == ws[0]), ws
-print("SSGD_GPU_OK rank=%d np=%d order=%s" % (r, n, opt.reducer.sched.order()), flush=True)
+print("SSGD_GPU_OK rank=%d np=%d order=%s" % (r, n, opt.reducer.tracker.order()), flush=True)
 kf.finalize()

@@ -86,6 +86,18 @@ def main():
     print("host enqueue %.2f ms/step, wall %.2f ms/step, gpu %.2f ms/step" % (
         1e3 * (h1 - h0) / n, 1e3 * (h2 - h0) / n, e0.elapsed_time(e1) / n))
     print("host phases (ms/step): " + ", ".join("%s %.2f" % (k, 1e3 * v / n) for k, v in ph.items()))
+    # the loop above lets the host run ahead until the launch queue pushes back, so its "enqueue" time
+    # includes waiting for the GPU; here every step starts with the GPU idle: the host's own cost
+    cold = []
+    for _ in range(n):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        cold.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    cold.sort()
+    print("host enqueue from an idle GPU (no backpressure): median %.2f ms/step, min %.2f" % (
+        1e3 * cold[len(cold) // 2], 1e3 * cold[0]))
     if os.environ.get("CPROFILE"):
         import cProfile
         import pstats
@@ -96,7 +108,8 @@ def main():
             step()
         pr.disable()
         torch.cuda.synchronize()
-        pstats.Stats(pr).sort_stats("tottime").print_stats(30)
+        pstats.Stats(pr).sort_stats("tottime").print_stats(45)
+        pstats.Stats(pr).sort_stats("cumulative").print_stats(45)
     kf.finalize()
 
 
