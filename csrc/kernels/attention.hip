@@ -406,11 +406,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
         }
 }
 
-// KUNGFU_ATTN_BWD_WAVES (dev knob, A/B): 8 (default) or 4 waves per S = 128 backward workgroup
-int attn_bwd_waves() {
-    static const int w = dev_knob("KUNGFU_ATTN_BWD_WAVES", 8) == 4 ? 4 : 8;
-    return w;
-}
+// 8 waves per S = 128 backward workgroup (4: one wave per SIMD, measured slower, r4t15)
+int attn_bwd_waves() { return 8; }
 
 AttnArgs make_args(const uint16_t *qkv, uint16_t *out, float *lse, const uint16_t *dout, uint16_t *dqkv, int H,
                    float scale, uint32_t seed, float p_drop) {

@@ -83,33 +83,14 @@ __device__ __forceinline__ void st16(uint4 *p, const uint4 &v, bool nt) {
 
 // default 1 (non-temporal loads): ResNet-50 step 21.73 -> 21.39 ms on MI355X, while
 // non-temporal stores did not pay in the full step (profiles/README.md, r3f)
-// KUNGFU_BN_SKIP_FINALIZE=1: TIMING EXPERIMENT ONLY -- the sums-finalize kernels are not launched
-// (coefficients stay stale: wrong numerics), to bound what folding them elsewhere could save.
-// Compiled in only with -DKUNGFU_DEV_EXPERIMENTS=1 (never in the release .so).
-#ifndef KUNGFU_DEV_EXPERIMENTS
-#define KUNGFU_DEV_EXPERIMENTS 0
-#endif
-bool bn_skip_finalize() {
-#if KUNGFU_DEV_EXPERIMENTS
-    static const bool b = [] {
-        const char *e = std::getenv("KUNGFU_BN_SKIP_FINALIZE");
-        return e && std::atoi(e) != 0;
-    }();
-    return b;
-#else
-    return false;
-#endif
-}
+// (the round-3 timing experiment that skipped the sums-finalize launches -- an upper bound of
+// 1.0 ms/step on what folding them elsewhere could save -- is retired with its knob, round 5)
+bool bn_skip_finalize() { return false; }
 
-int bn_nt_mode() {
-    static const int m = dev_knob("KUNGFU_BN_NT", 1);
-    return m;
-}
+// non-temporal loads, plain stores (bit 0 loads, bit 1 stores; the round-3 A/B above)
+int bn_nt_mode() { return 1; }
 
-int bn_max_grid(int def) {
-    static const int m = dev_knob("KUNGFU_BN_MAXGRID", 0);
-    return m > 0 ? m : def;
-}
+int bn_max_grid(int def) { return def; }
 
 struct Chunking {
     int64_t rows_per_chunk;

@@ -36,6 +36,28 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+__device__ __forceinline__ int wm_of(int wave, int wn) { return wave / wn; }
+
+// relu(v * scale + shift) on the 8 bf16 of an A fragment (8 consecutive input channels), or 0 for
+// a padding row; f32 math, one v_cvt_pk_bf16_f32 per pair (round to nearest even, as bn_apply)
+__device__ __forceinline__ void prebn_frag(bf16x8 &f, const float *sc, const float *sh, bool ok) {
+    uint4 u;
+    __builtin_memcpy(&u, &f, 16);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        float lo = __uint_as_float(w[d] << 16), hi = __uint_as_float(w[d] & 0xffff0000u);
+        lo = fmaxf(fmaf(lo, sc[2 * d], sh[2 * d]), 0.f);
+        hi = fmaxf(fmaf(hi, sc[2 * d + 1], sh[2 * d + 1]), 0.f);
+        uint32_t r;
+        asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+        o[d] = ok ? r : 0u;
+    }
+    u = make_uint4(o[0], o[1], o[2], o[3]);
+    __builtin_memcpy(&f, &u, 16);
+}
+
 __device__ __forceinline__ void unpack_bf16x8(const uint4 &v, float (&f)[8]) {
     const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
 #pragma unroll
@@ -225,10 +247,20 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int RED_BYTES = STATS ? NSUM * GROUPS * BN * 4 : 0;
     constexpr int EPI_BYTES = BM * CROW > RED_BYTES ? BM * CROW : RED_BYTES;
     constexpr int LDS_BYTES = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
-    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
+    constexpr bool PREBN = (EPI & kEpiPreBN) != 0;
+    constexpr int PRE_BYTES = PREBN ? 2 * 1024 * 4 : 0;  // [scale; shift] of up to 1024 input channels
+    static_assert(!PREBN || KS == 1 || KS == 3, "PreBN: 1x1 / 3x3 forward only");
+    static_assert(LDS_BYTES + PRE_BYTES <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES + PRE_BYTES];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if constexpr (PREBN) {
+        // the BN coefficients of every input channel into LDS once (one array with the staging ring,
+        // see cdna_hip_programming.md 'Projection GEMM' trap 4a), before any LDS-DMA is in flight
+        float *pc = reinterpret_cast<float *>(lds + LDS_BYTES);
+        for (int i = tid; i < 2 * g.C; i += NT) pc[i < g.C ? i : 1024 + i - g.C] = ea.pcoef[i];
+        __syncthreads();
+    }
 
     // XCD-aware bijective remap: blocks sharing an XCD get consecutive tile ids.
     const int nwg = gridDim.x, orig = blockIdx.x;
@@ -289,6 +321,28 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     }
     const int csteps = (g.C + kBK - 1) / kBK;
     const int ksteps = TAPS * csteps;
+    // PreBN: the taps at which each of this lane's A fragment rows reads a padding pixel (the BN
+    // output there is 0, not relu(shift)): bit tap of pre_ok[i] set = an in-image pixel
+    uint32_t pre_ok[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        pre_ok[i] = 0xffffffffu;
+        if constexpr (PREBN && KS == 3) {
+            const int m = m0 + wm_of(wave, WN) * WTM + i * 16 + (lane & 15);
+            pre_ok[i] = 0;
+            if (m < g.M) {
+                const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH;
+                const int ih0 = oh * g.stride - g.ph, iw0 = ow * g.stride - g.pw;
+#pragma unroll
+                for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < KW; ++kw)
+                        if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
+                            static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
+                            pre_ok[i] |= 1u << (kh * KW + kw);
+            }
+        }
+    }
 
 #if KUNGFU_CONV_BUFLD
     // LDS-DMA through buffer resources: 32-bit byte offsets, out-of-range lanes (padding taps,
@@ -395,6 +449,17 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         for (int j = 0; j < TN; ++j) {
             const int rb = wn * WTN + j * 16 + (lane & 15);
             bf1[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, 4 + (lane >> 4)));
+        }
+        if constexpr (PREBN) {
+            const int tap = ks / csteps, cc = ks - tap * csteps;
+            const float *pc = reinterpret_cast<const float *>(lds + LDS_BYTES);
+            const int c0 = cc * kBK + (lane >> 4) * 8;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const bool ok = (pre_ok[i] >> tap) & 1u;
+                prebn_frag(af0[i], pc + c0, pc + 1024 + c0, ok);
+                prebn_frag(af1[i], pc + c0 + 32, pc + 1024 + c0 + 32, ok);
+            }
         }
         mfma_block(af0, bf0);
         __builtin_amdgcn_sched_barrier(0);
@@ -728,17 +793,11 @@ int conv_tile_rules() {
 // Staggered staging issue in the 8-wave tiles: the two waves sharing a SIMD issue their LDS-DMA
 // pieces in different phases of the K-step (one before its fragment reads, one between its MFMA
 // clusters) instead of stalling on staging issue together.  ResNet-50 +0.8 % (21.43-21.49 ->
-// 21.28-21.29 ms/step, same box), Inception-v3 neutral.  KUNGFU_CONV_STAGGER=0 turns it off.
-int conv_stagger() {
-    static const int v = dev_knob("KUNGFU_CONV_STAGGER", 1);
-    return v;
-}
+// 21.28-21.29 ms/step, same box), Inception-v3 neutral.
+int conv_stagger() { return 1; }
 
-// KUNGFU_CONV_PRIO=1: static s_setprio 1 for the upper wave half of the 8-wave tiles (A/B)
-int conv_prio() {
-    static const int v = dev_knob("KUNGFU_CONV_PRIO", 0);
-    return v;
-}
+// static s_setprio 1 for the upper wave half of the 8-wave tiles: measured neutral (r3), off
+int conv_prio() { return 0; }
 
 // 256-byte zero page for padding rows (global_load_lds needs a real address).
 const void *zero_page() {
@@ -767,10 +826,9 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     g.ntiles = (g.K + BN - 1) / BN;
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
     if constexpr (STATS) {
-        // persistent blocks (KUNGFU_CONV_PERSIST_BLOCKS, default 1024 = 4 per CU): one atomic
+        // persistent blocks (4 per CU, fewer when the tile's LDS allows less): one atomic
         // statistics flush per block instead of per tile
-        // (KUNGFU_CONV_PERSIST_BLOCKS, default 4 per CU, fewer when the tile's LDS allows less)
-        static const int env_cap = dev_knob("KUNGFU_CONV_PERSIST_BLOCKS", 0);
+        constexpr int env_cap = 0;
         constexpr int kRow = 128, STG = ST * (BM + BN) * kRow, CT = BM * (BN * 2 + 16);
         constexpr int LDS = STG > CT ? STG : CT;
         constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
@@ -818,6 +876,10 @@ void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
         case A | kEpiAccEven | B: launch_epi<KS, WM, WN, ST, A | kEpiAccEven | B, TM, TN>(x, w, y, g, ea, s); break;
         case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu, TM, TN>(x, w, y, g, ea, s); break;
         case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate, TM, TN>(x, w, y, g, ea, s); break;
+        case kEpiPreBN: launch_epi<KS, WM, WN, ST, kEpiPreBN, TM, TN>(x, w, y, g, ea, s); break;
+        case kEpiPreBN | kEpiFwdStats:
+            launch_epi<KS, WM, WN, ST, kEpiPreBN | kEpiFwdStats, TM, TN>(x, w, y, g, ea, s);
+            break;
         default: throw std::invalid_argument("conv: unsupported epilogue combination");
         }
     }

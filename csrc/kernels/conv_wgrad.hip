@@ -842,11 +842,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
 
 // Staggered staging issue in the row-image kernels (see wgrad_kernel), default on (same-box A/Bs:
 // Inception-v3 21.62 -> 21.45 ms/step, VGG-16 34.85 -> 34.62, ResNet-50 neutral);
-// KUNGFU_WROWS_STAGGER=0 turns it off.
-int rows_stagger(bool /*rect*/) {
-    static const int v = dev_knob("KUNGFU_WROWS_STAGGER", 1);
-    return v;
-}
+int rows_stagger(bool /*rect*/) { return 1; }
 
 struct Tile {
     int wm, wn, tn;  // waves (co, ci) and 16-channel ci blocks per wave
@@ -924,17 +920,14 @@ void launch_t(const uint16_t *dy, const uint16_t *x, void *dw, float *part, cons
     // 2 for the 256x256 tile (64 KB per stage)
     constexpr int STAGE_BYTES = 64 * (64 * WM + 16 * TN * WN) * 2;
     constexpr int STAGES = 3 * STAGE_BYTES <= 160 * 1024 ? 3 : 2;
-    // staggered staging issue (KUNGFU_WGRAD_STAGGER=0/1 forces it off/on): default on for the 256x256
-    // tiles only -- BERT-base's long-K linear weight gradients +1.5 % step time, ResNet-50's 256x128
-    // tiles -0.8 % with it (tools/gpu_r3_envab.sh, same box)
-    static const int env_stagger = dev_knob("KUNGFU_WGRAD_STAGGER", -1);
-    const int stagger = env_stagger >= 0 ? env_stagger : (TN == 8 ? 1 : 0);
+    // staggered staging issue: on for the 256x256 tiles only -- BERT-base's long-K linear weight
+    // gradients +1.5 % step time, ResNet-50's 256x128 tiles -0.8 % with it (tools/gpu_r3_envab.sh)
+    const int stagger = TN == 8 ? 1 : 0;
     if (KUNGFU_WGRAD_BUFLD && (static_cast<int64_t>(g.P) * g.K * 2 >= kWBufOOB ||
                                static_cast<int64_t>(g.N) * g.H * g.W * g.C * 2 >= kWBufOOB))
         throw std::invalid_argument("conv_wgrad: dy or x of 2 GiB or more (buffer-resource staging)");
-    // 256x256 tiles: four 32-pixel stages (two K-steps in flight across each barrier) instead of two
-    // 64-pixel ones (KUNGFU_WGRAD_KB32, A/B)
-    static const int kb32 = dev_knob("KUNGFU_WGRAD_KB32", 0);
+    // 256x256 tiles with four 32-pixel stages instead of two 64-pixel ones: measured no better (r4t1)
+    constexpr int kb32 = 0;
     if constexpr (TN == 8) {
         if (kb32) {
             wgrad_kernel<KS, S, WM, WN, 4, TN, 32><<<g.tiles * g.splits, 64 * WM * WN, 0, s>>>(

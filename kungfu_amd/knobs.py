@@ -6,6 +6,7 @@ Three kinds:
   that route an op back to the library path);
 * ``launcher`` -- set by ``kungfu-run`` / the elastic runtime for its workers (the worker env
   contract, parity ``srcs/go/kungfu/env/envs.go``); users do not set these by hand;
+* ``test``     -- hooks the test suite uses (colocated ranks, injected pre-flight faults);
 * ``dev``      -- A/B switches kept for re-measuring a design decision (most of them select an
   alternative that measured slower, see profiles/README.md).  They are honoured ONLY when
   ``KUNGFU_DEV_KNOBS=1`` is also set -- in Python (:func:`get`) and in the kernels
@@ -27,7 +28,7 @@ from typing import Dict, NamedTuple, Optional
 
 class Knob(NamedTuple):
     default: Optional[str]
-    kind: str  # user | launcher | dev
+    kind: str  # user | launcher | test | dev
     doc: str
 
 
@@ -41,6 +42,10 @@ def _u(default, doc):
 
 def _l(doc):
     return Knob(None, "launcher", doc)
+
+
+def _t(default, doc):
+    return Knob(default, "test", doc)
 
 
 def _d(default, doc):
@@ -77,12 +82,12 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_RCCL_MIN_CTAS": _u("0", "ncclConfig_t.minCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
     "KUNGFU_RCCL_MAX_CTAS": _u("0", "ncclConfig_t.maxCTAs (0 = RCCL default); _<SCOPE> suffix per scope"),
     "KUNGFU_NATIVE_BACKTRACE": _u("0", "1: print a native backtrace on SIGSEGV/SIGBUS/SIGABRT (debugging)"),
-    "KUNGFU_RCCL_COLOCATE": _u("0", "1: several RCCL ranks on one GPU (socket transport; tests)"),
+    "KUNGFU_RCCL_COLOCATE": _t("0", "1: several RCCL ranks on one GPU (socket transport; tests)"),
     "KUNGFU_COMM_EMULATE": _u(None, "ranks=R,ctas=C,busbw=GB/s,lat_us=L: model an R-rank all-reduce on one GPU"),
     "KUNGFU_PREFLIGHT_TIMEOUT_S": _u("60", "bench pre-flight: deadline of each device check"),
-    "KUNGFU_PREFLIGHT_CORRUPT": _u(None, "test hook: this rank corrupts its pre-flight buffer"),
-    "KUNGFU_PREFLIGHT_CORRUPT_WHAT": _u("ipc", "test hook: ipc | allreduce | stall (reports a stall without stalling)"),
-    "KUNGFU_FORCE_DEVICE": _u(None, "pin every rank to this HIP device (colocated tests)"),
+    "KUNGFU_PREFLIGHT_CORRUPT": _t(None, "test hook: this rank corrupts its pre-flight buffer"),
+    "KUNGFU_PREFLIGHT_CORRUPT_WHAT": _t("ipc", "test hook: ipc | allreduce | stall (reports a stall without stalling)"),
+    "KUNGFU_FORCE_DEVICE": _t(None, "pin every rank to this HIP device (colocated tests)"),
     "KUNGFU_INIT_CKPT": _u(None, "elastic: initial checkpoint step"),
     # -- kernel routing kill switches (1 = our HIP kernel, 0 = library path) --------------------
     "KUNGFU_CONV3X3": _u("1", "3x3 convolutions on the MFMA kernel"),
@@ -92,7 +97,6 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_FUSED_BLOCK": _u("1", "ResNet bottleneck as one fused autograd node"),
     "KUNGFU_STEM": _u("1", "ResNet stem conv on the MFMA stem kernel"),
     "KUNGFU_LINEAR_WGRAD": _u("1", "linear-layer weight gradients on the split-K MFMA kernel"),
-    "KUNGFU_LINEAR_GEMM": _u("0", "linear forward / data gradient on gemm.hip's NT GEMM instead of hipBLASLt"),
     "KUNGFU_DEV_KNOBS": _u("0", "1: honour the dev (A/B) knobs below"),
     # -- launcher / worker env contract (csrc/launcher/job.cpp, csrc/runtime/peer.cpp) ---------
     "KUNGFU_SELF_SPEC": _l("this worker's host:port"),
@@ -108,36 +112,43 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_ALLOW_XGMI": _l("several workers may share a GPU (-allow-xgmi)"),
     "KUNGFU_SELF_IP": _l("this worker's IP (single mode)"),
     # -- dev A/B knobs (need KUNGFU_DEV_KNOBS=1) ----------------------------------------------
-    "KUNGFU_CONV_PRIO": _d("0", "s_setprio 1 for the upper wave half of 8-wave conv tiles (neutral)"),
-    "KUNGFU_CONV_STAGGER": _d("1", "staggered LDS-DMA issue in 8-wave conv tiles (0 = off, -0.8 %)"),
     "KUNGFU_CONV_TILE_RULES": _d("2", "1 = the round-2 conv tile defaults"),
-    "KUNGFU_CONV_PERSIST_BLOCKS": _d("0", "persistent conv blocks for the statistics epilogues (0 = 4/CU)"),
-    "KUNGFU_WGRAD_STAGGER": _d("-1", "wgrad staging stagger (-1 = on for 256x256 tiles only)"),
-    "KUNGFU_WROWS_STAGGER": _d("1", "row-image wgrad staging stagger"),
-    "KUNGFU_WGRAD_KB32": _d("0", "256x256 weight-gradient tiles with four 32-pixel LDS stages"),
-    "KUNGFU_WGRAD_STREAM": _d("0", "weight gradients on a side stream (-1.2 %)"),
-    "KUNGFU_BN_NT": _d("1", "BN non-temporal policy (0 none, 1 loads, 2 stores, 3 both)"),
-    "KUNGFU_BN_MAXGRID": _d("0", "BN apply grid cap (0 = kernel default)"),
-    "KUNGFU_BN_INLAUNCH_FIN": _d("0", "BN finalize inside the statistics conv's launch (slower)"),
-    "KUNGFU_BN_CONCAT": _d("1", "Inception branch BN+ReLU stores into the concatenation"),
-    "KUNGFU_STEM_FUSED_BWD": _d("0", "one-pass fused stem backward (slower)"),
-    "KUNGFU_LN_BIAS_LINK": _d("1", "bias gradients from the consuming LayerNorm backward"),
-    "KUNGFU_GELU_BIAS_LINK": _d("1", "FC1 bias gradient from the fused GELU-backward column sum"),
-    "KUNGFU_ATTN_BWD_WAVES": _d("8", "waves per S = 128 attention-backward workgroup (8 or 4)"),
-    "KUNGFU_BN_BATCH_FIN": _d("1", "Inception concatenation: its BNs' finalizes in one launch each way (0: one per BN)"),
-    "KUNGFU_LINEAR_WGRAD_ATOMICS": _d("0", "1: linear weight-gradient split-K tiles added into the f32 slot by atomics (not reproducible)"),
     "KUNGFU_VGG_FUSED": _d("1", "VGG-16 conv/ReLU/pool stack as one autograd node (0: the per-layer modules)"),
-    "KUNGFU_PAIR_NATIVE": _d("1", "pair-averaging prefetch on the native C++ thread (0: the Python thread)"),
-    "KUNGFU_FUSED_XENT": _d("1", "BERT MLM loss on xent.hip straight from the bf16 logits (0: torch f32 path)"),
-    "KUNGFU_GELU_FWD": _d("0", "1: erf-GELU forward on norms.hip's one-exponential kernel (measured 0.6 % slower than torch's)"),
-    "KUNGFU_RESIDUAL_LINK": _d("1", "transformer skip-input gradient added inside the consumer linear's dgrad GEMM"),
-    "KUNGFU_LINEAR_DIRECT_WGRAD": _d("1", "linear weight gradients reduced straight into the flat buffer"),
-    "KUNGFU_COMM_STREAM_PRIORITY": _d("0", "HIP priority of the comm stream (-1 measured 2x slower)"),
     "KUNGFU_GRAPH_MULTIRANK": _u("1", "0: GraphedStep keeps multi-rank RCCL steps eager (capture uses the comm stream as origin)"),
     "KUNGFU_GRAPH_SEGMENTED": _u("1", "N-rank capture as graph segments cut at every bucket launch, collectives issued "
                                        "eagerly between replays (0: one graph with the collectives inside)"),
-    "KUNGFU_BN_SKIP_FINALIZE": _d("0", "TIMING ONLY, wrong numerics: skip BN finalize (needs a -DKUNGFU_DEV_EXPERIMENTS=1 build)"),
-    "KUNGFU_BERT_GEMM": _d("0", "BERT linear layers on the hand-written GEMM"),
+}
+
+# Round 5: A/B knobs whose question is settled are gone -- the measured winner
+# is the only code path (or a module attribute the tests flip), the negative results are recorded in
+# profiles/README.md.  Setting one warns that it no longer does anything.
+RETIRED: Dict[str, str] = {
+    "KUNGFU_LINEAR_GEMM": "linear layers on gemm.hip measured slower than hipBLASLt (r4_gemm_nt.md)",
+    "KUNGFU_LINEAR_WGRAD_ATOMICS": "atomic split-K linear wgrad measured 3 % slower (r4t29)",
+    "KUNGFU_GELU_FWD": "the one-exponential GELU forward measured 0.6 % slower (r4t20)",
+    "KUNGFU_WGRAD_STREAM": "weight gradients on a side stream measured 1.2 % slower (r3)",
+    "KUNGFU_BN_INLAUNCH_FIN": "BN finalize inside the conv launch measured 0.55 ms/step slower (r3)",
+    "KUNGFU_CONV_PRIO": "s_setprio in the conv tiles measured neutral (r3)",
+    "KUNGFU_STEM_FUSED_BWD": "the one-pass fused stem backward measured slower (r3)",
+    "KUNGFU_COMM_STREAM_PRIORITY": "a high-priority comm stream measured 2x slower (r1)",
+    "KUNGFU_BN_SKIP_FINALIZE": "timing-only experiment (wrong numerics), retired",
+    "KUNGFU_BERT_GEMM": "unused",
+    "KUNGFU_CONV_STAGGER": "settled: on (+0.8 %, r3)",
+    "KUNGFU_CONV_PERSIST_BLOCKS": "settled: 4 persistent blocks per CU",
+    "KUNGFU_WGRAD_STAGGER": "settled: on for 256x256 tiles only (r3)",
+    "KUNGFU_WROWS_STAGGER": "settled: on (r3)",
+    "KUNGFU_WGRAD_KB32": "settled: off (r4t1)",
+    "KUNGFU_BN_NT": "settled: non-temporal loads (r3f)",
+    "KUNGFU_BN_MAXGRID": "settled: the kernel default grid",
+    "KUNGFU_ATTN_BWD_WAVES": "settled: 8 waves (r4t15)",
+    "KUNGFU_BN_CONCAT": "settled: on (module attribute ops.fused_bn.CONCAT_ENABLED)",
+    "KUNGFU_BN_BATCH_FIN": "settled: on (r4t25; module attribute ops.fused_bn._BATCH_FIN)",
+    "KUNGFU_LN_BIAS_LINK": "settled: on (module attribute ops.layernorm._BIAS_LINK)",
+    "KUNGFU_GELU_BIAS_LINK": "settled: on (module attribute ops.linear._GELU_LINK)",
+    "KUNGFU_RESIDUAL_LINK": "settled: on (r4t14; module attribute ops.linear._RES_LINK)",
+    "KUNGFU_LINEAR_DIRECT_WGRAD": "settled: on (module attribute ops.linear._DIRECT_WGRAD)",
+    "KUNGFU_FUSED_XENT": "settled: on (r4t22; module attribute ops.xent._ENABLED)",
+    "KUNGFU_PAIR_NATIVE": "settled: the native prefetch thread (r4t22)",
 }
 
 # compile-time switches (-D...), not environment variables; listed so the source lint knows them
@@ -186,6 +197,9 @@ def check_environ(environ=None) -> list:
             continue
         if name.startswith(PREFIXES):
             continue
+        if name in RETIRED:
+            msgs.append("%s is retired and has no effect: %s" % (name, RETIRED[name]))
+            continue
         close = difflib.get_close_matches(name, list(KNOBS), n=1, cutoff=0.75)
         msgs.append("unknown setting %s%s (see kungfu_amd/knobs.py)" % (
             name, " -- did you mean %s?" % close[0] if close else ""))
@@ -201,8 +215,18 @@ def check_environ_once() -> None:
 
 
 def table() -> str:
-    """Markdown table of every knob (docs/KNOBS.md is generated from this)."""
-    rows = ["| variable | kind | default | meaning |", "|---|---|---|---|"]
-    for n, k in KNOBS.items():
-        rows.append("| `%s` | %s | %s | %s |" % (n, k.kind, "" if k.default is None else "`%s`" % k.default, k.doc))
-    return "\n".join(rows) + "\n"
+    """Markdown tables of every knob, one per kind (docs/KNOBS.md is generated from this), then the
+    retired ones."""
+    heads = {"user": "Configuration", "dev": "Developer A/B switches (need KUNGFU_DEV_KNOBS=1)",
+             "test": "Test hooks", "launcher": "Worker environment set by the launcher (not set by hand)"}
+    out = []
+    for kind in ("user", "dev", "test", "launcher"):
+        rows = ["## %s" % heads[kind], "", "| variable | default | meaning |", "|---|---|---|"]
+        for n, k in KNOBS.items():
+            if k.kind == kind:
+                rows.append("| `%s` | %s | %s |" % (n, "" if k.default is None else "`%s`" % k.default, k.doc))
+        out.append("\n".join(rows))
+    rows = ["## Retired (setting one only warns)", "", "| variable | why |", "|---|---|"]
+    rows += ["| `%s` | %s |" % (n, why) for n, why in RETIRED.items()]
+    out.append("\n".join(rows))
+    return "\n\n".join(out) + "\n"

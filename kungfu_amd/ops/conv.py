@@ -61,7 +61,8 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor, w: torch.Tensor, stride: int, pad: 
         acc = torch.zeros(w.shape, dtype=torch.float32, device=x.device).contiguous(
             memory_format=torch.channels_last)
         for i in range(0, n, step):
-            hip().conv_wgrad(dy[i:i + step], x[i:i + step], ks, int(stride), out=acc, accumulate=True)
+            hip().conv_wgrad(dy[i:i + step], x[i:i + step], ks, int(stride), out=acc, accumulate=True,
+                             atomics=False)  # deterministic (split-K partials + reduce)
         return acc.to(torch.bfloat16)
     return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]

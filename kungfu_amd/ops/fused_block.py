@@ -45,7 +45,6 @@ from typing import List, Optional
 import torch
 import torch.nn.functional as F
 
-from .. import knobs
 from .._lib import buf_ok, hip, hip_available
 from ..parallel.mixed import SideStream, deliver, direct_target, shadow
 
@@ -77,7 +76,7 @@ def _sums(bn, dev) -> torch.Tensor:
 # workgroup must wait for its memory-side f64 slot atomics before it may arrive, and the arrivals
 # and the last workgroup's fold sit on the launch's critical path), although dropping the finalize
 # launches altogether would save 1.0 ms (KUNGFU_BN_SKIP_FINALIZE timing experiment).
-_INLAUNCH_FIN = knobs.get("KUNGFU_BN_INLAUNCH_FIN") == "1"
+_INLAUNCH_FIN = False  # BN finalize inside the statistics conv (r3: 0.55 ms/step slower); a switch for its test
 
 
 def _kw(**kw):

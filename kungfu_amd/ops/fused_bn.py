@@ -23,14 +23,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .. import knobs
 from .._lib import hip, hip_available
 from ..parallel.mixed import deliver, direct_target
 
 import os
 
 # KUNGFU_BN_CONCAT=0: apply deferred branch BNs and concatenate with torch.cat (A/B, tests)
-CONCAT_ENABLED = knobs.get("KUNGFU_BN_CONCAT") != "0"
+CONCAT_ENABLED = True  # module switch (tests)
 
 
 def available() -> bool:
@@ -194,7 +193,7 @@ class _ConcatSpec:
 
 # the concatenation's BN finalizes batched, one launch per direction (Inception-v3 12607 -> 12809 img/s,
 # r4t25); KUNGFU_BN_BATCH_FIN=0: one per BN
-_BATCH_FIN = knobs.get("KUNGFU_BN_BATCH_FIN") != "0"
+_BATCH_FIN = True  # module switch (tests)
 
 
 class _BNConcatFn(torch.autograd.Function):

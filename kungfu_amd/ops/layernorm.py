@@ -15,13 +15,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .. import knobs
 from .._lib import hip, hip_available
 from . import dropout_seed
 
 import os
 
-_BIAS_LINK = knobs.get("KUNGFU_LN_BIAS_LINK") != "0"  # A/B switch of the linear bias-gradient link
+_BIAS_LINK = True  # module switch of the linear bias-gradient link (tests)
 
 
 class _AddLayerNormFn(torch.autograd.Function):

@@ -17,7 +17,6 @@ import os
 import torch
 import torch.nn.functional as F
 
-from .. import knobs
 from .._lib import hip, hip_available
 
 _MAX_TOKENS = 1 << 23
@@ -55,7 +54,7 @@ class ResidualLink:
         self.armed, self.value = False, None
 
 
-_RES_LINK = knobs.get("KUNGFU_RESIDUAL_LINK") != "0"
+_RES_LINK = True  # module switch (tests / A/B)
 
 
 def residual_link(x: torch.Tensor):
@@ -67,13 +66,11 @@ def residual_link(x: torch.Tensor):
     return rl
 
 
-_DIRECT_WGRAD = knobs.get("KUNGFU_LINEAR_DIRECT_WGRAD") != "0"
-# split-K weight-gradient tiles added into the f32 slot with atomics (no partials, no reduce pass;
-# not bitwise reproducible) instead of the deterministic two-pass reduce
-_WGRAD_ATOMICS = knobs.get("KUNGFU_LINEAR_WGRAD_ATOMICS") == "1"  # A/B r4t29: 3 % slower on BERT-base
-# KUNGFU_LINEAR_GEMM=1: forward (x W^T + b) and data gradient (dy W, with W^T from the flat
-# space's per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt
-_GEMM = knobs.get("KUNGFU_LINEAR_GEMM") == "1"
+_DIRECT_WGRAD = True  # module switch (tests)
+# set_gemm_enabled(True): forward (x W^T + b) and data gradient (dy W, with W^T from the flat space's
+# per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt -- measured
+# slower (profiles/r4_gemm_nt.md), so off and not an environment knob any more (round 5)
+_GEMM = False
 
 
 def set_gemm_enabled(on: bool) -> bool:
@@ -155,7 +152,7 @@ class _LinearFn(torch.autograd.Function):
             space, i = tgt
             gv = space.grad_view(i)
             hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1, out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
-                             accumulate=True, atomics=_WGRAD_ATOMICS)
+                             accumulate=True, atomics=False)  # deterministic partials + reduce (atomics: -3 %, r4t29)
             space.sink.put_direct(i)
         elif ctx.needs_input_grad[1]:
             dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
@@ -206,9 +203,7 @@ class _GeluFn(torch.autograd.Function):
     def forward(ctx, u, blink):
         ctx.save_for_backward(u)
         ctx.blink = blink
-        if _GELU_FWD and u.dtype == torch.bfloat16 and u.is_contiguous() and u.numel() % 8 == 0:
-            return hip().gelu_forward(u)  # norms.hip: one-exponential erf (no faster than torch's erff: VALU-bound)
-        return F.gelu(u)
+        return F.gelu(u)  # norms.hip gelu_forward measured 0.6 % slower end to end (r4t20): not used
 
     @staticmethod
     def backward(ctx, dy):
@@ -220,8 +215,7 @@ class _GeluFn(torch.autograd.Function):
         return du, None
 
 
-_GELU_LINK = knobs.get("KUNGFU_GELU_BIAS_LINK") != "0"
-_GELU_FWD = knobs.get("KUNGFU_GELU_FWD") == "1"  # A/B: BERT-base 7089-7112 (on) vs 7150-7152 seq/s (off), r4t20
+_GELU_LINK = True  # module switch (tests)
 
 
 def gelu(u: torch.Tensor, bias_link: bool = False) -> torch.Tensor:

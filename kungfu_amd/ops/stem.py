@@ -18,13 +18,12 @@ from typing import Optional
 
 import torch
 
-from .. import knobs
 from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_STEM", "1") != "0"
 # One-pass fused stem backward (``_StemBlockFn``); off by default until it beats the layered
 # BN-pool backward + weight-gradient kernels (tools/bench_stem.py).
-FUSED_BACKWARD = knobs.get("KUNGFU_STEM_FUSED_BWD") == "1"
+FUSED_BACKWARD = False  # one-pass fused stem backward: measured slower (r3); kept for its test
 
 
 def set_enabled(on: bool) -> bool:

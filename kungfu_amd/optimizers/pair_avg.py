@@ -276,9 +276,7 @@ class _PairAveraging(KungFuOptimizer):
             self.store = DeviceModelStore(self.space.numel, self.space.device, fused_model_name)
             self._other = torch.empty_like(self.space.flat_param)
             if prefetch:
-                from .. import knobs
-
-                native = knobs.get("KUNGFU_PAIR_NATIVE") != "0" and hasattr(hip(), "PairPrefetcher")
+                native = hasattr(hip(), "PairPrefetcher")
                 self.prefetcher = (_NativePrefetcher if native else _Prefetcher)(self.store, self._other)
         self._consumed: Optional[torch.cuda.Event] = None
 

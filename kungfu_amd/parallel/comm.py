@@ -34,7 +34,6 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
-from .. import knobs
 from .._lib import dtype_code, hip, op_code, runtime
 
 _U8 = 0
@@ -174,8 +173,7 @@ class DeviceComm(_StreamOrdered, _DeviceStats):
         self.ctas = tuple(self.comm.ctas())  # (min, max); 0 = RCCL's default
         # Normal priority: a high-priority HIP stream measured 2x SLOWER for the
         # whole ResNet-50 step on MI355X (63 vs 32 ms, 1 GPU, profiles/README.md).
-        prio = knobs.get_int("KUNGFU_COMM_STREAM_PRIORITY")
-        self.stream = torch.cuda.Stream(device=self.device, priority=prio)
+        self.stream = torch.cuda.Stream(device=self.device)
 
     # -- collectives on an explicit stream (default: the comm stream) ---------
     def _s(self, stream) -> int:

@@ -30,7 +30,7 @@ def _source_names():
 def test_every_source_knob_is_registered():
     missing = []
     for n in sorted(_source_names()):
-        if n in knobs.KNOBS or n in knobs.MACROS or n.startswith(knobs.PREFIXES):
+        if n in knobs.KNOBS or n in knobs.MACROS or n in knobs.RETIRED or n.startswith(knobs.PREFIXES):
             continue
         if n.endswith("_") and any(k.startswith(n) for k in knobs.KNOBS):  # a prefix built at run time
             continue
@@ -39,21 +39,23 @@ def test_every_source_knob_is_registered():
 
 
 def test_unknown_and_dev_knobs_warn():
-    env = {"KUNGFU_BUCKET_MBB": "8", "KUNGFU_CONV_PRIO": "1", "KUNGFU_BUCKET_MB": "16", "PATH": "/x"}
+    env = {"KUNGFU_BUCKET_MBB": "8", "KUNGFU_CONV_TILE_RULES": "1", "KUNGFU_BUCKET_MB": "16", "PATH": "/x",
+           "KUNGFU_LINEAR_GEMM": "1"}
     msgs = knobs.check_environ(env)
     assert any("KUNGFU_BUCKET_MBB" in m and "did you mean KUNGFU_BUCKET_MB" in m for m in msgs), msgs
-    assert any("KUNGFU_CONV_PRIO" in m and "IGNORED" in m for m in msgs), msgs
+    assert any("KUNGFU_CONV_TILE_RULES" in m and "IGNORED" in m for m in msgs), msgs
+    assert any("KUNGFU_LINEAR_GEMM" in m and "retired" in m for m in msgs), msgs
     assert not any("KUNGFU_BUCKET_MB " in m or m.endswith("KUNGFU_BUCKET_MB") for m in msgs), msgs
     env["KUNGFU_DEV_KNOBS"] = "1"
-    assert not any("CONV_PRIO" in m for m in knobs.check_environ(env))
+    assert not any("TILE_RULES" in m for m in knobs.check_environ(env))
 
 
 def test_dev_knob_needs_dev_flag(monkeypatch):
-    monkeypatch.setenv("KUNGFU_WGRAD_STREAM", "1")
+    monkeypatch.setenv("KUNGFU_VGG_FUSED", "0")
     monkeypatch.delenv("KUNGFU_DEV_KNOBS", raising=False)
-    assert knobs.get("KUNGFU_WGRAD_STREAM") == "0"
+    assert knobs.get("KUNGFU_VGG_FUSED") == "1"
     monkeypatch.setenv("KUNGFU_DEV_KNOBS", "1")
-    assert knobs.get("KUNGFU_WGRAD_STREAM") == "1"
+    assert knobs.get("KUNGFU_VGG_FUSED") == "0"
     with pytest.raises(KeyError):
         knobs.get("KUNGFU_NOT_A_KNOB")
 
