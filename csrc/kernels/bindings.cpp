@@ -1553,6 +1553,67 @@ at::Tensor stem_wgrad(at::Tensor dy, at::Tensor x4, int64_t splits) {
     return dw;
 }
 
+// Small image stem (stem3.hip, Inception's Conv2d_1a): w [32, 3, KH, KW] channels_last bf16 -> packed [32, 64]
+at::Tensor stem3_pack_weight(at::Tensor w) {
+    TORCH_CHECK(w.is_cuda() && w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(0) == 32 && w.size(1) == 3 &&
+                    w.size(2) <= 4 && w.size(3) <= 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem3_pack_weight: w must be [32, 3, KH<=4, KW<=4] channels_last bf16");
+    c10::DeviceGuard gd(w.device());
+    auto wp = at::empty({32, 64}, w.options().memory_format(at::MemoryFormat::Contiguous));
+    kfk::launch_stem3_pack_weight(reinterpret_cast<const uint16_t *>(w.data_ptr()),
+                                  reinterpret_cast<uint16_t *>(wp.data_ptr()), w.size(2), w.size(3), stream_of(w, 0));
+    return wp;
+}
+
+static void check_img3(const at::Tensor &x, const char *name) {
+    TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat) && x.dim() == 4 &&
+                    x.size(1) == 3 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                name, ": x must be the [N, 3, H, W] channels_last f32 / bf16 image");
+}
+
+at::Tensor stem3_forward(at::Tensor x, at::Tensor wp, int64_t kh, int64_t kw, int64_t stride, int64_t ph, int64_t pw,
+                         c10::optional<at::Tensor> stats) {
+    check_img3(x, "stem3_forward");
+    TORCH_CHECK(wp.scalar_type() == at::kBFloat16 && wp.numel() == 32 * 64 && wp.is_contiguous() &&
+                    wp.device() == x.device(),
+                "stem3_forward: wp must be the packed [32, 64] weights");
+    const int N = x.size(0), H = x.size(2), W = x.size(3);
+    double *sp = nullptr;
+    if (stats && stats->defined()) {
+        TORCH_CHECK(stats->is_cuda() && stats->scalar_type() == at::kDouble && stats->numel() == 2 * 32 * kfk::kStatSlots &&
+                        stats->is_contiguous() && stats->device() == x.device(),
+                    "stem3_forward: stats must be a contiguous f64 [slots*2*32] tensor");
+        sp = stats->data_ptr<double>();
+    }
+    c10::DeviceGuard gd(x.device());
+    const int OH = kfk::stem3_out(H, kh, stride, ph), OW = kfk::stem3_out(W, kw, stride, pw);
+    TORCH_CHECK(OH > 0 && OW > 0, "stem3_forward: empty output");
+    auto y = at::empty({N, 32, OH, OW}, x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem3_forward(x.data_ptr(), x.scalar_type() == at::kFloat, reinterpret_cast<const uint16_t *>(wp.data_ptr()),
+                              reinterpret_cast<uint16_t *>(y.data_ptr()), sp, N, H, W, kh, kw, stride, ph, pw,
+                              stream_of(x, 0));
+    return y;
+}
+
+at::Tensor stem3_wgrad(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, int64_t stride, int64_t ph, int64_t pw,
+                       bool out_f32) {
+    check_img3(x, "stem3_wgrad");
+    const int N = x.size(0), H = x.size(2), W = x.size(3);
+    const int OH = kfk::stem3_out(H, kh, stride, ph), OW = kfk::stem3_out(W, kw, stride, pw);
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 && dy.size(0) == N && dy.size(1) == 32 &&
+                    dy.size(2) == OH && dy.size(3) == OW && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dy.device() == x.device(),
+                "stem3_wgrad: dy must be the [N, 32, OH, OW] channels_last bf16 output gradient");
+    c10::DeviceGuard gd(x.device());
+    auto part = at::empty({kfk::stem3_wgrad_workspace(N, H, W, kh, kw, stride, ph, pw)}, x.options().dtype(at::kFloat));
+    auto dw = at::empty({32, 3, kh, kw}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16)
+                                            .memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem3_wgrad(reinterpret_cast<const uint16_t *>(dy.data_ptr()), x.data_ptr(), x.scalar_type() == at::kFloat,
+                            dw.data_ptr(), out_f32, part.data_ptr<float>(), N, H, W, kh, kw, stride, ph, pw,
+                            stream_of(x, 0));
+    return dw;
+}
+
 // Returns (dx, dweight, dbias).
 std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Tensor x, at::Tensor mean,
                                          at::Tensor invstd, at::Tensor weight, at::Tensor fcoef, bool training,
@@ -1951,6 +2012,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
           py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false,
           py::arg("fin") = py::none(), py::arg("pre_coef") = py::none());
+    m.def("stem3_pack_weight", &stem3_pack_weight, "pack [32, 3, KH, KW] stem weights for stem3_forward");
+    m.def("stem3_forward", &stem3_forward, "small image-stem conv (<= 4x4 window, 3 -> 32 channels) with the BN-sums "
+          "epilogue", py::arg("x"), py::arg("wp"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("ph"),
+          py::arg("pw"), py::arg("stats") = py::none());
+    m.def("stem3_wgrad", &stem3_wgrad, "its weight gradient (MFMA over pixels, deterministic)", py::arg("dy"),
+          py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("ph"), py::arg("pw"),
+          py::arg("out_f32") = false);
     m.def("bn_fin_desc", &bn_fin_desc, "pack an in-launch BN finalize descriptor (CPU uint8; copy it to the GPU)",
           py::arg("mode"), py::arg("tensors"), py::arg("rows"), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5,
           py::arg("training") = true);

@@ -315,6 +315,18 @@ void launch_stem_pad4(const uint16_t *x, uint16_t *x4, int64_t npix, hipStream_t
 void launch_stem_pad4_f32(const float *x, uint16_t *x4, int64_t npix, hipStream_t s);  // + cast to bf16
 void launch_stem_pack_weight(const uint16_t *w, uint16_t *wp, hipStream_t s);
 int stem_out(int h);
+// Small image stem (stem3.hip): KH x KW <= 4 x 4 window, any stride / padding, 3 -> 32 channels (Inception's
+// Conv2d_1a); x = the NHWC 3-channel image (f32 or bf16), wp = stem3 packed weights [32][64]; stats: the BN's
+// f64 slots [slots][2][32].
+int stem3_out(int h, int k, int stride, int pad);
+void launch_stem3_pack_weight(const uint16_t *w, uint16_t *wp, int KH, int KW, hipStream_t s);
+void launch_stem3_forward(const void *x, bool x_f32, const uint16_t *wp, uint16_t *y, double *stats, int N, int H,
+                          int W, int KH, int KW, int stride, int ph, int pw, hipStream_t s);
+int stem3_wgrad_blocks(int N, int H, int W, int KH, int KW, int stride, int ph, int pw);
+int64_t stem3_wgrad_workspace(int N, int H, int W, int KH, int KW, int stride, int ph, int pw);  // floats
+// dw [32][KH][KW][3] (channels_last [32, 3, KH, KW]), f32 or bf16; deterministic
+void launch_stem3_wgrad(const uint16_t *dy, const void *x, bool x_f32, void *dw, bool out_f32, float *part, int N,
+                        int H, int W, int KH, int KW, int stride, int ph, int pw, hipStream_t s);
 void launch_stem_forward(const uint16_t *x4, const uint16_t *wp, uint16_t *y, double *stats, int N, int H, int W,
                          hipStream_t s);
 // dw [64][7][7][3] bf16; part: stem_wgrad_workspace(...) floats.

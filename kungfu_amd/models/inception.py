@@ -43,6 +43,18 @@ class BasicConv2d(nn.Module):
 
             c = self.conv
             w = shadow(c.weight)
+            from ..ops import stem as stem_ops
+
+            if stem_ops.stem3_eligible(c, x):
+                # the 3-channel image stem (Conv2d_1a) on stem3.hip: MFMA conv + BN-statistics epilogue
+                # straight from the f32 image (no cast pass, no MIOpen, no BN statistics pass)
+                ws = self.bn.stats_workspace(x.device)
+                y = stem_ops.stem3_conv(c, x, w, ws)
+                if defer:
+                    from ..ops.fused_bn import Deferred
+
+                    return Deferred(y, self.bn, ws)
+                return self.bn(y, sums=ws, link=link)
             if w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16:
                 ws = self.bn.stats_workspace(x.device)
                 y = conv2d_stats(x, w, c.stride, c.padding, ws, master=c.weight)

@@ -63,7 +63,7 @@ class _StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (x4,) = ctx.saved_tensors
+        (x,) = ctx.saved_tensors
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dw = hip().stem_wgrad(dy, x4) if ctx.needs_input_grad[1] else None
@@ -118,3 +118,63 @@ def stem_block(x: torch.Tensor, w: torch.Tensor, bn, sums: Optional[torch.Tensor
     ``BatchNormAct2d`` (its parameters, running statistics and ``num_batches_tracked``)."""
     (gamma, beta, rm, rv, use_batch, momentum, eps), nbt = bn._args()
     return _StemBlockFn.apply(x, w, gamma, beta, rm, rv, momentum, eps, use_batch, nbt, sums)
+
+
+# ---------------------------------------------------------------------------------------------
+# Small image stems (csrc/kernels/stem3.hip): a <= 4x4 window over the 3-channel image, 32 output
+# channels, any stride / zero padding -- Inception-v3's Conv2d_1a (3x3, stride 2, no padding).
+
+
+def stem3_eligible(conv: torch.nn.Conv2d, x: torch.Tensor) -> bool:
+    if not (_ENABLED and x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and not x.requires_grad):
+        return False
+    if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous(memory_format=torch.channels_last):
+        return False
+    if x.dtype != torch.bfloat16 and not (torch.is_autocast_enabled("cuda") and
+                                          torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    kh, kw = conv.kernel_size
+    sh, sw = conv.stride
+    ph, pw = conv.padding
+    if not (conv.in_channels == 3 and conv.out_channels == 32 and kh <= 4 and kw <= 4 and sh == sw and sh >= 1
+            and ph < kh and pw < kw and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros"):
+        return False
+    return (x.shape[2] + 2 * ph - kh) // sh + 1 >= 1 and (x.shape[3] + 2 * pw - kw) // sw + 1 >= 1 and hip_available()
+
+
+class _Stem3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, geo, stats):
+        H = hip()
+        kh, kw, s, ph, pw = geo
+        wb = w if w.dtype == torch.bfloat16 else w.to(torch.bfloat16)
+        if not wb.is_contiguous(memory_format=torch.channels_last):
+            wb = wb.contiguous(memory_format=torch.channels_last)
+        # the f32 (or bf16) image is read as it is: no cast / pad pass
+        y = H.stem3_forward(x, H.stem3_pack_weight(wb), kh, kw, s, ph, pw, stats)
+        ctx.save_for_backward(x)
+        ctx.geo = geo
+        ctx.wdtype = w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        if not ctx.needs_input_grad[1]:
+            return None, None, None, None
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        kh, kw, s, ph, pw = ctx.geo
+        dw = hip().stem3_wgrad(dy.to(torch.bfloat16), x, kh, kw, s, ph, pw, out_f32=ctx.wdtype == torch.float32)
+        if dw.dtype != ctx.wdtype:
+            dw = dw.to(ctx.wdtype)
+        return None, dw, None, None
+
+
+def stem3_conv(conv: torch.nn.Conv2d, x: torch.Tensor, w: torch.Tensor,
+               stats: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``conv(x)`` with ``w`` (the bf16 shadow of ``conv.weight`` or the weight) on stem3.hip ->
+    bf16 [N, 32, OH, OW] channels_last; ``stats``: the following BN's f64 slotted sums workspace."""
+    geo = (conv.kernel_size[0], conv.kernel_size[1], conv.stride[0], conv.padding[0], conv.padding[1])
+    return _Stem3Fn.apply(x, w, geo, stats)

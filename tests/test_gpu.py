@@ -6,6 +6,7 @@ import sys
 
 import pytest
 import torch
+import torch.nn.functional as F
 
 from conftest import ROOT, kungfu_run, worker
 
@@ -1833,3 +1834,74 @@ def test_conv_prebn_matches_bn_apply_then_conv(H, ks, c, cout, hw):
     assert torch.equal(got2, got)
     s = st.view(slots, 2, cout).sum(0)
     torch.testing.assert_close(s[0], got.double().sum(dim=(0, 2, 3)), rtol=1e-6, atol=1e-3)
+
+
+@needs_gpu
+@pytest.mark.parametrize("n,h,w,k,s,p", [(3, 37, 37, 3, 2, 0), (2, 29, 31, 3, 1, 1), (2, 33, 33, 4, 2, 1),
+                                         (4, 20, 18, 2, 1, 0), (256, 224, 224, 3, 2, 0)])
+def test_stem3_forward_and_wgrad_match_fp32(H, n, h, w, k, s, p):
+    """stem3.hip (Inception's Conv2d_1a on MFMA: <= 4x4 window, 3 -> 32 channels): forward from the f32
+    image and from bf16, the BN-statistics epilogue, and the deterministic weight gradient -- vs the
+    float32 torch convolution of the same bf16-rounded operands."""
+    torch.manual_seed(n * 7 + k)
+    x = torch.randn(n, 3, h, w, device="cuda").contiguous(memory_format=torch.channels_last)
+    wt = (torch.randn(32, 3, k, k, device="cuda") * 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
+    xb = x.bfloat16()
+    ref = F.conv2d(xb.float(), wt.float(), stride=s, padding=p)
+    wp = H.stem3_pack_weight(wt)
+    slots = H.conv_stat_slots
+    for src in (x, xb):
+        st = torch.zeros(slots * 2 * 32, dtype=torch.float64, device="cuda")
+        y = H.stem3_forward(src, wp, k, k, s, p, p, st)
+        assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+        err = (y.float() - ref).abs().max().item()
+        assert err <= 2 ** -7 * ref.abs().max().item() + 1e-3, err
+        yd = y.double()
+        sums = st.view(slots, 2, 32).sum(0)
+        # per-lane partial sums are f32 (as in conv.hip's statistics epilogue), folded in f64
+        torch.testing.assert_close(sums[0], yd.sum(dim=(0, 2, 3)), rtol=1e-5, atol=1e-2)
+        torch.testing.assert_close(sums[1], (yd * yd).sum(dim=(0, 2, 3)), rtol=1e-5, atol=1e-2)
+    dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=torch.channels_last)
+    dw = H.stem3_wgrad(dy, xb, k, k, s, p, p, out_f32=True)
+    dref = torch.nn.grad.conv2d_weight(xb.float(), wt.shape, dy.float(), stride=s, padding=p)
+    assert dw.shape == dref.shape
+    assert ((dw - dref).norm() / dref.norm()).item() < 1e-5
+    assert torch.equal(dw, H.stem3_wgrad(dy, xb, k, k, s, p, p, out_f32=True))  # no atomics: reproducible
+    assert ((H.stem3_wgrad(dy, x, k, k, s, p, p, out_f32=True) - dw).norm() / dw.norm()).item() < 1e-6  # f32 image
+    dwb = H.stem3_wgrad(dy, xb, k, k, s, p, p)
+    assert dwb.dtype == torch.bfloat16 and torch.equal(dwb, dw.bfloat16())
+
+
+@needs_gpu
+def test_inception_stem_runs_on_stem3(monkeypatch):
+    """The fused Inception-v3 takes its 3-channel Conv2d_1a through stem3.hip (not MIOpen): forward +
+    backward of a small batch calls it once and produces finite gradients for its weight."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.inception import inception_v3
+    from kungfu_amd.ops import stem as stem_ops
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+    calls = []
+    orig = stem_ops.stem3_conv
+
+    def spy(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+
+    monkeypatch.setattr(stem_ops, "stem3_conv", spy)
+    torch.manual_seed(0)
+    m = inception_v3(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.01),
+                                                named_parameters=m.named_parameters())
+    enable_bf16_shadow(m, opt)
+    x = torch.randn(4, 3, 224, 224, device="cuda").to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (4,), device="cuda")
+    opt.zero_grad()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        F.cross_entropy(m(x).float(), y).backward()
+    opt.reducer.synchronize()
+    assert calls == [1]
+    i = opt.space.names.index("stem.0.conv.weight")
+    g = opt.space.grad_view(i)
+    assert torch.isfinite(g).all() and g.abs().sum() > 0
