@@ -92,6 +92,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 template <int ROW>
 __device__ __forceinline__ int hswz(int row) {
     if constexpr (ROW >= 256) return (row & 3) | (((row >> 3) & 1) << 2);
+    else if constexpr (ROW == 64) return (row >> 3) & 1;  // 4 rows per 256-byte bank cycle: flip rows 8..15
     else return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
 }
 
@@ -572,6 +573,10 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
 //     (R + KH - 1) x (L + KW - 1) image around the segment of 64 output pixels;
 //   * tap (kh, kw) reads the image at row offset kh * XW + kw (transposing LDS reads with
 //     per-lane row addresses: the im2col shift is only an address offset).
+// CT = the channel tile (both co and ci): 64, or 32 for the channel counts that are not multiples
+// of 64 (Inception's 32 / 80 / 96 / 160 / 48: no zero-padded half tiles, 64-byte staged rows, a
+// 32 x 32 wave tile) -- CT 32 also writes its split partials in dw layout ([split][co][tap][ci],
+// exactly K * taps * C floats, no tile padding), summed by wgrad_dense_reduce_kernel.
 // Replaces MIOpen's igemm_wrw for these shapes (r2o_inception_wgrad.txt: 170-275 TF/s there).
 struct RRGeo {
     int N, H, W, C, K, OH, OW;
@@ -579,20 +584,45 @@ struct RRGeo {
     int L, R, spr, gpi, nseg;
     int XW, xrows, xpieces;
     int mtiles, ntiles, tiles, splits, kps;
+    int stage;  // LDS bytes per ring stage: dy | image | 1 KB dummy
 };
 
-template <int NWV, int STAGES>
+// s_waitcnt until at most n * (S - 2) loads of this wave are in flight (n = its loads per stage,
+// wave-uniform, 1..5): the oldest outstanding stage of an S-deep ring has landed
+template <int S>
+__device__ __forceinline__ void wait_ring(int n) {
+    if constexpr (S <= 2) {
+        wait_vmcnt<0>();
+    } else {
+        switch (n) {
+            case 1: wait_vmcnt<1 * (S - 2)>(); break;
+            case 2: wait_vmcnt<2 * (S - 2)>(); break;
+            case 3: wait_vmcnt<3 * (S - 2)>(); break;
+            case 4: wait_vmcnt<4 * (S - 2)>(); break;
+            case 5: wait_vmcnt<5 * (S - 2)>(); break;
+            default: wait_vmcnt<0>();
+        }
+    }
+}
+
+template <int NWV, int STAGES, int CT = 64, bool DENSE = (CT == 32)>
 __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_t *__restrict__ dy,
                                                                    const uint16_t *__restrict__ x,
                                                                    float *__restrict__ part, void *__restrict__ dw,
                                                                    const uint16_t *__restrict__ zero, RRGeo g,
                                                                    int out_f32, int accumulate, int atomic_out,
                                                                    int stagger = 0) {
-    constexpr int ROW = 128;                      // 64 channels
-    constexpr int MAXP = (8 + 25 + NWV - 1) / NWV;  // 1 KB pieces per wave per K-step
-    constexpr int STAGE = (8 + 25 + 1) * 1024;     // dy 8 KB | input image <= 25 KB | dummy 1 KB
-    constexpr int DUMMY = (8 + 25) * 1024;
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[STAGES * STAGE];
+    constexpr int ROW = 2 * CT;                    // staged bytes per pixel (CT channels)
+    constexpr int TI = CT / 16;                    // 16-wide MFMA blocks per tile side
+    constexpr int LPR = ROW / 16;                  // lanes (16 B each) per staged row
+    constexpr int RPP = 64 / LPR;                  // rows per 1 KB piece
+    constexpr int DYP = 64 / RPP;                  // dy pieces per K-step (64 pixels)
+    constexpr int DYB = DYP * 1024;
+    constexpr int MAXP = (DYP + 25 + NWV - 1) / NWV;  // 1 KB pieces per wave per K-step (bound)
+    static_assert(MAXP <= 5, "wait_ring covers 5 loads per stage");
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];  // STAGES x g.stage bytes
+    const int STAGE = g.stage;                   // dy | input image (<= 25 KB) | dummy 1 KB
+    const int DUMMY = g.stage - 1024;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -604,7 +634,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     const int split = wg / per_split, rem0 = wg - split * per_split;
     const int tg = rem0 / mn, ctile = rem0 - tg * mn;
     const int mt = ctile / g.ntiles, nt = ctile - mt * g.ntiles;
-    const int m0 = mt * 64, n0 = nt * 64;
+    const int m0 = mt * CT, n0 = nt * CT;
     const int tap = tg * NWV + wave;  // >= g.taps: staging-only wave
     const bool has_tap = tap < g.taps;
     const int kh = has_tap ? tap / g.KW : 0, kw = has_tap ? tap - kh * g.KW : 0;
@@ -613,16 +643,17 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     if (nsteps > g.kps) nsteps = g.kps;
 
     // ---- staging descriptors: wave issues pieces wave + NWV u; piece < 8: dy, else input image
-    const int total = 8 + g.xpieces;
+    const int total = DYP + g.xpieces;
+    const int nload = (total + NWV - 1) / NWV;  // pieces per wave per stage (a ring > 2 issues them all)
     int p_kind[MAXP], p_r[MAXP], p_c[MAXP], p_col[MAXP];  // kind 0 dy, 1 x, 2 dummy
     bool p_cok[MAXP];
 #pragma unroll
     for (int u = 0; u < MAXP; ++u) {
         const int pq = wave + NWV * u;
-        const int pc = lane & 7;
+        const int pc = lane % LPR;
         p_cok[u] = false;
-        if (pq < 8) {
-            const int t = pq * 8 + (lane >> 3);  // dy slot
+        if (pq < DYP) {
+            const int t = pq * RPP + lane / LPR;  // dy slot
             p_kind[u] = 0;
             p_r[u] = t / g.L;
             p_c[u] = t - p_r[u] * g.L;
@@ -630,7 +661,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
             p_col[u] = m0 + ((((pc >> 1) ^ hswz<ROW>(t)) << 1) | (pc & 1)) * 8;
             p_cok[u] = p_col[u] < g.K;
         } else if (pq < total) {
-            const int t = (pq - 8) * 8 + (lane >> 3);  // image row
+            const int t = (pq - DYP) * RPP + lane / LPR;  // image row
             p_kind[u] = 1;
             p_r[u] = t / g.XW;
             p_c[u] = t - p_r[u] * g.XW;
@@ -651,7 +682,14 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
         uint8_t *base = lds + buf * STAGE;
 #pragma unroll
         for (int u = 0; u < MAXP; ++u) {
+            if (u >= nload) break;
             const int pq = wave + NWV * u;
+            if constexpr (STAGES == 2) {
+                // every K-step waits for all of its loads (vmcnt 0), so no dummy issue keeps the
+                // count; lanes of channels past Cout / Cin leave their LDS bytes stale (they only
+                // reach outputs that are dropped)
+                if (p_kind[u] == 2 || !p_cok[u]) continue;
+            }
             const uint16_t *src = zero;
             uint8_t *dst = base + DUMMY;
             if (p_kind[u] == 0) {
@@ -673,10 +711,10 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     // ---- fragment addresses.  lane = 16 fg + 4 fq + fp; K-slots j = 8 fg + fq + {0, 4, 32, 36}.
     const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
     const int rowa0 = 8 * fg + fq;
-    int aoff[4];
+    int aoff[TI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) aoff[i] = rowa0 * ROW + 32 * (i ^ hswz<ROW>(rowa0)) + 8 * fp;
-    int boff[4][4];  // [sub-read][ci block]
+    for (int i = 0; i < TI; ++i) aoff[i] = rowa0 * ROW + 32 * (i ^ hswz<ROW>(rowa0)) + 8 * fp;
+    int boff[4][TI];  // [sub-read][ci block]
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int j = rowa0 + (s & 1) * 4 + (s >> 1) * 32;
@@ -685,19 +723,19 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
         const int trow = jrow + kh * g.XW + kw;
         const int h = hswz<ROW>(trow);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) boff[s][i] = 8192 + trow * ROW + 32 * (i ^ h) + 8 * fp;
+        for (int i = 0; i < TI; ++i) boff[s][i] = DYB + trow * ROW + 32 * (i ^ h) + 8 * fp;
     }
 
-    f32x4 acc[4][4];
+    f32x4 acc[TI][TI];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mfma_block = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[4]) {
+        for (int j = 0; j < TI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma_block = [&](const bf16x8 (&af)[TI], const bf16x8 (&bfr)[TI]) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TI; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     };
 
@@ -707,7 +745,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     int buf = 0;
     const bool early = stagger && ((wave >> 2) & 1);  // see wgrad_kernel: staggered staging issue
     for (int ks = 0; ks < nsteps; ++ks) {
-        if (ks + STAGES - 1 <= nsteps) wait_vmcnt<MAXP * (STAGES - 2)>();
+        if (ks + STAGES - 1 <= nsteps) wait_ring<STAGES>(nload);
         else wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -720,14 +758,14 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
         __builtin_amdgcn_sched_barrier(0);
         const uint8_t *base = lds + buf * STAGE;
         if (has_tap) {  // wave-uniform
-            bf16x8 af0[4], bf0[4], af1[4], bf1[4];
+            bf16x8 af0[TI], bf0[TI], af1[TI], bf1[TI];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < TI; ++i) {
                 af0[i] = tr_frag(base + aoff[i], base + aoff[i] + 4 * ROW);
                 bf0[i] = tr_frag(base + boff[0][i], base + boff[1][i]);
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < TI; ++i) {
                 af1[i] = tr_frag(base + aoff[i] + 32 * ROW, base + aoff[i] + 36 * ROW);
                 bf1[i] = tr_frag(base + boff[2][i], base + boff[3][i]);
             }
@@ -747,11 +785,27 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     if (!has_tap) return;
 
     // ---- epilogue (wgrad_kernel's three forms; tile = this wave's tap)
+    if constexpr (DENSE) {
+        if (!atomic_out && g.splits > 1) {  // dw-layout partial of this split: plain f32 stores
+            float *dst = part + static_cast<int64_t>(split) * g.K * g.taps * g.C;
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+                for (int j = 0; j < TI; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int co = m0 + i * 16 + (lane >> 4) * 4 + r;
+                        const int ci = n0 + j * 16 + (lane & 15);
+                        if (co < g.K && ci < g.C) dst[(static_cast<int64_t>(co) * g.taps + tap) * g.C + ci] = acc[i][j][r];
+                    }
+            return;
+        }
+    }
     if (atomic_out || g.splits == 1) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < TI; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int co = m0 + i * 16 + (lane >> 4) * 4 + r;
@@ -770,13 +824,57 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
                         *o = f32_to_bf16(v);
                     }
                 }
-    } else {
+    } else if constexpr (!DENSE) {
         const int tile = tap * mn + mt * g.ntiles + nt;
         f32x4 *dst = reinterpret_cast<f32x4 *>(part + (static_cast<int64_t>(split) * g.tiles + tile) * 4096) + lane;
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * 64);
+    }
+}
+
+// dw[e] (+)= the sum over the splits of part[split][e] (deterministic: a fixed order for a given
+// shape); e over the n = K * taps * C outputs in dw layout, as float4 columns (n % 4 == 0: C % 8).
+// Block = 256 threads = (256 >> sgl) columns x (1 << sgl) split groups: group g sums splits g, g + G,
+// ... in order, then the G group sums meet in LDS in group order -- a few thousand columns over
+// hundreds of splits (Conv2d_2a: 2,304 x 768) still keep every CU's loads in flight.
+__global__ __launch_bounds__(256) void wgrad_dense_reduce_kernel(const float *__restrict__ part, int splits, int64_t n,
+                                                                 void *__restrict__ dw, int out_f32, int accumulate,
+                                                                 int sgl) {
+    __shared__ f32x4 red[256];
+    const int G = 1 << sgl, COLS = 256 >> sgl;
+    const int t = threadIdx.x, c = t & (COLS - 1), grp = t >> (8 - sgl);
+    const int64_t n4 = n / 4, col = static_cast<int64_t>(blockIdx.x) * COLS + c;
+    f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (col < n4) {
+        const f32x4 *src = reinterpret_cast<const f32x4 *>(part) + col;
+        int sp = grp;
+        for (; sp + G < splits; sp += 2 * G) {
+            const f32x4 u = __builtin_nontemporal_load(src + sp * n4), v = __builtin_nontemporal_load(src + (sp + G) * n4);
+            a += u;
+            a += v;
+        }
+        if (sp < splits) a += __builtin_nontemporal_load(src + sp * n4);
+    }
+    red[t] = a;
+    __syncthreads();
+    if (grp != 0 || col >= n4) return;
+    f32x4 sum = red[c];
+    for (int k = 1; k < G; ++k) sum += red[k * COLS + c];
+    const int64_t e = col * 4;
+    if (out_f32) {
+        f32x4 *o = reinterpret_cast<f32x4 *>(static_cast<float *>(dw) + e);
+        if (accumulate) sum += *o;
+        *o = sum;
+    } else {
+        uint16_t *o = static_cast<uint16_t *>(dw) + e;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float v = sum[k];
+            if (accumulate) v += bf16_to_f32(o[k]);
+            o[k] = f32_to_bf16(v);
+        }
     }
 }
 
@@ -854,6 +952,14 @@ struct Tile {
 constexpr Tile kTiles[] = {{2, 2, 4}, {2, 1, 4}, {1, 2, 4}, {1, 1, 4}, {4, 2, 4}, {2, 4, 4}, {0, 0, 0}, {4, 2, 8}};
 constexpr int kNumVariants = 8;
 constexpr int kRowsVariant = 6;
+// conv_wgrad_rect only: the row-image kernel with segments chosen for the fewest staged rows, an
+// LDS ring sized to the segment, dw-layout partials: 8 / 9 / 10 = 32-channel tiles with a 2 / 3 /
+// 4-stage ring, 11 / 12 = 64-channel tiles with a 3 / 4-stage ring
+constexpr int kRowsExFirst = 8, kRowsExLast = 12;
+struct RowsEx {
+    int ct, stages;
+};
+constexpr RowsEx kRowsEx[] = {{32, 2}, {32, 3}, {32, 4}, {64, 3}, {64, 4}};
 
 bool rows_supported(int Cin, int Cout, int ks, int stride) {
     return ks == 3 && stride == 1 && Cin % 64 == 0 && Cout % 64 == 0;
@@ -1110,23 +1216,43 @@ WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int p
 
 namespace {
 // the row-image kernel's segments / tap groups for a stride-1 KH x KW window (xpieces > 25: unsupported)
-RRGeo rows_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw) {
+RRGeo rows_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int ct = 64,
+                    bool legacy = true) {
     RRGeo g{};
     g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
     g.OH = H + 2 * ph - kh + 1, g.OW = W + 2 * pw - kw + 1;
     g.KH = kh, g.KW = kw, g.ph = ph, g.pw = pw, g.taps = kh * kw;
     const int nwv = g.taps % 7 == 0 ? 7 : 9;
     g.tgroups = (g.taps + nwv - 1) / nwv;
-    if (g.OW >= 64) {
-        g.L = 64, g.R = 1, g.spr = (g.OW + 63) / 64, g.gpi = g.OH;
+    auto shape = [&](int L, int R) {
+        g.L = L, g.R = R, g.spr = (g.OW + L - 1) / L, g.gpi = (g.OH + R - 1) / R;
+        g.nseg = N * g.gpi * g.spr;
+        g.XW = g.L + kw - 1;
+        g.xrows = (g.R + kh - 1) * g.XW;
+    };
+    if (legacy) {
+        if (g.OW >= 64) shape(64, 1);
+        else shape(g.OW, 64 / g.OW);
     } else {
-        g.L = g.OW, g.R = 64 / g.OW, g.spr = 1, g.gpi = (g.OH + g.R - 1) / g.R;
+        // 64-byte rows: the R x L segment of 64 slots with the fewest staged rows (dy + image) in
+        // total -- R > 1 on the wide maps too (Conv2d_2a's 109-wide rows: 16 x 4 stages 1.7 input
+        // rows per output pixel where 64 x 1 stages 3.1)
+        int64_t best = -1;
+        int bl = 64, br = 1;
+        for (int R = 1; R <= 64; ++R) {
+            const int L = std::min(g.OW, 64 / R);
+            if (L < 1 || (R > 1 && (R - 1) * L >= 64)) break;
+            if (R > g.OH + 1) break;
+            shape(L, R);
+            if (g.xrows * 2 * ct > 25 * 1024) continue;
+            const int64_t cost = static_cast<int64_t>(g.nseg) * (64 + g.xrows);
+            if (best < 0 || cost < best) best = cost, bl = L, br = R;
+        }
+        shape(bl, br);
     }
-    g.nseg = N * g.gpi * g.spr;
-    g.XW = g.L + kw - 1;
-    g.xrows = (g.R + kh - 1) * g.XW;
-    g.xpieces = (g.xrows + 7) / 8;
-    g.mtiles = (Cout + 63) / 64, g.ntiles = (Cin + 63) / 64;
+    g.xpieces = (g.xrows * 2 * ct + 1023) / 1024;
+    g.mtiles = (Cout + ct - 1) / ct, g.ntiles = (Cin + ct - 1) / ct;
+    g.stage = 64 * 2 * ct + (legacy ? 26 : g.xpieces + 1) * 1024;
     g.tiles = g.mtiles * g.ntiles * g.taps;
     return g;
 }
@@ -1139,9 +1265,42 @@ bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int 
     return rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw).xpieces <= 25;
 }
 
+// Row-image variant per shape, from the Inception-v3 sweep (profiles/r5_inception_wgrad.md): 32-channel
+// tiles (8) when both channel counts fit one; the 64-tile kernel as before (6) when both are
+// multiples of 64; otherwise 64-channel tiles on the fewest-rows segments with a 4-stage ring (12) on
+// the small maps (<= 32 x 32: few segments per workgroup, the ring's depth pays) when it fits in
+// 96 KB, else a 3-stage ring (11: two workgroups per CU on the 54 x 54 / 109 x 109 maps)
+int conv_wgrad_rows_rect_auto(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw) {
+    if (Cin <= 32 && Cout <= 32) return 8;
+    if (Cin % 64 == 0 && Cout % 64 == 0) return kRowsVariant;
+    const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, 64, false);
+    return (H * W <= 1024 && 4 * rg.stage <= 96 * 1024) ? 12 : 11;
+}
+
 WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride,
                                int variant) {
     WgradPlan pl;
+    if (variant == 13) {
+        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+            throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
+        variant = conv_wgrad_rows_rect_auto(N, H, W, Cin, Cout, kh, kw, ph, pw);
+    }
+    if (variant >= kRowsExFirst && variant <= kRowsExLast) {
+        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+            throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
+        const RowsEx vx = kRowsEx[variant - kRowsExFirst];
+        const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false);
+        pl.variant = variant;
+        const int ct = rg.mtiles * rg.ntiles * rg.tgroups;
+        // as many workgroups as fit at once: LDS ring per CU, <= 3 of 7-9 waves
+        const int occ = std::max(1, std::min(3, 160 * 1024 / (vx.stages * rg.stage)));
+        int splits = std::max(1, (256 * occ + ct / 2) / ct);
+        splits = std::max(1, std::min(splits, std::max(1, rg.nseg / 4)));
+        pl.kps = (rg.nseg + splits - 1) / splits;
+        pl.splits = (rg.nseg + pl.kps - 1) / pl.kps;
+        pl.ws_floats = pl.splits > 1 ? static_cast<int64_t>(pl.splits) * Cout * rg.taps * Cin : 0;
+        return pl;
+    }
     if (variant == kRowsVariant) {
         if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
@@ -1176,6 +1335,45 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
                             bool out_f32, bool accumulate, hipStream_t s) {
     if (!conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) throw std::invalid_argument("conv_wgrad_rect: unsupported");
     const bool atomic_out = out_f32 && accumulate && plan.splits > 1;
+    if (plan.variant >= kRowsExFirst && plan.variant <= kRowsExLast) {
+        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+            throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
+        const RowsEx vx = kRowsEx[plan.variant - kRowsExFirst];
+        RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false);
+        rg.splits = plan.splits, rg.kps = plan.kps;
+        if (rg.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad_rect: needs the workspace");
+        const int grid = rg.mtiles * rg.ntiles * rg.tgroups * rg.splits;
+        const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
+        const int lds = vx.stages * rg.stage;
+        const bool t7 = rg.taps % 7 == 0;
+        static bool attr_set[kRowsExLast - kRowsExFirst + 1][2] = {};  // per instantiation, once
+        auto go = [&](auto kern, int nwv) {
+            bool &done = attr_set[plan.variant - kRowsExFirst][t7 ? 1 : 0];
+            if (!done) {
+                (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          160 * 1024);
+                done = true;
+            }
+            kern<<<grid, 64 * nwv, lds, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out, rows_stagger(true));
+        };
+        switch (plan.variant) {
+            case 8: t7 ? go(wgrad_rows_rect_kernel<7, 2, 32, true>, 7) : go(wgrad_rows_rect_kernel<9, 2, 32, true>, 9); break;
+            case 9: t7 ? go(wgrad_rows_rect_kernel<7, 3, 32, true>, 7) : go(wgrad_rows_rect_kernel<9, 3, 32, true>, 9); break;
+            case 10: t7 ? go(wgrad_rows_rect_kernel<7, 4, 32, true>, 7) : go(wgrad_rows_rect_kernel<9, 4, 32, true>, 9); break;
+            case 11: t7 ? go(wgrad_rows_rect_kernel<7, 3, 64, true>, 7) : go(wgrad_rows_rect_kernel<9, 3, 64, true>, 9); break;
+            default: t7 ? go(wgrad_rows_rect_kernel<7, 4, 64, true>, 7) : go(wgrad_rows_rect_kernel<9, 4, 64, true>, 9); break;
+        }
+        if (rg.splits > 1 && !atomic_out) {
+            const int64_t n = static_cast<int64_t>(Cout) * rg.taps * Cin;
+            // split groups: up to 64, ~8 splits each, while >= 1,024 blocks of columns... or fewer
+            int sgl = 0;
+            while (sgl < 6 && (8 << sgl) < rg.splits && (n / 4) * (2 << sgl) <= int64_t(1024) * 256) ++sgl;
+            const int cols = 256 >> sgl;
+            wgrad_dense_reduce_kernel<<<static_cast<int>((n / 4 + cols - 1) / cols), 256, 0, s>>>(
+                part, rg.splits, n, dw, out_f32, accumulate, sgl);
+        }
+        return;
+    }
     if (plan.variant == kRowsVariant) {
         if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
@@ -1184,12 +1382,20 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
         if (rg.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad_rect: needs the workspace");
         const int grid = rg.mtiles * rg.ntiles * rg.tgroups * rg.splits;
         const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
+        static const bool attr = [] {
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(wgrad_rows_rect_kernel<7, 2>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(wgrad_rows_rect_kernel<9, 2>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            return true;
+        }();
+        (void)attr;
         if (rg.taps % 7 == 0)
-            wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
-                                                               rows_stagger(true));
+            wgrad_rows_rect_kernel<7, 2><<<grid, 64 * 7, 2 * rg.stage, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate,
+                                                                          atomic_out, rows_stagger(true));
         else
-            wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 0, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate, atomic_out,
-                                                               rows_stagger(true));
+            wgrad_rows_rect_kernel<9, 2><<<grid, 64 * 9, 2 * rg.stage, s>>>(dy, x, part, dw, z, rg, out_f32, accumulate,
+                                                                          atomic_out, rows_stagger(true));
         if (rg.splits > 1 && !atomic_out) {
             WGeo g{};
             g.C = Cin, g.K = Cout, g.mtiles = rg.mtiles, g.ntiles = rg.ntiles, g.taps = rg.taps, g.tiles = rg.tiles;

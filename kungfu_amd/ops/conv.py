@@ -242,12 +242,13 @@ def _rect_wgrad(dy, x, w, s, ph, pw):
     # measured per Inception-v3 shape (tools/bench_inception_wgrad.py, profiles/r3q_inception_wgrad.txt):
     # the split-K kernel wins every 1x1 (2-3x) and the multi-tap windows over >= 256 input
     # channels; the narrow stride-1 multi-tap ones (32..192 inputs) take the row-image kernel
-    # (all taps of a workgroup share one staged input image: 54x54 80->192 3x3 992 -> 478 us,
-    # 12x12 160->160 1x7 79 -> 56 us vs MIOpen); stride-2 narrow ones stay on MIOpen
+    # (all taps of a workgroup share one staged input image: 54x54 80->192 3x3 992 -> 405 us,
+    # 111x111 32->32 3x3 438 -> 167 us on 32-channel tiles, 12x12 160->160 1x7 79 -> 55 us vs
+    # MIOpen, profiles/r5_inception_wgrad.md); stride-2 narrow ones stay on MIOpen
     if (_WGRAD and _WGRAD_RECT and s == 1 and kh * kw > 1 and cin <= 192
             and hip().conv_wgrad_rows_rect_supported(int(x.shape[0]), int(x.shape[2]), int(x.shape[3]), cin, cout,
                                                      kh, kw, ph, pw, 1)):
-        return hip().conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, 6)
+        return hip().conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, 13)  # 13: the per-shape row-image variant
     wide = kh * kw == 1 or cin % 128 == 0 or cin >= 256
     if (_WGRAD and _WGRAD_RECT and wide and min(cin, cout) >= 32 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
             and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):

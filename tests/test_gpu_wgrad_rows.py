@@ -1,6 +1,8 @@
 """Row-image weight gradient for stride-1 KH x KW windows and channel counts % 8
-(csrc/kernels/conv_wgrad.hip wgrad_rows_rect_kernel, ``conv_wgrad_rect(..., variant=6)``)
-against an fp32 PyTorch reference of the same weight gradient."""
+(csrc/kernels/conv_wgrad.hip wgrad_rows_rect_kernel, ``conv_wgrad_rect(..., variant=6)`` on 64-channel
+tiles; ``variant=8..12``: segments sized for the fewest staged rows, a 2-4 stage LDS ring, 32- or
+64-channel tiles, dw-layout split partials) against an fp32 PyTorch reference of the same weight
+gradient."""
 import pytest
 import torch
 
@@ -23,11 +25,13 @@ CASES = [
     (2, 71, 71, 32, 32, 3, 3, 0, 0),
     (5, 9, 9, 24, 40, 3, 3, 1, 1),       # channel counts below one tile
     (16, 25, 25, 48, 64, 5, 5, 2, 2),    # many segments: split-K + reduce
+    (2, 111, 111, 32, 32, 3, 3, 0, 0),   # Conv2d_2a's 109-wide rows: 32-tile segments of R > 1 rows
 ]
 
 
+@pytest.mark.parametrize("variant", [6, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("N,H,W,cin,cout,kh,kw,ph,pw", CASES)
-def test_wgrad_rows_rect_matches_fp32(N, H, W, cin, cout, kh, kw, ph, pw):
+def test_wgrad_rows_rect_matches_fp32(N, H, W, cin, cout, kh, kw, ph, pw, variant):
     from kungfu_amd._lib import hip
 
     Hh = hip()
@@ -36,7 +40,8 @@ def test_wgrad_rows_rect_matches_fp32(N, H, W, cin, cout, kh, kw, ph, pw):
     x = _cl(torch.randn(N, cin, H, W, device="cuda").bfloat16())
     oh, ow = H + 2 * ph - kh + 1, W + 2 * pw - kw + 1
     dy = _cl(torch.randn(N, cout, oh, ow, device="cuda").bfloat16())
-    dw = Hh.conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, 6)
+    dw = Hh.conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, variant)
+    assert torch.equal(dw, Hh.conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, variant))  # no atomics: reproducible
     ref = torch.nn.grad.conv2d_weight(x.float(), (cout, cin, kh, kw), dy.float(), 1, (ph, pw))
     assert dw.shape == ref.shape
     rel = ((dw.float() - ref).norm() / ref.norm()).item()

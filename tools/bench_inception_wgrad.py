@@ -76,6 +76,12 @@ def main():
             t = timeit(f)
             best = min(best, t)
             row += "  rows %7.1f%s" % (t, "" if err < 2e-2 else " ERR%.3f" % err)
+            for v in (8, 9, 10, 11, 12):  # the segment-sized ring variants (conv_wgrad.hip kRowsEx)
+                f = lambda: H.conv_wgrad_rect(dy, x, kh, kw, s, pad[0], pad[1], v)  # noqa: E731
+                err = ((f().float() - ref).abs().max() / ref.abs().max()).item()
+                t = timeit(f)
+                best = min(best, t)
+                row += "  v%d %6.1f%s" % (v, t, "" if err < 2e-2 else " ERR%.3f" % err)
         if kh == kw and pad[0] == pad[1] == (kh - 1) // 2 and H.conv_wgrad_supported(cin, cout, kh, s):
             f = lambda: H.conv_wgrad(dy, x, kh, s)  # noqa: E731
             t = timeit(f)
