@@ -2049,7 +2049,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("variant") = -1);
     m.def("conv_wgrad_rect_supported", &kfk::conv_wgrad_rect_supported);
     m.def("conv_wgrad_rows_rect_auto", &kfk::conv_wgrad_rows_rect_auto, "the row-image weight-gradient variant "
-          "conv_wgrad_rect(..., 13) picks for this stride-1 shape (args: N, H, W, Cin, Cout, kh, kw, ph, pw)");
+          "conv_wgrad_rect(..., 13) picks for this shape (args: N, H, W, Cin, Cout, kh, kw, ph, pw, stride)");
     m.def("conv_wgrad_rows_rect_supported", &kfk::conv_wgrad_rows_rect_supported, "row-image weight-gradient kernel "
           "covers this stride-1 window (args: N, H, W, Cin, Cout, kh, kw, ph, pw, stride)");
     m.def("conv_wgrad", &conv_wgrad, "weight gradient of the 1x1/3x3 NHWC bf16 convolution (split-K MFMA GEMM)",

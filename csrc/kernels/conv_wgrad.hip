@@ -585,6 +585,7 @@ struct RRGeo {
     int XW, xrows, xpieces;
     int mtiles, ntiles, tiles, splits, kps;
     int stage;  // LDS bytes per ring stage: dy | image | 1 KB dummy
+    int S;      // stride (1, or 2 on the kRowsEx variants)
 };
 
 // s_waitcnt until at most n * (S - 2) loads of this wave are in flight (n = its loads per stage,
@@ -698,7 +699,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
                     src = dy + static_cast<uint32_t>(((n * g.OH + oh) * g.OW + ow) * g.K + p_col[u]);
                 dst = base + pq * 1024;
             } else if (p_kind[u] == 1) {
-                const int ih = oh0 + p_r[u] - g.ph, iw = ow0 + p_c[u] - g.pw;
+                const int ih = oh0 * g.S + p_r[u] - g.ph, iw = ow0 * g.S + p_c[u] - g.pw;
                 if (static_cast<unsigned>(ih) < static_cast<unsigned>(g.H) &&
                     static_cast<unsigned>(iw) < static_cast<unsigned>(g.W) && p_cok[u])
                     src = x + static_cast<uint32_t>(((n * g.H + ih) * g.W + iw) * g.C + p_col[u]);
@@ -719,7 +720,9 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
     for (int s = 0; s < 4; ++s) {
         const int j = rowa0 + (s & 1) * 4 + (s >> 1) * 32;
         const int r = j / g.L, c = j - r * g.L;
-        const int jrow = r < g.R ? r * g.XW + c : 0;  // slots past the segment read a staged row (dy is 0)
+        // output (r, c) of the segment sits at image row S r, column S c; slots past it read a staged
+        // row (their dy is 0)
+        const int jrow = r < g.R ? r * g.S * g.XW + g.S * c : 0;
         const int trow = jrow + kh * g.XW + kw;
         const int h = hswz<ROW>(trow);
 #pragma unroll
@@ -1217,18 +1220,18 @@ WGeo make_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int p
 namespace {
 // the row-image kernel's segments / tap groups for a stride-1 KH x KW window (xpieces > 25: unsupported)
 RRGeo rows_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int ct = 64,
-                    bool legacy = true) {
+                    bool legacy = true, int stride = 1) {
     RRGeo g{};
-    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout;
-    g.OH = H + 2 * ph - kh + 1, g.OW = W + 2 * pw - kw + 1;
+    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.S = stride;
+    g.OH = (H + 2 * ph - kh) / stride + 1, g.OW = (W + 2 * pw - kw) / stride + 1;
     g.KH = kh, g.KW = kw, g.ph = ph, g.pw = pw, g.taps = kh * kw;
     const int nwv = g.taps % 7 == 0 ? 7 : 9;
     g.tgroups = (g.taps + nwv - 1) / nwv;
     auto shape = [&](int L, int R) {
         g.L = L, g.R = R, g.spr = (g.OW + L - 1) / L, g.gpi = (g.OH + R - 1) / R;
         g.nseg = N * g.gpi * g.spr;
-        g.XW = g.L + kw - 1;
-        g.xrows = (g.R + kh - 1) * g.XW;
+        g.XW = stride * (g.L - 1) + kw;
+        g.xrows = (stride * (g.R - 1) + kh) * g.XW;
     };
     if (legacy) {
         if (g.OW >= 64) shape(64, 1);
@@ -1260,9 +1263,11 @@ RRGeo rows_rect_geo(int N, int H, int W, int Cin, int Cout, int kh, int kw, int 
 
 bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw,
                                     int stride) {
-    if (stride != 1 || kh * kw < 2 || !conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) return false;
-    if (H + 2 * ph - kh + 1 <= 0 || W + 2 * pw - kw + 1 <= 0) return false;
-    return rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw).xpieces <= 25;
+    if ((stride != 1 && stride != 2) || kh * kw < 2 || !conv_wgrad_rect_supported(Cin, Cout, kh, kw, stride)) return false;
+    if (H + 2 * ph - kh < 0 || W + 2 * pw - kw < 0) return false;
+    if (stride == 1) return rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw).xpieces <= 25;
+    // stride 2: the kRowsEx variants only (64-channel tiles bound the staged image)
+    return rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, 64, false, 2).xpieces <= 25;
 }
 
 // Row-image variant per shape, from the Inception-v3 sweep (profiles/r5_inception_wgrad.md): 32-channel
@@ -1270,10 +1275,16 @@ bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int 
 // multiples of 64; otherwise 64-channel tiles on the fewest-rows segments with a 4-stage ring (12) on
 // the small maps (<= 32 x 32: few segments per workgroup, the ring's depth pays) when it fits in
 // 96 KB, else a 3-stage ring (11: two workgroups per CU on the 54 x 54 / 109 x 109 maps)
-int conv_wgrad_rows_rect_auto(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw) {
+int conv_wgrad_rows_rect_auto(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride) {
     if (Cin <= 32 && Cout <= 32) return 8;
-    if (Cin % 64 == 0 && Cout % 64 == 0) return kRowsVariant;
-    const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, 64, false);
+    if (stride == 2) {
+        // r5 stride-2 sweep: 25x25 96->96 34 us on 10 (MIOpen 50), 288->384 241 on 8 (tap-tiled 266,
+        // MIOpen 324), 12x12 192->192 / 192->320 33 / 41 on 12 (MIOpen 29 / 41)
+        if (Cin % 64 != 0 || Cout % 64 != 0) return (H * W <= 1024 && Cout <= 128) ? 10 : 8;
+        return 12;
+    }
+    if (stride == 1 && Cin % 64 == 0 && Cout % 64 == 0) return kRowsVariant;
+    const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, 64, false, stride);
     return (H * W <= 1024 && 4 * rg.stage <= 96 * 1024) ? 12 : 11;
 }
 
@@ -1283,13 +1294,14 @@ WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, i
     if (variant == 13) {
         if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
-        variant = conv_wgrad_rows_rect_auto(N, H, W, Cin, Cout, kh, kw, ph, pw);
+        variant = conv_wgrad_rows_rect_auto(N, H, W, Cin, Cout, kh, kw, ph, pw, stride);
     }
     if (variant >= kRowsExFirst && variant <= kRowsExLast) {
         if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
         const RowsEx vx = kRowsEx[variant - kRowsExFirst];
-        const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false);
+        const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false, stride);
+        if (rg.xpieces > 25) throw std::invalid_argument("conv_wgrad_rect: image segment too large for this variant");
         pl.variant = variant;
         const int ct = rg.mtiles * rg.ntiles * rg.tgroups;
         // as many workgroups as fit at once: LDS ring per CU, <= 3 of 7-9 waves
@@ -1302,7 +1314,7 @@ WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, i
         return pl;
     }
     if (variant == kRowsVariant) {
-        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+        if (stride != 1 || !conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
         const RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw);
         pl.variant = variant;
@@ -1339,7 +1351,7 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
         if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
         const RowsEx vx = kRowsEx[plan.variant - kRowsExFirst];
-        RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false);
+        RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw, vx.ct, false, stride);
         rg.splits = plan.splits, rg.kps = plan.kps;
         if (rg.splits > 1 && !atomic_out && part == nullptr) throw std::invalid_argument("conv_wgrad_rect: needs the workspace");
         const int grid = rg.mtiles * rg.ntiles * rg.tgroups * rg.splits;
@@ -1375,7 +1387,7 @@ void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, flo
         return;
     }
     if (plan.variant == kRowsVariant) {
-        if (!conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
+        if (stride != 1 || !conv_wgrad_rows_rect_supported(N, H, W, Cin, Cout, kh, kw, ph, pw, stride))
             throw std::invalid_argument("conv_wgrad_rect: row-image variant unsupported for this shape");
         RRGeo rg = rows_rect_geo(N, H, W, Cin, Cout, kh, kw, ph, pw);
         rg.splits = plan.splits, rg.kps = plan.kps;

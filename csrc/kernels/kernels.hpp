@@ -303,7 +303,7 @@ WgradPlan conv_wgrad_rect_plan(int N, int H, int W, int Cin, int Cout, int kh, i
                                int variant = -1);
 // the row-image variant for a stride-1 multi-tap shape (6, or 8 / 11 / 12: see conv_wgrad.hip kRowsEx);
 // conv_wgrad_rect(..., variant = 13) runs it
-int conv_wgrad_rows_rect_auto(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw);
+int conv_wgrad_rows_rect_auto(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw, int stride);
 bool conv_wgrad_rows_rect_supported(int N, int H, int W, int Cin, int Cout, int kh, int kw, int ph, int pw,
                                     int stride);
 void launch_conv_wgrad_rect(const uint16_t *dy, const uint16_t *x, void *dw, float *part, int N, int H, int W,

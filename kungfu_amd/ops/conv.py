@@ -244,11 +244,17 @@ def _rect_wgrad(dy, x, w, s, ph, pw):
     # channels; the narrow stride-1 multi-tap ones (32..192 inputs) take the row-image kernel
     # (all taps of a workgroup share one staged input image: 54x54 80->192 3x3 992 -> 405 us,
     # 111x111 32->32 3x3 438 -> 167 us on 32-channel tiles, 12x12 160->160 1x7 79 -> 55 us vs
-    # MIOpen, profiles/r5_inception_wgrad.md); stride-2 narrow ones stay on MIOpen
+    # MIOpen, profiles/r5_inception_wgrad.md)
     if (_WGRAD and _WGRAD_RECT and s == 1 and kh * kw > 1 and cin <= 192
             and hip().conv_wgrad_rows_rect_supported(int(x.shape[0]), int(x.shape[2]), int(x.shape[3]), cin, cout,
                                                      kh, kw, ph, pw, 1)):
         return hip().conv_wgrad_rect(dy, x, kh, kw, 1, ph, pw, 13)  # 13: the per-shape row-image variant
+    if (_WGRAD and _WGRAD_RECT and s == 2 and kh * kw > 1
+            and hip().conv_wgrad_rows_rect_supported(int(x.shape[0]), int(x.shape[2]), int(x.shape[3]), cin, cout,
+                                                     kh, kw, ph, pw, 2)):
+        # the stride-2 windows (Mixed_6a / 7a reductions) on the row-image ring variants: 96->96 on
+        # 25x25 34 vs MIOpen 50 us, 288->384 241 vs 266 tap-tiled (profiles/r5_inception_wgrad.md)
+        return hip().conv_wgrad_rect(dy, x, kh, kw, 2, ph, pw, 13)
     wide = kh * kw == 1 or cin % 128 == 0 or cin >= 256
     if (_WGRAD and _WGRAD_RECT and wide and min(cin, cout) >= 32 and hip().conv_wgrad_rect_supported(cin, cout, kh, kw, s)
             and int(dy.shape[0]) * int(dy.shape[2]) * int(dy.shape[3]) < (1 << 23)):

@@ -9,4 +9,4 @@ rc=$?; grep -E "FAILED|ERROR|Error" $O/r5t14_pytest.log | head -20; tail -1 $O/r
 j() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["config"]["hip_graph"], d["config"]["final_loss"])'; }
 timeout -k 10 300 python bench.py --model inception_v3 --steps 30 --warmup 6 > $O/r5t14_inc.log 2>&1 || { tail -5 $O/r5t14_inc.log; exit 1; }
 echo "inception: $(tail -1 $O/r5t14_inc.log | j)"
-bash tools/gpu_prof.sh r5t14 inception_v3 > $O/r5t14_prof.log 2>&1 && head -24 $O/r5t14_inception_v3_summary.md
+bash tools/gpu_prof.sh r5t14 inception_v3 > $O/r5t14_prof.log 2>&1 && head -24 $O/r5t14_inception_v3_summary.md && { grep -c "igemm\|MIOpen\|miopen" $O/r5t14_inception_v3_shapes.md || true; }
