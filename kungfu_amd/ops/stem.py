@@ -63,7 +63,7 @@ class _StemFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
+        (x4,) = ctx.saved_tensors
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dw = hip().stem_wgrad(dy, x4) if ctx.needs_input_grad[1] else None
