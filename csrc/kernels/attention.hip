@@ -7,8 +7,8 @@
 // workgroup per (sequence, head) keeps Q, K, V (and dO) in LDS, computes every product on the
 // MFMA cores (v_mfma_f32_16x16x32_bf16) and touches HBM once per operand:
 //
-//   forward   S = Q K^T (wave w: query rows 32w..32w+31), row softmax in registers (16-lane
-//             butterflies), dropout mask from a counter hash of (seed, sequence*heads + head,
+//   forward   S^T = K Q^T (wave w: query rows 32w..32w+31; each lane holds 4 consecutive keys of
+//             a query), row softmax in registers (2 cross-group shuffles), dropout mask from a counter hash of (seed, sequence*heads + head,
 //             query, key) -- nothing stored -- P_drop staged in LDS, O^T = V^T P_drop^T so each
 //             lane ends with 4 consecutive head dims of one query (8-byte stores straight
 //             into [B, S, H*64]); the row log-sum-exp is kept for the backward.
@@ -76,7 +76,6 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8 &a, const bf16x8 &b, const f3
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
 }
-__device__ __forceinline__ uint16_t bf16_bits(float a) { return static_cast<uint16_t>(pack2(a, 0.f) & 0xffffu); }
 
 // Dropout keep test: a counter hash of (seed, sequence*heads + head, query, key).  The same
 // function is reproduced in torch by the tests (kungfu_amd/ops/attention.py: dropout_keep).
@@ -116,18 +115,6 @@ __device__ __forceinline__ void stage_images(uint8_t *lds, const uint16_t *const
     }
 }
 
-// 16-lane (same lane>>4) reductions of the C layout's row values
-__device__ __forceinline__ float red_max16(float v) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ float red_sum16(float v) {
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 struct AttnArgs {
     const uint16_t *qkv;  // [B, S, 3, H, 64]
     uint16_t *out;        // [B, S, H, 64]
@@ -165,11 +152,15 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
 
     const int q0 = wave * QW;
-    f32x4 acc[TQ][TK];
+    // S^T = K Q^T: acc[j][i] holds keys 16 j + 4 (lane >> 4) + r of query q0 + 16 i + (lane & 15), so a
+    // query's softmax is 32 in-lane values + 2 cross-group shuffles, and its 4 consecutive keys of a
+    // P row leave in ONE 8-byte LDS store (the S = Q K^T layout needed 16-lane butterflies and a
+    // 2-byte store per element)
+    f32x4 acc[TK][TQ];
 #pragma unroll
-    for (int i = 0; i < TQ; ++i)
+    for (int j = 0; j < TK; ++j)
 #pragma unroll
-        for (int j = 0; j < TK; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < TQ; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DH / 32; ++s) {
         bf16x8 qa[TQ], kb[TK];
@@ -178,39 +169,46 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < TK; ++j) kb[j] = row_frag<128>(Ki, 16 * j, 32 * s, lane);
 #pragma unroll
-        for (int i = 0; i < TQ; ++i)
+        for (int j = 0; j < TK; ++j)
 #pragma unroll
-            for (int j = 0; j < TK; ++j) acc[i][j] = mfma(qa[i], kb[j], acc[i][j]);
+            for (int i = 0; i < TQ; ++i) acc[j][i] = mfma(kb[j], qa[i], acc[j][i]);
     }
-    // softmax over keys (row = q0 + 16 i + 4 (lane >> 4) + r, key = 16 j + (lane & 15))
     const int lg = lane >> 4, lc = lane & 15;
 #pragma unroll
-    for (int i = 0; i < TQ; ++i)
+    for (int i = 0; i < TQ; ++i) {
+        const int row = q0 + 16 * i + lc;  // the query
+        float m = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = q0 + 16 * i + 4 * lg + r;
-            float m = -INFINITY;
+        for (int j = 0; j < TK; ++j)
 #pragma unroll
-            for (int j = 0; j < TK; ++j) m = fmaxf(m, acc[i][j][r] * a.scale);
-            m = red_max16(m);
-            float sum = 0.f;
+            for (int r = 0; r < 4; ++r) m = fmaxf(m, acc[j][i][r] * a.scale);
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        float sum = 0.f;
 #pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const float e = __expf(acc[i][j][r] * a.scale - m);
-                acc[i][j][r] = e;
+        for (int j = 0; j < TK; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float e = __expf(acc[j][i][r] * a.scale - m);
+                acc[j][i][r] = e;
                 sum += e;
             }
-            sum = red_sum16(sum);
-            const float inv = 1.f / sum;
-            if (lc == 0) a.lse[static_cast<int64_t>(bh) * S + row] = m + __logf(sum);
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float inv = 1.f / sum;
+        if (lg == 0) a.lse[static_cast<int64_t>(bh) * S + row] = m + __logf(sum);
 #pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int key = 16 * j + lc;
-                float p = acc[i][j][r] * inv;
-                p = keep_elem(seed, bh, row, key, a.thresh) ? p * a.inv_keep : 0.f;
-                *reinterpret_cast<uint16_t *>(Pi + off<PROW>(row, key)) = bf16_bits(p);
+        for (int j = 0; j < TK; ++j) {
+            const int kb0 = 16 * j + 4 * lg;
+            float p[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = acc[j][i][r] * inv;
+                p[r] = keep_elem(seed, bh, row, kb0 + r, a.thresh) ? v * a.inv_keep : 0.f;
             }
+            *reinterpret_cast<uint2 *>(Pi + off<PROW>(row, kb0)) = make_uint2(pack2(p[0], p[1]), pack2(p[2], p[3]));
         }
+    }
     __syncthreads();
     // O^T[d][q] = sum_key V[key][d] P[q][key]: lane -> 4 consecutive d of one query
     f32x4 o[4][TQ];
@@ -291,11 +289,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
     const int lg = lane >> 4, lc = lane & 15;
     // ---- phase 1: query rows q0 .. q0 + QW - 1
     const int q0 = wave * QW;
-    f32x4 sc[TQ][TK], dp[TQ][TK];
+    // transposed products (as the forward): sc[j][i] / dp[j][i] hold keys 16 j + 4 lg + r of query
+    // q0 + 16 i + lc -- one lse / D load per query and 8-byte P / dS row stores
+    f32x4 sc[TK][TQ], dp[TK][TQ];
 #pragma unroll
-    for (int i = 0; i < TQ; ++i)
+    for (int j = 0; j < TK; ++j)
 #pragma unroll
-        for (int j = 0; j < TK; ++j) sc[i][j] = dp[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < TQ; ++i) sc[j][i] = dp[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DH / 32; ++s) {
         bf16x8 qa[TQ], ga[TQ], kb[TK], vb[TK];
@@ -310,31 +310,34 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
             vb[j] = row_frag<128>(Vi, 16 * j, 32 * s, lane);
         }
 #pragma unroll
-        for (int i = 0; i < TQ; ++i)
+        for (int j = 0; j < TK; ++j)
 #pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                sc[i][j] = mfma(qa[i], kb[j], sc[i][j]);
-                dp[i][j] = mfma(ga[i], vb[j], dp[i][j]);
+            for (int i = 0; i < TQ; ++i) {
+                sc[j][i] = mfma(kb[j], qa[i], sc[j][i]);
+                dp[j][i] = mfma(vb[j], ga[i], dp[j][i]);
             }
     }
 #pragma unroll
-    for (int i = 0; i < TQ; ++i)
+    for (int i = 0; i < TQ; ++i) {
+        const int row = q0 + 16 * i + lc;  // the query
+        const float l = a.lse[static_cast<int64_t>(bh) * S + row];
+        const float dd = dsum[row];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = q0 + 16 * i + 4 * lg + r;
-            const float l = a.lse[static_cast<int64_t>(bh) * S + row];
-            const float dd = dsum[row];
+        for (int j = 0; j < TK; ++j) {
+            const int kb0 = 16 * j + 4 * lg;
+            float pv[4], sv[4];
 #pragma unroll
-            for (int j = 0; j < TK; ++j) {
-                const int key = 16 * j + lc;
-                const float p = __expf(sc[i][j][r] * a.scale - l);
-                const bool kp = keep_elem(seed, bh, row, key, a.thresh);
-                const float pd = kp ? p * a.inv_keep : 0.f;
-                const float dpd = kp ? dp[i][j][r] * a.inv_keep : 0.f;
-                *reinterpret_cast<uint16_t *>(Pi + off<PROW>(row, key)) = bf16_bits(pd);
-                *reinterpret_cast<uint16_t *>(Si + off<PROW>(row, key)) = bf16_bits(p * (dpd - dd));
+            for (int r = 0; r < 4; ++r) {
+                const float p = __expf(sc[j][i][r] * a.scale - l);
+                const bool kp = keep_elem(seed, bh, row, kb0 + r, a.thresh);
+                const float dpd = kp ? dp[j][i][r] * a.inv_keep : 0.f;
+                pv[r] = kp ? p * a.inv_keep : 0.f;
+                sv[r] = p * (dpd - dd);
             }
+            *reinterpret_cast<uint2 *>(Pi + off<PROW>(row, kb0)) = make_uint2(pack2(pv[0], pv[1]), pack2(pv[2], pv[3]));
+            *reinterpret_cast<uint2 *>(Si + off<PROW>(row, kb0)) = make_uint2(pack2(sv[0], sv[1]), pack2(sv[2], sv[3]));
         }
+    }
     __syncthreads();
     // dQ^T[d][q] = scale * sum_key K[key][d] dS[q][key]
     {
