@@ -395,12 +395,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // transposed product (MFMA A operand = the weight fragment): acc[i][j] holds C^T of block (i, j),
+    // lane -> output pixel (lane & 15), 4 consecutive output channels 4 (lane >> 4) + r -- one 8-byte
+    // LDS store per block in the epilogue instead of four 2-byte ones
     auto mfma_block = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     };
 
     // prologue: STAGES-1 tiles in flight
@@ -483,29 +486,34 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     __syncthreads();  // all ds_reads of the last tile done before the LDS is reused
 
     // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
-    // C/D map (16x16): col = lane & 15, row = (lane >> 4) * 4 + r.
-    float bcol[TN];
+    // C^T map (16x16): pixel row = lane & 15, channel col = (lane >> 4) * 4 + r.
+    float bcol[TN][4];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        bcol[j] = 0.f;
-        if constexpr (BIAS) {
-            const int c = n0 + wn * WTN + j * 16 + (lane & 15);
-            if (c < g.K) bcol[j] = bf16_to_f32(ea.bias[c]);
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            bcol[j][r] = 0.f;
+            if constexpr (BIAS) {
+                const int c = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+                if (c < g.K) bcol[j][r] = bf16_to_f32(ea.bias[c]);
+            }
         }
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int j = 0; j < TN; ++j) {
+            const int row = wm * WTM + i * 16 + (lane & 15);
+            const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
+            uint32_t h[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-                const int col = wn * WTN + j * 16 + (lane & 15);
                 float v = acc[i][j][r];
-                if constexpr (BIAS) v += bcol[j];
+                if constexpr (BIAS) v += bcol[j][r];
                 if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
-                *reinterpret_cast<uint16_t *>(lds + row * CROW + col * 2) = f32_to_bf16(v);
+                h[r] = f32_to_bf16(v);
             }
+            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        }
     __syncthreads();
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
     // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
