@@ -109,8 +109,16 @@ def _elastic_launch(schedule: str) -> int:
 
     sizes = [int(p.split(":")[0]) for p in schedule.split(",") if p]
 
+    # below the kernel's ephemeral range: the running job's own sockets (RCCL bootstrap / proxy,
+    # stores) get ephemeral ports, which could take a port of a block checked free earlier
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            floor = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        floor = 32768
+
     def free_block(n):
-        for base in range(21000 + (os.getpid() % 97) * 211, 60000, 97):
+        for base in list(range(11000 + (os.getpid() % 97) * 97, floor - n, 97)) + list(range(11000, floor - n, 89)):
             ok = True
             for q in range(base, base + n):
                 sk = socket.socket()

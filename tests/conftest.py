@@ -24,16 +24,31 @@ def pytest_sessionstart(session):
         subprocess.check_call(["make", "-C", ROOT, "-j8", "runtime", "launcher"])
 
 
-_port_base = [20000 + (os.getpid() % 200) * 100]
+def _ephemeral_floor() -> int:
+    """Lowest port of the kernel's ephemeral range: fixed ports are picked below it, where no
+    socket of a running job (RCCL bootstrap / proxy, torch stores) is handed one by the kernel --
+    a block that was free when checked could otherwise be taken before a worker binds it."""
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            return int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        return 32768
+
+
+_EPHEMERAL_FLOOR = _ephemeral_floor()
+_PORT_LO = 10000
+_port_base = [_PORT_LO + (os.getpid() % 200) * 100]
 
 
 def free_port_block(n: int = 16) -> int:
     """Returns the first port of n consecutive free TCP ports."""
+    top = _EPHEMERAL_FLOOR if _EPHEMERAL_FLOOR > _PORT_LO + 4 * n else 60000
     while True:
         base = _port_base[0]
+        if base + n >= top:
+            _port_base[0] = _PORT_LO
+            continue
         _port_base[0] += n + 7
-        if _port_base[0] > 60000:
-            _port_base[0] = 20000
         ok = True
         for p in range(base, base + n):
             s = socket.socket()
