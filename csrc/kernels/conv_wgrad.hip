@@ -348,7 +348,7 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * TN + j) * NT);
+            for (int j = 0; j < TN; ++j) dst[(i * TN + j) * NT] = acc[i][j];
     }
 }
 
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(576) void wgrad_rows_kernel(const uint16_t *__restr
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * 64);
+            for (int j = 0; j < 4; ++j) dst[(i * 4 + j) * 64] = acc[i][j];
     }
 }
 
@@ -833,7 +833,7 @@ __global__ __launch_bounds__(64 * NWV) void wgrad_rows_rect_kernel(const uint16_
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(acc[i][j], dst + (i * 4 + j) * 64);
+            for (int j = 0; j < 4; ++j) dst[(i * 4 + j) * 64] = acc[i][j];
     }
 }
 
@@ -854,11 +854,11 @@ __global__ __launch_bounds__(256) void wgrad_dense_reduce_kernel(const float *__
         const f32x4 *src = reinterpret_cast<const f32x4 *>(part) + col;
         int sp = grp;
         for (; sp + G < splits; sp += 2 * G) {
-            const f32x4 u = __builtin_nontemporal_load(src + sp * n4), v = __builtin_nontemporal_load(src + (sp + G) * n4);
+            const f32x4 u = src[sp * n4], v = src[(sp + G) * n4];
             a += u;
             a += v;
         }
-        if (sp < splits) a += __builtin_nontemporal_load(src + sp * n4);
+        if (sp < splits) a += src[sp * n4];
     }
     red[t] = a;
     __syncthreads();
@@ -901,13 +901,13 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float *__restri
         const f32x4 *src = reinterpret_cast<const f32x4 *>(part) + idx;
         int sp = sg;
         for (; sp + 3 * SG < g.splits; sp += 4 * SG) {
-            const f32x4 a = __builtin_nontemporal_load(src + sp * stride_split);
-            const f32x4 b = __builtin_nontemporal_load(src + (sp + SG) * stride_split);
-            const f32x4 c = __builtin_nontemporal_load(src + (sp + 2 * SG) * stride_split);
-            const f32x4 d = __builtin_nontemporal_load(src + (sp + 3 * SG) * stride_split);
+            const f32x4 a = src[sp * stride_split];
+            const f32x4 b = src[(sp + SG) * stride_split];
+            const f32x4 c = src[(sp + 2 * SG) * stride_split];
+            const f32x4 d = src[(sp + 3 * SG) * stride_split];
             s += (a + b) + (c + d);
         }
-        for (; sp < g.splits; sp += SG) s += __builtin_nontemporal_load(src + sp * stride_split);
+        for (; sp < g.splits; sp += SG) s += src[sp * stride_split];
     }
     red[t] = s;
     __syncthreads();
