@@ -904,6 +904,16 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     if (variant < 0) {
         const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);  // (K % 256 == 0 only)
         variant = g.K <= 32 ? 11 : g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
+        if (variant == 7 && g.K % 128 == 0) {
+            // tile quantisation: 256x256 tiles run one workgroup per CU (135 KB of LDS), so a grid
+            // of T tiles takes ceil(T / 256) rounds; when the 256x128 grid fills its rounds >= 10 %
+            // better it wins despite the smaller tile (r5t21: 256->1024 at 14x14 63 -> 51 us; the
+            // 56x56 / 28x28 / 7x7 shapes keep 256x256, tools/bench_conv1x1_variants.py)
+            const int64_t t7 = tiles256, t1 = t7 * 2;
+            const double e7 = static_cast<double>(t7) / (((t7 + 255) / 256) * 256);
+            const double e1 = static_cast<double>(t1) / (((t1 + 255) / 256) * 256);
+            if (e1 > 1.1 * e7) variant = 1;
+        }
         if (conv_tile_rules() >= 2 && g.K % 128 == 0 && g.K > 32) {
             // re-measured with the staggered staging (tools/bench_conv1x1_variants.py, profiles/r3_conv_variants.txt):
             // the accumulating data gradients (ResNet's conv1 dgrad into the residual gradient) run best on
