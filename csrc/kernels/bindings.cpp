@@ -1778,6 +1778,35 @@ at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c
     return c;
 }
 
+// gemm.hip GELU-gradient epilogue: (du [M, N] bf16, db [N]) with du = bf16(bf16(a . b^T) * gelu'(u)) and
+// db the column sums of du (f32 or bf16 as bias_dtype) -- the data gradient through GELU of the layer
+// whose output u (its pre-activation) fed gelu, and that layer's bias gradient, in one GEMM + fold.
+std::vector<at::Tensor> gemm_nt_gelu_grad(at::Tensor a, at::Tensor b, at::Tensor u, c10::optional<at::ScalarType> bias_dtype) {
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && u.is_cuda() && a.scalar_type() == at::kBFloat16 &&
+                    b.scalar_type() == at::kBFloat16 && u.scalar_type() == at::kBFloat16,
+                "gemm_nt_gelu_grad: bf16 GPU tensors");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+                "gemm_nt_gelu_grad: a [M, K], b [N, K] contiguous");
+    const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+    TORCH_CHECK(u.is_contiguous() && u.numel() == M * N, "gemm_nt_gelu_grad: u [M, N] contiguous");
+    TORCH_CHECK(kfk::gemm_nt_supported(M, N, K) && N % 256 == 0, "gemm_nt_gelu_grad: unsupported shape M=", M, " N=", N,
+                " K=", K);
+    c10::DeviceGuard gd(a.device());
+    auto c = at::empty({M, N}, a.options());
+    const int rows = kfk::gemm_nt_gelu_grad_rows(static_cast<int>(M));
+    auto part = at::empty({rows, N}, a.options().dtype(at::kFloat));
+    const bool f32 = !bias_dtype || *bias_dtype == at::kFloat;
+    auto db = at::empty({N}, a.options().dtype(f32 ? at::kFloat : at::kBFloat16));
+    const auto s = c10::hip::getCurrentHIPStream().stream();
+    kfk::launch_gemm_nt_gelu_grad(reinterpret_cast<const uint16_t *>(a.data_ptr()),
+                                  reinterpret_cast<const uint16_t *>(b.data_ptr()), reinterpret_cast<uint16_t *>(c.data_ptr()),
+                                  reinterpret_cast<const uint16_t *>(u.data_ptr()), part.data_ptr<float>(),
+                                  static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), s);
+    kfk::launch_colsum_fold(part.data_ptr<float>(), rows, static_cast<int>(N), f32 ? db.data_ptr<float>() : nullptr,
+                            f32 ? nullptr : reinterpret_cast<uint16_t *>(db.data_ptr()), s);
+    return {c, db};
+}
+
 // Collective-interference emulator (comm_emu.hip): stands in for one all-reduce of `bucket`.
 void comm_emulate(at::Tensor bucket, at::Tensor scratch, int64_t traffic_bytes, int64_t ctas, double seconds,
                   int64_t stream) {
@@ -2143,6 +2172,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("bn") = -1,
           "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
     m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
+    m.def("gemm_nt_gelu_grad", &gemm_nt_gelu_grad, "(du, db): the GELU backward fused into the data-gradient NT GEMM "
+          "(du = bf16(bf16(a . b^T) * gelu'(u)), db = column sums of du)", py::arg("a"), py::arg("b"), py::arg("u"),
+          py::arg("bias_dtype") = py::none());
     m.def("embedding_backward", &embedding_backward, py::arg("grad"), py::arg("ids"), py::arg("dy"), py::arg("ch") = 0,
           "grad[ids[t]] += dy[t] by f32 atomics (graph-replayable embedding gradient)");
     m.def(

@@ -200,7 +200,9 @@ __device__ __forceinline__ void mfma_row(f32x4 (&acc)[TN], const bf16x8 (&b)[TN]
 template <int BN, int EPI>
 __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict__ A, const uint16_t *__restrict__ B,
                                                       uint16_t *__restrict__ C, const uint16_t *__restrict__ bias,
-                                                      int M, int N, int K, int mtiles, int ntiles) {
+                                                      int M, int N, int K, int mtiles, int ntiles,
+                                                      const uint16_t *__restrict__ aux = nullptr,
+                                                      float *__restrict__ part = nullptr) {
     constexpr int TN = BN / 64;           // 16-column blocks per wave (4 waves along N)
     constexpr int TM = 8;                 // 16-row blocks per wave (2 waves along M)
     constexpr int BBYTES = BN * kRowB;
@@ -333,6 +335,22 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
     // ---- epilogue: this wave's 128 x WCOLS sub-tile as bf16 into its own LDS region (8-byte
     // writes of 4 consecutive columns; 16-byte chunk index XOR (row & 7)), then 16-byte row stores
     uint8_t *ew = lds + wave * (128 * EROW);
+    constexpr bool GG = (EPI & kGemmGeluGrad) != 0;
+    static_assert(!GG || (BN == 256 && EPI == kGemmGeluGrad), "GELU-gradient epilogue: 256-wide tiles, alone");
+    // GELU gradient: every u row of this lane (16 x 16 bytes) requested before the LDS pass, so the
+    // loads land under it instead of one HBM round trip per few stored rows
+    constexpr int GNR = GG ? 128 / (64 / (WCOLS / 8)) : 1;
+    uint4 guv[GNR];
+    if constexpr (GG) {
+        const int gch = lane % (WCOLS / 8), grs = lane / (WCOLS / 8);
+        const int gcl = n0 + wn * WCOLS + gch * 8;
+#pragma unroll
+        for (int q = 0; q < GNR; ++q) {
+            const int grow = m0 + wm * 128 + q * (64 / (WCOLS / 8)) + grs;
+            guv[q] = grow < M ? *reinterpret_cast<const uint4 *>(aux + static_cast<int64_t>(grow) * N + gcl)
+                              : make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
     const int em = lane & 15, en = (lane >> 4) * 4;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -366,14 +384,34 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
         }
     }
     const bool lane_ok = rsub < RPI;
-#pragma unroll 4
+    // GELU-gradient epilogue (kGemmGeluGrad, 256-wide tiles: CPR = 8, one column chunk per lane,
+    // rows rsub + 8 k): du = bf16(dh * gelu'(u)) with dh the bf16 GEMM value, and this lane's
+    // column sums of the bf16 du (the gelu_bwd_colsum numerics, norms.hip)
+    float cs[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs[k] = 0.f;
+#pragma unroll(GG ? 16 : 4)
     for (int r0 = 0; r0 < 128; r0 += RPI) {
         const int row = r0 + rsub;
         const int grow = m0 + wm * 128 + row;
         if (!lane_ok || row >= 128 || grow >= M) continue;
         uint4 v = *reinterpret_cast<const uint4 *>(ew + row * EROW + ((ch ^ (row & 7)) << 4));
         uint16_t *dst = C + static_cast<int64_t>(grow) * N + gcol;
-        if constexpr (EPI != 0) {
+        if constexpr (GG) {
+            const uint4 uv = guv[r0 / RPI];
+            const uint32_t uw[4] = {uv.x, uv.y, uv.z, uv.w};
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint16_t r0b = f32_to_bf16(__uint_as_float(w[k] << 16) * gelu_grad_fast(__uint_as_float(uw[k] << 16)));
+                const uint16_t r1b = f32_to_bf16(__uint_as_float(w[k] & 0xffff0000u) *
+                                                 gelu_grad_fast(__uint_as_float(uw[k] & 0xffff0000u)));
+                cs[2 * k] += bf16_to_f32(r0b);
+                cs[2 * k + 1] += bf16_to_f32(r1b);
+                w[k] = static_cast<uint32_t>(r0b) | (static_cast<uint32_t>(r1b) << 16);
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        } else if constexpr (EPI != 0) {
             uint32_t w[4] = {v.x, v.y, v.z, v.w};
             uint32_t o[4] = {0u, 0u, 0u, 0u};
             if constexpr ((EPI & kGemmAccum) != 0) {
@@ -393,6 +431,23 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
             v = make_uint4(w[0], w[1], w[2], w[3]);
         }
         *reinterpret_cast<uint4 *>(dst) = v;
+    }
+    if constexpr (GG) {
+        // the 8 lanes of a column chunk (lane bits 3..5 = rsub) fold their rows in a fixed order;
+        // one partial row per (M-tile, M-wave): part[2 mt + wm][n]
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float t = cs[k];
+            t += __shfl_xor(t, 8);
+            t += __shfl_xor(t, 16);
+            t += __shfl_xor(t, 32);
+            cs[k] = t;
+        }
+        if (rsub == 0) {
+            float *pp = part + static_cast<int64_t>(2 * mt + wm) * N + gcol;
+            *reinterpret_cast<float4 *>(pp) = make_float4(cs[0], cs[1], cs[2], cs[3]);
+            *reinterpret_cast<float4 *>(pp + 4) = make_float4(cs[4], cs[5], cs[6], cs[7]);
+        }
     }
 }
 
@@ -596,6 +651,16 @@ void launch_bn(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t
 }
 
 }  // namespace
+
+int gemm_nt_gelu_grad_rows(int M) { return 2 * ((M + kGM - 1) / kGM); }
+
+void launch_gemm_nt_gelu_grad(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *u, float *part, int M,
+                              int N, int K, hipStream_t s) {
+    if (!gemm_nt_supported(M, N, K) || N % 256) throw std::invalid_argument("gemm_nt_gelu_grad: unsupported shape");
+    if (!u || !part) throw std::invalid_argument("gemm_nt_gelu_grad: needs the pre-activation and the partials");
+    const int mtiles = (M + kGM - 1) / kGM, ntiles = N / 256;
+    gemm_nt_kernel<256, kGemmGeluGrad><<<mtiles * ntiles, 512, 0, s>>>(a, b, c, nullptr, M, N, K, mtiles, ntiles, u, part);
+}
 
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K) {
     return M > 0 && N >= 128 && N % 128 == 0 && K >= 32 && K % 32 == 0 && M * K * 2 < (int64_t(1) << 31) &&

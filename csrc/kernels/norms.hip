@@ -316,19 +316,6 @@ __global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x
     }
 }
 
-// gelu'(x) = Phi(x) + x phi(x) with ONE exponential: erf(x / sqrt 2) by Abramowitz-Stegun 7.1.26
-// (|error| < 1.5e-7, far below a bf16 ulp of the result) whose e^{-x^2/2} factor is phi's own.
-// ~12 vector instructions instead of erff + expf (~40): the fused pass below is memory-bound.
-__device__ __forceinline__ float gelu_grad_fast(float x) {
-    const float z = fabsf(x) * 0.70710678118654752f;
-    const float e = __expf(-0.5f * x * x);  // = e^{-z^2}
-    const float t = __frcp_rn(1.f + 0.3275911f * z);
-    const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f +
-                                                                                            t * 1.061405429f))));
-    const float erf_abs = 1.f - poly * e;
-    const float cdf = 0.5f * (1.f + (x < 0.f ? -erf_abs : erf_abs));
-    return cdf + x * (e * 0.39894228040143268f);
-}
 
 // Phi(x) = 0.5 (1 + erf(x / sqrt 2)) by the same Abramowitz-Stegun form (one exponential)
 __device__ __forceinline__ float gelu_cdf_fast(float x) {
@@ -476,6 +463,10 @@ void launch_colsum_bf16(const uint16_t *x, int64_t T, int O, float *part, float 
     dim3 g1(chunks, (OV + kColVec - 1) / kColVec);
     colsum_stage1<<<g1, 256, 0, s>>>(reinterpret_cast<const uint4 *>(x), T, OV, rows_per, part);
     colsum_stage2<<<(O + 31) / 32, 32 * kC2Lanes, 0, s>>>(part, chunks, O, out_f32, out_bf16);
+}
+
+void launch_colsum_fold(const float *part, int rows, int O, float *out_f32, uint16_t *out_bf16, hipStream_t s) {
+    colsum_stage2<<<(O + 31) / 32, 32 * kC2Lanes, 0, s>>>(part, rows, O, out_f32, out_bf16);
 }
 
 void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s) {

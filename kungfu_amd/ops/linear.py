@@ -54,7 +54,21 @@ class ResidualLink:
         self.armed, self.value = False, None
 
 
+class GeluLink:
+    """Link from ``gelu(u)`` to the ONE linear layer that consumes it (BERT's FC2): that layer's
+    backward forms ``du = gelu'(u) * (dy W)`` inside its data-gradient GEMM (gemm.hip's GELU-gradient
+    epilogue) together with the column sums of ``du`` -- the bias gradient of the layer that produced
+    ``u``, handed on through its :class:`BiasLink` -- and returns ``du`` in place of the gradient of
+    ``gelu(u)``; the GELU node then passes it through (``ptr`` checks that it receives exactly that
+    tensor).  Replaces hipBLASLt's data-gradient GEMM plus the separate GELU-backward + column-sum pass."""
+    __slots__ = ("u", "blink", "ptr")
+
+    def __init__(self, u, blink):
+        self.u, self.blink, self.ptr = u, blink, 0
+
+
 _RES_LINK = True  # module switch (tests / A/B)
+_GELU_GEMM = True  # module switch (tests / A/B): FC2's data gradient + GELU backward on gemm.hip
 
 
 def residual_link(x: torch.Tensor):
@@ -95,12 +109,21 @@ def _wt_cache(target, w):
     return fc, target[1]
 
 
+def _gelu_gemm_ok(M: int, in_f: int, out_f: int) -> bool:
+    return _GELU_GEMM and in_f % 256 == 0 and hip().gemm_nt_supported(M, in_f, out_f)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, target=None, rlink=None):
+    def forward(ctx, x, w, b, target=None, rlink=None, glink=None):
         ctx.save_for_backward(x, w)
         ctx.target = target
         ctx.rlink = rlink
+        ctx.glink = ctx.wt_g = None
+        if glink is not None and target is not None and rlink is None:
+            out_f, in_f = w.shape
+            if _gelu_gemm_ok(x.numel() // in_f, in_f, out_f):
+                ctx.glink, ctx.wt_g = glink, _wt_cache(target, w)
         if rlink is not None:
             rlink.armed = True
         ctx.has_b = b is not None
@@ -130,7 +153,19 @@ class _LinearFn(torch.autograd.Function):
             rl, g = ctx.rlink, None
             if rl is not None and rl.value is not None:  # the consuming AddLayerNorm's skip gradient
                 g, rl.value = rl.value.reshape(-1, in_f), None
-            if ctx.wt is not None:  # dx = dy . W = dy . (W^T)^T on the NT GEMM
+            gl = ctx.glink
+            if gl is not None:
+                # x = gelu(u): du = gelu'(u) * (dy . W) and u's layer's bias gradient in one GEMM (W^T from
+                # the flat space's per-step transpose); the GELU node passes du through
+                fc, i = ctx.wt_g
+                bl = gl.blink
+                du, dbu = hip().gemm_nt_gelu_grad(dy2, fc.get(i).view(in_f, out_f), gl.u.reshape(-1, in_f),
+                                                  bl.dtype if bl is not None else torch.float32)
+                gl.ptr = du.data_ptr()
+                if bl is not None:
+                    bl.value, bl.ptr = dbu, du.data_ptr()
+                dx = du.view(x.shape)
+            elif ctx.wt is not None:  # dx = dy . W = dy . (W^T)^T on the NT GEMM
                 fc, i = ctx.wt
                 dx = hip().gemm_nt(dy2, fc.get(i).view(in_f, out_f))
                 if g is not None:
@@ -167,7 +202,7 @@ class _LinearFn(torch.autograd.Function):
                 db = hip().colsum(dy2, ctx.b_dtype)
             else:
                 db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -187,7 +222,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target
         rl = getattr(x, "_kf_rlink", None)
         if rl is not None and (rl.armed or x.dtype != torch.bfloat16):
             rl = None  # one linear consumer per link
-        y = _LinearFn.apply(x, w, b, grad_target, rl)
+        gl = getattr(x, "_kf_glink", None)
+        y = _LinearFn.apply(x, w, b, grad_target, rl, gl)
         if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
             y._kf_blink = y.grad_fn.blink
         return y
@@ -200,19 +236,28 @@ class _GeluFn(torch.autograd.Function):
     backward through its :class:`BiasLink`, which then skips its own column-sum pass)."""
 
     @staticmethod
-    def forward(ctx, u, blink):
+    def forward(ctx, u, blink, glink):
         ctx.save_for_backward(u)
         ctx.blink = blink
+        ctx.glink = glink
         return F.gelu(u)  # norms.hip gelu_forward measured 0.6 % slower end to end (r4t20): not used
 
     @staticmethod
     def backward(ctx, dy):
+        gl = ctx.glink
+        if gl is not None and gl.ptr:
+            # the consuming linear already formed du (and u's layer's bias gradient) in its GEMM
+            if dy.data_ptr() != gl.ptr:
+                raise RuntimeError("gelu: the gradient received is not the consuming linear's fused GELU gradient "
+                                   "(gelu(u) must have that linear as its only consumer)")
+            gl.ptr = 0
+            return dy, None, None
         (u,) = ctx.saved_tensors
         bl = ctx.blink
         du, db = hip().gelu_backward_colsum(dy.contiguous(), u, bl.dtype if bl is not None else torch.float32)
         if bl is not None:
             bl.value, bl.ptr = db, du.data_ptr()
-        return du, None
+        return du, None, None
 
 
 _GELU_LINK = True  # module switch (tests)
@@ -224,6 +269,12 @@ def gelu(u: torch.Tensor, bias_link: bool = False) -> torch.Tensor:
     bl = getattr(u, "_kf_blink", None) if bias_link and _GELU_LINK else None
     if (u.is_cuda and u.dtype == torch.bfloat16 and u.is_contiguous() and u.shape[-1] % 8 == 0 and hip_available()
             and (bl is not None or not bias_link)):
-        return _GeluFn.apply(u, bl)
+        # bias_link also promises that gelu(u) has one consumer: a linear layer may fuse the GELU
+        # backward into its data-gradient GEMM (GeluLink)
+        gl = GeluLink(u, bl) if bias_link and _GELU_GEMM and torch.is_grad_enabled() else None
+        h = _GeluFn.apply(u, bl, gl)
+        if gl is not None:
+            h._kf_glink = gl
+        return h
     return F.gelu(u)
 

@@ -158,3 +158,73 @@ def test_linear_gemm_path_matches_library_path():
         assert abs(x - y) < 2e-3 * abs(x), (la, lb)
     for x, y in zip(ga, gb):
         assert _rel(y, x) < 3e-2, _rel(y, x)
+
+
+@pytest.mark.parametrize("M,K,N", [(16384, 768, 3072), (1000, 768, 512), (300, 256, 256)])
+def test_gemm_nt_gelu_grad_matches_fp32(M, K, N):
+    """gemm.hip's GELU-gradient epilogue: du = gelu'(u) * (dy . W) (b = W^T [N, K]) and the column
+    sums of du (the bias gradient of the layer that produced u) vs the fp32 torch autograd of F.gelu;
+    M tails; deterministic (no atomics)."""
+    H = _hip()
+    torch.manual_seed(5)
+    dy = torch.randn(M, K, device="cuda").bfloat16()
+    wt = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    u = (torch.randn(M, N, device="cuda") * 2).bfloat16()
+    du, db = H.gemm_nt_gelu_grad(dy, wt, u)
+    uf = u.float().requires_grad_(True)
+    F.gelu(uf).backward(dy.float() @ wt.float().t())
+    assert du.shape == (M, N) and du.dtype == torch.bfloat16
+    assert _rel(du, uf.grad) < 1.5e-2
+    assert db.dtype == torch.float32 and _rel(db, du.double().sum(0)) < 1e-5  # sums of the bf16 du written
+    assert _rel(db, uf.grad.double().sum(0)) < 2e-2
+    du2, db2 = H.gemm_nt_gelu_grad(dy, wt, u)
+    assert torch.equal(du, du2) and torch.equal(db, db2)
+    dbb = H.gemm_nt_gelu_grad(dy, wt, u, torch.bfloat16)[1]
+    assert dbb.dtype == torch.bfloat16 and _rel(dbb, db) < 1e-2
+
+
+def test_linear_fused_gelu_grad_matches_unfused():
+    """ops.linear.GeluLink: FC2's data gradient and the GELU backward (+ FC1's bias gradient) in one
+    gemm.hip GEMM vs hipBLASLt's GEMM + the separate GELU-backward pass, in a 2-layer BERT with the
+    bf16 shadow engine: identical losses (the forward is unchanged), flat gradients equal up to bf16
+    rounding, over two optimizer steps (the W^T cache refreshes)."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
+    from kungfu_amd.ops import linear as lin
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(on):
+        old, lin._GELU_GEMM = lin._GELU_GEMM, on
+        try:
+            torch.manual_seed(0)
+            m = BertForPreTraining(layers=2).cuda()
+            for l in m.layers:
+                l.dropout = 0.0
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
+                                                        named_parameters=m.named_parameters())
+            enable_bf16_shadow(m, opt)
+            g = torch.Generator(device="cuda").manual_seed(1)
+            batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
+            losses, grads = [], []
+            for _ in range(2):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = pretraining_loss(m, batch)
+                loss.backward()
+                opt.reducer.synchronize()
+                grads.append(opt.space.flat_grad.clone())
+                losses.append(loss.item())
+                opt.step()
+            torch.cuda.synchronize()
+            return losses, grads
+        finally:
+            lin._GELU_GEMM = old
+
+    la, ga = run(False)
+    lb, gb = run(True)
+    assert la[0] == lb[0], (la, lb)
+    assert abs(la[1] - lb[1]) < 2e-3 * abs(la[1]), (la, lb)
+    for x, y in zip(ga, gb):
+        assert _rel(y, x) < 2e-2, _rel(y, x)
