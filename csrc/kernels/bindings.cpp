@@ -674,10 +674,18 @@ at::Tensor conv_wgrad_rect(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, 
 }
 
 // fused softmax cross-entropy over bf16 logits [R, V]: (lse [R] f32, per-row loss [R] f32)
+// Rows may be padded (x.stride(0) = ld >= V, a multiple of 8, 16-byte aligned base: the vocabulary
+// projection's gemm_nt_ld output): the 16-byte-load kernels; those also serve contiguous rows of V % 8 == 0
+static int64_t xent_ld(const at::Tensor &x) {
+    const int64_t ld = x.stride(0), V = x.size(1);
+    const bool al = reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0;
+    return (x.stride(1) == 1 && ld >= V && ld % 8 == 0 && al) ? ld : 0;
+}
+
 std::vector<at::Tensor> xent_forward(at::Tensor x, at::Tensor labels) {
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
-                    x.size(1) % 2 == 0,
-                "xent_forward: contiguous bf16 [R, V] logits, V even");
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 &&
+                    (xent_ld(x) > 0 || (x.is_contiguous() && x.size(1) % 2 == 0)),
+                "xent_forward: bf16 [R, V] logits, contiguous with V even or rows padded to a multiple of 8");
     TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == at::kLong && labels.is_contiguous() &&
                     labels.numel() == x.size(0) && labels.device() == x.device(),
                 "xent_forward: int64 labels [R] on the logits' device");
@@ -687,26 +695,28 @@ std::vector<at::Tensor> xent_forward(at::Tensor x, at::Tensor labels) {
     auto loss = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
     kfk::launch_xent_forward(reinterpret_cast<const uint16_t *>(x.data_ptr()), labels.data_ptr<int64_t>(), x.size(0),
                              static_cast<int>(x.size(1)), lse.data_ptr<float>(), loss.data_ptr<float>(),
-                             stream_of(x, 0));
+                             stream_of(x, 0), xent_ld(x));
     return {lse, loss};
 }
 
-// its backward: d logits (bf16 [R, V]) = (softmax - onehot(label)) * scale[0]
+// its backward: d logits (bf16 [R, V]) = (softmax - onehot(label)) * scale[0]; padded logits give a
+// gradient with the same padded row stride (a [R, V] view of [R, ld], the padding of the last chunk zero)
 at::Tensor xent_backward(at::Tensor x, at::Tensor labels, at::Tensor lse, at::Tensor scale) {
-    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() &&
-                    x.size(1) % 2 == 0,
-                "xent_backward: contiguous bf16 [R, V] logits, V even");
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 &&
+                    (xent_ld(x) > 0 || (x.is_contiguous() && x.size(1) % 2 == 0)),
+                "xent_backward: bf16 [R, V] logits, contiguous with V even or rows padded to a multiple of 8");
     TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous() && labels.numel() == x.size(0) &&
                     lse.scalar_type() == at::kFloat && lse.numel() == x.size(0) && scale.scalar_type() == at::kFloat &&
                     scale.numel() >= 1 && labels.device() == x.device() && lse.device() == x.device() &&
                     scale.device() == x.device(),
                 "xent_backward: labels int64 [R], lse f32 [R], scale f32 [1] on the logits' device");
     c10::DeviceGuard gd(x.device());
-    auto dx = at::empty_like(x);
+    const int64_t ld = xent_ld(x);
+    auto dxp = ld > 0 ? at::empty({x.size(0), ld}, x.options()) : at::empty_like(x);
     kfk::launch_xent_backward(reinterpret_cast<const uint16_t *>(x.data_ptr()), labels.data_ptr<int64_t>(),
                               lse.data_ptr<float>(), scale.data_ptr<float>(), x.size(0), static_cast<int>(x.size(1)),
-                              reinterpret_cast<uint16_t *>(dx.data_ptr()), stream_of(x, 0));
-    return dx;
+                              reinterpret_cast<uint16_t *>(dxp.data_ptr()), stream_of(x, 0), ld);
+    return ld > 0 && ld != x.size(1) ? dxp.narrow(1, 0, x.size(1)) : dxp;
 }
 
 // erf-GELU forward of a contiguous bf16 tensor (numel % 8 == 0)
@@ -1744,6 +1754,35 @@ void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy, int64_t 
 }
 
 // gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
+// C[M, ldc] (only columns < N written, the chunk holding column N - 1 whole) = a . b^T (+ bias), for a
+// ragged N (BERT's 30,522-entry vocabulary): rows of C padded to ldc (a multiple of 8) stay 16-byte aligned
+at::Tensor gemm_nt_ld(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, int64_t ldc, int64_t bn) {
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
+                "gemm_nt_ld: bf16 GPU tensors");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+                "gemm_nt_ld: a [M, K], b [N, K] contiguous");
+    const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+    if (ldc <= 0) ldc = (N + 7) / 8 * 8;
+    TORCH_CHECK(kfk::gemm_nt_ld_supported(M, N, K, ldc), "gemm_nt_ld: unsupported shape M=", M, " N=", N, " K=", K,
+                " ldc=", ldc);
+    int epi = 0;
+    const uint16_t *bp = nullptr;
+    if (bias && bias->defined()) {
+        TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kBFloat16 && bias->numel() == N &&
+                        bias->is_contiguous(),
+                    "gemm_nt_ld: bias bf16 [N]");
+        bp = reinterpret_cast<const uint16_t *>(bias->data_ptr());
+        epi |= kfk::kGemmBias;
+    }
+    auto c = at::empty({M, ldc}, a.options());
+    c10::DeviceGuard gd(a.device());
+    kfk::launch_gemm_nt_ld(reinterpret_cast<const uint16_t *>(a.data_ptr()),
+                           reinterpret_cast<const uint16_t *>(b.data_ptr()), reinterpret_cast<uint16_t *>(c.data_ptr()),
+                           bp, static_cast<int>(M), static_cast<int>(N), static_cast<int>(K), static_cast<int>(ldc), epi,
+                           bn > 0 ? static_cast<int>(bn) : 256, c10::hip::getCurrentHIPStream().stream());
+    return c;
+}
+
 at::Tensor gemm_nt(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> out,
                    bool accumulate, int64_t bn) {
     TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
@@ -2172,6 +2211,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("accumulate") = false, py::arg("bn") = -1,
           "bf16 a[M,K] . b[N,K]^T (+bias) (+out) on the pipelined 256 x bn MFMA GEMM (gemm.hip)");
     m.def("gemm_nt_supported", &kfk::gemm_nt_supported);
+    m.def("gemm_nt_ld", &gemm_nt_ld, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("ldc") = 0,
+          py::arg("bn") = 256, "C [M, ldc] = a . b^T (+ bias) for any N (columns >= N of C unspecified)");
+    m.def("gemm_nt_ld_supported", &kfk::gemm_nt_ld_supported);
     m.def("gemm_nt_gelu_grad", &gemm_nt_gelu_grad, "(du, db): the GELU backward fused into the data-gradient NT GEMM "
           "(du = bf16(bf16(a . b^T) * gelu'(u)), db = column sums of du)", py::arg("a"), py::arg("b"), py::arg("u"),
           py::arg("bias_dtype") = py::none());

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
                                                       uint16_t *__restrict__ C, const uint16_t *__restrict__ bias,
                                                       int M, int N, int K, int mtiles, int ntiles,
                                                       const uint16_t *__restrict__ aux = nullptr,
-                                                      float *__restrict__ part = nullptr) {
+                                                      float *__restrict__ part = nullptr, int ldc = 0) {
     constexpr int TN = BN / 64;           // 16-column blocks per wave (4 waves along N)
     constexpr int TM = 8;                 // 16-row blocks per wave (2 waves along M)
     constexpr int BBYTES = BN * kRowB;
@@ -248,7 +248,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
         const int row = (i * 8 + wave) * 16 + srow;  // < BN for the instructions this wave issues
-        b_off[i] = static_cast<uint32_t>(((n0 + row) * K + schk * 8) * 2);
+        // rows past N (the last tile of a ragged N) read zeros: an offset past num_records
+        b_off[i] = n0 + row < N ? static_cast<uint32_t>(((n0 + row) * K + schk * 8) * 2) : kOOB;
     }
     const bool b_extra = B_REM && wave < B_REM;
     const int slabs = K / kSlabK;
@@ -371,19 +372,27 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
     constexpr int RPI = 64 / CPR;  // rows per wave instruction (8 / 10.67 / 16) -- CPR divides 64 for 8 and 4
     const int ch = lane % CPR, rsub = lane / CPR;
     const int gcol = n0 + wn * WCOLS + ch * 8;
+    const int64_t ldo = ldc > 0 ? ldc : N;  // C row stride (>= N rounded up to 8 when N is ragged)
     float bv[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) bv[k] = 0.f;
     if constexpr ((EPI & kGemmBias) != 0) {
-        const uint4 braw = *reinterpret_cast<const uint4 *>(bias + gcol);
-        const uint32_t bw[4] = {braw.x, braw.y, braw.z, braw.w};
+        if (gcol + 8 <= N) {
+            const uint4 braw = *reinterpret_cast<const uint4 *>(bias + gcol);
+            const uint32_t bw[4] = {braw.x, braw.y, braw.z, braw.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            bv[2 * k] = bf16_to_f32(static_cast<uint16_t>(bw[k] & 0xffff));
-            bv[2 * k + 1] = bf16_to_f32(static_cast<uint16_t>(bw[k] >> 16));
+            for (int k = 0; k < 4; ++k) {
+                bv[2 * k] = bf16_to_f32(static_cast<uint16_t>(bw[k] & 0xffff));
+                bv[2 * k + 1] = bf16_to_f32(static_cast<uint16_t>(bw[k] >> 16));
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) bv[k] = gcol + k < N ? bf16_to_f32(bias[gcol + k]) : 0.f;
         }
     }
-    const bool lane_ok = rsub < RPI;
+    // a ragged N: the chunk holding column N - 1 is stored whole (its columns past N land in the row
+    // padding, ldc >= N rounded up to 8), chunks past it not at all
+    const bool lane_ok = rsub < RPI && gcol < N;
     // GELU-gradient epilogue (kGemmGeluGrad, 256-wide tiles: CPR = 8, one column chunk per lane,
     // rows rsub + 8 k): du = bf16(dh * gelu'(u)) with dh the bf16 GEMM value, and this lane's
     // column sums of the bf16 du (the gelu_bwd_colsum numerics, norms.hip)
@@ -396,7 +405,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
         const int grow = m0 + wm * 128 + row;
         if (!lane_ok || row >= 128 || grow >= M) continue;
         uint4 v = *reinterpret_cast<const uint4 *>(ew + row * EROW + ((ch ^ (row & 7)) << 4));
-        uint16_t *dst = C + static_cast<int64_t>(grow) * N + gcol;
+        uint16_t *dst = C + grow * ldo + gcol;
         if constexpr (GG) {
             const uint4 uv = guv[r0 / RPI];
             const uint32_t uw[4] = {uv.x, uv.y, uv.z, uv.w};
@@ -636,15 +645,24 @@ void launch_bn4(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_
 
 template <int BN>
 void launch_bn(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K, int epi,
-               hipStream_t s) {
-    const int mtiles = (M + kGM - 1) / kGM, ntiles = N / BN;
+               hipStream_t s, int ldc = 0) {
+    const int mtiles = (M + kGM - 1) / kGM, ntiles = (N + BN - 1) / BN;
     const dim3 grid(mtiles * ntiles), block(512);
     switch (epi) {
-    case 0: gemm_nt_kernel<BN, 0><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
-    case kGemmBias: gemm_nt_kernel<BN, kGemmBias><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
-    case kGemmAccum: gemm_nt_kernel<BN, kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles); break;
+    case 0:
+        gemm_nt_kernel<BN, 0><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr, ldc);
+        break;
+    case kGemmBias:
+        gemm_nt_kernel<BN, kGemmBias><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr,
+                                                            ldc);
+        break;
+    case kGemmAccum:
+        gemm_nt_kernel<BN, kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr,
+                                                             ldc);
+        break;
     case kGemmBias | kGemmAccum:
-        gemm_nt_kernel<BN, kGemmBias | kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles);
+        gemm_nt_kernel<BN, kGemmBias | kGemmAccum><<<grid, block, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles,
+                                                                         nullptr, nullptr, ldc);
         break;
     default: throw std::invalid_argument("gemm_nt: unsupported epilogue");
     }
@@ -678,6 +696,23 @@ int gemm_nt_pick_bn(int64_t M, int64_t N) {
     for (int bn : cand)
         if (N % bn == 0 && mt * (N / bn) >= 512) return bn;
     return N % 256 == 0 && mt * (N / 256) >= 256 ? 256 : 128;
+}
+
+bool gemm_nt_ld_supported(int64_t M, int64_t N, int64_t K, int64_t ldc) {
+    return M > 0 && N > 0 && K >= 32 && K % 32 == 0 && ldc % 8 == 0 && ldc >= (N + 7) / 8 * 8 &&
+           M * K * 2 < (int64_t(1) << 31) && N * K * 2 < (int64_t(1) << 31) && M * ldc < (int64_t(1) << 40);
+}
+
+void launch_gemm_nt_ld(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
+                       int ldc, int epi, int bn, hipStream_t s) {
+    if (!gemm_nt_ld_supported(M, N, K, ldc)) throw std::invalid_argument("gemm_nt_ld: unsupported shape / row stride");
+    if ((epi & kGemmBias) && !bias) throw std::invalid_argument("gemm_nt_ld: bias epilogue without bias");
+    switch (bn) {
+    case 256: launch_bn<256>(a, b, c, bias, M, N, K, epi, s, ldc); break;
+    case 192: launch_bn<192>(a, b, c, bias, M, N, K, epi, s, ldc); break;
+    case 128: launch_bn<128>(a, b, c, bias, M, N, K, epi, s, ldc); break;
+    default: throw std::invalid_argument("gemm_nt_ld: tile width must be 128, 192 or 256");
+    }
 }
 
 void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,

@@ -35,6 +35,11 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 int gemm_nt_pick_bn(int64_t M, int64_t N);
 void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
                     int epi, int bn, hipStream_t s);
+// any N >= 1 (rows of B past N read zeros) with C's row stride ldc (% 8 == 0, >= N rounded up to 8):
+// the chunk of 8 columns holding column N - 1 is stored whole, into the row padding
+bool gemm_nt_ld_supported(int64_t M, int64_t N, int64_t K, int64_t ldc);
+void launch_gemm_nt_ld(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
+                       int ldc, int epi, int bn, hipStream_t s);
 // The GELU backward fused into the data-gradient GEMM of the layer that consumes gelu(u):
 // c = bf16(bf16(a . b^T) * gelu'(u)) (u: the pre-activation [M, N]) on 256 x 256 tiles (N % 256 == 0),
 // and part[gemm_nt_gelu_grad_rows(M)][N] f32 = per-128-row column sums of c -- folded by
@@ -118,10 +123,11 @@ class PairPrefetcher {
 
 // Softmax cross-entropy over bf16 logits [R, V] (V even; xent.hip): per-row log-sum-exp and loss
 // (0 where the label is outside [0, V)); backward writes the bf16 gradient scaled by *scale.
+// ld > 0: rows padded to ld classes (ld % 8 == 0, 16-byte aligned; 16-byte loads), dx likewise.
 void launch_xent_forward(const uint16_t *x, const int64_t *labels, int64_t R, int V, float *lse, float *loss,
-                         hipStream_t s);
+                         hipStream_t s, int64_t ld = 0);
 void launch_xent_backward(const uint16_t *x, const int64_t *labels, const float *lse, const float *scale, int64_t R,
-                          int V, uint16_t *dx, hipStream_t s);
+                          int V, uint16_t *dx, hipStream_t s, int64_t ld = 0);
 
 // y = gelu(u) (erf form, bf16, n % 8 == 0; norms.hip)
 void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s);

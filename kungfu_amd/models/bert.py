@@ -11,6 +11,7 @@ import torch.nn.functional as F
 
 from ..ops.attention import self_attention
 from ..ops.embedding import embedding
+from ..ops.vocab import vocab_projection
 from ..ops.xent import cross_entropy
 from ..ops.linear import gelu, residual_link
 
@@ -96,7 +97,8 @@ class BertForPreTraining(nn.Module):
         if mlm_positions is not None:
             hs = torch.gather(x, 1, mlm_positions.unsqueeze(-1).expand(-1, -1, x.shape[-1]))
         h = self.mlm_ln(F.gelu(self.mlm_dense(hs)))
-        mlm = F.linear(h, self.tok.weight, self.mlm_bias)  # tied output embedding
+        # tied output embedding; gemm.hip's ragged-N GEMM with padded logits rows (ops/vocab.py)
+        mlm = vocab_projection(h, self.tok.weight, self.mlm_bias)
         return mlm, self.nsp(x[:, 0])
 
 

@@ -39,5 +39,10 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     V = logits.shape[-1]
     if (_ENABLED and logits.is_cuda and logits.dtype == torch.bfloat16 and V % 2 == 0 and labels.dtype == torch.long
             and hip_available()):
-        return _XentFn.apply(logits.reshape(-1, V).contiguous(), labels.reshape(-1).contiguous())
+        x2 = logits.reshape(-1, V)
+        # rows padded to a multiple of 8 classes (ops/vocab.py's logits: a [R, V] view of [R, ld]) are read
+        # in place by the 16-byte-load kernels; anything else is made contiguous
+        if not (x2.stride(1) == 1 and x2.stride(0) >= V and x2.stride(0) % 8 == 0):
+            x2 = x2.contiguous()
+        return _XentFn.apply(x2, labels.reshape(-1).contiguous())
     return F.cross_entropy(logits.float().reshape(-1, V), labels.reshape(-1))

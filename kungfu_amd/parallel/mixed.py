@@ -56,6 +56,40 @@ def deliver(target: Tuple[FlatParamSpace, int], g: torch.Tensor) -> None:
     space.sink.put(i, g)
 
 
+# Parameters with SEVERAL direct producers in one backward (a tied embedding: the lookup's scatter-add
+# and the vocabulary projection's weight gradient, ops/embedding.py + ops/vocab.py).  Every forward use
+# calls use_direct; each producer adds its share into the flat f32 slot itself and calls landed_direct,
+# and the LAST one hands the parameter to the sink's bucket accounting (put_direct) -- so the bucket
+# launches once, after the whole gradient is in the slot, whatever order the producers run in.
+_PENDING: Dict[Tuple[int, int], int] = {}
+_EMBED_DIRECT = True  # module switch (tests / A/B)
+
+
+def use_direct(target: Tuple[FlatParamSpace, int]) -> None:
+    k = (id(target[0]), target[1])
+    _PENDING[k] = _PENDING.get(k, 0) + 1
+
+
+def landed_direct(target: Tuple[FlatParamSpace, int]) -> None:
+    space, i = target
+    k = (id(space), i)
+    n = _PENDING.get(k, 1) - 1
+    if n > 0:
+        _PENDING[k] = n
+        return
+    _PENDING.pop(k, None)
+    space.sink.put_direct(i)
+
+
+def embedding_target(p: Optional[torch.Tensor]) -> Optional[Tuple[FlatParamSpace, int]]:
+    """(space, index) of a registered embedding table whose direct producers land in its flat slot
+    (needs a sink with ``put_direct``); None otherwise."""
+    t = _DIRECT.get(id(p)) if p is not None and _EMBED_DIRECT else None
+    if t is None or not hasattr(t[0].sink, "put_direct") or not p.is_cuda:
+        return None
+    return t
+
+
 def _bf16_autocast(dev: str) -> bool:
     return torch.is_autocast_enabled(dev) and torch.get_autocast_dtype(dev) == torch.bfloat16
 
@@ -254,6 +288,10 @@ def enable_bf16_shadow(model: nn.Module, optimizer, bn_direct: bool = True) -> i
                 if m.bias is not None:
                     register(m.bias)
                 m.forward = types.MethodType(_linear_forward, m)
+        elif type(m).forward is nn.Embedding.forward and m.weight.dtype == torch.float32:
+            # looked up by ops/embedding.py (f32 master) and, when tied, projected onto by ops/vocab.py
+            # (bf16 shadow): both add their gradients straight into the flat slot (use_direct)
+            register(m.weight)
         elif bn_direct and isinstance(m, (BatchNormAct2d, AddLayerNorm)):
             # the fused BN / residual+LayerNorm kernels hand their f32 gamma/beta gradients to the sink
             register(m.weight)

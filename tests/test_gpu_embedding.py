@@ -87,3 +87,64 @@ def test_fused_cross_entropy_matches_torch(R, V):
     torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(x.grad.float(), xr.grad.bfloat16().float(), rtol=1e-2, atol=1e-6)
     assert x.grad[::5].abs().sum().item() == 0.0
+
+
+@pytest.mark.parametrize("R,V", [(2560, 30522), (33, 1000), (9, 13)])
+def test_fused_cross_entropy_padded_rows(R, V):
+    """The 16-byte-load kernels over logits rows padded to ld (a [R, V] view of [R, ld], the vocabulary
+    projection's layout; junk in the padding): same loss / gradient as the contiguous path's reference,
+    and the gradient comes back with the same padded row stride, its last-chunk padding zero."""
+    from kungfu_amd.ops.xent import cross_entropy
+
+    ld = (V + 7) // 8 * 8 + 8
+    g = torch.Generator(device="cuda").manual_seed(2)
+    base = (torch.randn(R, ld, device="cuda", generator=g) * 4).bfloat16()
+    base[:, V:] = 1e4  # must never be read as a class
+    x = base[:, :V]
+    lab = torch.randint(0, V, (R,), device="cuda", generator=g)
+    lab[::4] = -100
+    xg = x.detach().requires_grad_(True)
+    loss = cross_entropy(xg, lab)
+    loss.backward(torch.tensor(2.0, device="cuda"))
+    xr = x.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(xr, lab)
+    ref.backward(torch.tensor(2.0, device="cuda"))
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(xg.grad.float(), xr.grad.bfloat16().float(), rtol=1e-2, atol=1e-6)
+    from kungfu_amd._lib import hip
+
+    lse = hip().xent_forward(x, lab)[0]
+    dx = hip().xent_backward(x, lab, lse, torch.ones(1, device="cuda"))
+    assert dx.stride() == (ld, 1)
+    full = dx.as_strided((R, ld), (ld, 1))
+    assert full[:, V:(V + 7) // 8 * 8].abs().sum().item() == 0.0
+
+
+def test_vocab_projection_matches_fp32():
+    """ops.vocab.vocab_projection (gemm.hip ragged-N GEMM, padded logits rows) + cross_entropy vs
+    F.linear + F.cross_entropy in f32 on the same bf16 operands: loss, d h, d W, d b."""
+    from kungfu_amd.ops.vocab import vocab_projection
+    from kungfu_amd.ops.xent import cross_entropy
+
+    torch.manual_seed(5)
+    M, V, D = 300, 30522, 768
+    h = (torch.randn(4, M // 4, D, device="cuda")).bfloat16().requires_grad_(True)
+    w = (torch.randn(V, D, device="cuda") * 0.02).requires_grad_(True)  # f32 master, as the tied embedding
+    b = (torch.randn(V, device="cuda") * 0.1).requires_grad_(True)
+    lab = torch.randint(0, V, (4, M // 4), device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        logits = vocab_projection(h, w, b)
+        assert logits.shape == (4, M // 4, V) and logits.dtype == torch.bfloat16
+        loss = cross_entropy(logits, lab)
+    loss.backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr = w.detach().bfloat16().float().requires_grad_(True)
+    br = b.detach().bfloat16().float().requires_grad_(True)
+    lr = F.linear(hr, wr, br)
+    ref = F.cross_entropy(lr.reshape(-1, V), lab.reshape(-1))
+    ref.backward()
+    torch.testing.assert_close(logits.float(), lr.detach(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(loss.float(), ref, rtol=2e-3, atol=2e-3)
+    for got, want in ((h.grad, hr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        rel = ((got.float() - want).norm() / want.norm()).item()
+        assert rel < 2e-2, rel

@@ -228,3 +228,77 @@ def test_linear_fused_gelu_grad_matches_unfused():
     assert abs(la[1] - lb[1]) < 2e-3 * abs(la[1]), (la, lb)
     for x, y in zip(ga, gb):
         assert _rel(y, x) < 2e-2, _rel(y, x)
+
+
+@pytest.mark.parametrize("M,K,N", [(2560, 768, 30522), (300, 256, 1000), (17, 64, 9), (520, 768, 2304)])
+@pytest.mark.parametrize("bn", [128, 192, 256])
+def test_gemm_nt_ld_ragged_matches_fp32(M, K, N, bn):
+    """gemm_nt_ld: any N (B rows past N read zeros), C rows padded to ld; columns < N against the
+    fp32 product + bias; a row stride that is not a multiple of 8 is refused."""
+    H = _hip()
+    torch.manual_seed(4)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda").bfloat16()
+    ld = (N + 7) // 8 * 8 + 16
+    c = H.gemm_nt_ld(a, b, bias, ld, bn)
+    assert c.shape == (M, ld)
+    ref = a.float() @ b.float().t() + bias.float()
+    assert _rel(c[:, :N], ref) < 1e-2
+    c0 = H.gemm_nt_ld(a, b, None, 0, bn)
+    assert c0.shape == (M, (N + 7) // 8 * 8) and _rel(c0[:, :N], a.float() @ b.float().t()) < 1e-2
+    assert not H.gemm_nt_ld_supported(M, N, K, N + 1 if N % 8 == 0 else N)
+
+
+def test_bert_vocab_head_and_tied_direct_landing_match_stock():
+    """BERT's MLM head on ops/vocab.py (padded logits rows, hipBLASLt / gemm.hip) with the tied
+    embedding's two gradient producers landing straight in its flat slot (parallel.mixed.use_direct)
+    against the stock head (F.linear under autocast, autograd-summed tied gradient): loss and the
+    per-parameter flat gradients of the tied table, the other tables and the decoder bias."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
+    from kungfu_amd.ops import vocab
+    from kungfu_amd.parallel import mixed
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(on):
+        old = vocab._ENABLED, mixed._EMBED_DIRECT
+        vocab._ENABLED = mixed._EMBED_DIRECT = on
+        try:
+            torch.manual_seed(0)
+            m = BertForPreTraining(layers=2).cuda()
+            for l in m.layers:
+                l.dropout = 0.0
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
+                                                        named_parameters=m.named_parameters())
+            enable_bf16_shadow(m, opt)
+            g = torch.Generator(device="cuda").manual_seed(1)
+            batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
+            losses, grads = [], []
+            for _ in range(2):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = pretraining_loss(m, batch)
+                loss.backward()
+                opt.reducer.synchronize()
+                sp = opt.space
+                grads.append({n: sp.grad_view(sp.index(p)).clone() for n, p in
+                              (("tok", m.tok.weight), ("pos", m.pos.weight), ("typ", m.typ.weight),
+                               ("mlm_bias", m.mlm_bias))})
+                losses.append(loss.item())
+                opt.step()
+            torch.cuda.synchronize()
+            return losses, grads
+        finally:
+            vocab._ENABLED, mixed._EMBED_DIRECT = old
+
+    la, ga = run(False)
+    lb, gb = run(True)
+    for x, y in zip(la, lb):
+        assert abs(x - y) < 2e-3 * abs(x), (la, lb)
+    for x, y in zip(ga, gb):
+        for n in x:
+            assert y[n].abs().sum().item() > 0, n
+            assert _rel(y[n], x[n]) < 2e-2, (n, _rel(y[n], x[n]))

@@ -1,0 +1,13 @@
+#!/bin/bash
+# r5 t25: ragged-N vocabulary GEMM + padded-row cross-entropy: tests, MLM head micro-bench, BERT bench + profile
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_gemm.py tests/test_gpu_embedding.py > $O/r5t25_pytest.log 2>&1
+rc=$?; tail -1 $O/r5t25_pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $O/r5t25_pytest.log | head -20; exit $rc; }
+timeout -k 10 300 python -u tools/bench_mlm_head.py > $O/r5t25_mlm.log 2>&1 || { tail -5 $O/r5t25_mlm.log; exit 1; }
+cat $O/r5t25_mlm.log
+j() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])'; }
+timeout -k 10 400 python bench.py --model bert_base --optimizer gns --steps 20 --warmup 5 > $O/r5t25_bert.log 2>&1 || { tail -5 $O/r5t25_bert.log; exit 1; }
+echo "bert: $(tail -1 $O/r5t25_bert.log | j)"
+bash tools/gpu_prof.sh r5t25 bert_base > $O/r5t25_prof.log 2>&1 && head -24 $O/r5t25_bert_base_summary.md
