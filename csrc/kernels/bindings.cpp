@@ -86,18 +86,26 @@ void sgd_step(at::Tensor w, at::Tensor g, c10::optional<at::Tensor> m, c10::opti
 }
 
 void adam_step(at::Tensor w, at::Tensor g, at::Tensor m, at::Tensor v, double lr, c10::optional<at::Tensor> lr_t,
-               double b1, double b2, double eps, double wd, bool adamw, double gscale, at::Tensor step) {
+               double b1, double b2, double eps, double wd, bool adamw, double gscale, at::Tensor step,
+               c10::optional<at::Tensor> shadow) {
     for (auto *t : {&w, &g, &m, &v}) {
         check_gpu(*t, "adam buffer");
         TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == w.numel(), "adam_step: f32 buffers of equal size");
     }
     TORCH_CHECK(step.is_cuda() && step.scalar_type() == at::kFloat, "adam_step: step must be an f32 GPU tensor");
     const float *lrp = (lr_t && lr_t->defined()) ? lr_t->data_ptr<float>() : nullptr;
+    uint16_t *sh = nullptr;
+    if (shadow && shadow->defined()) {
+        TORCH_CHECK(shadow->is_cuda() && shadow->scalar_type() == at::kBFloat16 && shadow->is_contiguous() &&
+                        shadow->numel() == w.numel() && shadow->device() == w.device(),
+                    "adam_step: shadow must be a contiguous bf16 buffer of the weights' size");
+        sh = reinterpret_cast<uint16_t *>(shadow->data_ptr());
+    }
     c10::DeviceGuard gd(w.device());
     kfk::launch_adam(w.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), w.numel(),
                      static_cast<float>(lr), lrp, static_cast<float>(b1), static_cast<float>(b2),
                      static_cast<float>(eps), static_cast<float>(wd), adamw, static_cast<float>(gscale),
-                     step.data_ptr<float>(), stream_of(w, 0));
+                     step.data_ptr<float>(), stream_of(w, 0), sh);
 }
 
 void axpby(at::Tensor y, at::Tensor x, c10::optional<at::Tensor> z, double a, double b) {
@@ -2057,7 +2065,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sgd_step", &sgd_step, "K8: fused SGD/momentum/nesterov/wd step on flat f32 buffers", py::arg("w"),
           py::arg("g"), py::arg("m"), py::arg("shadow"), py::arg("lr"), py::arg("lr_t"), py::arg("mu"),
           py::arg("damp"), py::arg("wd"), py::arg("gscale"), py::arg("nesterov"), py::arg("first"));
-    m.def("adam_step", &adam_step, "fused Adam/AdamW step on flat f32 buffers");
+    m.def("adam_step", &adam_step, "fused Adam/AdamW step on flat f32 buffers (shadow: also bf16(w) there)",
+          py::arg("w"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("lr"), py::arg("lr_t"), py::arg("b1"),
+          py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("adamw"), py::arg("gscale"), py::arg("step"),
+          py::arg("shadow") = py::none());
     m.def("axpby", &axpby, "y = a*y + b*x (optionally also z = y)", py::arg("y"), py::arg("x"), py::arg("z"),
           py::arg("a"), py::arg("b"));
     m.def("scale_", &scale_, "x *= alpha");

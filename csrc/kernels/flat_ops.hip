@@ -197,7 +197,8 @@ template <bool ADAMW>
 __global__ __launch_bounds__(kBlock) void adam_f32x4(float4 *__restrict__ w, const float4 *__restrict__ g,
                                                      float4 *__restrict__ m, float4 *__restrict__ v, size_t n4,
                                                      float lr, const float *lr_dev, float b1, float b2, float eps,
-                                                     float wd, float gscale, const float *step_dev) {
+                                                     float wd, float gscale, const float *step_dev,
+                                                     ushort4 *__restrict__ shadow) {
     if (lr_dev) lr = *lr_dev;
     float t = *step_dev;
     float bc1 = 1.f - __powf(b1, t), bc2 = 1.f - __powf(b2, t);
@@ -222,13 +223,15 @@ __global__ __launch_bounds__(kBlock) void adam_f32x4(float4 *__restrict__ w, con
         w[i] = wv;
         m[i] = mv;
         v[i] = vv;
+        // the bf16 compute shadow of the new weights (parallel/flat.py: the forward's cast is skipped)
+        if (shadow) shadow[i] = make_ushort4(f32_to_bf16(pw[0]), f32_to_bf16(pw[1]), f32_to_bf16(pw[2]), f32_to_bf16(pw[3]));
     }
 }
 
 template <bool ADAMW>
 __global__ void adam_f32_tail(float *w, const float *g, float *m, float *v, size_t begin, size_t n, float lr,
                               const float *lr_dev, float b1, float b2, float eps, float wd, float gscale,
-                              const float *step_dev) {
+                              const float *step_dev, uint16_t *shadow) {
     if (lr_dev) lr = *lr_dev;
     size_t i = begin + blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
@@ -243,6 +246,7 @@ __global__ void adam_f32_tail(float *w, const float *g, float *m, float *v, size
     m[i] = mm;
     v[i] = vv;
     w[i] = ww - (lr / bc1) * mm / (sqrtf(vv) * rsqrtf(bc2) + eps);
+    if (shadow) shadow[i] = f32_to_bf16(w[i]);
 }
 
 // ---------------------------------------------------------------- axpby / scale / square
@@ -414,18 +418,23 @@ void launch_sgd(float *w, const float *g, float *m, uint16_t *shadow, size_t n, 
 }
 
 void launch_adam(float *w, const float *g, float *m, float *v, size_t n, float lr, const float *lr_dev, float b1,
-                 float b2, float eps, float wd, bool adamw, float gscale, const float *step_dev, hipStream_t s) {
+                 float b2, float eps, float wd, bool adamw, float gscale, const float *step_dev, hipStream_t s,
+                 uint16_t *shadow) {
     if (n == 0) return;
-    size_t n4 = (aligned16(w) && aligned16(g) && aligned16(m) && aligned16(v)) ? n / 4 : 0;
+    size_t n4 = (aligned16(w) && aligned16(g) && aligned16(m) && aligned16(v) &&
+                 (!shadow || (reinterpret_cast<uintptr_t>(shadow) & 7u) == 0))
+                    ? n / 4
+                    : 0;
 #define KFK_ADAM(AW)                                                                                               \
     do {                                                                                                           \
         if (n4)                                                                                                    \
             adam_f32x4<AW><<<grid_for(n4), kBlock, 0, s>>>(                                                        \
                 reinterpret_cast<float4 *>(w), reinterpret_cast<const float4 *>(g), reinterpret_cast<float4 *>(m), \
-                reinterpret_cast<float4 *>(v), n4, lr, lr_dev, b1, b2, eps, wd, gscale, step_dev);                 \
+                reinterpret_cast<float4 *>(v), n4, lr, lr_dev, b1, b2, eps, wd, gscale, step_dev,                  \
+                reinterpret_cast<ushort4 *>(shadow));                                                              \
         if (n4 * 4 < n)                                                                                            \
             adam_f32_tail<AW><<<static_cast<int>((n - n4 * 4 + kBlock - 1) / kBlock), kBlock, 0, s>>>(              \
-                w, g, m, v, n4 * 4, n, lr, lr_dev, b1, b2, eps, wd, gscale, step_dev);                             \
+                w, g, m, v, n4 * 4, n, lr, lr_dev, b1, b2, eps, wd, gscale, step_dev, shadow);                     \
     } while (0)
     if (adamw) KFK_ADAM(true);
     else KFK_ADAM(false);

@@ -63,9 +63,11 @@ void launch_sgd(float *w, const float *g, float *m, uint16_t *shadow, size_t n, 
                 float mu, float damp, float wd, float gscale, bool nesterov, bool first, hipStream_t s);
 
 // Fused Adam / AdamW step on flat f32 buffers.  step_dev points at a float
-// step counter already incremented for this step (bias correction on device).
+// step counter already incremented for this step (bias correction on device).  shadow (optional):
+// also writes bf16(w) there -- the bf16 compute copy of the new weights.
 void launch_adam(float *w, const float *g, float *m, float *v, size_t n, float lr, const float *lr_dev, float b1,
-                 float b2, float eps, float wd, bool adamw, float gscale, const float *step_dev, hipStream_t s);
+                 float b2, float eps, float wd, bool adamw, float gscale, const float *step_dev, hipStream_t s,
+                 uint16_t *shadow = nullptr);
 
 // K3/K4: y = a*y + b*x (f32 or bf16), optionally also writing the result to z.
 void launch_axpby(void *y, const void *x, void *z, size_t n, float a, float b, int dtype, hipStream_t s);

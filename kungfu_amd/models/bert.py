@@ -61,11 +61,11 @@ class BertForPreTraining(nn.Module):
         self.tok = nn.Embedding(vocab, d)
         self.pos = nn.Embedding(max_pos, d)
         self.typ = nn.Embedding(type_vocab, d)
-        self.ln = nn.LayerNorm(d, eps=1e-12)
-        self.layers = nn.ModuleList([BertLayer(d, heads, ffn) for _ in range(layers)])
-        self.mlm_dense = nn.Linear(d, d)
         from ..ops.layernorm import AddLayerNorm
 
+        self.ln = AddLayerNorm(d, eps=1e-12)  # embedding LayerNorm (an nn.LayerNorm: same parameters / state dict)
+        self.layers = nn.ModuleList([BertLayer(d, heads, ffn) for _ in range(layers)])
+        self.mlm_dense = nn.Linear(d, d)
         self.mlm_ln = AddLayerNorm(d, eps=1e-12)  # HIP LayerNorm on the bf16 head (torch's off the GPU path)
         self.mlm_bias = nn.Parameter(torch.zeros(vocab))
         self.nsp = nn.Linear(d, 2)
@@ -87,10 +87,14 @@ class BertForPreTraining(nn.Module):
         pos = torch.arange(S, device=ids.device)
         types = torch.zeros_like(ids) if types is None else types
         # scatter-add embedding gradients (ops/embedding.py): fixed-shape, graph-replayable
-        x = self.ln(embedding(ids, self.tok.weight) + embedding(pos, self.pos.weight)[None]
-                    + embedding(types, self.typ.weight))
-        if torch.is_autocast_enabled(x.device.type) and x.is_cuda:
-            x = x.to(torch.get_autocast_dtype(x.device.type))  # bf16 residual stream from here on
+        e = embedding(ids, self.tok.weight) + embedding(pos, self.pos.weight)[None] + embedding(types, self.typ.weight)
+        if torch.is_autocast_enabled(e.device.type) and e.is_cuda:
+            # bf16 residual stream from here on: the f32 embedding sum is cast BEFORE its LayerNorm, which
+            # then runs on the HIP kernels (layernorm.hip: one pass each way, gamma/beta straight to the flat
+            # space) instead of torch's f32 LayerNorm (input-gradient + 12-block gamma/beta kernels: 88 us,
+            # plus the cast of its f32 output; r5t26)
+            e = e.to(torch.get_autocast_dtype(e.device.type))
+        x = self.ln(e)
         for layer in self.layers:
             x = layer(x)
         hs = x

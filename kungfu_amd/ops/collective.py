@@ -285,6 +285,9 @@ def all_reduce_with(x: torch.Tensor, tree: Sequence[int], op: str = "sum") -> to
 def inplace_broadcast_(x: torch.Tensor, name: Optional[str] = None) -> torch.Tensor:
     """Broadcast from rank 0 in place."""
     _ensure()
+    from ..parallel.flat import note_param_write
+
+    note_param_write()
     if x.is_cuda and not _gpu_host_staging():
         c = x if x.is_contiguous() else x.contiguous()
         _dev_comm().broadcast(c, root=0, stream=_cs())

@@ -144,8 +144,13 @@ class FusedAdam(torch.optim.Optimizer):
         if self._gpu:
             if not torch.cuda.is_current_stream_capturing():
                 self._lr_t.fill_(lr)
+            # the bf16 compute shadow is written by the same kernel (eager steps): the next forward's cast of
+            # the whole model is skipped (FlatParamSpace.mark_shadow_fresh; -0.14 ms per BERT-base step)
+            sh = sp.flat_shadow if (sp.flat_shadow is not None and not torch.cuda.is_current_stream_capturing()) else None
             hip().adam_step(sp.flat_param, sp.flat_grad, self.exp_avg, self.exp_avg_sq, lr, self._lr_t, b1, b2, eps,
-                            wd, self.adamw, self.grad_scale, self._step_t)
+                            wd, self.adamw, self.grad_scale, self._step_t, sh)
+            if sh is not None:
+                sp.mark_shadow_fresh()
         else:
             t = float(self._step_t.item())
             gr = sp.flat_grad * self.grad_scale

@@ -333,6 +333,9 @@ class _PairAveraging(KungFuOptimizer):
         cur = torch.cuda.current_stream(self.space.device)
         if done is not True:
             cur.wait_event(done)  # normally complete already: no stall
+        from ..parallel.flat import note_param_write
+
+        note_param_write()
         hip().axpby(self.space.flat_param, self._other, None, 0.5, 0.5)
         self.pulls += 1
         ev = torch.cuda.Event()

@@ -77,6 +77,7 @@ class FlatParamSpace:
         # gradient sink that direct-gradient autograd functions deliver to.
         self.flat_shadow: Optional[torch.Tensor] = None
         self.shadow_gen = 0  # bumped by every refresh_shadow (caches derived from the shadow key on it)
+        self._shadow_token = None  # set when an optimizer step wrote the shadow with the weights (mark_shadow_fresh)
         self.sink = None
 
     @staticmethod
@@ -111,9 +112,25 @@ class FlatParamSpace:
             self.flat_shadow = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
             self.refresh_shadow()
 
+    def _param_token(self):
+        # what a later in-place weight update would change: the parameters' and the flat buffer's
+        # version counters, and the epoch of the non-autograd writers (note_param_write)
+        return (sum(p._version for p in self.params), self.flat_param._version, _PARAM_EPOCH[0])
+
+    def mark_shadow_fresh(self):
+        """The optimizer step that just ran also wrote flat_shadow = bf16(new flat_param) (ops.adam_step's
+        shadow output): the next refresh_shadow skips its cast kernel unless the weights changed since."""
+        self._shadow_token = self._param_token()
+
     @torch.no_grad()
     def refresh_shadow(self):
-        """flat_shadow = bf16(flat_param): one cast kernel for the whole model."""
+        """flat_shadow = bf16(flat_param): one cast kernel for the whole model (none when the optimizer
+        step already wrote it and nothing touched the weights since, see mark_shadow_fresh)."""
+        tok, self._shadow_token = self._shadow_token, None
+        if (self.flat_shadow is not None and tok is not None and tok == self._param_token()
+                and not (self.flat_param.is_cuda and torch.cuda.is_current_stream_capturing())):
+            self.shadow_gen += 1
+            return
         if self.flat_shadow is not None:
             # Version counter preserved: shadow views saved by a still-pending
             # backward (gradient accumulation over several forwards) stay valid;
@@ -155,8 +172,18 @@ class FlatParamSpace:
         return list(zip(self.params, self.offsets))
 
 
+_PARAM_EPOCH = [0]
+
+
+def note_param_write() -> None:
+    """A weight buffer was (or may have been) written outside autograd's version counters (a HIP kernel,
+    a collective): optimizer-written bf16 shadows are stale (FlatParamSpace.refresh_shadow recasts)."""
+    _PARAM_EPOCH[0] += 1
+
+
 def axpby_(y: torch.Tensor, x: torch.Tensor, a: float, b: float) -> torch.Tensor:
     """y <- a*y + b*x: one fused HIP kernel (K3/K4) on GPU, torch ops on CPU."""
+    note_param_write()
     if y.is_cuda:
         from .._lib import hip
 

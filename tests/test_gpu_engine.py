@@ -722,3 +722,33 @@ def test_segmented_capture_with_emulated_comm_matches_eager(monkeypatch):
     lg, pg = run(True)
     print("eager", le, "\ngraph", lg)
     assert le == lg and torch.equal(pe, pg), (le, lg)
+
+
+def test_fused_adam_writes_the_bf16_shadow():
+    """FusedAdam's kernel writes bf16(new weights) into the space's shadow (exactly the cast
+    refresh_shadow would produce) and the next refresh skips its cast; an in-place edit of a
+    weight after the step makes it recast."""
+    from kungfu_amd.optimizers.fused import FusedAdam
+    from kungfu_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 1000), torch.nn.Linear(1000, 3)).cuda()
+    sp = FlatParamSpace(list(m.parameters()))
+    sp.enable_shadow()
+    opt = FusedAdam(sp, lr=1e-2, weight_decay=0.01)
+    for _ in range(2):
+        opt.zero_grad()
+        m(torch.randn(8, 64, device="cuda")).square().sum().backward()
+        opt.step()
+        torch.cuda.synchronize()
+        assert torch.equal(sp.flat_shadow, sp.flat_param.to(torch.bfloat16))
+        gen = sp.shadow_gen
+        sp.flat_shadow.zero_()
+        sp.refresh_shadow()  # skipped: the step wrote it
+        assert sp.shadow_gen == gen + 1 and sp.flat_shadow.abs().sum().item() == 0
+        sp.refresh_shadow()
+    opt.step()
+    with torch.no_grad():
+        m[0].weight.mul_(3.0)
+    sp.refresh_shadow()
+    assert torch.equal(sp.flat_shadow, sp.flat_param.to(torch.bfloat16))
