@@ -72,6 +72,18 @@ gs = torch.zeros(V, D, device="cuda")
 torch.addmm(gs, dl.t(), h, out_dtype=torch.float32, out=gs)
 torch.addmm(gs, dl.t(), h, out_dtype=torch.float32, out=gs)
 print("f32 accumulate rel err %.2e" % ((gs - 2 * (dl.float().t() @ h.float())).norm() / gs.norm()).item(), flush=True)
+ref_dh = (dlp[:, :V].float() @ w.float())
+for S in (2, 3, 6):
+    Kc = V // S
+    A = dlp.as_strided((S, M, Kc), (Kc, dlp.stride(0), 1))
+    B = w.as_strided((S, Kc, D), (Kc * D, D, 1))
+    cands["dgrad split-K bmm S=%d bf16" % S] = (lambda A=A, B=B: torch.bmm(A, B).sum(0))
+    try:
+        r = torch.bmm(A, B, out_dtype=torch.float32).sum(0)
+        print("split S=%d f32 rel err %.2e" % (S, ((r - ref_dh).norm() / ref_dh.norm()).item()), flush=True)
+        cands["dgrad split-K bmm S=%d f32" % S] = (lambda A=A, B=B: torch.bmm(A, B, out_dtype=torch.float32).sum(0))
+    except Exception as e:  # noqa: BLE001
+        print("bmm out_dtype:", str(e)[:200], flush=True)
 dlT = dl.t().contiguous()  # [V, M]: a transposed cross-entropy gradient
 cands["dgrad blas from dlT (mm(dlT^T, W))"] = lambda: torch.mm(dlT.t(), w)
 cands["dgrad blas W^T dlT -> dh^T"] = lambda: torch.mm(w.t(), dlT)
