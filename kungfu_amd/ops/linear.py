@@ -81,6 +81,7 @@ def residual_link(x: torch.Tensor):
 
 
 _DIRECT_WGRAD = True  # module switch (tests)
+_WGRAD_SIDE = os.environ.get("KUNGFU_LINEAR_WGRAD_SIDE", "0") == "1"  # A/B in progress (r5t30)
 # set_gemm_enabled(True): forward (x W^T + b) and data gradient (dy W, with W^T from the flat space's
 # per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt -- measured
 # slower (profiles/r4_gemm_nt.md), so off and not an environment knob any more (round 5)
@@ -186,8 +187,29 @@ class _LinearFn(torch.autograd.Function):
             # (deterministic, accumulating): no bf16 weight gradient, no landing pass
             space, i = tgt
             gv = space.grad_view(i)
-            hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1, out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
-                             accumulate=True, atomics=False)  # deterministic partials + reduce (atomics: -3 %, r4t29)
+
+            def wg():
+                hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1,
+                                 out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
+                                 accumulate=True, atomics=False)  # deterministic partials + reduce (atomics: -3 %, r4t29)
+
+            if _WGRAD_SIDE and dy2.is_cuda and not torch.cuda.is_current_stream_capturing():
+                # on the side stream: the split-K kernel and its (memory-bound) reduce overlap the next
+                # layers' data-gradient GEMMs; the bucket launch / end of backward joins it
+                from ..parallel.mixed import SideStream
+
+                main = torch.cuda.current_stream()
+                side = SideStream.stream(dy2.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    wg()
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                dy2.record_stream(side)
+                x2.record_stream(side)
+                SideStream._pending.append(ev)
+            else:
+                wg()
             space.sink.put_direct(i)
         elif ctx.needs_input_grad[1]:
             dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)

@@ -407,6 +407,9 @@ class GradReducer:
     @traced("ssgd::bucket_launch")
     def _launch(self, b: Bucket):
         b.launched = True
+        from .mixed import SideStream
+
+        SideStream.join()  # direct weight gradients reduced into this bucket on the side stream
         self._land(b)
         if self.skip:
             return
