@@ -81,7 +81,9 @@ def residual_link(x: torch.Tensor):
 
 
 _DIRECT_WGRAD = True  # module switch (tests)
-_WGRAD_SIDE = os.environ.get("KUNGFU_LINEAR_WGRAD_SIDE", "0") == "1"  # A/B in progress (r5t30)
+# direct weight gradients on the side stream (module switch): BERT-base + GNS 16.57-16.61 -> 16.45 ms/step
+# on one box, two interleaved rounds (r5t30); the conv weight gradients measured the other way (mixed.SideStream)
+_WGRAD_SIDE = True
 # set_gemm_enabled(True): forward (x W^T + b) and data gradient (dy W, with W^T from the flat space's
 # per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt -- measured
 # slower (profiles/r4_gemm_nt.md), so off and not an environment knob any more (round 5)
