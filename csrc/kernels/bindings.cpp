@@ -1764,6 +1764,28 @@ void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy, int64_t 
 // gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
 // C[M, ldc] (only columns < N written, the chunk holding column N - 1 whole) = a . b^T (+ bias), for a
 // ragged N (BERT's 30,522-entry vocabulary): rows of C padded to ldc (a multiple of 8) stay 16-byte aligned
+// (u, h): u = a . b^T + bias and h = gelu(u) (erf) in one launch (a linear layer feeding a GELU)
+std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias, int64_t bn) {
+    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
+                "gemm_nt_gelu: bf16 GPU tensors");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+                "gemm_nt_gelu: a [M, K], b [N, K] contiguous");
+    const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+    TORCH_CHECK(kfk::gemm_nt_supported(M, N, K), "gemm_nt_gelu: unsupported shape M=", M, " N=", N, " K=", K);
+    TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kBFloat16 && bias.numel() == N && bias.is_contiguous(),
+                "gemm_nt_gelu: bias bf16 [N]");
+    auto u = at::empty({M, N}, a.options());
+    auto h = at::empty({M, N}, a.options());
+    c10::DeviceGuard gd(a.device());
+    kfk::launch_gemm_nt_gelu(reinterpret_cast<const uint16_t *>(a.data_ptr()),
+                             reinterpret_cast<const uint16_t *>(b.data_ptr()), reinterpret_cast<uint16_t *>(u.data_ptr()),
+                             reinterpret_cast<uint16_t *>(h.data_ptr()),
+                             reinterpret_cast<const uint16_t *>(bias.data_ptr()), static_cast<int>(M),
+                             static_cast<int>(N), static_cast<int>(K), static_cast<int>(bn),
+                             c10::hip::getCurrentHIPStream().stream());
+    return {u, h};
+}
+
 at::Tensor gemm_nt_ld(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, int64_t ldc, int64_t bn) {
     TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
                 "gemm_nt_ld: bf16 GPU tensors");
@@ -2225,6 +2247,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemm_nt_ld", &gemm_nt_ld, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("ldc") = 0,
           py::arg("bn") = 256, "C [M, ldc] = a . b^T (+ bias) for any N (columns >= N of C unspecified)");
     m.def("gemm_nt_ld_supported", &kfk::gemm_nt_ld_supported);
+    m.def("gemm_nt_gelu", &gemm_nt_gelu, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("bn") = 0,
+          "(u, h): u = a . b^T + bias, h = gelu(u), one launch");
     m.def("gemm_nt_gelu_grad", &gemm_nt_gelu_grad, "(du, db): the GELU backward fused into the data-gradient NT GEMM "
           "(du = bf16(bf16(a . b^T) * gelu'(u)), db = column sums of du)", py::arg("a"), py::arg("b"), py::arg("u"),
           py::arg("bias_dtype") = py::none());

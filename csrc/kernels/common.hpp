@@ -105,4 +105,15 @@ __device__ __forceinline__ float gelu_grad_fast(float x) {
     return cdf + x * (e * 0.39894228040143268f);
 }
 
+// Phi(x) = 0.5 (1 + erf(x / sqrt 2)) by the same Abramowitz-Stegun form (one exponential)
+__device__ __forceinline__ float gelu_cdf_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float e = __expf(-0.5f * x * x);
+    const float t = __frcp_rn(1.f + 0.3275911f * z);
+    const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f +
+                                                                                            t * 1.061405429f))));
+    const float erf_abs = 1.f - poly * e;
+    return 0.5f * (1.f + (x < 0.f ? -erf_abs : erf_abs));
+}
+
 }  // namespace kfk

@@ -30,7 +30,7 @@ const uint32_t *dropout_seed_base();
 
 // gemm.hip: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (+ C) in bf16, f32 accumulation, on a
 // 256 x bn tile (bn 128 | 192 | 256, <= 0: by shape) with a 3-slab-deep LDS-DMA pipeline.
-constexpr int kGemmBias = 1, kGemmAccum = 2, kGemmGeluGrad = 4;
+constexpr int kGemmBias = 1, kGemmAccum = 2, kGemmGeluGrad = 4, kGemmGelu = 8;
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 int gemm_nt_pick_bn(int64_t M, int64_t N);
 void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
@@ -48,6 +48,10 @@ int gemm_nt_gelu_grad_rows(int M);
 void launch_gemm_nt_gelu_grad(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *u, float *part, int M,
                               int N, int K, hipStream_t s);
 void launch_colsum_fold(const float *part, int rows, int O, float *out_f32, uint16_t *out_bf16, hipStream_t s);
+// u = a . b^T + bias (bf16, into c) and h = gelu(u) (erf GELU of the bf16 u, into h) in one launch: a linear
+// layer whose only consumer is a GELU (BERT's FC1)
+void launch_gemm_nt_gelu(const uint16_t *a, const uint16_t *b, uint16_t *c, uint16_t *h, const uint16_t *bias, int M,
+                         int N, int K, int bn, hipStream_t s);
 
 // comm_emu.hip: the local footprint of one all-reduce of `bytes` (bench.py --emulate-comm):
 // `ctas` workgroups copying `traffic_bytes` of the bucket into `scratch` (>= bytes), paced over

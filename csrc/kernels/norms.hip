@@ -317,17 +317,6 @@ __global__ __launch_bounds__(256) void colsum_stage1(const uint4 *__restrict__ x
 }
 
 
-// Phi(x) = 0.5 (1 + erf(x / sqrt 2)) by the same Abramowitz-Stegun form (one exponential)
-__device__ __forceinline__ float gelu_cdf_fast(float x) {
-    const float z = fabsf(x) * 0.70710678118654752f;
-    const float e = __expf(-0.5f * x * x);
-    const float t = __frcp_rn(1.f + 0.3275911f * z);
-    const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f +
-                                                                                            t * 1.061405429f))));
-    const float erf_abs = 1.f - poly * e;
-    return 0.5f * (1.f + (x < 0.f ? -erf_abs : erf_abs));
-}
-
 // y = x Phi(x) (erf GELU, torch's F.gelu default) on bf16, 16-byte vectors, two per trip.  Both this
 // and torch's erff kernel are vector-issue bound (~2.5 TB/s on BERT-base's 16 K x 3072 FC1 output);
 // measured 0.6 % slower end to end than torch's (KUNGFU_GELU_FWD A/B, r4t20): off by default.

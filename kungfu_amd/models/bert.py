@@ -28,6 +28,7 @@ class BertLayer(nn.Module):
         # parameters and state_dict keys, torch composition off the GPU fast path
         self.ln1 = AddLayerNorm(d, eps=1e-12)
         self.fc1 = nn.Linear(d, ffn)
+        self.fc1._kf_gelu_out = True  # its only consumer is the GELU: u and gelu(u) from one GEMM (ops/linear.py)
         self.fc2 = nn.Linear(ffn, d)
         self.ln2 = AddLayerNorm(d, eps=1e-12)
         self.dropout = dropout

@@ -140,7 +140,8 @@ def _linear_forward(self, x):
     # reduces its splits straight into the weight's flat f32 gradient slot
     w = shadow(self.weight)
     return linear(x, w, shadow(self.bias) if self.bias is not None else None,
-                  grad_target=direct_target(self.weight) if w is not self.weight else None)
+                  grad_target=direct_target(self.weight) if w is not self.weight else None,
+                  gelu_out=getattr(self, "_kf_gelu_out", False))
 
 
 class SideStream:

@@ -302,3 +302,63 @@ def test_bert_vocab_head_and_tied_direct_landing_match_stock():
         for n in x:
             assert y[n].abs().sum().item() > 0, n
             assert _rel(y[n], x[n]) < 2e-2, (n, _rel(y[n], x[n]))
+
+
+def test_gemm_nt_gelu_matches_fp32():
+    """gemm_nt_gelu: u = a . b^T + bias and h = gelu(u) (erf, of the bf16 u) against fp32 references."""
+    H = _hip()
+    torch.manual_seed(6)
+    for M, K, N, bn in ((4096, 768, 3072, 256), (1000, 256, 768, 192), (300, 128, 256, 128)):
+        a = torch.randn(M, K, device="cuda").bfloat16()
+        b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+        bias = torch.randn(N, device="cuda").bfloat16()
+        u, h = H.gemm_nt_gelu(a, b, bias, bn)
+        ref = a.float() @ b.float().t() + bias.float()
+        assert _rel(u, ref) < 1e-2
+        assert (h.float() - F.gelu(u.float())).abs().max().item() < 2e-2
+        assert _rel(h, F.gelu(u.float())) < 5e-3
+
+
+def test_bert_fc1_gelu_gemm_matches_library_path():
+    """BERT with FC1 + GELU on one gemm.hip launch (ops.linear._GELU_FWD) vs hipBLASLt + torch GELU:
+    losses and the flat gradient over two AdamW steps."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
+    from kungfu_amd.ops import linear as lin
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+
+    kf.init()
+
+    def run(on):
+        old, lin._GELU_FWD = lin._GELU_FWD, on
+        try:
+            torch.manual_seed(0)
+            m = BertForPreTraining(layers=2).cuda()
+            for l in m.layers:
+                l.dropout = 0.0
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
+                                                        named_parameters=m.named_parameters())
+            enable_bf16_shadow(m, opt)
+            g = torch.Generator(device="cuda").manual_seed(1)
+            batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
+            losses, grads = [], []
+            for _ in range(2):
+                opt.zero_grad()
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    loss = pretraining_loss(m, batch)
+                loss.backward()
+                opt.reducer.synchronize()
+                grads.append(opt.space.flat_grad.clone())
+                losses.append(loss.item())
+                opt.step()
+            torch.cuda.synchronize()
+            return losses, grads
+        finally:
+            lin._GELU_FWD = old
+
+    la, ga = run(False)
+    lb, gb = run(True)
+    for x, y in zip(la, lb):
+        assert abs(x - y) < 2e-3 * abs(x), (la, lb)
+    for x, y in zip(ga, gb):
+        assert _rel(y, x) < 3e-2, _rel(y, x)
