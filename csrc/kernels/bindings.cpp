@@ -794,8 +794,9 @@ std::vector<at::Tensor> attention_forward(at::Tensor qkv, int64_t heads, double 
     return {out, lse};
 }
 
-at::Tensor attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at::Tensor dout, int64_t heads,
-                              double scale, int64_t seed, double p_drop) {
+std::vector<at::Tensor> attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at::Tensor dout,
+                                           int64_t heads, double scale, int64_t seed, double p_drop,
+                                           c10::optional<at::ScalarType> bias_dtype) {
     TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
                     qkv.size(2) == 3 * heads * 64 && kfk::attention_supported(qkv.size(1), 64),
                 "attention_backward: qkv must be a contiguous bf16 [B, S, 3*H*64] GPU tensor with S in {64, 128}");
@@ -809,12 +810,28 @@ at::Tensor attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at
                 "attention_backward: lse must be the forward's [B, H, S] f32");
     c10::DeviceGuard gd(qkv.device());
     auto dqkv = at::empty_like(qkv);
+    // bias_dtype: also the column sums of dqkv (the qkv projection's bias gradient): per-(sequence, wave)
+    // partials from the kernel, folded in a fixed order (launch_colsum_fold)
+    at::Tensor part, db;
+    const int O = 3 * H * 64;
+    if (bias_dtype) {
+        TORCH_CHECK(*bias_dtype == at::kFloat || *bias_dtype == at::kBFloat16, "attention_backward: bias dtype");
+        part = at::empty({static_cast<int64_t>(kfk::attention_bwd_partial_rows(B, S)), O},
+                         qkv.options().dtype(at::kFloat));
+        db = at::empty({O}, qkv.options().dtype(*bias_dtype));
+    }
     kfk::launch_attention_backward(reinterpret_cast<const uint16_t *>(qkv.data_ptr()),
                                    reinterpret_cast<const uint16_t *>(out.data_ptr()), lse.data_ptr<float>(),
                                    reinterpret_cast<const uint16_t *>(dout.data_ptr()),
                                    reinterpret_cast<uint16_t *>(dqkv.data_ptr()), B, S, H, static_cast<float>(scale),
-                                   static_cast<uint32_t>(seed), static_cast<float>(p_drop), stream_of(qkv, 0));
-    return dqkv;
+                                   static_cast<uint32_t>(seed), static_cast<float>(p_drop), stream_of(qkv, 0),
+                                   bias_dtype ? part.data_ptr<float>() : nullptr);
+    if (bias_dtype)
+        kfk::launch_colsum_fold(part.data_ptr<float>(), static_cast<int>(part.size(0)), O,
+                                *bias_dtype == at::kFloat ? db.data_ptr<float>() : nullptr,
+                                *bias_dtype == at::kBFloat16 ? reinterpret_cast<uint16_t *>(db.data_ptr()) : nullptr,
+                                stream_of(qkv, 0));
+    return {dqkv, db};
 }
 
 static void check_bias_act(const at::Tensor &y, const char *name) {
@@ -2187,7 +2204,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("qkv"), py::arg("heads"), py::arg("scale"), py::arg("seed"), py::arg("p_drop"));
     m.def("attention_backward", &attention_backward, "fused self-attention backward -> dqkv", py::arg("qkv"),
           py::arg("out"), py::arg("lse"), py::arg("dout"), py::arg("heads"), py::arg("scale"), py::arg("seed"),
-          py::arg("p_drop"));
+          py::arg("p_drop"), py::arg("bias_dtype") = py::none());
     m.def("conv_wgrad_max_pixels", &kfk::conv_wgrad_max_pixels, py::arg("N"), py::arg("H"), py::arg("W"),
           py::arg("Cin"), py::arg("Cout"), py::arg("ks"), py::arg("stride"));
     m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {

@@ -503,6 +503,9 @@ void launch_attention_forward(const uint16_t *qkv, uint16_t *out, float *lse, in
 // dqkv [B, S, 3, H, 64] (every element written)
 void launch_attention_backward(const uint16_t *qkv, const uint16_t *out, const float *lse, const uint16_t *dout,
                                uint16_t *dqkv, int B, int S, int H, float scale, uint32_t seed, float p_drop,
-                               hipStream_t s);
+                               hipStream_t s, float *bsum = nullptr);
+// rows of the backward's optional column-sum partials (bsum: [rows][3 * H * 64] f32, every entry written):
+// the column sums of dqkv as stored -- the bias gradient of the projection that produced qkv
+int attention_bwd_partial_rows(int B, int S);
 
 }  // namespace kfk

@@ -42,7 +42,8 @@ class BertLayer(nn.Module):
         qkv = self.qkv(x)
         if mask is None:
             # fused HIP attention straight from / into the projections' layouts (SDPA off that path)
-            a = self_attention(qkv, self.heads, p)
+            # qkv's only consumer: the attention backward also forms the projection's bias gradient
+            a = self_attention(qkv, self.heads, p, bias_link=True)
         else:
             q, k, v = qkv.view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)

@@ -362,3 +362,23 @@ def test_bert_fc1_gelu_gemm_matches_library_path():
         assert abs(x - y) < 2e-3 * abs(x), (la, lb)
     for x, y in zip(ga, gb):
         assert _rel(y, x) < 3e-2, _rel(y, x)
+
+
+@pytest.mark.parametrize("S", [128, 64])
+def test_attention_backward_bias_sums_match_colsum(S):
+    """attention_backward(..., bias_dtype): the dqkv column sums formed inside the kernel equal the
+    two-stage column sum of the returned dqkv (f32 rounding), and dqkv itself is unchanged."""
+    H = _hip()
+    torch.manual_seed(7)
+    B, NH = 6, 12
+    qkv = (torch.randn(B, S, 3 * NH * 64, device="cuda") * 0.5).bfloat16()
+    out, lse = H.attention_forward(qkv, NH, 0.125, 11, 0.1)
+    dout = torch.randn(B, S, NH * 64, device="cuda").bfloat16()
+    d0, none = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1)
+    assert none is None
+    d1, db = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1, torch.float32)
+    assert torch.equal(d0, d1)
+    ref = d1.float().reshape(-1, 3 * NH * 64).sum(0)
+    torch.testing.assert_close(db, ref, rtol=1e-4, atol=1e-3)
+    _, dbb = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1, torch.bfloat16)
+    assert dbb.dtype == torch.bfloat16 and _rel(dbb, ref) < 1e-2
