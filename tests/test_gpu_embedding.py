@@ -24,7 +24,11 @@ def test_embedding_backward_matches_torch(V, D, shape, dy_dtype):
     hip().embedding_backward(grad, ids.reshape(-1), dy)
     w = torch.zeros(V, D, device="cuda", requires_grad=True)
     F.embedding(ids, w).backward(dy.float())
-    torch.testing.assert_close(grad, w.grad, rtol=1e-5, atol=1e-4)
+    # f32 atomics: the summation order is run-dependent.  A row hit n times carries ~eps * sqrt(n) * |row sum|
+    # of order noise (BERT segment ids: 8,192 hits per row, sums ~90 -> ~5e-4), so the tolerance scales with it
+    n = int(torch.bincount(ids.reshape(-1).clamp_min(0), minlength=V).max())
+    atol = max(1e-4, 4e-7 * n ** 0.5 * float(w.grad.abs().max()))
+    torch.testing.assert_close(grad, w.grad, rtol=1e-5, atol=atol)
 
 
 def test_embedding_backward_skips_out_of_range_ids():
