@@ -2264,6 +2264,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemm_nt_ld", &gemm_nt_ld, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("ldc") = 0,
           py::arg("bn") = 256, "C [M, ldc] = a . b^T (+ bias) for any N (columns >= N of C unspecified)");
     m.def("gemm_nt_ld_supported", &kfk::gemm_nt_ld_supported);
+    m.def("set_layernorm_bwd_rows_per_wave", &kfk::set_layernorm_bwd_rows_per_wave,
+          "rows per wave of the LayerNorm backward (grid sizing; A/B)");
     m.def("gemm_nt_gelu", &gemm_nt_gelu, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("bn") = 0,
           "(u, h): u = a . b^T + bias, h = gelu(u), one launch");
     m.def("gemm_nt_gelu_grad", &gemm_nt_gelu_grad, "(du, db): the GELU backward fused into the data-gradient NT GEMM "

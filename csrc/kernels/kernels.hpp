@@ -481,6 +481,7 @@ void launch_global_avgpool_backward(const uint16_t *dy, uint16_t *dx, int64_t N,
 // dgamma/dbeta (f32) through [blocks][2][D] f32 partials.
 bool layernorm_supported(int D);
 int layernorm_bwd_blocks(int64_t rows);
+void set_layernorm_bwd_rows_per_wave(int r);
 void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
                               uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st,
                               float p = 0.f, uint32_t seed = 0);

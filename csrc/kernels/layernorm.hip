@@ -274,9 +274,14 @@ bool layernorm_supported(int D) {
     return D % 256 == 0 && (g == 1 || g == 2 || g == 3 || g == 4 || g == 6 || g == 8 || g == 12 || g == 16);
 }
 
+// rows per wave of the backward (grid-stride): more rows -> fewer [blocks][NS][D] partials for the column
+// sums, fewer rows -> more waves in flight per CU (settable for A/B: set_layernorm_bwd_rows_per_wave)
+static int g_ln_bwd_rpw = 8;
+void set_layernorm_bwd_rows_per_wave(int r) { g_ln_bwd_rpw = r < 1 ? 1 : r; }
+
 int layernorm_bwd_blocks(int64_t rows) {
-    int64_t b = (rows + kLnWaves * 8 - 1) / (kLnWaves * 8);  // >= 8 rows per wave
-    if (b > 1024) b = 1024;
+    int64_t b = (rows + kLnWaves * g_ln_bwd_rpw - 1) / (kLnWaves * g_ln_bwd_rpw);
+    if (b > 4096) b = 4096;
     return static_cast<int>(b < 1 ? 1 : b);
 }
 
