@@ -260,10 +260,13 @@ def main():
     p.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="gradient dtype on the wire")
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
+    p.add_argument("--wgrad-side", type=int, default=0,
+                   help="1: fused-bottleneck conv weight gradients on a side stream (A/B switch)")
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--bf16-shadow", type=int, default=1,
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
-    p.add_argument("--lr", type=float, default=0.1)
+    p.add_argument("--lr", type=float, default=0.01,
+                   help="SGD learning rate; 0.01 = the reference benchmark's (benchmarks/system/benchmark_kungfu.py:99)")
     p.add_argument("--graph", type=int, default=-1,
                    help="1: capture the whole training step into a hipGraph after 3 eager steps and replay it "
                         "(kungfu_amd.parallel.graphs.GraphedStep; N > 1: graph segments with eager collectives); "
@@ -338,6 +341,10 @@ def main():
     torch.manual_seed(1234)  # same init everywhere (broadcast_parameters makes it exact)
 
     fused_bn = a.fused_bn
+    if a.wgrad_side:
+        from kungfu_amd.parallel.mixed import SideStream
+
+        SideStream.enabled = True
     if fused_bn < 0:
         from kungfu_amd.ops import fused_bn as fb
 
@@ -442,18 +449,24 @@ def main():
 
     t_w0 = time.time()
     first_loss = None
+    warm_losses = []
     for i in range(a.warmup):
         l0 = step().detach()  # no reference to the step's autograd graph outlives the step
+        warm_losses.append(float(l0))
         if i == 0:
             first_loss = float(l0)
     sync()
     warm_s = time.time() - t_w0
+    # the timed steps' losses: one 4-byte device copy per step (a replayed graph returns the same
+    # static tensor every step), read back after the timed region
+    loss_buf = torch.zeros(a.steps, dtype=torch.float32, device=dev)
 
     kf.run_barrier()
     sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         loss = step().detach()
+        loss_buf[i].copy_(loss)
     sync()
     kf.run_barrier()
     dt = time.perf_counter() - t0
@@ -524,6 +537,11 @@ def main():
     }
     if sync_algo and not consistent:
         print("bench.py: REPLICAS DIVERGED: per-rank checksums %s" % cks.tolist(), file=sys.stderr, flush=True)
+    losses = [round(v, 4) for v in loss_buf.tolist()]
+    if rank == 0 and first_loss is not None and losses and losses[-1] > first_loss:
+        print("bench.py: WARNING: the loss rose over the run (%.4f -> %.4f at lr %g): a numerics regression or "
+              "a learning rate too high for this synthetic batch" % (first_loss, losses[-1], a.lr),
+              file=sys.stderr, flush=True)
     metric, base_per_gpu = MODEL_BASELINES.get(a.model, (METRIC.replace("ResNet-50", a.model), None))
     if a.emulate_comm:  # a model, never the headline: say so in the metric itself
         metric = "MODEL (1 GPU, %d-rank comm emulated): %s" % (a.emulate_comm, metric)
@@ -565,6 +583,9 @@ def main():
             "warmup_s": round(warm_s, 1),
             "initial_loss": round(first_loss, 4) if first_loss is not None else None,
             "final_loss": round(float(loss.detach()), 4),
+            "lr": a.lr if not bert else None,
+            "warmup_losses": [round(v, 4) for v in warm_losses],
+            "losses": losses,
             "comm": comm_info,
         },
         "verify": verify,

@@ -354,7 +354,7 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
                 c10::optional<at::Tensor> out, int64_t variant, c10::optional<at::Tensor> bn_x,
                 c10::optional<at::Tensor> bn_fcoef, c10::optional<at::Tensor> bn_mask,
                 c10::optional<at::Tensor> bias, bool gate, c10::optional<at::Tensor> acc_mask, bool acc_even,
-                c10::optional<at::Tensor> fin, c10::optional<at::Tensor> pre_coef) {
+                c10::optional<at::Tensor> fin) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                     x.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv: x must be a 4-D channels_last bf16 GPU tensor");
@@ -433,16 +433,6 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
         epi |= kfk::kEpiFwdStats;
     }
     TORCH_CHECK(!(epi & kfk::kEpiFwdStats) || !(epi & kfk::kEpiAccum), "conv: stats + accumulate unsupported");
-    if (pre_coef && pre_coef->defined()) {
-        // x is a BN's PRE-normalisation input: relu(x * scale + shift) applied to the A operand on load
-        TORCH_CHECK((epi == 0 || epi == kfk::kEpiFwdStats) && C % 64 == 0 && C <= 1024,
-                    "conv: pre_coef works with the plain / statistics epilogue and Cin % 64 == 0, <= 1024");
-        TORCH_CHECK(pre_coef->is_cuda() && pre_coef->scalar_type() == at::kFloat && pre_coef->is_contiguous() &&
-                        pre_coef->numel() >= 2 * C && pre_coef->device() == x.device(),
-                    "conv: pre_coef must be a contiguous f32 [scale(Cin); shift(Cin)] tensor on x's device");
-        ea.pcoef = pre_coef->data_ptr<float>();
-        epi |= kfk::kEpiPreBN;
-    }
     if (acc_mask && acc_mask->defined()) {
         // out = out * acc_mask + conv (out: a raw ReLU-output gradient, acc_mask: that ReLU's bits)
         TORCH_CHECK(accum && acc_mask->scalar_type() == at::kByte && acc_mask->numel() == y.numel() / 8 &&
@@ -2129,7 +2119,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("out") = py::none(), py::arg("variant") = -1, py::arg("bn_x") = py::none(),
           py::arg("bn_fcoef") = py::none(), py::arg("bn_mask") = py::none(), py::arg("bias") = py::none(),
           py::arg("gate") = false, py::arg("acc_mask") = py::none(), py::arg("acc_even") = false,
-          py::arg("fin") = py::none(), py::arg("pre_coef") = py::none());
+          py::arg("fin") = py::none());
     m.def("stem3_pack_weight", &stem3_pack_weight, "pack [32, 3, KH, KW] stem weights for stem3_forward");
     m.def("stem3_forward", &stem3_forward, "small image-stem conv (<= 4x4 window, 3 -> 32 channels) with the BN-sums "
           "epilogue", py::arg("x"), py::arg("wp"), py::arg("kh"), py::arg("kw"), py::arg("stride"), py::arg("ph"),

@@ -56,7 +56,7 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Non-temporal 16-byte accesses (KUNGFU_BN_NT: bit 0 loads, bit 1 stores), for the apply passes
+// Non-temporal 16-byte accesses (bn_nt_mode(): bit 0 loads, bit 1 stores), for the apply passes
 // that stream every byte exactly once.  A uniform runtime flag: both paths are in one kernel.
 typedef unsigned int kf_u32x4 __attribute__((ext_vector_type(4)));
 

@@ -22,695 +22,12 @@
 //
 // The same kernel computes the stride-1 data gradient: dx = conv3x3(dy, w')
 // with w'[ci, kh, kw, co] = w[co, 2-kh, 2-kw, ci] (conv3x3_flip_weight).
-#include "bn_fin.hpp"
-#include "common.hpp"
-#include "kernels.hpp"
-
-#include <cstdlib>
-#include <stdexcept>
+#include "conv_kernel.hpp"
 
 namespace kfk {
 
 namespace {
 
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-
-__device__ __forceinline__ int wm_of(int wave, int wn) { return wave / wn; }
-
-// relu(v * scale + shift) on the 8 bf16 of an A fragment (8 consecutive input channels), or 0 for
-// a padding row; f32 math, one v_cvt_pk_bf16_f32 per pair (round to nearest even, as bn_apply)
-__device__ __forceinline__ void prebn_frag(bf16x8 &f, const float *sc, const float *sh, bool ok) {
-    uint4 u;
-    __builtin_memcpy(&u, &f, 16);
-    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-    uint32_t o[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-        float lo = __uint_as_float(w[d] << 16), hi = __uint_as_float(w[d] & 0xffff0000u);
-        lo = fmaxf(fmaf(lo, sc[2 * d], sh[2 * d]), 0.f);
-        hi = fmaxf(fmaf(hi, sc[2 * d + 1], sh[2 * d + 1]), 0.f);
-        uint32_t r;
-        asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-        o[d] = ok ? r : 0u;
-    }
-    u = make_uint4(o[0], o[1], o[2], o[3]);
-    __builtin_memcpy(&f, &u, 16);
-}
-
-__device__ __forceinline__ void unpack_bf16x8(const uint4 &v, float (&f)[8]) {
-    const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        f[2 * k] = __uint_as_float(u[k] << 16);
-        f[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
-    }
-}
-
-constexpr int kBK = 64;              // channels per K-step
-constexpr int kRowBytes = kBK * 2;   // 128 B per staged row
-
-__device__ __forceinline__ int swz_chunk(int row, int chunk) { return chunk ^ (row & 7); }
-
-// LDS byte address of (row, 16-B chunk) in a staged tile image.
-__device__ __forceinline__ int img_off(int row, int chunk) { return row * kRowBytes + (swz_chunk(row, chunk) << 4); }
-
-struct Geo {
-    int N, H, W, C, OH, OW, K, stride;
-    int M;       // N*OH*OW
-    int mtiles;  // ceil(M / BM)
-    int ntiles;  // K / BN
-    // strided data gradient as parity phases (launch_conv_dgrad_s2):
-    int wtaps;   // taps per weight row (B row stride = wtaps * C)
-    int tapmap;  // -1: tap t reads weight tap t; else weight tap of tap t = nibble t
-    int scat;    // 1: output (n, a, b) of the OH x OW phase grid -> pixel (2a + pr, 2b + pc) of a dh x dw image
-    int pr, pc;
-    int dh, dw;  // scat: the data-gradient image (2OH x 2OW for an even input)
-    int ph, pw;  // zero padding (rows, columns)
-    int stagger;  // 1: the upper half of 8 waves issues its LDS-DMA staging before its fragment reads
-    int prio;     // 1: the upper (second-dispatched) wave half runs at s_setprio 1
-};
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Buffer-resource LDS-DMA staging in conv_kernel (KUNGFU_CONV_BUFLD): num_records = 2 GiB, so
-// the out-of-range offset kBufOOB returns zeros; dword 3 = the CDNA raw-buffer format word.
-#ifndef KUNGFU_CONV_BUFLD
-#define KUNGFU_CONV_BUFLD 1
-#endif
-constexpr uint32_t kBufOOB = 0x80000000u;
-constexpr int kBufFlags = 0x00020000;
-
-__device__ __forceinline__ __attribute__((address_space(3))) void *lds_ptr(uint8_t *p) {
-    return (__attribute__((address_space(3))) void *)(p);
-}
-
-// In-launch BN finalize (kernels.hpp BNFin): called by every workgroup after its slot atomics.
-// Completion-ordered hand-off (MI355X_MICROARCH.md, inter-workgroup visibility: "the workgroup whose
-// add came last, told by the value its add returned", sc1 loads of the handed-off words): each wave
-// waits for its own atomics (vmcnt counts them), the workgroup joins a barrier, one lane arrives on
-// its shard counter (blockIdx % 8) and the last arriver of a shard on the top counter; the last of
-// those folds every channel's slots with sc1 loads (the f64 adds were performed at the memory side,
-// no L2 holds them) and re-zeroes slots and counters with sc1 stores for the next launch.  No fence:
-// the outputs are read by later kernels only.
-// `red` (the kernel's own LDS, free once the statistics are out) holds red_doubles doubles and then
-// the flag word: a separate __shared__ variable would push the 256x64 tiles' 80 KB past the
-// two-workgroups-per-CU LDS budget.
-__device__ __forceinline__ void bn_finalize_last(const BNFin *__restrict__ fp, double *sums, int C, int nwg, int orig,
-                                                 int tid, int nt, double *red, int red_doubles) {
-    int &s_last = *reinterpret_cast<int *>(red + red_doubles);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const int shard = orig & 7;
-        const int nsh = nwg < 8 ? nwg : 8;
-        const unsigned nin = static_cast<unsigned>((nwg - shard + 7) / 8);
-        int last = 0;
-        unsigned *arrive = fp->arrive;
-        const unsigned o = __hip_atomic_fetch_add(arrive + shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (o == nin - 1) {
-            const unsigned o2 = __hip_atomic_fetch_add(arrive + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = o2 == static_cast<unsigned>(nsh - 1);
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // channel chunks staged through LDS (the main loop's buffers are free): every slot word of the
-    // chunk loaded once (sc1, all independent) and re-zeroed, then each channel folded in slot order
-    // k = 0..15 -- the order of bn_sums_finalize / bn_bwd_finalize_sums, so bit-identical to them
-    constexpr int KS2 = 2 * kStatSlots;
-    const int chunk = red_doubles / KS2 < C ? red_doubles / KS2 : C;
-    for (int c0 = 0; c0 < C; c0 += chunk) {
-        const int ch = C - c0 < chunk ? C - c0 : chunk;
-        const int items = KS2 * ch;
-#pragma unroll 8
-        for (int it = tid; it < items; it += nt) {
-            const int kw = it / ch, cc = it - kw * ch;  // kw = 2 k + which
-            double *a = sums + static_cast<int64_t>(kw) * C + c0 + cc;
-            red[it] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(a, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        for (int cc = tid; cc < ch; cc += nt) {
-            double s0 = 0, s1 = 0;
-            for (int k = 0; k < kStatSlots; ++k) {
-                s0 += red[(2 * k) * ch + cc];
-                s1 += red[(2 * k + 1) * ch + cc];
-            }
-            const int c = c0 + cc;
-            if (fp->mode == 1)
-                bn_fin_fwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
-                                   fp->run_var, fp->momentum, fp->eps, fp->coef);
-            else
-                bn_fin_bwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta,
-                                   fp->coef, fp->training != 0);
-        }
-        __syncthreads();
-    }
-    if (tid < 9) __hip_atomic_store(fp->arrive + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0 && fp->mode == 1 && fp->num_batches) fp->num_batches[0] += 1;
-}
-
-// The same finalize as a launch of its own (a non-persistent statistics launch: there every
-// workgroup would hold its CU through the wait for its atomics).
-__global__ void bn_fin_desc_kernel(const BNFin *__restrict__ fp, double *sums, int C) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    double v0[kStatSlots], v1[kStatSlots];
-#pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) {
-        v0[k] = sums[k * 2 * C + c];
-        v1[k] = sums[k * 2 * C + C + c];
-    }
-    double s0 = 0, s1 = 0;
-#pragma unroll
-    for (int k = 0; k < kStatSlots; ++k) {
-        s0 += v0[k];
-        s1 += v1[k];
-        sums[k * 2 * C + c] = 0.0;
-        sums[k * 2 * C + C + c] = 0.0;
-    }
-    if (fp->mode == 1) {
-        if (c == 0 && fp->num_batches) fp->num_batches[0] += 1;
-        bn_fin_fwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->beta, fp->mean, fp->invstd, fp->run_mean,
-                           fp->run_var, fp->momentum, fp->eps, fp->coef);
-    } else {
-        bn_fin_bwd_channel_p(c, C, s0, s1, fp->rows, fp->gamma, fp->mean, fp->invstd, fp->dgamma, fp->dbeta, fp->coef,
-                           fp->training != 0);
-    }
-}
-
-// WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
-// KS = 3 or 1: square window; KS = 0xHW (>= 16): an H x W window (Inception's 1x7 / 7x1 / 1x3 /
-// 3x1 / 5x5, and the parity phases of a stride-2 3x3 data gradient, launch_conv_dgrad_s2).  The
-// zero padding is g.ph / g.pw (out-of-range taps read the zero page).  EPI flags (kernels.hpp ConvEpi):
-//   kEpiAccum     y += conv (accumulate into the existing bf16 tensor, a residual gradient);
-//   kEpiFwdStats  per-channel sum / sum-of-squares of the bf16 outputs (the following BN's
-//                 batch statistics) -> f64 atomics into ea.stats[slot][2][K];
-//   kEpiBwdCoef / kEpiBwdBits  the output is the gradient of a BN(+ReLU) output whose input
-//                 is ea.bx: sum(dz) and sum(dz * x) with dz = grad * relu' from the forward
-//                 coefficients ea.fcoef (recomputed) or from the 1-bit mask ea.bmask.
-// PERSIST: the grid is smaller than the tile count; each block keeps ONE n-tile and walks
-// m-tiles mt0, mt0 + mstride, ... -- its per-channel statistics accumulate in registers
-// across all of them and reach the f64 slots with ONE set of atomics per block (instead of
-// one per tile: 3.2 M f64 atomics for a 56x56 64->256 conv at batch 256).
-template <int KS, int WM, int WN, int STAGES, int EPI, int TM = 4, int TN = 4, bool PERSIST = false>
-__global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__restrict__ x,
-                                                            const uint16_t *__restrict__ w,
-                                                            uint16_t *__restrict__ y,
-                                                            const uint16_t *__restrict__ zero, Geo g,
-                                                            EpiArgs ea) {
-    // wave tile (16*TM) x (16*TN): TM x TN accumulators of one 16x16x32 MFMA each
-    constexpr int WTM = 16 * TM, WTN = 16 * TN;
-    constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
-    constexpr int KH = KS >= 16 ? (KS >> 4) : KS, KW = KS >= 16 ? (KS & 15) : KS;
-    constexpr int TAPS = KH * KW;
-    constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
-    constexpr int STAGE = A_BYTES + B_BYTES;
-    constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
-    constexpr int B_INST = BN / 8 / NW;
-    constexpr int LOADS = A_INST + B_INST;
-    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
-    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
-    constexpr bool GATE = (EPI & kEpiGate) != 0;
-    constexpr bool GELU = (EPI & kEpiGelu) != 0, GELUG = (EPI & kEpiGeluGrad) != 0;
-    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias | kEpiGelu)) != 0;
-    constexpr int NSUM = (GATE || GELUG) ? 1 : 2;  // the gates need sum(y) only (a bias gradient)
-    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
-    constexpr int GROUPS = NT / VPR;
-    // the statistics reduction reuses the C tile's LDS once the last tile is stored
-    constexpr int RED_BYTES = STATS ? NSUM * GROUPS * BN * 4 : 0;
-    constexpr int EPI_BYTES = BM * CROW > RED_BYTES ? BM * CROW : RED_BYTES;
-    constexpr int LDS_BYTES = STAGES * STAGE > EPI_BYTES ? STAGES * STAGE : EPI_BYTES;
-    constexpr bool PREBN = (EPI & kEpiPreBN) != 0;
-    constexpr int PRE_BYTES = PREBN ? 2 * 1024 * 4 : 0;  // [scale; shift] of up to 1024 input channels
-    static_assert(!PREBN || KS == 1 || KS == 3, "PreBN: 1x1 / 3x3 forward only");
-    static_assert(LDS_BYTES + PRE_BYTES <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES + PRE_BYTES];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if constexpr (PREBN) {
-        // the BN coefficients of every input channel into LDS once (one array with the staging ring,
-        // see cdna_hip_programming.md 'Projection GEMM' trap 4a), before any LDS-DMA is in flight
-        float *pc = reinterpret_cast<float *>(lds + LDS_BYTES);
-        for (int i = tid; i < 2 * g.C; i += NT) pc[i < g.C ? i : 1024 + i - g.C] = ea.pcoef[i];
-        __syncthreads();
-    }
-
-    // XCD-aware bijective remap: blocks sharing an XCD get consecutive tile ids.
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
-    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-    const int mt_first = wg / g.ntiles, nt = wg - mt_first * g.ntiles;
-    const int n0 = nt * BN;
-    const int mstride = PERSIST ? nwg / g.ntiles : g.mtiles;  // nwg % ntiles == 0 when persistent
-    const int cv = tid % (BN / 8);  // the epilogue's fixed 8-channel group of this thread
-    float s1[8], s2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-    int mt_last = mt_first;
-    for (int mt = mt_first; mt < g.mtiles; mt += mstride) {
-    mt_last = mt;
-    const int m0 = mt * BM;
-    if (mt != mt_first) __syncthreads();  // every thread is done with the previous tile's LDS
-
-    // ---- per-lane staging descriptors (fixed for the whole K loop)
-    // lane l of a glds instruction writes image bytes [l*16, l*16+16) of its
-    // 8-row slab: row = l/8, image chunk = l%8 -> logical chunk (l%8)^(l/8).
-    // A rows: 32-bit element offset of the tap-(0,0) input pixel (linear in the
-    // tap: + (kh*W + kw)*C) and a 9-bit in-bounds mask per row.
-    const int srow = lane >> 3;
-    const int schunk = (lane & 7) ^ srow;
-    int a_off[A_INST];
-    uint32_t a_ok[A_INST];
-#pragma unroll
-    for (int j = 0; j < A_INST; ++j) {
-        const int r = (wave * A_INST + j) * 8 + srow;
-        const int m = m0 + r;
-        a_off[j] = 0;
-        a_ok[j] = 0;
-        if (m < g.M) {
-            const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
-            const int ih0 = oh * g.stride - g.ph, iw0 = ow * g.stride - g.pw;
-            a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
-            uint32_t ok = 0;
-#pragma unroll
-            for (int kh = 0; kh < KH; ++kh)
-#pragma unroll
-                for (int kw = 0; kw < KW; ++kw)
-                    if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
-                        static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
-                        ok |= 1u << (kh * KW + kw);
-            a_ok[j] = ok;
-        }
-    }
-    // Channel counts that are not multiples of the tile (Inception's 48, 80, 96, 160, ...): the
-    // K-step's 8-channel chunks past Cin and the B rows past Cout read the zero page.
-    int b_off[B_INST];
-    uint32_t b_ok = 0;
-#pragma unroll
-    for (int j = 0; j < B_INST; ++j) {
-        const int r = (wave * B_INST + j) * 8 + srow;
-        b_off[j] = (n0 + r) * g.wtaps * g.C + schunk * 8;
-        if (n0 + r < g.K) b_ok |= 1u << j;
-    }
-    const int csteps = (g.C + kBK - 1) / kBK;
-    const int ksteps = TAPS * csteps;
-    // PreBN: the taps at which each of this lane's A fragment rows reads a padding pixel (the BN
-    // output there is 0, not relu(shift)): bit tap of pre_ok[i] set = an in-image pixel
-    uint32_t pre_ok[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        pre_ok[i] = 0xffffffffu;
-        if constexpr (PREBN && KS == 3) {
-            const int m = m0 + wm_of(wave, WN) * WTM + i * 16 + (lane & 15);
-            pre_ok[i] = 0;
-            if (m < g.M) {
-                const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH;
-                const int ih0 = oh * g.stride - g.ph, iw0 = ow * g.stride - g.pw;
-#pragma unroll
-                for (int kh = 0; kh < KH; ++kh)
-#pragma unroll
-                    for (int kw = 0; kw < KW; ++kw)
-                        if (static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
-                            static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W))
-                            pre_ok[i] |= 1u << (kh * KW + kw);
-            }
-        }
-    }
-
-#if KUNGFU_CONV_BUFLD
-    // LDS-DMA through buffer resources: 32-bit byte offsets, out-of-range lanes (padding taps,
-    // channel chunks past Cin, B rows past Cout) get offset kBufOOB >= num_records and read
-    // zeros -- no 64-bit per-lane addresses, no zero-page select (the launcher checks that x and
-    // w are below 2 GiB).
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kBufOOB), kBufFlags);
-    const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(w), 0, static_cast<int>(kBufOOB), kBufFlags);
-#endif
-    auto stage = [&](int ks, int buf) {
-        const int tap = ks / csteps, cc = ks - tap * csteps;
-        const int kh = tap / KW, kw = tap - kh * KW;
-        const int toff = (kh * g.W + kw) * g.C + cc * kBK;  // wave-uniform
-        const int wtap = g.tapmap < 0 ? tap : (g.tapmap >> (4 * tap)) & 15;
-        const bool cin_ok = cc * kBK + schunk * 8 < g.C;
-        uint8_t *abase = lds + buf * STAGE;
-        uint8_t *bbase = abase + A_BYTES;
-#pragma unroll
-        for (int j = 0; j < A_INST; ++j) {
-            const bool ok = ((a_ok[j] >> tap) & 1u) && cin_ok;
-#if KUNGFU_CONV_BUFLD
-            const uint32_t vo = ok ? static_cast<uint32_t>(a_off[j] + toff) * 2u : kBufOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(abase + (wave * A_INST + j) * 1024), 16, vo, 0, 0,
-                                                     0);
-#else
-            const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
-            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
-#endif
-        }
-#pragma unroll
-        for (int j = 0; j < B_INST; ++j) {
-            const bool ok = ((b_ok >> j) & 1u) && cin_ok;
-#if KUNGFU_CONV_BUFLD
-            const uint32_t vo = ok ? static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK) * 2u : kBufOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, lds_ptr(bbase + (wave * B_INST + j) * 1024), 16, vo, 0, 0,
-                                                     0);
-#else
-            const uint16_t *src = ok ? w + static_cast<uint32_t>(b_off[j] + wtap * g.C + cc * kBK) : zero;
-            __builtin_amdgcn_global_load_lds(src, bbase + (wave * B_INST + j) * 1024, 16, 0, 0);
-#endif
-        }
-    };
-
-    const int wm = wave / WN, wn = wave % WN;
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // transposed product (MFMA A operand = the weight fragment): acc[i][j] holds C^T of block (i, j),
-    // lane -> output pixel (lane & 15), 4 consecutive output channels 4 (lane >> 4) + r -- one 8-byte
-    // LDS store per block in the epilogue instead of four 2-byte ones
-    auto mfma_block = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    };
-
-    // prologue: STAGES-1 tiles in flight
-#pragma unroll
-    for (int p = 0; p < STAGES - 1; ++p)
-        if (p < ksteps) stage(p, p);
-    int buf = 0;
-    // g.stagger 1: the upper wave half stages before its fragment reads; 2: after its second MFMA cluster
-    const bool upper = NW >= 8 && ((wave >> 2) & 1);
-    const bool early = g.stagger == 1 && upper, late = g.stagger == 2 && upper;
-    if (g.prio && upper) __builtin_amdgcn_s_setprio(1);
-    for (int ks = 0; ks < ksteps; ++ks) {
-        // tile ks landed (this wave's loads); later tiles may stay in flight
-        if (ks + STAGES - 1 <= ksteps) wait_vmcnt<LOADS * (STAGES - 2)>();
-        else wait_vmcnt<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // raw barrier: keeps the other tiles' LDS-DMA in flight
-        __builtin_amdgcn_sched_barrier(0);
-        if (early && ks + STAGES - 1 < ksteps) {
-            int nb = buf + STAGES - 1;
-            if (nb >= STAGES) nb -= STAGES;
-            stage(ks + STAGES - 1, nb);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const uint8_t *abase = lds + buf * STAGE;
-        const uint8_t *bbase = abase + A_BYTES;
-        // all 16 fragments of the K-step issued up front (substep 1 lands while
-        // substep 0's MFMAs run)
-        bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int ra = wm * WTM + i * 16 + (lane & 15);
-            af0[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, lane >> 4));
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int rb = wn * WTN + j * 16 + (lane & 15);
-            bf0[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, lane >> 4));
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int ra = wm * WTM + i * 16 + (lane & 15);
-            af1[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(ra, 4 + (lane >> 4)));
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int rb = wn * WTN + j * 16 + (lane & 15);
-            bf1[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(rb, 4 + (lane >> 4)));
-        }
-        if constexpr (PREBN) {
-            const int tap = ks / csteps, cc = ks - tap * csteps;
-            const float *pc = reinterpret_cast<const float *>(lds + LDS_BYTES);
-            const int c0 = cc * kBK + (lane >> 4) * 8;
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const bool ok = (pre_ok[i] >> tap) & 1u;
-                prebn_frag(af0[i], pc + c0, pc + 1024 + c0, ok);
-                prebn_frag(af1[i], pc + c0 + 32, pc + 1024 + c0 + 32, ok);
-            }
-        }
-        mfma_block(af0, bf0);
-        __builtin_amdgcn_sched_barrier(0);
-        // next tile's staging (VALU + LDS-DMA issue) between the two MFMA clusters
-        if (!early && !late && ks + STAGES - 1 < ksteps) {
-            int nb = buf + STAGES - 1;
-            if (nb >= STAGES) nb -= STAGES;
-            stage(ks + STAGES - 1, nb);  // the buffer read in iteration ks-1
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_block(af1, bf1);
-        if (late && ks + STAGES - 1 < ksteps) {
-            __builtin_amdgcn_sched_barrier(0);
-            int nb = buf + STAGES - 1;
-            if (nb >= STAGES) nb -= STAGES;
-            stage(ks + STAGES - 1, nb);
-        }
-        buf = buf + 1 == STAGES ? 0 : buf + 1;
-    }
-    wait_vmcnt<0>();
-    __syncthreads();  // all ds_reads of the last tile done before the LDS is reused
-
-    // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
-    // C^T map (16x16): pixel row = lane & 15, channel col = (lane >> 4) * 4 + r.
-    float bcol[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            bcol[j][r] = 0.f;
-            if constexpr (BIAS) {
-                const int c = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-                if (c < g.K) bcol[j][r] = bf16_to_f32(ea.bias[c]);
-            }
-        }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int row = wm * WTM + i * 16 + (lane & 15);
-            const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
-            uint32_t h[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float v = acc[i][j][r];
-                if constexpr (BIAS) v += bcol[j][r];
-                if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
-                h[r] = f32_to_bf16(v);
-            }
-            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        }
-    __syncthreads();
-    // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
-    // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
-    static_assert(NT % VPR == 0, "fixed channel group per thread");
-    // The global reads of the epilogue (old value, BN input, masks) of U rows are all issued
-    // before any of them is consumed: one load round trip per U rows instead of per row (the
-    // loop is otherwise a chain of dependent HBM latencies -- the stores to y may alias later
-    // reads as far as the compiler knows).
-    constexpr int ITER = BM * VPR / NT;
-    static_assert(ITER * NT == BM * VPR, "whole store iterations");
-    constexpr bool LD_OLD = (EPI & kEpiAccum) != 0;
-    constexpr bool LD_BX = GATE || GELUG || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
-    // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
-    // the 256x256 tile, whose 16 coefficient registers would otherwise spill)
-    constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
-    const bool col_ok = n0 + cv * 8 < g.K;  // this thread's 8 channels exist (Cout % BN != 0)
-    float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
-    if constexpr ((EPI & kEpiBwdCoef) != 0) {
-        if (col_ok)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[k] = ea.fcoef[n0 + cv * 8 + k];
-            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
-        }
-    }
-    for (int it0 = 0; it0 < ITER; it0 += U) {
-        uint4 val[U], old[U], bxv[U];
-        uint32_t amb[U], bmb[U];
-        int64_t ee[U];
-        bool ok[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int v = tid + (it0 + u) * NT;
-            const int row = v / VPR;
-            const int m = m0 + row;
-            ok[u] = m < g.M && col_ok;
-            int pix = m;
-            if (g.scat) {
-                const int t = m / g.OW, ow = m - t * g.OW;
-                const int n = t / g.OH, a = t - n * g.OH;
-                pix = (n * g.dh + 2 * a + g.pr) * g.dw + 2 * ow + g.pc;
-            }
-            const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
-            ee[u] = e;
-            val[u] = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
-            old[u] = bxv[u] = make_uint4(0u, 0u, 0u, 0u);
-            amb[u] = 0u;
-            bmb[u] = 0xffu;
-            if (ok[u]) {
-                if constexpr (LD_OLD) {
-                    bool here = true;
-                    if constexpr ((EPI & kEpiAccEven) != 0) {
-                        // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
-                        const int t = m / g.OW, ow = m - t * g.OW;
-                        here = ((ow | (t % g.OH)) & 1) == 0;
-                    }
-                    if (here) old[u] = *reinterpret_cast<const uint4 *>(y + e);
-                    if constexpr ((EPI & kEpiAccMask) != 0) amb[u] = ea.amask[e >> 3];  // 8 channels, 8-aligned e
-                }
-                if constexpr (LD_BX) bxv[u] = *reinterpret_cast<const uint4 *>(ea.bx + e);
-                if constexpr ((EPI & kEpiBwdBits) != 0) bmb[u] = ea.bmask[e >> 3];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            uint4 v = val[u];
-            if constexpr (LD_OLD) {
-                uint4 o0 = old[u];
-                if constexpr ((EPI & kEpiAccMask) != 0) {
-                    const uint32_t mb = amb[u];
-                    uint32_t *ow = reinterpret_cast<uint32_t *>(&o0);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        ow[k] &= (((mb >> (2 * k)) & 1u) ? 0xffffu : 0u) | (((mb >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
-                }
-                const uint32_t *a = reinterpret_cast<const uint32_t *>(&v);
-                const uint32_t *b = reinterpret_cast<const uint32_t *>(&o0);
-                uint32_t o[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float lo = bf16_to_f32(static_cast<uint16_t>(a[k] & 0xffffu)) +
-                                     bf16_to_f32(static_cast<uint16_t>(b[k] & 0xffffu));
-                    const float hi = bf16_to_f32(static_cast<uint16_t>(a[k] >> 16)) +
-                                     bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
-                    o[k] = static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
-                }
-                v = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-            if constexpr (GATE) {
-                // gradient of a ReLU output: keep y where bx > 0 (NaN passes), sum the kept values
-                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bxv[u]);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
-                                          (!(__uint_as_float(bw[k] & 0xffff0000u) <= 0.f) ? 0xffff0000u : 0u);
-                    vw[k] &= keep;
-                }
-            }
-            if constexpr (GELU) {
-                // v = u (bias added): saved for the backward, then y = gelu(u) in f32, one rounding
-                *reinterpret_cast<uint4 *>(ea.aux + ee[u]) = v;
-                float f[8];
-                unpack_bf16x8(v, f);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float a = f[2 * k], b = f[2 * k + 1];
-                    const float ga = 0.5f * a * (1.f + erff(a * 0.70710678118654752f));
-                    const float gb = 0.5f * b * (1.f + erff(b * 0.70710678118654752f));
-                    vw[k] = static_cast<uint32_t>(f32_to_bf16(ga)) | (static_cast<uint32_t>(f32_to_bf16(gb)) << 16);
-                }
-            }
-            if constexpr (GELUG) {
-                // gradient of gelu(u): dy * (Phi(u) + u * phi(u)), torch's GeluBackward in f32
-                float f[8], uf[8];
-                unpack_bf16x8(v, f);
-                unpack_bf16x8(bxv[u], uf);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    float d[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const float t = uf[2 * k + h];
-                        const float cdf = 0.5f * (1.f + erff(t * 0.70710678118654752f));
-                        const float pdf = __expf(-0.5f * t * t) * 0.39894228040143268f;
-                        d[h] = f[2 * k + h] * (cdf + t * pdf);
-                    }
-                    vw[k] = static_cast<uint32_t>(f32_to_bf16(d[0])) | (static_cast<uint32_t>(f32_to_bf16(d[1])) << 16);
-                }
-            }
-            *reinterpret_cast<uint4 *>(y + ee[u]) = v;
-            if constexpr (STATS) {
-                float f[8];
-                unpack_bf16x8(v, f);
-                if constexpr (GATE || GELUG) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s1[k] += f[k];
-                } else if constexpr ((EPI & kEpiFwdStats) != 0) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        s1[k] += f[k];
-                        s2[k] += f[k] * f[k];
-                    }
-                } else {
-                    // BN backward sums of the BN whose input is ea.bx:
-                    //   dz = grad * relu'(.) ; s1 += dz ; s2 += dz * x
-                    float xv[8];
-                    unpack_bf16x8(bxv[u], xv);
-                    const uint32_t mbits = bmb[u];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        bool on;
-                        if constexpr ((EPI & kEpiBwdBits) != 0) on = (mbits >> k) & 1u;
-                        else on = xv[k] * sc[k] + sh[k] > 0.f;
-                        const float dz = on ? f[k] : 0.f;
-                        s1[k] += dz;
-                        s2[k] += dz * xv[k];
-                    }
-                }
-            }
-        }
-    }
-    }  // m-tile loop
-    if constexpr (STATS) {
-        // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
-        float *red = reinterpret_cast<float *>(lds);
-        __syncthreads();
-        const int grp = tid / VPR;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            red[grp * BN + cv * 8 + k] = s1[k];
-            if constexpr (NSUM == 2) red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
-        }
-        __syncthreads();
-        for (int col = tid; col < BN; col += NT) {
-            double t1 = 0, t2 = 0;
-#pragma unroll 4
-            for (int p = 0; p < GROUPS; ++p) {
-                t1 += red[p * BN + col];
-                if constexpr (NSUM == 2) t2 += red[(GROUPS + p) * BN + col];
-            }
-            double *sl = ea.stats + ((mt_last + wg) % kStatSlots) * 2 * g.K;  // spread atomics over slots
-            if (n0 + col < g.K) {
-                atomicAdd(sl + n0 + col, t1);
-                if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
-            }
-        }
-        if constexpr (NSUM == 2) {
-            if (ea.fin != nullptr)
-                bn_finalize_last(ea.fin, ea.stats, g.K, nwg, orig, tid, NT, reinterpret_cast<double *>(lds),
-                                 LDS_BYTES / 8 - 2);
-        }
-    }
-}
 
 // w'[ci, kh, kw, co] = w[co, KS-1-kh, KS-1-kw, ci]  (the stride-1 data-gradient weights)
 __global__ void conv_flip_kernel(const uint16_t *__restrict__ w, uint16_t *__restrict__ wt, int Cout, int Cin,
@@ -825,127 +142,6 @@ void check_buf_extent(const Geo &g) {
         throw std::invalid_argument("conv: input or weight of 2 GiB or more (buffer-resource staging)");
 }
 
-template <int KS, int WM, int WN, int ST, int EPI, int TM = 4, int TN = 4>
-void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
-    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv: Cin and Cout must be multiples of 8");
-    check_buf_extent(g);
-    g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = (g.K + BN - 1) / BN;
-    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
-    if constexpr (STATS) {
-        // persistent blocks (4 per CU, fewer when the tile's LDS allows less): one atomic
-        // statistics flush per block instead of per tile
-        constexpr int env_cap = 0;
-        constexpr int kRow = 128, STG = ST * (BM + BN) * kRow, CT = BM * (BN * 2 + 16);
-        constexpr int LDS = STG > CT ? STG : CT;
-        constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
-        const int cap = env_cap > 0 ? env_cap : 256 * (OCC < 1 ? 1 : OCC);
-        const int per_n = cap / g.ntiles;
-        if (cap > 0 && per_n >= 1 && g.mtiles > 2 * per_n) {
-            conv_kernel<KS, WM, WN, ST, EPI, TM, TN, true><<<per_n * g.ntiles, 64 * WM * WN, 0, s>>>(
-                x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
-            return;
-        }
-    }
-    if (ea.fin) {
-        // one tile per workgroup: finalize in a launch of its own
-        EpiArgs e2 = ea;
-        e2.fin = nullptr;
-        conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
-            x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, e2);
-        bn_fin_desc_kernel<<<(g.K + 255) / 256, 256, 0, s>>>(ea.fin, ea.stats, g.K);
-        return;
-    }
-    conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
-        x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
-}
-
-// Tuning-only tile variants instantiate the plain epilogue; the defaults every fused one.
-template <int KS, int WM, int WN, int ST, bool ALL, int TM = 4, int TN = 4>
-void launch_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
-                    hipStream_t s) {
-    if constexpr (!ALL) {
-        if (epi != 0) throw std::invalid_argument("conv: fused epilogues need the default tile variant");
-        launch_epi<KS, WM, WN, ST, 0, TM, TN>(x, w, y, g, ea, s);
-    } else {
-        constexpr int A = kEpiAccum, M = kEpiAccMask, B = kEpiBwdBits, C = kEpiBwdCoef;
-        switch (epi) {
-        case 0: launch_epi<KS, WM, WN, ST, 0, TM, TN>(x, w, y, g, ea, s); break;
-        case kEpiFwdStats: launch_epi<KS, WM, WN, ST, kEpiFwdStats, TM, TN>(x, w, y, g, ea, s); break;
-        case A: launch_epi<KS, WM, WN, ST, A, TM, TN>(x, w, y, g, ea, s); break;
-        case C: launch_epi<KS, WM, WN, ST, C, TM, TN>(x, w, y, g, ea, s); break;
-        case B: launch_epi<KS, WM, WN, ST, B, TM, TN>(x, w, y, g, ea, s); break;
-        case A | B: launch_epi<KS, WM, WN, ST, A | B, TM, TN>(x, w, y, g, ea, s); break;
-        case A | C: launch_epi<KS, WM, WN, ST, A | C, TM, TN>(x, w, y, g, ea, s); break;
-        case A | M: launch_epi<KS, WM, WN, ST, A | M, TM, TN>(x, w, y, g, ea, s); break;
-        case A | M | B: launch_epi<KS, WM, WN, ST, A | M | B, TM, TN>(x, w, y, g, ea, s); break;
-        case A | kEpiAccEven: launch_epi<KS, WM, WN, ST, A | kEpiAccEven, TM, TN>(x, w, y, g, ea, s); break;
-        case A | kEpiAccEven | B: launch_epi<KS, WM, WN, ST, A | kEpiAccEven | B, TM, TN>(x, w, y, g, ea, s); break;
-        case kEpiBiasRelu: launch_epi<KS, WM, WN, ST, kEpiBiasRelu, TM, TN>(x, w, y, g, ea, s); break;
-        case kEpiGate: launch_epi<KS, WM, WN, ST, kEpiGate, TM, TN>(x, w, y, g, ea, s); break;
-        case kEpiPreBN: launch_epi<KS, WM, WN, ST, kEpiPreBN, TM, TN>(x, w, y, g, ea, s); break;
-        case kEpiPreBN | kEpiFwdStats:
-            launch_epi<KS, WM, WN, ST, kEpiPreBN | kEpiFwdStats, TM, TN>(x, w, y, g, ea, s);
-            break;
-        default: throw std::invalid_argument("conv: unsupported epilogue combination");
-        }
-    }
-}
-
-template <int KS>
-void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi, hipStream_t s,
-               int variant) {
-    // default per shape (re-measured with the fused epilogues, tools/bench_conv1x1_variants.py
-    // [KS3=1]; VGG's compute-bound 3x3 layers: tools/bench_vgg_conv.py, 1.15-1.17 PF/s): 256x256 /
-    // 8 waves whenever Cout % 256 == 0 and there are >= 128 such tiles (64->256 at 56x56 161 ->
-    // 123 us, 3x3 256->256 at 14x14 70 -> 57 us; fewer tiles under-fill the chip: 3x3 512->512 at
-    // 7x7 62 -> 100 us), else 256x128 / 8 waves (1x1 included: 4-13 % over 128x128), else 256x64
-    if (variant < 0) {
-        const int64_t tiles256 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256);  // (K % 256 == 0 only)
-        variant = g.K <= 32 ? 11 : g.K % 256 == 0 && tiles256 >= 128 ? 7 : g.K % 128 == 0 ? 1 : 2;
-        if (variant == 7 && g.K % 128 == 0) {
-            // tile quantisation: 256x256 tiles run one workgroup per CU (135 KB of LDS), so a grid
-            // of T tiles takes ceil(T / 256) rounds; when the 256x128 grid fills its rounds >= 10 %
-            // better it wins despite the smaller tile (r5t21: 256->1024 at 14x14 63 -> 51 us; the
-            // 56x56 / 28x28 / 7x7 shapes keep 256x256, tools/bench_conv1x1_variants.py)
-            const int64_t t7 = tiles256, t1 = t7 * 2;
-            const double e7 = static_cast<double>(t7) / (((t7 + 255) / 256) * 256);
-            const double e1 = static_cast<double>(t1) / (((t1 + 255) / 256) * 256);
-            if (e1 > 1.1 * e7) variant = 1;
-        }
-        if (conv_tile_rules() >= 2 && g.K % 128 == 0 && g.K > 32) {
-            // re-measured with the staggered staging (tools/bench_conv1x1_variants.py, profiles/r3_conv_variants.txt):
-            // the accumulating data gradients (ResNet's conv1 dgrad into the residual gradient) run best on
-            // 128x128 / 4 waves at every ResNet size (64->256@56 303 -> 290 us, 128->512@28 174 -> 156,
-            // 256->1024@14 90 -> 82, 512->2048@7 60 -> 57), and so do the stride-1 3x3 ones with 128 or
-            // 512 outputs that are not on 256x256 tiles (128->128@28 101 -> 88, 512->512@7 76 -> 71)
-            if ((epi & kEpiAccum) != 0 || (KS == 3 && g.stride == 1 && variant != 7)) variant = 0;
-        }
-    }
-    switch (variant) {
-    case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2, true>(x, w, y, g, ea, epi, s); break; }  // 128x128
-            [[fallthrough]];
-    case 1: if (g.K % 128 == 0) { launch_variant<KS, 4, 2, 3, true>(x, w, y, g, ea, epi, s); break; }  // 256x128
-            [[fallthrough]];
-    case 2: launch_variant<KS, 4, 1, 2, true>(x, w, y, g, ea, epi, s); break;                          // 256x64
-    case 3: launch_variant<KS, 4, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 256x64 3st
-    case 4: launch_variant<KS, 8, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 512x64
-    case 5: launch_variant<KS, 2, 1, 2, false>(x, w, y, g, ea, epi, s); break;                         // 128x64
-    case 6: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 3, false>(x, w, y, g, ea, epi, s); break; }
-            launch_variant<KS, 2, 1, 3, false>(x, w, y, g, ea, epi, s); break;                         // 128x64 3st
-    // larger wave tiles (tuning candidates for the compute-bound 3x3 shapes)
-    case 7: if (g.K % 256) throw std::invalid_argument("conv variant 7: Cout % 256");
-            launch_variant<KS, 4, 2, 2, true, 4, 8>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 64x128
-    case 8: if (g.K % 256) throw std::invalid_argument("conv variant 8: Cout % 256");
-            launch_variant<KS, 2, 4, 2, true, 8, 4>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 128x64
-    case 11: launch_variant<KS, 4, 1, 2, true, 4, 2>(x, w, y, g, ea, epi, s); break;                // 256x32 (Cout <= 32)
-    case 9: if (epi || g.K % 128) throw std::invalid_argument("conv variant 9: epi 0, Cout % 128");    // 256x128, 4w, 128x64
-            launch_epi<KS, 2, 2, 2, 0, 8, 4>(x, w, y, g, ea, s); break;
-    default: if (epi || g.K % 128) throw std::invalid_argument("conv variant 10: epi 0, Cout % 128");  // 128x128, 2w, 64x128 3st
-            launch_epi<KS, 2, 1, 3, 0, 4, 8>(x, w, y, g, ea, s); break;
-    }
-}
 
 int conv3x3_variants() { return 12; }
 
@@ -962,240 +158,13 @@ void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H
     g.stagger = conv_stagger();
     g.prio = conv_prio();
     g.ph = g.pw = pad;
-    if (ks == 1) launch_ks<1>(x, w, y, g, ea, epi, s, variant);
-    else launch_ks<3>(x, w, y, g, ea, epi, s, variant);
+    if (ks == 1) launch_conv_k1(x, w, y, g, ea, epi, s, variant);
+    else launch_conv_k3(x, w, y, g, ea, epi, s, variant);
 }
 
 // Rectangular windows (Inception-v3): plain, BN-statistics, accumulate and/or BN-backward-sums
 // (the gradient of a BN+ReLU output: sum dz, sum dz*x into the stats slots) epilogue, 256x128 / 8 waves when
 // Cout % 128 == 0, else 256x64.
-template <int KS>
-void launch_rect_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
-                   hipStream_t s) {
-    constexpr int A = kEpiAccum, C = kEpiBwdCoef;
-    if (g.K <= 32) {  // narrow outputs (Inception's 32-channel stem / pool branch): 256x32 tiles
-        switch (epi) {
-        case 0: launch_epi<KS, 4, 1, 2, 0, 4, 2>(x, w, y, g, ea, s); break;
-        case kEpiFwdStats: launch_epi<KS, 4, 1, 2, kEpiFwdStats, 4, 2>(x, w, y, g, ea, s); break;
-        case A: launch_epi<KS, 4, 1, 2, A, 4, 2>(x, w, y, g, ea, s); break;
-        case C: launch_epi<KS, 4, 1, 2, C, 4, 2>(x, w, y, g, ea, s); break;
-        case A | C: launch_epi<KS, 4, 1, 2, A | C, 4, 2>(x, w, y, g, ea, s); break;
-        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
-        }
-    } else if (g.K % 128 == 0) {
-        switch (epi) {
-        case 0: launch_epi<KS, 4, 2, 3, 0>(x, w, y, g, ea, s); break;
-        case kEpiFwdStats: launch_epi<KS, 4, 2, 3, kEpiFwdStats>(x, w, y, g, ea, s); break;
-        case A: launch_epi<KS, 4, 2, 3, A>(x, w, y, g, ea, s); break;
-        case C: launch_epi<KS, 4, 2, 3, C>(x, w, y, g, ea, s); break;
-        case A | C: launch_epi<KS, 4, 2, 3, A | C>(x, w, y, g, ea, s); break;
-        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
-        }
-    } else {
-        switch (epi) {
-        case 0: launch_epi<KS, 4, 1, 2, 0>(x, w, y, g, ea, s); break;
-        case kEpiFwdStats: launch_epi<KS, 4, 1, 2, kEpiFwdStats>(x, w, y, g, ea, s); break;
-        case A: launch_epi<KS, 4, 1, 2, A>(x, w, y, g, ea, s); break;
-        case C: launch_epi<KS, 4, 1, 2, C>(x, w, y, g, ea, s); break;
-        case A | C: launch_epi<KS, 4, 1, 2, A | C>(x, w, y, g, ea, s); break;
-        default: throw std::invalid_argument("conv_rect: unsupported epilogue");
-        }
-    }
-}
-
-// Linear layers: M tokens x K in-features -> N out-features, the 1x1 case of the kernel above
-// (H = W = 1) with the bias / GELU / GELU-gradient / accumulate epilogues.
-template <int WM, int WN, int ST, int TM, int TN>
-void launch_gemm_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
-                   hipStream_t s) {
-    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    if (g.K % BN) throw std::invalid_argument("gemm: out-features not a multiple of the tile");
-    g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = g.K / BN;
-    check_buf_extent(g);
-    const dim3 grid(g.mtiles * g.ntiles), block(64 * WM * WN);
-    const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
-    switch (epi) {
-    case 0: conv_kernel<1, WM, WN, ST, 0, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
-    case kEpiBias: conv_kernel<1, WM, WN, ST, kEpiBias, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
-    case kEpiGelu: conv_kernel<1, WM, WN, ST, kEpiGelu, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
-    case kEpiGeluGrad:
-        conv_kernel<1, WM, WN, ST, kEpiGeluGrad, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea);
-        break;
-    case kEpiAccum: conv_kernel<1, WM, WN, ST, kEpiAccum, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
-    default: throw std::invalid_argument("gemm: unsupported epilogue");
-    }
-}
-
-bool gemm_supported(int M, int K, int N) {
-    // x (M x K) and the (flipped) weight are staged through buffer resources: below 2 GiB of bf16
-    return M > 0 && K >= 64 && K % 64 == 0 && N % 64 == 0 && N >= 64 &&
-           static_cast<int64_t>(M) * (K > N ? K : N) < (int64_t(1) << 30);
-}
-
-void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K, int N, const EpiArgs &ea, int epi,
-                 hipStream_t s, int variant) {
-    if (!gemm_supported(M, K, N)) throw std::invalid_argument("gemm: unsupported shape");
-    Geo g;
-    g.N = M, g.H = g.W = 1, g.C = K, g.K = N, g.stride = 1;
-    g.OH = g.OW = 1, g.M = M;
-    g.mtiles = g.ntiles = 0;
-    g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0, g.dh = g.dw = 0;
-    g.stagger = conv_stagger();
-    g.prio = conv_prio();
-    if (variant < 0) {
-        // enough 256x256 tiles to fill the chip twice, else 256x128, else 128x128 (or 128x64)
-        const int64_t t256 = N % 256 ? 0 : ((M + 255) / 256) * (N / 256);
-        const int64_t t128 = N % 128 ? 0 : ((M + 255) / 256) * (N / 128);
-        variant = t256 >= 512 ? 0 : t128 >= 512 ? 1 : 2;
-    }
-    switch (variant) {
-    case 0: if (N % 256 == 0) { launch_gemm_t<4, 2, 2, 4, 8>(x, w, y, g, ea, epi, s); break; }  // 256x256, 8 waves
-            [[fallthrough]];
-    case 1: if (N % 128 == 0) { launch_gemm_t<4, 2, 3, 4, 4>(x, w, y, g, ea, epi, s); break; }  // 256x128, 8 waves
-            [[fallthrough]];
-    case 2: if (N % 128 == 0) { launch_gemm_t<2, 2, 2, 4, 4>(x, w, y, g, ea, epi, s); break; }  // 128x128, 4 waves
-            launch_gemm_t<2, 1, 2, 4, 4>(x, w, y, g, ea, epi, s); break;                       // 128x64
-    default: if (N % 256) throw std::invalid_argument("gemm variant 3: N % 256");
-            launch_gemm_t<2, 4, 2, 8, 4>(x, w, y, g, ea, epi, s); break;                       // 256x256, 128x64 waves
-    }
-}
-
-bool conv_rect_supported(int Cin, int Cout, int kh, int kw, int stride) {
-    // channel counts: multiples of 8 (16-byte chunks); the last K-step / N-tile is zero-padded
-    if (Cin % 8 || Cout % 8 || Cin < 16 || Cout < 16 || !(stride == 1 || stride == 2)) return false;
-    return (kh == 1 && kw == 1) || (kh == 3 && kw == 3) || (kh == 1 && kw == 7) || (kh == 7 && kw == 1) ||
-           (kh == 1 && kw == 3) || (kh == 3 && kw == 1) || (kh == 5 && kw == 5);
-}
-
-void launch_conv_rect(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
-                      int kh, int kw, int ph, int pw, int stride, const EpiArgs &ea, int epi, hipStream_t s) {
-    if (!conv_rect_supported(Cin, Cout, kh, kw, stride)) throw std::invalid_argument("conv_rect: unsupported shape");
-    Geo g;
-    g.N = N, g.H = H, g.W = W, g.C = Cin, g.K = Cout, g.stride = stride;
-    g.OH = (H + 2 * ph - kh) / stride + 1;
-    g.OW = (W + 2 * pw - kw) / stride + 1;
-    g.M = N * g.OH * g.OW;
-    g.mtiles = g.ntiles = 0;
-    g.wtaps = kh * kw, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.dh = g.dw = 0;
-    g.stagger = conv_stagger();
-    g.prio = conv_prio();
-    g.ph = ph, g.pw = pw;
-    if (kh == 1 && kw == 1) {
-        launch_ks<1>(x, w, y, g, ea, epi, s, -1);
-        return;
-    }
-    if (kh == 3 && kw == 3) {
-        launch_ks<3>(x, w, y, g, ea, epi, s, -1);
-        return;
-    }
-    if (kh == 1 && kw == 7) launch_rect_t<0x17>(x, w, y, g, ea, epi, s);
-    else if (kh == 7 && kw == 1) launch_rect_t<0x71>(x, w, y, g, ea, epi, s);
-    else if (kh == 1 && kw == 3) launch_rect_t<0x13>(x, w, y, g, ea, epi, s);
-    else if (kh == 3 && kw == 1) launch_rect_t<0x31>(x, w, y, g, ea, epi, s);
-    else launch_rect_t<0x55>(x, w, y, g, ea, epi, s);
-}
-
-// One parity phase of a stride-2 data gradient: the fused epilogues it needs (none, or the BN
-// backward sums of the BN that produced the forward input), 256x128 tiles when Cin % 128 == 0.
-template <int KS, int WM, int WN, int ST, int TM = 4, int TN = 4>
-void launch_phase_t(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, const EpiArgs &ea, int epi,
-                    hipStream_t s) {
-    constexpr int C = kEpiBwdCoef, B = kEpiBwdBits;
-    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    if (g.K % 8 || g.C % 8) throw std::invalid_argument("conv_dgrad_s2: channel counts must be multiples of 8");
-    g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = (g.K + BN - 1) / BN;  // a partial last N tile reads zero B rows, stores its valid columns
-    const int grid = g.mtiles * g.ntiles;
-    check_buf_extent(g);
-    const uint16_t *z = reinterpret_cast<const uint16_t *>(zero_page());
-    EpiArgs e2 = ea;
-    e2.fin = nullptr;  // one tile per workgroup: the finalize runs as a launch of its own
-    if (epi == 0) conv_kernel<KS, WM, WN, ST, 0, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
-    else if (epi == C) conv_kernel<KS, WM, WN, ST, C, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
-    else if (epi == B) conv_kernel<KS, WM, WN, ST, B, TM, TN><<<grid, 64 * WM * WN, 0, s>>>(dy, wt, dx, z, g, e2);
-    else throw std::invalid_argument("conv_dgrad_s2: unsupported epilogue");
-    if (ea.fin) bn_fin_desc_kernel<<<(g.K + 255) / 256, 256, 0, s>>>(ea.fin, ea.stats, g.K);
-}
-
-// Tile for the short-K phase GEMMs (variant >= 0 to override; tools/bench_dgrad_s2.py): 128x128
-// / 4 waves for the large-M 3x3 phases (>= 1024 such tiles: two blocks per CU overlap one
-// block's prologue/epilogue with the other's MFMAs), else 256x128 / 8 waves; 256x64 when
-// Cin % 128 != 0.  (One grid holding all four phases, per-block tap count, measured 5-50 %
-// slower than four launches.)
-template <int KS>
-void launch_phase(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, Geo g, const EpiArgs &ea, int epi,
-                  hipStream_t s, int v) {
-    if (v < 0) {
-        const int64_t t128 = ((static_cast<int64_t>(g.M) + 127) / 128) * (g.K / 128);
-        v = g.K % 128 ? 2 : (KS != 1 && t128 >= 1024) ? 0 : 1;
-    }
-    switch (v) {
-    case 0: if (g.K % 128 == 0) { launch_phase_t<KS, 2, 2, 2>(dy, wt, dx, g, ea, epi, s); break; }  // 128x128
-            [[fallthrough]];
-    case 5: launch_phase_t<KS, 2, 1, 2>(dy, wt, dx, g, ea, epi, s); break;                           // 128x64
-    case 1: if (g.K % 128 == 0) { launch_phase_t<KS, 4, 2, 3>(dy, wt, dx, g, ea, epi, s); break; }  // 256x128
-            [[fallthrough]];
-    default: launch_phase_t<KS, 4, 1, 2>(dy, wt, dx, g, ea, epi, s); break;                         // 256x64
-    }
-}
-
-void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, int N, int OH, int OW, int Cout,
-                          int Cin, int ks, const EpiArgs &ea, int epi, hipStream_t s, int variant, int DH, int DW,
-                          int pad) {
-    // variant: -1 = default; else the tile variant (0 128x128, 1 256x128, 2 256x64, 5 128x64)
-    const int tv = variant;
-    if (DH <= 0) DH = 2 * OH;
-    if (DW <= 0) DW = 2 * OW;
-    Geo g;
-    g.N = N, g.H = OH, g.W = OW, g.C = Cout, g.K = Cin, g.stride = 1;
-    g.mtiles = g.ntiles = 0;
-    g.wtaps = ks * ks, g.scat = 1;
-    g.dh = DH, g.dw = DW;
-    g.stagger = conv_stagger();
-    g.prio = conv_prio();
-    g.ph = g.pw = 0;
-    if (ks == 1) {
-        if (DH != 2 * OH || DW != 2 * OW || pad != 0) throw std::invalid_argument("conv_dgrad_s2: 1x1 needs an even input");
-        g.OH = OH, g.OW = OW, g.M = N * OH * OW;
-        g.tapmap = -1, g.pr = g.pc = 0;
-        launch_phase<1>(dy, wt, dx, g, ea, epi, s, tv);
-        return;
-    }
-    if (ks != 3 || (pad != 0 && pad != 1)) throw std::invalid_argument("conv_dgrad_s2: ks 3 needs pad 0 or 1");
-    if ((DH + 2 * pad - 3) / 2 + 1 != OH || (DW + 2 * pad - 3) / 2 + 1 != OW)
-        throw std::invalid_argument("conv_dgrad_s2: dy / dx sizes do not match a stride-2 3x3 convolution");
-    // dx row ih = 2a + pr sees the forward taps with 2 oh + kh = ih + pad: q = pr + pad odd -> kh = 1 at
-    // dy row a (one tap); q even -> kh = 2 at row a + q/2 - 1 and kh = 0 at row a + q/2 (two taps, the
-    // window starting q/2 - 1 rows past a, i.e. zero padding 1 - q/2).  Same for columns.  Flipped-weight
-    // tap index = 2 - kh; every dx pixel is written by exactly one phase.
-    if (ea.fin && (DH < 2 || DW < 2)) throw std::invalid_argument("conv_dgrad_s2: in-launch finalize needs dx >= 2x2");
-    // the BN-backward sums accumulate over all four phase launches: only the last one finalizes
-    EpiArgs ea_early = ea;
-    ea_early.fin = nullptr;
-    for (int pr = 0; pr < 2; ++pr)
-        for (int pc = 0; pc < 2; ++pc) {
-            const EpiArgs &eap = (pr == 1 && pc == 1) ? ea : ea_early;
-            const int qr = pr + pad, qc = pc + pad;
-            const int nh = (qr & 1) ? 1 : 2, nw = (qc & 1) ? 1 : 2;
-            const int PH = (DH - pr + 1) / 2, PW = (DW - pc + 1) / 2;
-            if (PH <= 0 || PW <= 0) continue;
-            int map = 0;
-            for (int th = 0; th < nh; ++th)
-                for (int tw = 0; tw < nw; ++tw) {
-                    const int rh = nh == 1 ? 1 : (th == 0 ? 0 : 2), rw = nw == 1 ? 1 : (tw == 0 ? 0 : 2);
-                    map |= (rh * 3 + rw) << (4 * (th * nw + tw));
-                }
-            g.tapmap = map, g.pr = pr, g.pc = pc;
-            g.OH = PH, g.OW = PW, g.M = N * PH * PW;
-            g.ph = nh == 1 ? 0 : 1 - qr / 2;
-            g.pw = nw == 1 ? 0 : 1 - qc / 2;
-            if (nh == 1 && nw == 1) launch_phase<1>(dy, wt, dx, g, eap, epi, s, tv);
-            else if (nh == 1) launch_phase<0x12>(dy, wt, dx, g, eap, epi, s, tv);
-            else if (nw == 1) launch_phase<0x21>(dy, wt, dx, g, eap, epi, s, tv);
-            else launch_phase<0x22>(dy, wt, dx, g, eap, epi, s, tv);
-        }
-}
 
 void launch_conv3x3(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout,
                     int stride, hipStream_t s, int variant) {
@@ -1216,5 +185,6 @@ void launch_conv_flip_weight_taps(const uint16_t *w, uint16_t *wt, int Cout, int
 void launch_conv3x3_flip_weight(const uint16_t *w, uint16_t *wt, int Cout, int Cin, hipStream_t s) {
     launch_conv_flip_weight(w, wt, Cout, Cin, 3, s);
 }
+
 
 }  // namespace kfk

@@ -246,13 +246,13 @@ __global__ __launch_bounds__(64 * WM * WN) void wgrad_kernel(const uint16_t *__r
     for (int p = 0; p < STAGES - 1; ++p)
         if (p < nsteps) stage(p, p);
     int buf = 0;
-    // stagger (KUNGFU_WGRAD_STAGGER): the upper half of the waves (one per SIMD with 8 waves) issues its
+    // stagger (fixed per tile in the launcher): the upper half of the waves (one per SIMD with 8 waves) issues its
     // LDS-DMA staging before its fragment reads instead of between its two MFMA clusters, so the two
     // waves sharing a SIMD do not stall on staging issue at the same time
     // stagger 1: stage before the fragment reads; 2: after the second MFMA cluster (upper wave half)
     const bool upper = NW >= 8 && ((wave >> 2) & 1);
     const bool early = (stagger & 3) == 1 && upper, late = (stagger & 3) == 2 && upper;
-    if ((stagger & 4) && upper) __builtin_amdgcn_s_setprio(1);  // KUNGFU_WGRAD_STAGGER bit 2: static priority
+    if ((stagger & 4) && upper) __builtin_amdgcn_s_setprio(1);  // stagger bit 2: static priority
     for (int ks = 0; ks < nsteps; ++ks) {
         if (ks + STAGES - 1 <= nsteps) wait_vmcnt<LOADS * (STAGES - 2)>();
         else wait_vmcnt<0>();

@@ -212,12 +212,9 @@ bool conv_supported(int Cin, int Cout, int ks, int stride);
 //                 of the layer that produced u).
 enum ConvEpi : int {
     kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
-    kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGelu = 512, kEpiGeluGrad = 1024,
-    // not an epilogue: the A operand is the PRE-BN input x of a BN(+ReLU) -- the kernel applies
-    // relu(x * scale + shift) (ea.pcoef, [scale(Cin); shift(Cin)] f32) to every A fragment after its
-    // ds_read, and zeroes the padding taps' rows (BN1 / BN2 normalised on load).
-    // 1x1 / 3x3 forward only, Cin % 64 == 0, Cin <= 1024.
-    kEpiPreBN = 2048
+    kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGelu = 512, kEpiGeluGrad = 1024
+    // (round 6: the BN normalise-on-load A operand, 2048, is gone -- +2.56 ms/step on ResNet-50,
+    // profiles/r5_prebn.md)
 };
 // In-launch BN finalize of a statistics epilogue (kEpiFwdStats / kEpiBwdCoef / kEpiBwdBits): every
 // workgroup waits for its slot atomics, arrives on a two-level counter (per blockIdx % 8 shard,
@@ -250,7 +247,6 @@ struct EpiArgs {
     const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output
     const float *fcoef = nullptr;    // bwd coef: forward [scale(K); shift(K)]
     const uint8_t *bmask = nullptr;  // bwd bits: ReLU mask, one byte per 8 channels
-    const float *pcoef = nullptr;    // kEpiPreBN: the producing BN's [scale(Cin); shift(Cin)]
 };
 void launch_conv(const uint16_t *x, const uint16_t *w, uint16_t *y, int N, int H, int W, int Cin, int Cout, int ks,
                  int stride, const EpiArgs &ea, int epi, hipStream_t s, int variant = -1);

@@ -51,6 +51,20 @@ from ..parallel.mixed import SideStream, deliver, direct_target, shadow
 _ENABLED = os.environ.get("KUNGFU_FUSED_BLOCK", "1") != "0"
 
 
+# Test hook (tests/test_gpu_engine.py): a list that every backward appends each BN's gradient inputs
+# and its (dgamma, dbeta) to, so the fused BN-backward sums can be checked against an f64 reduction
+# of the SAME bf16 tensors; None (the default) records nothing.
+_CAPTURE = None
+
+
+def _capture(bn, kind, dz, x, mean, invstd, gate, dg, db):
+    """kind "relu": gate = the forward [scale; shift] (relu'(x*scale+shift)); "mask": gate = the
+    1-bit ReLU mask; "plain": no gate (the downsample BN inside the residual add)."""
+    _CAPTURE.append(dict(bn=bn, kind=kind, dz=dz.detach().clone(), x=x.detach().clone(), mean=mean.clone(),
+                         invstd=invstd.clone(), gate=None if gate is None else gate.clone(),
+                         dg=dg.detach().clone(), db=db.detach().clone()))
+
+
 def set_enabled(on: bool) -> bool:
     global _ENABLED
     old, _ENABLED = _ENABLED, bool(on)
@@ -70,7 +84,7 @@ def _sums(bn, dev) -> torch.Tensor:
     return ws
 
 
-# KUNGFU_BN_INLAUNCH_FIN=1: the statistics-producing conv finalizes its BN in its own launch
+# _INLAUNCH_FIN (module attribute; the retired KUNGFU_BN_INLAUNCH_FIN): the statistics-producing conv finalizes its BN in its own launch
 # (last-arriving workgroup, csrc/kernels/conv.hip bn_finalize_last; bit-identical).  Off by default:
 # measured 0.55-1.25 ms/step SLOWER on ResNet-50 than the separate finalize launches (every
 # workgroup must wait for its memory-side f64 slot atomics before it may arrive, and the arrivals
@@ -376,11 +390,15 @@ class _BottleneckFn(torch.autograd.Function):
                                             ws[2] if use3 else None, dres_x=yd if spec.ds else None,
                                             dres_sums=ws[3] if spec.ds else None, **_kw(pre=pre3))
         dbn[2] = (dg3, db3)
+        if _CAPTURE is not None:
+            _capture(spec.bns[2], "mask", dout, y3, m3, i3, mask3, dg3, db3)
         fin2, pre2 = _fin_bwd(spec.bns[1], ctx.gens[1])
         dz2 = _dgrad(dy3, z2, w[2], 1, 0, flipped=fl[2], bn=(ws[1], y2, c2, None, fin2))
         dw[2] = wgrad(dy3, z2, w[2], 1, 0)
         dy2, _, dg2, db2 = H.bn_backward(dz2, y2, m2, i2, g[1], c2, None, True, True, False, ws[1], **_kw(pre=pre2))
         dbn[1] = (dg2, db2)
+        if _CAPTURE is not None:
+            _capture(spec.bns[1], "relu", dz2, y2, m2, i2, c2, dg2, db2)
         fin1, pre1 = _fin_bwd(spec.bns[0], ctx.gens[0])
         dz1 = _dgrad(dy2, z1, w[1], s, 1, flipped=fl[1], bn=(ws[0], y1, c1, None, fin1))
         fused1 = _dgrad.fused
@@ -388,10 +406,14 @@ class _BottleneckFn(torch.autograd.Function):
         dy1, _, dg1, db1 = H.bn_backward(dz1, y1, m1, i1, g[0], c1, None, True, True, False,
                                          ws[0] if fused1 else None, **_kw(pre=pre1 if fused1 else None))
         dbn[0] = (dg1, db1)
+        if _CAPTURE is not None:
+            _capture(spec.bns[0], "relu", dz1, y1, m1, i1, c1, dg1, db1)
         acc_even = False
         if spec.ds:
             dyd, _, dgd, dbd = H.bn_backward(didt, yd, md, idd, g[3], cd, None, False, True, False, ws[3])
             dbn[3] = (dgd, dbd)
+            if _CAPTURE is not None:
+                _capture(spec.bns[3], "plain", didt, yd, md, idd, None, dgd, dbd)
             if s == 2 and _even_s2(x, dyd, 1):
                 # even pixels only; conv1's data gradient below stores the odd ones
                 dx = _dgrad_s2_even(dyd, x, w[3], flipped=fl[3])

@@ -28,7 +28,7 @@ from ..parallel.mixed import deliver, direct_target
 
 import os
 
-# KUNGFU_BN_CONCAT=0: apply deferred branch BNs and concatenate with torch.cat (A/B, tests)
+# CONCAT_ENABLED = False (module attribute): apply deferred branch BNs and concatenate with torch.cat (A/B, tests)
 CONCAT_ENABLED = True  # module switch (tests)
 
 

@@ -127,7 +127,7 @@ def _data_grad(dy2, wb):
         a = dy2.as_strided((S, dy2.shape[0], Kc), (Kc, dy2.stride(0), 1), dy2.storage_offset())
         b = wb.as_strided((S, Kc, D), (Kc * D, D, 1), wb.storage_offset())
         try:
-            return torch.bmm(a, b, out_dtype=torch.float32).sum(0, dtype=wb.dtype)
+            return torch.bmm(a, b, out_dtype=torch.float32).sum(0).to(wb.dtype)  # f32 slice sum, one rounding
         except (RuntimeError, TypeError):
             pass
     return torch.mm(dy2, wb)

@@ -542,8 +542,9 @@ class GradReducer:
         return False
 
     def _finish(self):
-        from .mixed import SideStream
+        from .mixed import SideStream, reset_pending
 
+        reset_pending()  # a tied table's use whose producer never ran in this backward is stale
         for j in self.tracker.flush():
             self._launch(self.buckets[j])
         if self._hier is not None:

@@ -65,6 +65,13 @@ _PENDING: Dict[Tuple[int, int], int] = {}
 _EMBED_DIRECT = True  # module switch (tests / A/B)
 
 
+def reset_pending() -> None:
+    """Forget every outstanding forward use (called at the end of each backward): a forward that
+    never got a backward (grad-enabled eval, a skipped step) would otherwise keep its table's count
+    above zero and its bucket would only launch at the end-of-backward flush from then on."""
+    _PENDING.clear()
+
+
 def use_direct(target: Tuple[FlatParamSpace, int]) -> None:
     k = (id(target[0]), target[1])
     _PENDING[k] = _PENDING.get(k, 0) + 1
@@ -145,9 +152,11 @@ def _linear_forward(self, x):
 
 
 class SideStream:
-    """Weight gradients on a side stream, overlapping the backward data-gradient chain
-    (``KUNGFU_WGRAD_STREAM=1``): a weight gradient depends only on its layer's output
-    gradient and input, and nothing on the critical path of backward reads it, so it can
+    """Weight gradients on a side stream, overlapping the backward data-gradient chain.  The linear
+    layers' direct split-K weight gradients always use it (ops/linear.py ``_WGRAD_SIDE``); the conv
+    weight gradients of the fused bottleneck only when ``enabled`` is set.  A weight gradient
+    depends only on its layer's output gradient and input, and nothing on the critical path of
+    backward reads it, so it can
     run beside the next layers' data gradients and the memory-bound BN passes (filling the
     CUs an under-sized grid leaves idle).  Its results reach the flat gradient buffer only
     through a gradient sink, which makes the landing stream wait for every side-stream
@@ -198,15 +207,34 @@ class ImmediateSink:
 
     def __init__(self, space: FlatParamSpace):
         self.space = space
+        self._join_armed = False
 
     def put(self, i: int, g: torch.Tensor) -> None:
         SideStream.join()
         with torch.no_grad():
             self.space.grad_view(i).add_(g)
 
+    def _end_of_backward(self) -> None:
+        self._join_armed = False
+        SideStream.join()
+        reset_pending()  # a use whose producer never ran (forward without this backward) is stale
+
+    def _arm(self, fn) -> bool:
+        """Queue ``fn`` for the end of the running backward; False (nothing queued) outside one."""
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(fn)
+            return True
+        except RuntimeError:
+            return False
+
     def put_direct(self, i: int) -> None:
-        """Parameter ``i``'s gradient was already added into its flat f32 slot by its producer
-        (on the current stream): nothing to land."""
+        """Parameter ``i``'s gradient was already added into its flat f32 slot by its producer.  The
+        producer may still be running on :class:`SideStream` (ops/linear.py): the end of backward
+        joins it, so the optimizer step on the main stream never reads a slot still being written."""
+        if not self._join_armed:
+            self._join_armed = self._arm(self._end_of_backward)
+            if not self._join_armed:
+                self._end_of_backward()
 
 
 class BatchedSink(ImmediateSink):
@@ -227,19 +255,24 @@ class BatchedSink(ImmediateSink):
             return super().put(i, g)
         self._staged.append(g)
         self._offs.append(self.space.offsets[i][0])
+        self._arm_flush()
+
+    def put_direct(self, i: int) -> None:
+        self._arm_flush()  # the flush joins the side stream even when nothing is staged
+
+    def _arm_flush(self) -> None:
         if not self._armed:
-            try:
-                torch.autograd.Variable._execution_engine.queue_callback(self.flush)
-                self._armed = True
-            except RuntimeError:  # not inside a backward pass: land now
+            self._armed = self._arm(self.flush)
+            if not self._armed:  # not inside a backward pass: land now
                 self.flush()
 
     def flush(self) -> None:
         self._armed = False
+        SideStream.join()
+        reset_pending()
         if self._staged:
             from .._lib import hip
 
-            SideStream.join()
             hip().grad_accumulate(self.space.flat_grad, self._staged, self._offs, 1.0)
             self._staged, self._offs = [], []
 

@@ -1809,34 +1809,6 @@ def test_bench_emulate_comm_model():
 
 
 @needs_gpu
-@pytest.mark.parametrize("ks,c,cout,hw", [(1, 64, 256, 14), (1, 128, 128, 9), (3, 64, 64, 11), (3, 128, 256, 7)])
-def test_conv_prebn_matches_bn_apply_then_conv(H, ks, c, cout, hw):
-    """conv.hip kEpiPreBN (the BN normalise-on-load prototype, tools/bench_prebn.py): convolving the PRE-BN
-    input with relu(x*scale+shift) applied to the A fragments on load -- padding taps zero, not
-    relu(shift) -- equals convolving the BN apply pass's output, bitwise (same f32 FMA, same RNE)."""
-    torch.manual_seed(ks * 100 + c)
-    x = (torch.randn(3, c, hw, hw, device="cuda") * 2 + 0.3).bfloat16().contiguous(memory_format=torch.channels_last)
-    w = (torch.randn(cout, c, ks, ks, device="cuda") / (c * ks * ks) ** 0.5).bfloat16().contiguous(
-        memory_format=torch.channels_last)
-    scale = torch.rand(c, device="cuda") + 0.5
-    shift = torch.randn(c, device="cuda") * 0.5
-    coef = torch.cat([scale, shift])
-    y = torch.relu(torch.addcmul(shift.view(1, -1, 1, 1), x.float(), scale.view(1, -1, 1, 1))).bfloat16()
-    y = y.contiguous(memory_format=torch.channels_last)
-    ref = H.conv(y, w, 1)
-    got = H.conv(x, w, 1, pre_coef=coef)
-    assert got.shape == ref.shape
-    # torch's addcmul may round differently from one FMA: compare within one bf16 ulp of the inputs' effect
-    assert ((got.float() - ref.float()).norm() / ref.float().norm()).item() < 2e-3
-    slots = H.conv_stat_slots
-    st = torch.zeros(slots * 2 * cout, dtype=torch.float64, device="cuda")
-    got2 = H.conv(x, w, 1, st, pre_coef=coef)
-    assert torch.equal(got2, got)
-    s = st.view(slots, 2, cout).sum(0)
-    torch.testing.assert_close(s[0], got.double().sum(dim=(0, 2, 3)), rtol=1e-6, atol=1e-3)
-
-
-@needs_gpu
 @pytest.mark.parametrize("n,h,w,k,s,p", [(3, 37, 37, 3, 2, 0), (2, 29, 31, 3, 1, 1), (2, 33, 33, 4, 2, 1),
                                          (4, 20, 18, 2, 1, 0), (256, 224, 224, 3, 2, 0)])
 def test_stem3_forward_and_wgrad_match_fp32(H, n, h, w, k, s, p):

@@ -303,6 +303,61 @@ def test_resnet50_engine_gradients_within_stock_bf16_envelope():
 
 
 @needs_gpu
+def test_resnet50_bn_param_grads_match_f64_on_shared_inputs():
+    """the model-level pin of the 104 block-BN gamma/beta gradients (the stock-bf16
+    envelope above is vacuous for them -- a sign-flipped gradient scores 2.0 against a bound of 2.2-3.0).
+    One engine forward/backward of ResNet-50 (224x224, batch 32, after one lr-0.1 step so the BNs are
+    not at gamma=1/beta=0) records every fused block BN's backward inputs (ops/fused_block._CAPTURE:
+    the gradient at the BN(+ReLU) output, the bf16 BN input, mean/invstd, the ReLU gate); an f64
+    reduction of those SAME tensors (utils/numerics.bn_param_grads_f64) must match the fused
+    kernels' dgamma/dbeta -- which come from the conv epilogues' BNLink sums (slotted f64 atomics),
+    the cross-block tail link and the finalize -- to 1e-3 relative L2, and the flat gradient slots
+    the sink landed them in must hold exactly those values."""
+    import kungfu_amd as kf
+    from kungfu_amd.models import resnet50
+    from kungfu_amd.ops import fused_block
+    from kungfu_amd.parallel.mixed import enable_bf16_shadow
+    from kungfu_amd.utils.numerics import bn_param_grads_f64, check_bn_param_grads, rel_err
+
+    kf.init()
+    torch.manual_seed(4321)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(32, 3, 224, 224, device="cuda", generator=g).to(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (32,), device="cuda", generator=g)
+    m = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
+    opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9),
+                                                named_parameters=m.named_parameters())
+    enable_bf16_shadow(m, opt)
+    for cap in (False, True):
+        opt.zero_grad()
+        fused_block._CAPTURE = [] if cap else None
+        try:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(m(x).float(), y)
+            loss.backward()
+            opt.reducer.synchronize()
+            recs = fused_block._CAPTURE
+        finally:
+            fused_block._CAPTURE = None
+        if not cap:
+            opt.step()
+    assert len(recs) == 52, len(recs)  # 16 blocks x 3 BNs + 4 downsample BNs
+    index = {id(p): i for i, p in enumerate(opt.space.params)}
+    kinds, worst = {}, 0.0
+    for r in recs:
+        ref = bn_param_grads_f64(r["dz"], r["x"], r["mean"], r["invstd"], r["kind"], r["gate"])
+        msg = check_bn_param_grads(ref, (r["dg"], r["db"]), tol=1e-3)
+        assert msg is None, (r["kind"], tuple(r["x"].shape), msg)
+        worst = max(worst, rel_err(ref[0], r["dg"]), rel_err(ref[1], r["db"]))
+        kinds[r["kind"]] = kinds.get(r["kind"], 0) + 1
+        # landed in the flat slots exactly (zeroed by zero_grad, one landing per parameter)
+        for prm, v in ((r["bn"].weight, r["dg"]), (r["bn"].bias, r["db"])):
+            assert torch.equal(opt.space.grad_view(index[id(prm)]).view(-1), v.float().view(-1)), r["kind"]
+    print("BN param grads vs f64 on shared inputs: %s, worst rel %.2e" % (kinds, worst))
+    assert kinds == {"mask": 16, "relu": 32, "plain": 4}, kinds
+
+
+@needs_gpu
 def test_resnet50_full_size_engine_memorises_batch_like_stock():
     """lr 0.01 (no chaotic phase): stock and engine both memorise one fixed 224x224 batch of 64
     (7.16 -> ~4.2 in 10 steps) and agree within 2 % at every step (measured within 0.5 %).  The
