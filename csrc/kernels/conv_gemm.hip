@@ -49,25 +49,11 @@ void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K
     g.wtaps = 1, g.tapmap = -1, g.scat = 0, g.pr = g.pc = 0, g.ph = g.pw = 0, g.dh = g.dw = 0;
     g.stagger = conv_stagger();
     g.prio = conv_prio();
-    // no epilogue / bias: the persistent pipelined kernel (conv_pipe_kernel) on the default tile;
-    // variants 10 / 11 / 12 force it on 256x256 / 256x128 / 128x128, 0..3 force conv_kernel (A/B)
-    const bool pipe_ok = (epi == 0 || epi == kEpiBias) && pipe_eligible(g, ea, 0);
-    int pv = -1;
-    if (variant >= 10 && variant <= 12) {
-        if (!pipe_ok) throw std::invalid_argument("gemm: pipe variants 10-12 need no epilogue or a bias");
-        pv = variant == 10 ? 7 : variant == 11 ? 1 : 0;
-    }
     if (variant < 0) {
         // enough 256x256 tiles to fill the chip twice, else 256x128, else 128x128 (or 128x64)
         const int64_t t256 = N % 256 ? 0 : ((M + 255) / 256) * (N / 256);
         const int64_t t128 = N % 128 ? 0 : ((M + 255) / 256) * (N / 128);
         variant = t256 >= 512 ? 0 : t128 >= 512 ? 1 : 2;
-        if (pipe_ok) pv = variant == 0 ? 7 : variant == 1 ? 1 : (N % 128 == 0 ? 0 : 2);
-    }
-    if (pv >= 0) {
-        if (epi == 0) launch_pipe_variant<0>(x, w, y, g, ea, pv, s);
-        else launch_pipe_variant<kEpiBias>(x, w, y, g, ea, pv, s);
-        return;
     }
     switch (variant) {
     case 0: if (N % 256 == 0) { launch_gemm_t<4, 2, 2, 4, 8>(x, w, y, g, ea, epi, s); break; }  // 256x256, 8 waves

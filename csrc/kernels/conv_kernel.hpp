@@ -67,7 +67,6 @@ void launch_conv_k3(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, co
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 __device__ __forceinline__ int wm_of(int wave, int wn) { return wave / wn; }
@@ -670,284 +669,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     }
 }
 
-// ---------------------------------------------------------------- persistent pipelined 1x1 / GEMM
-// Round 6.  conv_kernel's persistent walk runs its tiles back to back with nothing in flight between
-// them: the next tile's staging is issued after the epilogue, and its first `s_waitcnt vmcnt` also
-// waits for every epilogue store (loads, stores and LDS-DMA retire in issue order,
-// MI355X_MICROARCH.md "vmcnt").  For a 1x1 convolution with 64-256 input channels (1-4 K-steps) the
-// tile IS mostly prologue and epilogue: the ResNet-50 expansions (64 -> 256 at 56x56) write 128 KB
-// per 256x256 tile and ran at 3.8 TB/s, the 14x14 / 7x7 layers at 1.7-2.6 TB/s.
-//
-// conv_pipe_kernel keeps ONE staging pipeline across the workgroup's whole tile sequence:
-//   * the K loop runs over (tile, K-step) pairs; step s+1's LDS-DMA is issued during step s even when
-//     s+1 belongs to the next tile, so the next tile's operands land while this tile's epilogue runs;
-//   * the epilogue stages C through the ring buffer the last K-step just consumed (unpadded rows,
-//     16-byte chunks XOR-swizzled by row; PARTS row blocks when C is larger than one buffer), with
-//     raw s_barrier + lgkmcnt(0) only -- a __syncthreads() would drain the in-flight staging;
-//   * C leaves through buffer stores (rows past M / columns past N get an out-of-range offset and are
-//     dropped) so every wave issues exactly STORES of them, and the next step's wait is the counted
-//     vmcnt(STORES): the stores stay in flight while the next tile computes.
-// Epilogues: none, BN statistics (the persistent per-channel register sums of conv_kernel), bias.
-// Each workgroup keeps one N tile and walks M tiles mt0, mt0 + mstride, ... (XCD-contiguous ids).
-constexpr int pipe_lds_bytes(int bm, int bn) { return 2 * (bm + bn) * kRowBytes; }
-
-// conv_pipe_kernel staging helpers.  A row m0 + 8 u of the tile (one 8-row slab per u) -> byte offset
-// of its 16-byte chunk `schunk` at K-step 0 (kBufOOB past M).
-template <int A_INST>
-__device__ __forceinline__ void pipe_a_offsets(uint32_t *a_off, int m_first, int schunk, const Geo &g) {
-#pragma unroll
-    for (int u = 0; u < A_INST; ++u) {
-        const int m = m_first + u * 8;
-        uint32_t o = kBufOOB;
-        if (m < g.M) {
-            const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
-            o = static_cast<uint32_t>((((n * g.H + oh * g.stride) * g.W + ow * g.stride) * g.C + schunk * 8) * 2);
-        }
-        a_off[u] = o;
-    }
-}
-
-// One K-step's LDS-DMA: A_INST + B_INST 16-byte buffer loads per lane into the stage at `base`.
-template <int A_INST, int B_INST, int A_BYTES>
-__device__ __forceinline__ void pipe_stage_issue(uint8_t *base, const uint16_t *x, const uint16_t *w,
-                                                 const uint32_t *a_off, const uint32_t *b_off, int wave, uint32_t kb) {
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kBufOOB), kBufFlags);
-    const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(w), 0, static_cast<int>(kBufOOB), kBufFlags);
-#pragma unroll
-    for (int u = 0; u < A_INST; ++u)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(base + (wave * A_INST + u) * 1024), 16,
-                                                 a_off[u] == kBufOOB ? kBufOOB : a_off[u] + kb, 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < B_INST; ++u)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, lds_ptr(base + A_BYTES + (wave * B_INST + u) * 1024), 16,
-                                                 b_off[u] == kBufOOB ? kBufOOB : b_off[u] + kb, 0, 0, 0);
-}
-
-template <int WM, int WN, int TM, int TN, int EPI>
-__global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const uint16_t *__restrict__ x,
-                                                                 const uint16_t *__restrict__ w,
-                                                                 uint16_t *__restrict__ y, Geo g, EpiArgs ea) {
-    constexpr int WTM = 16 * TM, WTN = 16 * TN;
-    constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
-    constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes, STAGE = A_BYTES + B_BYTES;
-    constexpr int A_INST = BM / 8 / NW, B_INST = BN / 8 / NW;
-    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
-    constexpr int CROW = BN * 2;                   // bytes per C row (unpadded, swizzled)
-    constexpr int CCH = BN / 8;                    // 16-byte chunks per C row
-    constexpr int SWZ = CCH < 16 ? CCH - 1 : 15;   // chunk XOR mask
-    constexpr int PARTS = (BM * CROW + STAGE - 1) / STAGE;
-    constexpr int PROWS = BM / PARTS;
-    static_assert(PROWS * PARTS == BM && PROWS % WTM == 0, "a C part is whole wave rows");
-    constexpr bool STATS = (EPI & kEpiFwdStats) != 0;
-    constexpr bool BIAS = (EPI & kEpiBias) != 0;
-    static_assert((EPI & ~(kEpiFwdStats | kEpiBias)) == 0, "conv_pipe_kernel: none / statistics / bias");
-    constexpr int VPR = BN / 8;
-    static_assert(NT % VPR == 0, "fixed channel group per thread");
-    constexpr int ITER = PROWS * VPR / NT;         // C vectors per thread per part
-    static_assert(ITER * NT == PROWS * VPR, "whole store iterations");
-    constexpr int STORES = ITER * PARTS;
-    static_assert(STORES <= 48, "vmcnt budget");
-    constexpr int GROUPS = NT / VPR;
-    static_assert(2 * GROUPS * BN * 4 <= 2 * STAGE, "statistics reduction fits the ring");
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[pipe_lds_bytes(BM, BN)];
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nwg = gridDim.x, orig = blockIdx.x;
-    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
-    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
-    const int mt0 = wg / g.ntiles, ntile = wg - mt0 * g.ntiles;
-    const int mstride = nwg / g.ntiles;  // nwg % ntiles == 0 (launcher)
-    const int n0 = ntile * BN;
-    const int ntl = mt0 < g.mtiles ? (g.mtiles - mt0 + mstride - 1) / mstride : 0;
-    const int ksteps = g.C / kBK;  // Cin % 64 == 0 (launcher)
-    const int steps = ntl * ksteps;
-
-    const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y, 0, static_cast<int>(kBufOOB), kBufFlags);
-
-    const int srow = lane >> 3, schunk = (lane & 7) ^ srow;
-    // B rows: fixed for the whole walk
-    uint32_t b_off[B_INST];
-#pragma unroll
-    for (int j = 0; j < B_INST; ++j) {
-        const int r = (wave * B_INST + j) * 8 + srow;
-        b_off[j] = n0 + r < g.K ? static_cast<uint32_t>(((n0 + r) * g.C + schunk * 8) * 2) : kBufOOB;
-    }
-    // A rows of the tile being staged (recomputed when the staged step starts a new tile).  Helpers
-    // taking plain pointers, no lambda: hipcc's (ROCm 7.2) host pass fails to substitute arrays whose
-    // bound is a template-dependent local constexpr (reference-to-array parameters, lambda captures)
-    // and then silently drops the kernel's host launch stub -- an undefined __device_stub__ at load.
-    uint32_t a_off[A_INST];
-    int a_tile = -1;
-#define KF_PIPE_STAGE(st_, buf_)                                                                              \
-    do {                                                                                                      \
-        const int sj_ = (st_) / ksteps, sk_ = (st_) - sj_ * ksteps;                                           \
-        if (sj_ != a_tile) {                                                                                  \
-            a_tile = sj_;                                                                                     \
-            pipe_a_offsets<A_INST>(a_off, (mt0 + sj_ * mstride) * BM + wave * A_INST * 8 + srow, schunk, g);  \
-        }                                                                                                     \
-        pipe_stage_issue<A_INST, B_INST, A_BYTES>(lds + (buf_) * STAGE, x, w, a_off, b_off, wave,                      \
-                                                  static_cast<uint32_t>(sk_ * kBK * 2));                       \
-    } while (0)
-
-    const int wm = wave / WN, wn = wave % WN;
-    const int cv = tid % VPR;  // the epilogue's fixed 8-channel group
-    const bool col_ok = n0 + cv * 8 < g.K;
-    float s1[8], s2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
-    float bcol[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            bcol[j][r] = 0.f;
-            if constexpr (BIAS) {
-                const int c = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-                if (c < g.K) bcol[j][r] = bf16_to_f32(ea.bias[c]);
-            }
-        }
-
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mfma_block = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    };
-
-    if (steps > 0) KF_PIPE_STAGE(0, 0);
-    int k = 0, tile = 0;
-    for (int st = 0; st < steps; ++st) {
-        const int buf = st & 1;
-        // step st landed: the previous step ended a tile -> its STORES epilogue stores are younger
-        if (k == 0 && st > 0) wait_vmcnt<STORES>();
-        else wait_vmcnt<0>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        const uint8_t *abase = lds + buf * STAGE;
-        const uint8_t *bbase = abase + A_BYTES;
-        bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-            af0[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(wm * WTM + i * 16 + (lane & 15), lane >> 4));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-            bf0[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(wn * WTN + j * 16 + (lane & 15), lane >> 4));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-            af1[i] = *reinterpret_cast<const bf16x8 *>(abase + img_off(wm * WTM + i * 16 + (lane & 15), 4 + (lane >> 4)));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-            bf1[j] = *reinterpret_cast<const bf16x8 *>(bbase + img_off(wn * WTN + j * 16 + (lane & 15), 4 + (lane >> 4)));
-        mfma_block(af0, bf0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (st + 1 < steps) KF_PIPE_STAGE(st + 1, buf ^ 1);  // possibly the NEXT tile's first step
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_block(af1, bf1);
-        if (++k < ksteps) continue;
-
-        // ---- epilogue of tile `tile`: C through this step's (consumed) buffer
-        k = 0;
-        const int m0 = (mt0 + tile * mstride) * BM;
-        ++tile;
-        uint8_t *cbuf = lds + buf * STAGE;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave's fragment reads of this buffer are done
-#pragma unroll
-        for (int part = 0; part < PARTS; ++part) {
-            if (part > 0) {
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();  // the previous part's rows are read out
-            }
-            if (wm * WTM / PROWS == part) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        const int row = wm * WTM + i * 16 + (lane & 15) - part * PROWS;
-                        const int col = wn * WTN + j * 16 + (lane >> 4) * 4;  // channel
-                        uint32_t h[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) h[r] = f32_to_bf16(acc[i][j][r] + bcol[j][r]);
-                        const int chunk = (col >> 3) ^ (row & SWZ);
-                        const uint2 pk = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-                        bf16x4 pb;
-                        __builtin_memcpy(&pb, &pk, 8);
-                        *reinterpret_cast<bf16x4 *>(cbuf + row * CROW + chunk * 16 + (col & 4) * 2) = pb;
-                    }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-#pragma unroll
-            for (int it = 0; it < ITER; ++it) {
-                const int row = (tid + it * NT) / VPR;  // within the part
-                const int m = m0 + part * PROWS + row;
-                // bf16-typed LDS accesses: hipcc (ROCm 7.2) puts a vmcnt(0) -- draining the in-flight
-                // staging -- in front of integer-typed ds_read/ds_write here, not in front of these
-                const bf16x8 vb = *reinterpret_cast<const bf16x8 *>(cbuf + row * CROW + ((cv ^ (row & SWZ)) << 4));
-                uint4 v;
-                __builtin_memcpy(&v, &vb, 16);
-                const bool ok = m < g.M && col_ok;
-                const uint32_t off = ok ? static_cast<uint32_t>((static_cast<int64_t>(m) * g.K + n0 + cv * 8) * 2) : kBufOOB;
-                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-                v4u vv;
-                vv.x = v.x, vv.y = v.y, vv.z = v.z, vv.w = v.w;
-                __builtin_amdgcn_raw_buffer_store_b128(vv, yr, off, 0, 0);
-                if constexpr (STATS) {
-                    if (ok) {
-                        float f[8];
-                        unpack_bf16x8(v, f);
-#pragma unroll
-                        for (int c = 0; c < 8; ++c) {
-                            s1[c] += f[c];
-                            s2[c] += f[c] * f[c];
-                        }
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if constexpr (STATS) {
-        // per channel group: reduce the NT / VPR threads through LDS, then f64 atomics into a slot
-        wait_vmcnt<0>();
-        __syncthreads();
-        float *red = reinterpret_cast<float *>(lds);
-        const int grp = tid / VPR;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            red[grp * BN + cv * 8 + c] = s1[c];
-            red[(GROUPS + grp) * BN + cv * 8 + c] = s2[c];
-        }
-        __syncthreads();
-        for (int col = tid; col < BN; col += NT) {
-            double t1 = 0, t2 = 0;
-#pragma unroll 4
-            for (int p = 0; p < GROUPS; ++p) {
-                t1 += red[p * BN + col];
-                t2 += red[(GROUPS + p) * BN + col];
-            }
-            double *sl = ea.stats + (wg % kStatSlots) * 2 * g.K;
-            if (n0 + col < g.K && ntl > 0) {
-                atomicAdd(sl + n0 + col, t1);
-                atomicAdd(sl + g.K + n0 + col, t2);
-            }
-        }
-    }
-#undef KF_PIPE_STAGE
-}
-
 template <int KS, int WM, int WN, int ST, int EPI, int TM = 4, int TN = 4>
 void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
     constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
@@ -982,45 +703,6 @@ void launch_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const 
     }
     conv_kernel<KS, WM, WN, ST, EPI, TM, TN><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
         x, w, y, reinterpret_cast<const uint16_t *>(zero_page()), g, ea);
-}
-
-// conv_pipe_kernel launch: persistent grid of (occupancy x 256 CUs) workgroups, rounded to whole
-// N-tile columns (each workgroup keeps one N tile).
-template <int WM, int WN, int TM, int TN, int EPI>
-void launch_pipe(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
-    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-    constexpr int LDS = 2 * (BM + BN) * kRowBytes;
-    constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
-    check_buf_extent(g);
-    g.mtiles = (g.M + BM - 1) / BM;
-    g.ntiles = (g.K + BN - 1) / BN;
-    int per_n = (256 * (OCC < 1 ? 1 : OCC)) / g.ntiles;
-    if (per_n < 1) per_n = 1;
-    if (per_n > g.mtiles) per_n = g.mtiles;
-    conv_pipe_kernel<WM, WN, TM, TN, EPI><<<per_n * g.ntiles, 64 * WM * WN, 0, s>>>(x, w, y, g, ea);
-}
-
-// 1x1 convolutions (any stride, pad 0) with no epilogue or the BN-statistics one, on the default
-// tile of launch_ks: the pipelined persistent kernel.  Its C stores address y with 32-bit byte offsets.
-#ifndef KUNGFU_CONV_PIPE
-#define KUNGFU_CONV_PIPE 1
-#endif
-inline bool pipe_eligible(const Geo &g, const EpiArgs &ea, int epi) {
-    return KUNGFU_CONV_PIPE && (epi == 0 || epi == kEpiFwdStats) && ea.fin == nullptr && g.C % 64 == 0 &&
-           g.K % 8 == 0 && static_cast<int64_t>(g.M) * g.K * 2 < static_cast<int64_t>(kBufOOB);
-}
-
-template <int EPI>
-void launch_pipe_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int variant,
-                         hipStream_t s) {
-    switch (variant) {
-    case 0: launch_pipe<2, 2, 4, 4, EPI>(x, w, y, g, ea, s); break;   // 128x128, 4 waves
-    case 1: launch_pipe<4, 2, 4, 4, EPI>(x, w, y, g, ea, s); break;   // 256x128, 8 waves
-    case 2: launch_pipe<4, 1, 4, 4, EPI>(x, w, y, g, ea, s); break;   // 256x64, 4 waves
-    case 7: launch_pipe<4, 2, 4, 8, EPI>(x, w, y, g, ea, s); break;   // 256x256, 8 waves
-    case 11: launch_pipe<4, 1, 4, 2, EPI>(x, w, y, g, ea, s); break;  // 256x32, 4 waves
-    default: throw std::invalid_argument("conv_pipe: tile variant");
-    }
 }
 
 // Every fused epilogue on one tile shape.
@@ -1079,15 +761,6 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     // the per-shape defaults only (round 6: the tuning-only tiles -- 256x64 3-stage, 512x64, 128x64,
     // 256x256 of 128x64 waves, the 2- and 4-wave 64x128 -- never won a default, see
     // profiles/r3_conv_variants.txt, and are no longer instantiated)
-    if constexpr (KS == 1) {
-        if (pipe_eligible(g, ea, epi)) {
-            int v = variant;
-            if ((v == 0 || v == 1) && g.K % 128) v = 2;  // the fallthroughs below
-            if (epi == 0) launch_pipe_variant<0>(x, w, y, g, ea, v, s);
-            else launch_pipe_variant<kEpiFwdStats>(x, w, y, g, ea, v, s);
-            return;
-        }
-    }
     switch (variant) {
     case 0: if (g.K % 128 == 0) { launch_variant<KS, 2, 2, 2>(x, w, y, g, ea, epi, s); break; }  // 128x128
             [[fallthrough]];

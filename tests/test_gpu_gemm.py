@@ -59,31 +59,6 @@ def test_gemm_gelu_grad_and_bias_sums(M, K, N):
     assert _rel(db, uf.grad.double().sum(0)) < 2e-2
 
 
-@pytest.mark.parametrize("M,K,N", [(4096, 768, 2304), (1000, 768, 768), (2048, 3072, 768), (520, 256, 192),
-                                   (16384, 768, 3072)])
-@pytest.mark.parametrize("variant", [10, 11, 12])
-def test_gemm_pipe_variants(M, K, N, variant):
-    """The persistent pipelined kernel (conv_kernel.hpp conv_pipe_kernel) as the linear forward:
-    every tile (10 256x256, 11 256x128, 12 128x128), M / N tails, plain and bias, plus a one-hot probe
-    of the output map (row t of the product must be column t % K of w)."""
-    H = _hip()
-    if variant == 10 and N % 256:
-        pytest.skip("256-wide tile")
-    torch.manual_seed(13)
-    x = torch.randn(M, K, device="cuda").bfloat16()
-    w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
-    b = torch.randn(N, device="cuda").bfloat16()
-    ref = x.float() @ w.float().t()
-    y = H.gemm(x, w, variant=variant)[0]
-    assert y.shape == (M, N) and _rel(y, ref) < 1e-2
-    yb = H.gemm(x, w, b, variant=variant)[0]
-    assert _rel(yb, ref + b.float()) < 1e-2
-    e = torch.zeros(M, K, device="cuda").bfloat16()
-    e[torch.arange(M), torch.arange(M) % K] = 1
-    pick = H.gemm(e, w, variant=variant)[0]
-    assert torch.equal(pick, w[:, torch.arange(M, device="cuda") % K].t().contiguous())
-
-
 def test_gemm_accumulate():
     H = _hip()
     torch.manual_seed(7)
