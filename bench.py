@@ -260,8 +260,6 @@ def main():
     p.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="gradient dtype on the wire")
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
-    p.add_argument("--wgrad-side", type=int, default=0,
-                   help="1: fused-bottleneck conv weight gradients on a side stream (A/B switch)")
     p.add_argument("--bucket-mb", type=float, default=None)
     p.add_argument("--bf16-shadow", type=int, default=1,
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
@@ -341,10 +339,6 @@ def main():
     torch.manual_seed(1234)  # same init everywhere (broadcast_parameters makes it exact)
 
     fused_bn = a.fused_bn
-    if a.wgrad_side:
-        from kungfu_amd.parallel.mixed import SideStream
-
-        SideStream.enabled = True
     if fused_bn < 0:
         from kungfu_amd.ops import fused_bn as fb
 

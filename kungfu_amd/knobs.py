@@ -115,8 +115,6 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_CONV_TILE_RULES": _d("2", "1 = the round-2 conv tile defaults"),
     "KUNGFU_VGG_FUSED": _d("1", "VGG-16 conv/ReLU/pool stack as one autograd node (0: the per-layer modules)"),
     "KUNGFU_GRAPH_MULTIRANK": _u("1", "0: GraphedStep keeps multi-rank RCCL steps eager (capture uses the comm stream as origin)"),
-    "KUNGFU_GRAPH_SEGMENTED": _u("1", "N-rank capture as graph segments cut at every bucket launch, collectives issued "
-                                       "eagerly between replays (0: one graph with the collectives inside)"),
 }
 
 # Round 5: A/B knobs whose question is settled are gone -- the measured winner
@@ -133,22 +131,23 @@ RETIRED: Dict[str, str] = {
     "KUNGFU_COMM_STREAM_PRIORITY": "a high-priority comm stream measured 2x slower (r1)",
     "KUNGFU_BN_SKIP_FINALIZE": "timing-only experiment (wrong numerics), retired",
     "KUNGFU_BERT_GEMM": "unused",
-    "KUNGFU_CONV_STAGGER": "settled: on (+0.8 %, r3)",
-    "KUNGFU_CONV_PERSIST_BLOCKS": "settled: 4 persistent blocks per CU",
-    "KUNGFU_WGRAD_STAGGER": "settled: on for 256x256 tiles only (r3)",
-    "KUNGFU_WROWS_STAGGER": "settled: on (r3)",
-    "KUNGFU_WGRAD_KB32": "settled: off (r4t1)",
-    "KUNGFU_BN_NT": "settled: non-temporal loads (r3f)",
-    "KUNGFU_BN_MAXGRID": "settled: the kernel default grid",
-    "KUNGFU_ATTN_BWD_WAVES": "settled: 8 waves (r4t15)",
-    "KUNGFU_BN_CONCAT": "settled: on (module attribute ops.fused_bn.CONCAT_ENABLED)",
-    "KUNGFU_BN_BATCH_FIN": "settled: on (r4t25; module attribute ops.fused_bn._BATCH_FIN)",
-    "KUNGFU_LN_BIAS_LINK": "settled: on (module attribute ops.layernorm._BIAS_LINK)",
-    "KUNGFU_GELU_BIAS_LINK": "settled: on (module attribute ops.linear._GELU_LINK)",
-    "KUNGFU_RESIDUAL_LINK": "settled: on (r4t14; module attribute ops.linear._RES_LINK)",
-    "KUNGFU_LINEAR_DIRECT_WGRAD": "settled: on (module attribute ops.linear._DIRECT_WGRAD)",
-    "KUNGFU_FUSED_XENT": "settled: on (r4t22; module attribute ops.xent._ENABLED)",
-    "KUNGFU_PAIR_NATIVE": "settled: the native prefetch thread (r4t22)",
+    "KUNGFU_CONV_STAGGER": "the measured winner is the only path: on (+0.8 %, r3)",
+    "KUNGFU_CONV_PERSIST_BLOCKS": "the measured winner is the only path: 4 persistent blocks per CU",
+    "KUNGFU_WGRAD_STAGGER": "the measured winner is the only path: on for 256x256 tiles only (r3)",
+    "KUNGFU_WROWS_STAGGER": "the measured winner is the only path: on (r3)",
+    "KUNGFU_WGRAD_KB32": "the measured winner is the only path: off (r4t1)",
+    "KUNGFU_BN_NT": "the measured winner is the only path: non-temporal loads (r3f)",
+    "KUNGFU_BN_MAXGRID": "the measured winner is the only path: the kernel default grid",
+    "KUNGFU_ATTN_BWD_WAVES": "the measured winner is the only path: 8 waves (r4t15)",
+    "KUNGFU_BN_CONCAT": "the measured winner is the only path: on (module attribute ops.fused_bn.CONCAT_ENABLED)",
+    "KUNGFU_BN_BATCH_FIN": "the measured winner is the only path: on (r4t25; module attribute ops.fused_bn._BATCH_FIN)",
+    "KUNGFU_LN_BIAS_LINK": "the measured winner is the only path: on (module attribute ops.layernorm._BIAS_LINK)",
+    "KUNGFU_GELU_BIAS_LINK": "the measured winner is the only path: on (module attribute ops.linear._GELU_LINK)",
+    "KUNGFU_RESIDUAL_LINK": "the measured winner is the only path: on (r4t14; module attribute ops.linear._RES_LINK)",
+    "KUNGFU_LINEAR_DIRECT_WGRAD": "the measured winner is the only path: on (module attribute ops.linear._DIRECT_WGRAD)",
+    "KUNGFU_FUSED_XENT": "the measured winner is the only path: on (r4t22; module attribute ops.xent._ENABLED)",
+    "KUNGFU_PAIR_NATIVE": "the measured winner is the only path: the native prefetch thread (r4t22)",
+    "KUNGFU_GRAPH_SEGMENTED": "the whole-graph N-rank layout is gone: N-rank capture is always segmented (r6)",
 }
 
 # compile-time switches (-D...), not environment variables; listed so the source lint knows them

@@ -46,7 +46,7 @@ import torch
 import torch.nn.functional as F
 
 from .._lib import buf_ok, hip, hip_available
-from ..parallel.mixed import SideStream, deliver, direct_target, shadow
+from ..parallel.mixed import deliver, direct_target, shadow
 
 _ENABLED = os.environ.get("KUNGFU_FUSED_BLOCK", "1") != "0"
 
@@ -363,14 +363,9 @@ class _BottleneckFn(torch.autograd.Function):
                     fl[k] = src[0].get(src[1])
         dbn = [None] * nb  # (dgamma, dbeta)
         dw = [None] * nb
-        # weight gradients on the side stream when every one of them goes to a gradient sink
-        # (bf16 shadow weights): the sink joins the side stream before landing them
-        side = SideStream.enabled and spec.wsrc is not None and all(v is not None for v in spec.wsrc)
-
-        def wgrad(dy_, x_, w_, s_, p_):
-            if side:
-                return SideStream.run(lambda a_, b_: _wgrad(a_, b_, w_, s_, p_), dy_, x_)
-            return _wgrad(dy_, x_, w_, s_, p_)
+        # (the conv weight gradients on a side stream measured slower twice: eager 1.2 % in r3, as
+        # hipGraph branches 20.44 -> 21.05 ms/step in r6t4 -- removed, round 6)
+        wgrad = _wgrad
 
         ws = [_sums(b, dout.device) for b in spec.bns]
         tail = ctx.tail

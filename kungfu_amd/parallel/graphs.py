@@ -20,7 +20,7 @@ What makes a step capturable here:
   collective order (rank 0's order is adopted on the second step) and every lazily allocated
   workspace (BN statistics slots, flip caches, comm buffers) exists.
 
-N-rank steps (``KUNGFU_GRAPH_SEGMENTED=1``, the default): the step is captured as a chain of graph
+N-rank steps: the step is captured as a chain of graph
 SEGMENTS cut at every bucket launch and at the end-of-backward join; a replay runs segment 0, issues
 the bucket's RCCL collective eagerly on the comm stream (event-fenced after the segment), replays
 segment 1, ... -- the compute stream never carries a collective, and the collectives overlap the
@@ -182,25 +182,15 @@ class GraphedStep:
             err = RuntimeError("the cross-host hierarchical all-reduce cannot be captured")
         elif multi and knobs.get("KUNGFU_GRAPH_MULTIRANK") != "1":
             err = RuntimeError("multi-rank RCCL capture is disabled (KUNGFU_GRAPH_MULTIRANK=0)")
-        segmented = multi and knobs.get("KUNGFU_GRAPH_SEGMENTED") != "0"
         try:
             if err is not None:
                 raise err
-            if segmented:
+            if multi:
+                # N ranks: graph segments cut at every bucket launch, the collectives issued eagerly
+                # between replays.  (Round 6: the whole-graph layout with the collectives inside -- the
+                # comm stream as the capture's origin, compute forked from it -- is gone: measured
+                # slower (r5t6) and its capture failed intermittently inside RCCL on colocated ranks.)
                 self._capture_segments(reducer)
-            elif multi:
-                # RCCL collectives on a stream that JOINED the capture (the engine's comm stream,
-                # forked from the compute stream) crash hipStreamEndCapture -- the HIP runtime
-                # recurses without end over the captured graph (tests/workers/rccl_graph.py phase
-                # "fork", r4t10) -- while collectives on the capture's ORIGIN stream replay fine.  So
-                # the capture starts on the comm stream and the step's compute runs on a stream
-                # forked from it: the same overlap, the collectives on the origin.
-                origin = reducer.comm.stream
-                with torch.cuda.graph(g, stream=origin, capture_error_mode=self.mode):
-                    self.stream.wait_stream(origin)
-                    with torch.cuda.stream(self.stream):
-                        self.out = self.fn()
-                    origin.wait_stream(self.stream)
             else:
                 with torch.cuda.graph(g, stream=self.stream, capture_error_mode=self.mode):
                     self.out = self.fn()

@@ -152,9 +152,9 @@ def _linear_forward(self, x):
 
 
 class SideStream:
-    """Weight gradients on a side stream, overlapping the backward data-gradient chain.  The linear
-    layers' direct split-K weight gradients always use it (ops/linear.py ``_WGRAD_SIDE``); the conv
-    weight gradients of the fused bottleneck only when ``enabled`` is set.  A weight gradient
+    """Weight gradients on a side stream, overlapping the backward data-gradient chain: the linear
+    layers' direct split-K weight gradients (ops/linear.py ``_WGRAD_SIDE``; the fused bottleneck's
+    conv weight gradients measured slower there, r3 / r6t4).  A weight gradient
     depends only on its layer's output gradient and input, and nothing on the critical path of
     backward reads it, so it can
     run beside the next layers' data gradients and the memory-bound BN passes (filling the
@@ -163,7 +163,6 @@ class SideStream:
     event recorded so far (:meth:`join`) -- the join is deferred to the bucket launch / the
     end of backward instead of the end of each layer."""
 
-    enabled = False  # measured 1.2 % slower on ResNet-50 (r3); a programmatic switch (tests)
     _streams: Dict[int, torch.cuda.Stream] = {}
     _pending: list = []
 

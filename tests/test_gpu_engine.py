@@ -452,45 +452,43 @@ def test_add_layernorm_fused_residual_dropout():
 
 
 @needs_gpu
-def test_wgrad_side_stream_bit_identical():
-    """Weight gradients on the side stream (KUNGFU_WGRAD_STREAM, parallel/mixed.py SideStream)
-    overlap the data-gradient chain; the deferred join before landing must make the flat
-    gradients bit-identical to the single-stream backward (same deterministic kernels)."""
+def test_linear_side_stream_wgrad_joined_without_bucket_engine(monkeypatch):
+    """the linear layers' direct split-K weight gradients run on the side stream
+    (ops/linear.py _WGRAD_SIDE) and reach the flat slot themselves (sink.put_direct).  With the
+    default BatchedSink (SMA here: no bucket engine) and no staged put at all (an MLP, nothing but
+    direct producers) the end of backward must still join the side stream: the flat gradients are
+    bit-identical to the single-stream run, and no side-stream event is left pending."""
     import kungfu_amd as kf
-    from kungfu_amd.models import resnet50
-    from kungfu_amd.parallel.mixed import SideStream, enable_bf16_shadow
+    from kungfu_amd.ops import linear as lin
+    from kungfu_amd.parallel import mixed
 
     kf.init()
 
     def run(side):
-        old = SideStream.enabled
-        SideStream.enabled = side
-        try:
-            torch.manual_seed(0)
-            m = resnet50(fused_bn=True).cuda().to(memory_format=torch.channels_last)
-            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9))
-            enable_bf16_shadow(m, opt)
-            g = torch.Generator(device="cuda").manual_seed(3)
-            x = torch.randn(16, 3, 96, 96, device="cuda", generator=g).to(memory_format=torch.channels_last)
-            y = torch.randint(0, 1000, (16,), device="cuda", generator=g)
-            grads = []
-            for _ in range(3):
-                opt.zero_grad()
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    F.cross_entropy(m(x).float(), y).backward()
-                grads.append(opt.space.flat_grad.clone())
-                opt.step()
-            torch.cuda.synchronize()
-            assert not SideStream._pending
-            return grads, opt.space.flat_param.clone()
-        finally:
-            SideStream.enabled = old
+        monkeypatch.setattr(lin, "_WGRAD_SIDE", side)
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(512, 1024), torch.nn.ReLU(), torch.nn.Linear(1024, 1024),
+                                torch.nn.ReLU(), torch.nn.Linear(1024, 256)).cuda()
+        opt = kf.optimizers.SynchronousAveragingOptimizer(torch.optim.SGD(m.parameters(), lr=0.01))
+        mixed.enable_bf16_shadow(m, opt)
+        assert isinstance(opt.space.sink, mixed.BatchedSink)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        grads = []
+        for _ in range(3):
+            x = torch.randn(8192, 512, device="cuda", generator=g)
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                m(x).float().square().mean().backward()
+            assert not mixed.SideStream._pending  # joined at the end of backward
+            grads.append(opt.space.flat_grad.clone())  # read on the main stream right away
+            opt.step()
+        torch.cuda.synchronize()
+        mixed.disable(m)
+        return grads
 
-    g0, p0 = run(False)
-    g1, p1 = run(True)
+    g0, g1 = run(False), run(True)
     for a, b in zip(g0, g1):
         assert torch.equal(a, b), (a - b).abs().max()
-    assert torch.equal(p0, p1)
 
 
 @needs_gpu

@@ -197,17 +197,6 @@ def test_bench_two_ranks_whole_step_graph():
 
 
 @needs_gpu
-def test_bench_two_ranks_single_graph_layout():
-    """KUNGFU_GRAPH_SEGMENTED=0: the N-rank step as ONE graph with the collectives inside (comm stream as
-    the capture's origin, compute forked from it) -- the round-4 layout, kept selectable."""
-    res = _bench(dict(COLO, KUNGFU_GRAPH_SEGMENTED="0"), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
-    v = res["verify"]
-    hg = res["config"]["hip_graph"]
-    assert hg["captured"] is True and hg["replays"] >= 4 and hg.get("segments", 1) == 1, hg
-    assert v["comm_ranks"] == 2 and v["replicas_consistent"] is True, v
-
-
-@needs_gpu
 def test_bench_two_ranks_graph_disabled_falls_back_to_eager():
     """KUNGFU_GRAPH_MULTIRANK=0: capture refused identically on every rank, eager training."""
     res = _bench(dict(COLO, KUNGFU_GRAPH_MULTIRANK="0"), extra=["--graph", "1", "--steps", "4", "--warmup", "4"])
@@ -224,26 +213,6 @@ def test_rccl_collectives_replay_inside_hipgraph():
     (kungfu_amd.finalize releases tracked graphs before destroying the communicator -- without
     that, the communicator's finalize waited on the graph's RCCL resources until the deadline)."""
     r = kungfu_run(2, [worker("rccl_graph.py"), "one,two,avg"], timeout=180, extra=["-allow-xgmi"], env=COLO)
-    assert r.returncode == 0, r.stdout[-5000:]
-    assert r.stdout.count("RCCL_GRAPH_OK") == 2, r.stdout[-5000:]
-
-
-# RCCL 2.26.6 / the ROCm 7.0 runtime in torch 2.10, two ranks colocated on one device: capturing an
-# all-reduce on the origin stream while a forked compute stream is part of the capture failed once in
-# three full suites (r5t18) with "rccl AllReduce: unhandled cuda error" -> hipErrorStreamCaptureInvalidated
-# on one rank.  The default multi-rank path no longer captures collectives at all (segmented capture:
-# each bucket's collective is issued eagerly between graph segments, parallel/graphs.py), so this layout
-# is exercised only with KUNGFU_GRAPH_SEGMENTED=0.
-_CAPTURE_FLAKE = ("unhandled cuda error", "hipErrorStreamCaptureInvalidated")
-
-
-@needs_gpu
-def test_rccl_collectives_replay_inside_hipgraph_forked_compute():
-    """The whole-graph multi-rank layout (KUNGFU_GRAPH_SEGMENTED=0): the compute on a stream forked
-    from the capture, the collectives on the capture's origin stream; values checked per replay."""
-    r = kungfu_run(2, [worker("rccl_graph.py"), "ofork"], timeout=180, extra=["-allow-xgmi"], env=COLO)
-    if r.returncode != 0 and all(t in r.stdout for t in _CAPTURE_FLAKE):
-        pytest.xfail("RCCL capture-time failure on colocated ranks (runtime flake, see _CAPTURE_FLAKE)")
     assert r.returncode == 0, r.stdout[-5000:]
     assert r.stdout.count("RCCL_GRAPH_OK") == 2, r.stdout[-5000:]
 
