@@ -126,27 +126,7 @@ struct AttnArgs {
     uint32_t seed, thresh;
     float inv_keep;
     const uint32_t *seed_base;  // device word mixed into the seed (graph replays advance it), or null
-    float *bsum;  // backward, optional: per-(sequence, wave) column sums of dqkv as stored, [B * NW][3 * H * 64]
 };
-
-// this wave's column sums of one 16 x 64 block product (lane: row lc, columns 16 c + 4 lg .. + 3) as stored in
-// bf16, summed over the 16 rows (xor-shuffles within each 16-lane row group) and accumulated into acc[c][r]
-__device__ __forceinline__ void colsum_rows16(const uint2 (&st)[4], float (&acc)[4][4]) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        float v[4] = {__uint_as_float(st[c].x << 16), __uint_as_float(st[c].x & 0xffff0000u),
-                      __uint_as_float(st[c].y << 16), __uint_as_float(st[c].y & 0xffff0000u)};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            float t = v[r];
-            t += __shfl_xor(t, 1);
-            t += __shfl_xor(t, 2);
-            t += __shfl_xor(t, 4);
-            t += __shfl_xor(t, 8);
-            acc[c][r] += t;
-        }
-    }
-}
 
 // the per-call seed mixed with the device seed base (dropout_seed_base)
 __device__ __forceinline__ uint32_t call_seed(const AttnArgs &a) {
@@ -378,26 +358,15 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
                 for (int i = 0; i < TQ; ++i) o[c][i] = mfma(ka[c], sb[i], o[c][i]);
         }
-        float cq[4][4] = {};
 #pragma unroll
-        for (int i = 0; i < TQ; ++i) {
-            uint2 st[4];
+        for (int i = 0; i < TQ; ++i)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 const int q = q0 + 16 * i + lc;
                 uint16_t *dst = a.dqkv + (static_cast<int64_t>(b) * S + q) * RS + h * DH + 16 * c + 4 * lg;
-                st[c] = make_uint2(pack2(o[c][i][0] * a.scale, o[c][i][1] * a.scale),
-                                   pack2(o[c][i][2] * a.scale, o[c][i][3] * a.scale));
-                *reinterpret_cast<uint2 *>(dst) = st[c];
+                *reinterpret_cast<uint2 *>(dst) = make_uint2(pack2(o[c][i][0] * a.scale, o[c][i][1] * a.scale),
+                                                             pack2(o[c][i][2] * a.scale, o[c][i][3] * a.scale));
             }
-            if (a.bsum) colsum_rows16(st, cq);
-        }
-        if (a.bsum && lc == 0) {
-            float *pr = a.bsum + static_cast<int64_t>(b * NW + wave) * (3 * D) + h * DH + 4 * lg;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                *reinterpret_cast<float4 *>(pr + 16 * c) = make_float4(cq[c][0], cq[c][1], cq[c][2], cq[c][3]);
-        }
     }
     // ---- phase 2: key rows k0 .. k0 + QW - 1
     const int k0 = wave * QW;
@@ -427,33 +396,17 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_kernel(AttnArgs a) {
                 dk[c][j] = mfma(qa[c], sb[j], dk[c][j]);
             }
     }
-    float ck[4][4] = {}, cv[4][4] = {};
 #pragma unroll
-    for (int j = 0; j < TQ; ++j) {
-        uint2 sk[4], sv[4];
+    for (int j = 0; j < TQ; ++j)
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             const int key = k0 + 16 * j + lc;
             uint16_t *row = a.dqkv + (static_cast<int64_t>(b) * S + key) * RS + h * DH + 16 * c + 4 * lg;
-            sk[c] = make_uint2(pack2(dk[c][j][0] * a.scale, dk[c][j][1] * a.scale),
-                               pack2(dk[c][j][2] * a.scale, dk[c][j][3] * a.scale));
-            sv[c] = make_uint2(pack2(dv[c][j][0], dv[c][j][1]), pack2(dv[c][j][2], dv[c][j][3]));
-            *reinterpret_cast<uint2 *>(row + D) = sk[c];
-            *reinterpret_cast<uint2 *>(row + 2 * D) = sv[c];
+            *reinterpret_cast<uint2 *>(row + D) = make_uint2(pack2(dk[c][j][0] * a.scale, dk[c][j][1] * a.scale),
+                                                             pack2(dk[c][j][2] * a.scale, dk[c][j][3] * a.scale));
+            *reinterpret_cast<uint2 *>(row + 2 * D) =
+                make_uint2(pack2(dv[c][j][0], dv[c][j][1]), pack2(dv[c][j][2], dv[c][j][3]));
         }
-        if (a.bsum) {
-            colsum_rows16(sk, ck);
-            colsum_rows16(sv, cv);
-        }
-    }
-    if (a.bsum && lc == 0) {
-        float *pr = a.bsum + static_cast<int64_t>(b * NW + wave) * (3 * D) + h * DH + 4 * lg;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            *reinterpret_cast<float4 *>(pr + D + 16 * c) = make_float4(ck[c][0], ck[c][1], ck[c][2], ck[c][3]);
-            *reinterpret_cast<float4 *>(pr + 2 * D + 16 * c) = make_float4(cv[c][0], cv[c][1], cv[c][2], cv[c][3]);
-        }
-    }
 }
 
 // 8 waves per S = 128 backward workgroup (4: one wave per SIMD, measured slower, r4t15)
@@ -464,7 +417,6 @@ AttnArgs make_args(const uint16_t *qkv, uint16_t *out, float *lse, const uint16_
     AttnArgs a;
     a.qkv = qkv, a.out = out, a.lse = lse, a.dout = dout, a.dqkv = dqkv, a.H = H, a.scale = scale, a.seed = seed;
     a.seed_base = dropout_seed_base();
-    a.bsum = nullptr;
     const double t = static_cast<double>(p_drop) * 4294967296.0;
     a.thresh = p_drop <= 0.f ? 0u : (t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t));
     a.inv_keep = p_drop < 1.f ? 1.f / (1.f - p_drop) : 0.f;
@@ -474,8 +426,6 @@ AttnArgs make_args(const uint16_t *qkv, uint16_t *out, float *lse, const uint16_
 }  // namespace
 
 bool attention_supported(int S, int head_dim) { return head_dim == DH && (S == 64 || S == 128); }
-
-int attention_bwd_partial_rows(int B, int S) { return B * (S == 128 ? attn_bwd_waves() : 4); }
 
 void launch_attention_forward(const uint16_t *qkv, uint16_t *out, float *lse, int B, int S, int H, float scale,
                               uint32_t seed, float p_drop, hipStream_t s) {
@@ -487,11 +437,10 @@ void launch_attention_forward(const uint16_t *qkv, uint16_t *out, float *lse, in
 
 void launch_attention_backward(const uint16_t *qkv, const uint16_t *out, const float *lse, const uint16_t *dout,
                                uint16_t *dqkv, int B, int S, int H, float scale, uint32_t seed, float p_drop,
-                               hipStream_t s, float *bsum) {
+                               hipStream_t s) {
     if (!attention_supported(S, DH)) throw std::invalid_argument("attention: S must be 64 or 128");
     AttnArgs a = make_args(qkv, const_cast<uint16_t *>(out), const_cast<float *>(lse), dout, dqkv, H, scale, seed,
                            p_drop);
-    a.bsum = bsum;
     if (S == 128) {
         if (attn_bwd_waves() == 8) attn_bwd_kernel<128, 8><<<B * H, 512, 0, s>>>(a);
         else attn_bwd_kernel<128, 4><<<B * H, 256, 0, s>>>(a);

@@ -47,7 +47,7 @@ __device__ __forceinline__ uint4 pack8v(const float (&f)[8]) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        w[i] = static_cast<uint32_t>(f32_to_bf16(f[2 * i])) | (static_cast<uint32_t>(f32_to_bf16(f[2 * i + 1])) << 16);
+        w[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 

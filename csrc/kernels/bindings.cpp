@@ -457,12 +457,12 @@ at::Tensor conv(at::Tensor x, at::Tensor w, int64_t stride, c10::optional<at::Te
 }
 
 // Linear layer on the MFMA kernel: y[M, N] = x[M, K] @ w[N, K]^T (both row-major bf16).
-//   bias:            y += bias (bf16 [N]);  gelu (needs bias): returns (gelu(u), u), u = x w^T + b;
+//   bias:            y += bias (bf16 [N]);
 //   out:             y = out += x w^T (accumulate into an existing [M, N] bf16 tensor);
 //   gelu_u + stats:  y = (x w^T) * gelu'(gelu_u), stats[slot][0][n] += sum_m y (a bias gradient;
 //                    stats: zeroed f64 kStatSlots x 2 x N workspace).
-std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, bool gelu,
-                             c10::optional<at::Tensor> out, c10::optional<at::Tensor> gelu_u,
+std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, c10::optional<at::Tensor> out,
+                             c10::optional<at::Tensor> gelu_u,
                              c10::optional<at::Tensor> stats, int64_t variant) {
     TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
                 "gemm: x must be a contiguous 2-D bf16 GPU tensor");
@@ -475,15 +475,15 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
     c10::DeviceGuard gd(x.device());
     kfk::EpiArgs ea;
     int epi = 0;
-    at::Tensor y, u;
+    at::Tensor y;
     auto check_mn = [&](const at::Tensor &t, const char *what) {
         TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.dim() == 2 && t.size(0) == M && t.size(1) == N &&
                         t.is_contiguous() && t.device() == x.device(),
                     "gemm: ", what, " must be a contiguous [M, N] bf16 tensor on x's device");
     };
     if (out && out->defined()) {
-        TORCH_CHECK(!(bias && bias->defined()) && !gelu && !(gelu_u && gelu_u->defined()),
-                    "gemm: out (accumulate) excludes bias / gelu / gelu_u");
+        TORCH_CHECK(!(bias && bias->defined()) && !(gelu_u && gelu_u->defined()),
+                    "gemm: out (accumulate) excludes bias / gelu_u");
         check_mn(*out, "out");
         y = *out;
         epi = kfk::kEpiAccum;
@@ -496,13 +496,6 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
                     "gemm: bias must be a contiguous bf16 [N] tensor on x's device");
         ea.bias = reinterpret_cast<const uint16_t *>(bias->data_ptr());
         epi = kfk::kEpiBias;
-        if (gelu) {
-            u = at::empty({M, N}, x.options());
-            ea.aux = reinterpret_cast<uint16_t *>(u.data_ptr());
-            epi = kfk::kEpiGelu;
-        }
-    } else {
-        TORCH_CHECK(!gelu, "gemm: gelu needs a bias");
     }
     if (gelu_u && gelu_u->defined()) {
         TORCH_CHECK(epi == 0, "gemm: gelu_u excludes bias / out");
@@ -517,7 +510,6 @@ std::vector<at::Tensor> gemm(at::Tensor x, at::Tensor w, c10::optional<at::Tenso
     kfk::launch_gemm(reinterpret_cast<const uint16_t *>(x.data_ptr()), reinterpret_cast<const uint16_t *>(w.data_ptr()),
                      reinterpret_cast<uint16_t *>(y.data_ptr()), static_cast<int>(M), static_cast<int>(K),
                      static_cast<int>(N), ea, epi, stream_of(x, 0), static_cast<int>(variant));
-    if (u.defined()) return {y, u};
     return {y};
 }
 
@@ -717,18 +709,6 @@ at::Tensor xent_backward(at::Tensor x, at::Tensor labels, at::Tensor lse, at::Te
     return ld > 0 && ld != x.size(1) ? dxp.narrow(1, 0, x.size(1)) : dxp;
 }
 
-// erf-GELU forward of a contiguous bf16 tensor (numel % 8 == 0)
-at::Tensor gelu_forward(at::Tensor u) {
-    TORCH_CHECK(u.is_cuda() && u.scalar_type() == at::kBFloat16 && u.is_contiguous() && u.numel() % 8 == 0,
-                "gelu_forward: contiguous bf16, numel % 8");
-    c10::DeviceGuard gd(u.device());
-    auto y = at::empty_like(u);
-    if (u.numel() > 0)
-        kfk::launch_gelu_forward(reinterpret_cast<const uint16_t *>(u.data_ptr()), reinterpret_cast<uint16_t *>(y.data_ptr()),
-                                 u.numel(), stream_of(u, 0));
-    return y;
-}
-
 // GELU backward fused with the bias gradient: (du, colsum(du)) for bf16 dy, u [..., O] (O % 8 == 0).
 std::vector<at::Tensor> gelu_backward_colsum(at::Tensor dy, at::Tensor u, at::ScalarType dtype) {
     TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && u.sizes() == dy.sizes() &&
@@ -784,9 +764,8 @@ std::vector<at::Tensor> attention_forward(at::Tensor qkv, int64_t heads, double 
     return {out, lse};
 }
 
-std::vector<at::Tensor> attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at::Tensor dout,
-                                           int64_t heads, double scale, int64_t seed, double p_drop,
-                                           c10::optional<at::ScalarType> bias_dtype) {
+at::Tensor attention_backward(at::Tensor qkv, at::Tensor out, at::Tensor lse, at::Tensor dout, int64_t heads,
+                              double scale, int64_t seed, double p_drop) {
     TORCH_CHECK(qkv.is_cuda() && qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3 && qkv.is_contiguous() &&
                     qkv.size(2) == 3 * heads * 64 && kfk::attention_supported(qkv.size(1), 64),
                 "attention_backward: qkv must be a contiguous bf16 [B, S, 3*H*64] GPU tensor with S in {64, 128}");
@@ -800,28 +779,12 @@ std::vector<at::Tensor> attention_backward(at::Tensor qkv, at::Tensor out, at::T
                 "attention_backward: lse must be the forward's [B, H, S] f32");
     c10::DeviceGuard gd(qkv.device());
     auto dqkv = at::empty_like(qkv);
-    // bias_dtype: also the column sums of dqkv (the qkv projection's bias gradient): per-(sequence, wave)
-    // partials from the kernel, folded in a fixed order (launch_colsum_fold)
-    at::Tensor part, db;
-    const int O = 3 * H * 64;
-    if (bias_dtype) {
-        TORCH_CHECK(*bias_dtype == at::kFloat || *bias_dtype == at::kBFloat16, "attention_backward: bias dtype");
-        part = at::empty({static_cast<int64_t>(kfk::attention_bwd_partial_rows(B, S)), O},
-                         qkv.options().dtype(at::kFloat));
-        db = at::empty({O}, qkv.options().dtype(*bias_dtype));
-    }
     kfk::launch_attention_backward(reinterpret_cast<const uint16_t *>(qkv.data_ptr()),
                                    reinterpret_cast<const uint16_t *>(out.data_ptr()), lse.data_ptr<float>(),
                                    reinterpret_cast<const uint16_t *>(dout.data_ptr()),
                                    reinterpret_cast<uint16_t *>(dqkv.data_ptr()), B, S, H, static_cast<float>(scale),
-                                   static_cast<uint32_t>(seed), static_cast<float>(p_drop), stream_of(qkv, 0),
-                                   bias_dtype ? part.data_ptr<float>() : nullptr);
-    if (bias_dtype)
-        kfk::launch_colsum_fold(part.data_ptr<float>(), static_cast<int>(part.size(0)), O,
-                                *bias_dtype == at::kFloat ? db.data_ptr<float>() : nullptr,
-                                *bias_dtype == at::kBFloat16 ? reinterpret_cast<uint16_t *>(db.data_ptr()) : nullptr,
-                                stream_of(qkv, 0));
-    return {dqkv, db};
+                                   static_cast<uint32_t>(seed), static_cast<float>(p_drop), stream_of(qkv, 0));
+    return dqkv;
 }
 
 static void check_bias_act(const at::Tensor &y, const char *name) {
@@ -1559,6 +1522,38 @@ at::Tensor stem_forward(at::Tensor x4, at::Tensor wp, c10::optional<at::Tensor> 
 }
 
 // dw [64, 3, 7, 7] channels_last bf16 from dy [N, 64, OH, OW] and x4
+at::Tensor stem_wgrad_bnp(at::Tensor y, at::Tensor x4, at::Tensor dyp, at::Tensor arg, at::Tensor fcoef,
+                          at::Tensor bcoef, int64_t splits) {
+    TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
+                    x4.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem_wgrad_bnp: x4 must be [N, 4, H, W] channels_last bf16");
+    const int N = x4.size(0), H = x4.size(2), W = x4.size(3);
+    const int OH = kfk::stem_out(H), OW = kfk::stem_out(W);
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 && y.size(2) == OH &&
+                    y.size(3) == OW && y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.device() == x4.device(),
+                "stem_wgrad_bnp: y must be the [N, 64, OH, OW] channels_last bf16 conv output");
+    TORCH_CHECK(dyp.scalar_type() == at::kBFloat16 && dyp.dim() == 4 && dyp.size(0) == N && dyp.size(1) == 64 &&
+                    dyp.size(2) == kfk::pool_out(OH) && dyp.size(3) == kfk::pool_out(OW) &&
+                    dyp.is_contiguous(at::MemoryFormat::ChannelsLast) && dyp.device() == x4.device(),
+                "stem_wgrad_bnp: dyp must be the pooled [N, 64, PH, PW] channels_last bf16 gradient");
+    TORCH_CHECK(arg.scalar_type() == at::kByte && arg.numel() == dyp.numel() && arg.device() == x4.device(),
+                "stem_wgrad_bnp: arg must hold the window argmax byte of every pooled element");
+    TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() == 128 && bcoef.scalar_type() == at::kFloat &&
+                    bcoef.numel() == 192 && fcoef.is_contiguous() && bcoef.is_contiguous(),
+                "stem_wgrad_bnp: fcoef [2 x 64] / bcoef [3 x 64] f32");
+    TORCH_CHECK(kfk::stem_wgrad_bnp_supported(N, H, W), "stem_wgrad_bnp: image too wide for the row kernel");
+    c10::DeviceGuard gd(x4.device());
+    const int sp = splits > 0 ? static_cast<int>(splits) : kfk::stem_wgrad_splits(N, H, W);
+    auto part = at::empty({kfk::stem_wgrad_workspace(N, H, W, sp)}, x4.options().dtype(at::kFloat));
+    auto dw = at::empty({64, 3, 7, 7}, x4.options().memory_format(at::MemoryFormat::ChannelsLast));
+    kfk::launch_stem_wgrad_bnp(reinterpret_cast<const uint16_t *>(y.data_ptr()),
+                               reinterpret_cast<const uint16_t *>(x4.data_ptr()),
+                               reinterpret_cast<uint16_t *>(dw.data_ptr()), part.data_ptr<float>(), N, H, W, sp,
+                               reinterpret_cast<const uint16_t *>(dyp.data_ptr()), arg.data_ptr<uint8_t>(),
+                               fcoef.data_ptr<float>(), bcoef.data_ptr<float>(), stream_of(x4, 0));
+    return dw;
+}
+
 at::Tensor stem_wgrad(at::Tensor dy, at::Tensor x4, int64_t splits) {
     TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
                     x4.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1642,7 +1637,7 @@ at::Tensor stem3_wgrad(at::Tensor dy, at::Tensor x, int64_t kh, int64_t kw, int6
 // Returns (dx, dweight, dbias).
 std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Tensor x, at::Tensor mean,
                                          at::Tensor invstd, at::Tensor weight, at::Tensor fcoef, bool training,
-                                         c10::optional<at::Tensor> xarg) {
+                                         c10::optional<at::Tensor> xarg, bool apply) {
     auto sh = bn_shape(x);
     const int C = sh.channels;
     const int H = static_cast<int>(x.size(2)), W = static_cast<int>(x.size(3));
@@ -1655,7 +1650,9 @@ std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Ten
     TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() == 2 * C, "bn_pool_backward: fcoef must be 2C");
     c10::DeviceGuard gd(x.device());
     auto fopt = x.options().dtype(at::kFloat);
-    auto dx = at::empty_like(x, at::MemoryFormat::ChannelsLast);
+    // apply = false: statistics + finalize only -- dx is not formed (an empty tensor), the backward
+    // coefficients [k1; k2; k3] are returned for the caller's own pass (stem_wgrad_bnp)
+    auto dx = apply ? at::empty_like(x, at::MemoryFormat::ChannelsLast) : at::empty({0}, x.options());
     auto dw = at::empty({C}, fopt), db = at::empty({C}, fopt), coef = at::empty({3 * C}, fopt);
     auto partial = at::empty({2 * static_cast<int64_t>(kfk::bn_num_chunks(sh)) * C}, fopt);
     const bool pooled = training && xarg && xarg->defined();
@@ -1670,49 +1667,11 @@ std::vector<at::Tensor> bn_pool_backward(at::Tensor dyp, at::Tensor arg, at::Ten
                                  reinterpret_cast<const uint16_t *>(x.data_ptr()), fcoef.data_ptr<float>(),
                                  mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(), sh, H, W,
                                  training, partial.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
-                                 coef.data_ptr<float>(), reinterpret_cast<uint16_t *>(dx.data_ptr()),
+                                 coef.data_ptr<float>(), apply ? reinterpret_cast<uint16_t *>(dx.data_ptr()) : nullptr,
                                  stream_of(x, 0),
                                  pooled ? reinterpret_cast<const uint16_t *>(xarg->data_ptr()) : nullptr,
-                                 pooled ? sums.data_ptr<double>() : nullptr);
-    return {dx, dw, db};
-}
-
-// Fused stem backward (stem.hip): (dw [64,3,7,7] channels_last bf16, dgamma, dbeta) from the
-// pooled gradient of BN+ReLU+MaxPool over the stem conv output y.
-std::vector<at::Tensor> stem_backward(at::Tensor dyp, at::Tensor arg, at::Tensor y, at::Tensor fcoef, at::Tensor mean,
-                                      at::Tensor invstd, at::Tensor weight, at::Tensor x4, bool training,
-                                      int64_t splits) {
-    TORCH_CHECK(x4.is_cuda() && x4.scalar_type() == at::kBFloat16 && x4.dim() == 4 && x4.size(1) == 4 &&
-                    x4.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "stem_backward: x4 must be [N, 4, H, W] channels_last bf16");
-    const int N = x4.size(0), H = x4.size(2), W = x4.size(3);
-    const int OH = kfk::stem_out(H), OW = kfk::stem_out(W);
-    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.dim() == 4 && y.size(0) == N && y.size(1) == 64 &&
-                    y.size(2) == OH && y.size(3) == OW && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                    y.device() == x4.device(),
-                "stem_backward: y must be the [N, 64, OH, OW] channels_last bf16 conv output");
-    if (!dyp.is_contiguous(at::MemoryFormat::ChannelsLast)) dyp = dyp.contiguous(at::MemoryFormat::ChannelsLast);
-    TORCH_CHECK(dyp.scalar_type() == at::kBFloat16 && dyp.dim() == 4 && dyp.size(0) == N && dyp.size(1) == 64 &&
-                    dyp.size(2) == kfk::pool_out(OH) && dyp.size(3) == kfk::pool_out(OW) && dyp.device() == x4.device(),
-                "stem_backward: dyp must be the pooled [N, 64, PH, PW] gradient");
-    TORCH_CHECK(arg.scalar_type() == at::kByte && arg.numel() == dyp.numel() && arg.is_contiguous(),
-                "stem_backward: bad argmax");
-    TORCH_CHECK(fcoef.scalar_type() == at::kFloat && fcoef.numel() >= 128 && mean.numel() == 64 &&
-                    invstd.numel() == 64 && weight.numel() == 64 && weight.scalar_type() == at::kFloat,
-                "stem_backward: BN tensors must be f32 [64] (fcoef [128])");
-    c10::DeviceGuard gd(x4.device());
-    const int sp = splits > 0 ? static_cast<int>(splits) : 512;
-    auto fopt = x4.options().dtype(at::kFloat);
-    auto ws = at::empty({kfk::stem_bwd_workspace(sp)}, fopt);
-    auto dg = at::empty({64}, fopt), db = at::empty({64}, fopt);
-    auto dw = at::empty({64, 3, 7, 7}, x4.options().memory_format(at::MemoryFormat::ChannelsLast));
-    kfk::launch_stem_backward(reinterpret_cast<const uint16_t *>(dyp.data_ptr()), arg.data_ptr<uint8_t>(),
-                              reinterpret_cast<const uint16_t *>(y.data_ptr()), fcoef.data_ptr<float>(),
-                              mean.data_ptr<float>(), invstd.data_ptr<float>(), weight.data_ptr<float>(),
-                              reinterpret_cast<const uint16_t *>(x4.data_ptr()), N, H, W, training, sp,
-                              ws.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(),
-                              reinterpret_cast<uint16_t *>(dw.data_ptr()), stream_of(x4, 0));
-    return {dw, dg, db};
+                                 pooled ? sums.data_ptr<double>() : nullptr, apply);
+    return {dx, dw, db, coef};
 }
 
 // ---- device model store: HIP IPC export / import ------------------------------------
@@ -1771,28 +1730,6 @@ void embedding_backward(at::Tensor grad, at::Tensor ids, at::Tensor dy, int64_t 
 // gemm.hip: out[M, N] = a[M, K] . b[N, K]^T (+ bias) (+ out when accumulate), bf16.
 // C[M, ldc] (only columns < N written, the chunk holding column N - 1 whole) = a . b^T (+ bias), for a
 // ragged N (BERT's 30,522-entry vocabulary): rows of C padded to ldc (a multiple of 8) stay 16-byte aligned
-// (u, h): u = a . b^T + bias and h = gelu(u) (erf) in one launch (a linear layer feeding a GELU)
-std::vector<at::Tensor> gemm_nt_gelu(at::Tensor a, at::Tensor b, at::Tensor bias, int64_t bn) {
-    TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
-                "gemm_nt_gelu: bf16 GPU tensors");
-    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
-                "gemm_nt_gelu: a [M, K], b [N, K] contiguous");
-    const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-    TORCH_CHECK(kfk::gemm_nt_supported(M, N, K), "gemm_nt_gelu: unsupported shape M=", M, " N=", N, " K=", K);
-    TORCH_CHECK(bias.is_cuda() && bias.scalar_type() == at::kBFloat16 && bias.numel() == N && bias.is_contiguous(),
-                "gemm_nt_gelu: bias bf16 [N]");
-    auto u = at::empty({M, N}, a.options());
-    auto h = at::empty({M, N}, a.options());
-    c10::DeviceGuard gd(a.device());
-    kfk::launch_gemm_nt_gelu(reinterpret_cast<const uint16_t *>(a.data_ptr()),
-                             reinterpret_cast<const uint16_t *>(b.data_ptr()), reinterpret_cast<uint16_t *>(u.data_ptr()),
-                             reinterpret_cast<uint16_t *>(h.data_ptr()),
-                             reinterpret_cast<const uint16_t *>(bias.data_ptr()), static_cast<int>(M),
-                             static_cast<int>(N), static_cast<int>(K), static_cast<int>(bn),
-                             c10::hip::getCurrentHIPStream().stream());
-    return {u, h};
-}
-
 at::Tensor gemm_nt_ld(at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias, int64_t ldc, int64_t bn) {
     TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16,
                 "gemm_nt_ld: bf16 GPU tensors");
@@ -2135,9 +2072,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("stride") = 1, py::arg("ph") = 0, py::arg("pw") = 0, py::arg("stats") = py::none(),
           py::arg("out") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_fcoef") = py::none());
     m.def("conv_rect_supported", &kfk::conv_rect_supported);
-    m.def("gemm", &gemm, "linear layer x @ w^T on the MFMA kernel with bias / GELU / GELU-gradient(+bias-gradient "
+    m.def("gemm", &gemm, "linear layer x @ w^T on the MFMA kernel with bias / GELU-gradient(+bias-gradient "
           "sums) / accumulate epilogues", py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
-          py::arg("gelu") = false, py::arg("out") = py::none(), py::arg("gelu_u") = py::none(),
+          py::arg("out") = py::none(), py::arg("gelu_u") = py::none(),
           py::arg("stats") = py::none(), py::arg("variant") = -1);
     m.def("gemm_supported", &kfk::gemm_supported);
     m.def("conv_dgrad_s2", &conv_dgrad_s2, "data gradient of a stride-2 1x1/3x3 NHWC bf16 convolution (parity-phase "
@@ -2147,7 +2084,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("fin") = py::none());
     m.def("xent_forward", &xent_forward, "fused softmax cross-entropy over bf16 logits: (lse, per-row loss)");
     m.def("xent_backward", &xent_backward, "its bf16 logit gradient, scaled by scale[0]");
-    m.def("gelu_forward", &gelu_forward, "erf-GELU forward (bf16, one-exponential erf)");
     m.def("gelu_backward_colsum", &gelu_backward_colsum, "erf-GELU backward du and the column sums of du",
           py::arg("dy"), py::arg("u"), py::arg("dtype"));
     m.def("colsum", &colsum, "column sums of a bf16 [T, O] matrix (bias gradient), deterministic", py::arg("x"),
@@ -2194,7 +2130,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
           py::arg("qkv"), py::arg("heads"), py::arg("scale"), py::arg("seed"), py::arg("p_drop"));
     m.def("attention_backward", &attention_backward, "fused self-attention backward -> dqkv", py::arg("qkv"),
           py::arg("out"), py::arg("lse"), py::arg("dout"), py::arg("heads"), py::arg("scale"), py::arg("seed"),
-          py::arg("p_drop"), py::arg("bias_dtype") = py::none());
+          py::arg("p_drop"));
     m.def("conv_wgrad_max_pixels", &kfk::conv_wgrad_max_pixels, py::arg("N"), py::arg("H"), py::arg("W"),
           py::arg("Cin"), py::arg("Cout"), py::arg("ks"), py::arg("stride"));
     m.def("conv_wgrad_plan", [](int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
@@ -2235,15 +2171,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("stem_pack_weight", &stem_pack_weight, "[64,3,7,7] stem weights -> packed [64,224] for stem_forward");
     m.def("stem_forward", &stem_forward, "7x7/2 pad-3 stem conv on MFMA with fused BN statistics",
           py::arg("x4"), py::arg("wp"), py::arg("stats") = py::none());
-    m.def("stem_backward", &stem_backward,
-          "fused stem backward: pool-gradient gather + BN backward + conv weight gradient -> (dw, dgamma, dbeta)",
-          py::arg("dyp"), py::arg("arg"), py::arg("y"), py::arg("fcoef"), py::arg("mean"), py::arg("invstd"),
-          py::arg("weight"), py::arg("x4"), py::arg("training") = true, py::arg("splits") = -1);
     m.def("stem_wgrad", &stem_wgrad, "stem conv weight gradient (split-K MFMA)", py::arg("dy"), py::arg("x4"),
           py::arg("splits") = -1);
-    m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias)",
+    m.def("bn_pool_backward", &bn_pool_backward, "stem BN+ReLU+MaxPool backward -> (dx, dweight, dbias, coef)",
           py::arg("dy"), py::arg("arg"), py::arg("x"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
-          py::arg("fcoef"), py::arg("training"), py::arg("xarg") = py::none());
+          py::arg("fcoef"), py::arg("training"), py::arg("xarg") = py::none(), py::arg("apply") = true);
+    m.def("stem_wgrad_bnp", &stem_wgrad_bnp, "stem conv weight gradient with dy formed from the BN+ReLU+MaxPool "
+          "backward while staging (the BN input gradient is never materialised)", py::arg("y"), py::arg("x4"),
+          py::arg("dyp"), py::arg("arg"), py::arg("fcoef"), py::arg("bcoef"), py::arg("splits") = -1);
+    m.def("stem_wgrad_bnp_supported", &kfk::stem_wgrad_bnp_supported);
     m.def("ipc_alloc", &ipc_alloc, "dedicated f32 device buffer exportable over HIP IPC");
     m.def("ipc_handle", &ipc_handle, "HIP IPC handle (64 bytes) of an ipc_alloc buffer");
     m.def("ipc_open", &ipc_open, "map a peer's exported buffer as an f32 tensor");
@@ -2254,10 +2190,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("gemm_nt_ld", &gemm_nt_ld, py::arg("a"), py::arg("b"), py::arg("bias") = py::none(), py::arg("ldc") = 0,
           py::arg("bn") = 256, "C [M, ldc] = a . b^T (+ bias) for any N (columns >= N of C unspecified)");
     m.def("gemm_nt_ld_supported", &kfk::gemm_nt_ld_supported);
-    m.def("set_layernorm_bwd_rows_per_wave", &kfk::set_layernorm_bwd_rows_per_wave,
-          "rows per wave of the LayerNorm backward (grid sizing; A/B)");
-    m.def("gemm_nt_gelu", &gemm_nt_gelu, py::arg("a"), py::arg("b"), py::arg("bias"), py::arg("bn") = 0,
-          "(u, h): u = a . b^T + bias, h = gelu(u), one launch");
     m.def("gemm_nt_gelu_grad", &gemm_nt_gelu_grad, "(du, db): the GELU backward fused into the data-gradient NT GEMM "
           "(du = bf16(bf16(a . b^T) * gelu'(u)), db = column sums of du)", py::arg("a"), py::arg("b"), py::arg("u"),
           py::arg("bias_dtype") = py::none());

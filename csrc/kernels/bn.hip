@@ -52,7 +52,7 @@ __device__ __forceinline__ uint4 pack8(const float (&f)[8]) {
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        w[i] = static_cast<uint32_t>(f32_to_bf16(f[2 * i])) | (static_cast<uint32_t>(f32_to_bf16(f[2 * i + 1])) << 16);
+        w[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -944,7 +944,8 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
                           double *sums = nullptr, const uint16_t *dres_x = nullptr, double *dres_sums = nullptr,
                           bool prefinalized = false, int phase = 0) {
     // phase 0: everything; 1: the reduce pass only (statistics path, no sums); 2: the apply pass only
-    // (coef already finalized -- bn_bwd_finalize_multi)
+    // (coef already finalized -- bn_bwd_finalize_multi); 3: statistics + finalize, no apply (the
+    // caller consumes coef itself: the stem's fused weight gradient)
     const int C = sh.channels, cvec = C / 8;
     const int64_t nvec = sh.rows * cvec;
     Chunking ch = chunking(sh);
@@ -971,6 +972,7 @@ void launch_backward_impl(G grad, const uint16_t *x, const float *fcoef, const u
     bn_bwd_finalize<<<(C + kFoldCh - 1) / kFoldCh, kBlock, 0, s>>>(partial, ch.nchunks, C, sh.rows, gamma, mean,
                                                                    invstd, dgamma, dbeta, coef, training);
     }
+    if (phase == 3) return;
     const int g = apply_grid(nvec, cvec);
     uint4 *o = reinterpret_cast<uint4 *>(dx), *r = reinterpret_cast<uint4 *>(dres);
     dispatch_cvec(cvec, [&](auto cvc) {
@@ -1125,7 +1127,7 @@ void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *
 void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                             hipStream_t s, const uint16_t *xarg, double *sums) {
+                             hipStream_t s, const uint16_t *xarg, double *sums, bool apply) {
     if (xarg && sums && training) {
         const int C = sh.channels, cvec = C / 8;
         const int64_t nvec = sh.rows / (static_cast<int64_t>(H) * W) * pool_out(H) * pool_out(W) * cvec;
@@ -1145,7 +1147,7 @@ void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint
     PoolGrad pg{reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint2 *>(arg), H, W, pool_out(H),
                 pool_out(W), m_hw, m_w};
     launch_backward_impl(pg, x, fcoef, nullptr, mean, invstd, gamma, sh, RM_COEF, training, partial, dgamma, dbeta,
-                         coef, dx, nullptr, s, sums);
+                         coef, dx, nullptr, s, sums, nullptr, nullptr, false, apply ? 0 : 3);
 }
 
 }  // namespace kfk

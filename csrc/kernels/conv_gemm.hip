@@ -21,7 +21,6 @@ void launch_gemm_t(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, con
     switch (epi) {
     case 0: conv_kernel<1, WM, WN, ST, 0, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
     case kEpiBias: conv_kernel<1, WM, WN, ST, kEpiBias, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
-    case kEpiGelu: conv_kernel<1, WM, WN, ST, kEpiGelu, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea); break;
     case kEpiGeluGrad:
         conv_kernel<1, WM, WN, ST, kEpiGeluGrad, TM, TN><<<grid, block, 0, s>>>(x, w, y, z, g, ea);
         break;

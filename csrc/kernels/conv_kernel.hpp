@@ -237,8 +237,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
     constexpr bool GATE = (EPI & kEpiGate) != 0;
-    constexpr bool GELU = (EPI & kEpiGelu) != 0, GELUG = (EPI & kEpiGeluGrad) != 0;
-    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias | kEpiGelu)) != 0;
+    constexpr bool GELUG = (EPI & kEpiGeluGrad) != 0;
+    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias)) != 0;
     constexpr int NSUM = (GATE || GELUG) ? 1 : 2;  // the gates need sum(y) only (a bias gradient)
     constexpr int VPR = BN / 8;  // 16-byte vectors per C row
     constexpr int GROUPS = NT / VPR;
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                                      bf16_to_f32(static_cast<uint16_t>(b[k] & 0xffffu));
                     const float hi = bf16_to_f32(static_cast<uint16_t>(a[k] >> 16)) +
                                      bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
-                    o[k] = static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
+                    o[k] = pack_bf16x2(lo, hi);
                 }
                 v = make_uint4(o[0], o[1], o[2], o[3]);
             }
@@ -569,20 +569,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                     const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
                                           (!(__uint_as_float(bw[k] & 0xffff0000u) <= 0.f) ? 0xffff0000u : 0u);
                     vw[k] &= keep;
-                }
-            }
-            if constexpr (GELU) {
-                // v = u (bias added): saved for the backward, then y = gelu(u) in f32, one rounding
-                *reinterpret_cast<uint4 *>(ea.aux + ee[u]) = v;
-                float f[8];
-                unpack_bf16x8(v, f);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float a = f[2 * k], b = f[2 * k + 1];
-                    const float ga = 0.5f * a * (1.f + erff(a * 0.70710678118654752f));
-                    const float gb = 0.5f * b * (1.f + erff(b * 0.70710678118654752f));
-                    vw[k] = static_cast<uint32_t>(f32_to_bf16(ga)) | (static_cast<uint32_t>(f32_to_bf16(gb)) << 16);
                 }
             }
             if constexpr (GELUG) {
@@ -601,7 +587,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
                         const float pdf = __expf(-0.5f * t * t) * 0.39894228040143268f;
                         d[h] = f[2 * k + h] * (cdf + t * pdf);
                     }
-                    vw[k] = static_cast<uint32_t>(f32_to_bf16(d[0])) | (static_cast<uint32_t>(f32_to_bf16(d[1])) << 16);
+                    vw[k] = pack_bf16x2(d[0], d[1]);
                 }
             }
             *reinterpret_cast<uint4 *>(y + ee[u]) = v;

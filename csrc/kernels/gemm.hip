@@ -202,8 +202,7 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
                                                       uint16_t *__restrict__ C, const uint16_t *__restrict__ bias,
                                                       int M, int N, int K, int mtiles, int ntiles,
                                                       const uint16_t *__restrict__ aux = nullptr,
-                                                      float *__restrict__ part = nullptr, int ldc = 0,
-                                                      uint16_t *__restrict__ hout = nullptr) {
+                                                      float *__restrict__ part = nullptr, int ldc = 0) {
     constexpr int TN = BN / 64;           // 16-column blocks per wave (4 waves along N)
     constexpr int TM = 8;                 // 16-row blocks per wave (2 waves along M)
     constexpr int BBYTES = BN * kRowB;
@@ -360,10 +359,8 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
         for (int j = 0; j < TN; ++j) {
             const int row = i * 16 + em;
             const int col = j * 16 + en;  // 4 columns col..col+3, inside 16-byte chunk col / 8
-            uint32_t lo = static_cast<uint32_t>(f32_to_bf16(acc[i][j][0])) |
-                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][1])) << 16);
-            uint32_t hi = static_cast<uint32_t>(f32_to_bf16(acc[i][j][2])) |
-                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][3])) << 16);
+            uint32_t lo = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+            uint32_t hi = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
             const int chunk = (col >> 3) ^ (row & 7);
             *reinterpret_cast<uint2 *>(ew + row * EROW + chunk * 16 + (col & 7) * 2) = make_uint2(lo, hi);
         }
@@ -423,7 +420,6 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
             v = make_uint4(w[0], w[1], w[2], w[3]);
         } else if constexpr (EPI != 0) {
             uint32_t w[4] = {v.x, v.y, v.z, v.w};
-            uint32_t hw[4] = {0u, 0u, 0u, 0u};
             uint32_t o[4] = {0u, 0u, 0u, 0u};
             if constexpr ((EPI & kGemmAccum) != 0) {
                 const uint4 ov = *reinterpret_cast<const uint4 *>(dst);
@@ -437,17 +433,9 @@ __global__ __launch_bounds__(512) void gemm_nt_kernel(const uint16_t *__restrict
                     x0 += bf16_to_f32(static_cast<uint16_t>(o[k] & 0xffff));
                     x1 += bf16_to_f32(static_cast<uint16_t>(o[k] >> 16));
                 }
-                w[k] = static_cast<uint32_t>(f32_to_bf16(x0)) | (static_cast<uint32_t>(f32_to_bf16(x1)) << 16);
-                if constexpr ((EPI & kGemmGelu) != 0) {
-                    // h = gelu(u) of the bf16 u (torch's bf16 F.gelu: f32 math on the stored input)
-                    const float u0 = __uint_as_float(w[k] << 16), u1 = __uint_as_float(w[k] & 0xffff0000u);
-                    hw[k] = static_cast<uint32_t>(f32_to_bf16(u0 * gelu_cdf_fast(u0))) |
-                            (static_cast<uint32_t>(f32_to_bf16(u1 * gelu_cdf_fast(u1))) << 16);
-                }
+                w[k] = pack_bf16x2(x0, x1);
             }
             v = make_uint4(w[0], w[1], w[2], w[3]);
-            if constexpr ((EPI & kGemmGelu) != 0)
-                *reinterpret_cast<uint4 *>(hout + grow * ldo + gcol) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
         }
         *reinterpret_cast<uint4 *>(dst) = v;
     }
@@ -581,10 +569,8 @@ __global__ __launch_bounds__(256) void gemm_nt4_kernel(const uint16_t *__restric
         for (int j = 0; j < TN; ++j) {
             const int row = i * 16 + em;
             const int col = j * 16 + en;
-            uint32_t lo = static_cast<uint32_t>(f32_to_bf16(acc[i][j][0])) |
-                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][1])) << 16);
-            uint32_t hi = static_cast<uint32_t>(f32_to_bf16(acc[i][j][2])) |
-                          (static_cast<uint32_t>(f32_to_bf16(acc[i][j][3])) << 16);
+            uint32_t lo = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+            uint32_t hi = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
             const int chunk = ((col >> 3) ^ (row & 7)) & (CH - 1);
             *reinterpret_cast<uint2 *>(ew + row * EROW + chunk * 16 + (col & 7) * 2) = make_uint2(lo, hi);
         }
@@ -627,7 +613,7 @@ __global__ __launch_bounds__(256) void gemm_nt4_kernel(const uint16_t *__restric
                     x0 += bf16_to_f32(static_cast<uint16_t>(o[k] & 0xffff));
                     x1 += bf16_to_f32(static_cast<uint16_t>(o[k] >> 16));
                 }
-                w[k] = static_cast<uint32_t>(f32_to_bf16(x0)) | (static_cast<uint32_t>(f32_to_bf16(x1)) << 16);
+                w[k] = pack_bf16x2(x0, x1);
             }
             v = make_uint4(w[0], w[1], w[2], w[3]);
         }
@@ -681,31 +667,6 @@ void launch_bn(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t
 }  // namespace
 
 int gemm_nt_gelu_grad_rows(int M) { return 2 * ((M + kGM - 1) / kGM); }
-
-void launch_gemm_nt_gelu(const uint16_t *a, const uint16_t *b, uint16_t *c, uint16_t *h, const uint16_t *bias, int M,
-                         int N, int K, int bn, hipStream_t s) {
-    if (!gemm_nt_supported(M, N, K)) throw std::invalid_argument("gemm_nt_gelu: unsupported shape");
-    if (!bias || !h) throw std::invalid_argument("gemm_nt_gelu: needs the bias and the GELU output");
-    if (bn <= 0) bn = gemm_nt_pick_bn(M, N);
-    if (N % bn) throw std::invalid_argument("gemm_nt_gelu: N not a multiple of the tile width");
-    constexpr int E = kGemmBias | kGemmGelu;
-    const int mtiles = (M + kGM - 1) / kGM, ntiles = N / bn;
-    switch (bn) {
-    case 256:
-        gemm_nt_kernel<256, E><<<mtiles * ntiles, 512, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr,
-                                                               0, h);
-        break;
-    case 192:
-        gemm_nt_kernel<192, E><<<mtiles * ntiles, 512, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr,
-                                                               0, h);
-        break;
-    case 128:
-        gemm_nt_kernel<128, E><<<mtiles * ntiles, 512, 0, s>>>(a, b, c, bias, M, N, K, mtiles, ntiles, nullptr, nullptr,
-                                                               0, h);
-        break;
-    default: throw std::invalid_argument("gemm_nt_gelu: tile width must be 128, 192 or 256");
-    }
-}
 
 void launch_gemm_nt_gelu_grad(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *u, float *part, int M,
                               int N, int K, hipStream_t s) {

@@ -30,7 +30,7 @@ const uint32_t *dropout_seed_base();
 
 // gemm.hip: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (+ C) in bf16, f32 accumulation, on a
 // 256 x bn tile (bn 128 | 192 | 256, <= 0: by shape) with a 3-slab-deep LDS-DMA pipeline.
-constexpr int kGemmBias = 1, kGemmAccum = 2, kGemmGeluGrad = 4, kGemmGelu = 8;
+constexpr int kGemmBias = 1, kGemmAccum = 2, kGemmGeluGrad = 4;
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 int gemm_nt_pick_bn(int64_t M, int64_t N);
 void launch_gemm_nt(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *bias, int M, int N, int K,
@@ -48,10 +48,6 @@ int gemm_nt_gelu_grad_rows(int M);
 void launch_gemm_nt_gelu_grad(const uint16_t *a, const uint16_t *b, uint16_t *c, const uint16_t *u, float *part, int M,
                               int N, int K, hipStream_t s);
 void launch_colsum_fold(const float *part, int rows, int O, float *out_f32, uint16_t *out_bf16, hipStream_t s);
-// u = a . b^T + bias (bf16, into c) and h = gelu(u) (erf GELU of the bf16 u, into h) in one launch: a linear
-// layer whose only consumer is a GELU (BERT's FC1)
-void launch_gemm_nt_gelu(const uint16_t *a, const uint16_t *b, uint16_t *c, uint16_t *h, const uint16_t *bias, int M,
-                         int N, int K, int bn, hipStream_t s);
 
 // comm_emu.hip: the local footprint of one all-reduce of `bytes` (bench.py --emulate-comm):
 // `ctas` workgroups copying `traffic_bytes` of the bucket into `scratch` (>= bytes), paced over
@@ -136,7 +132,6 @@ void launch_xent_backward(const uint16_t *x, const int64_t *labels, const float 
                           int V, uint16_t *dx, hipStream_t s, int64_t ld = 0);
 
 // y = gelu(u) (erf form, bf16, n % 8 == 0; norms.hip)
-void launch_gelu_forward(const uint16_t *u, uint16_t *y, int64_t n, hipStream_t s);
 void launch_gelu_bwd_colsum(const uint16_t *dy, const uint16_t *u, uint16_t *du, int64_t T, int O, float *part,
                             float *out_f32, uint16_t *out_bf16, hipStream_t s);
 void launch_sumsq2(const void *a, const void *b, size_t n, int dtype, float *partials, float *out, hipStream_t s);
@@ -205,16 +200,15 @@ bool conv_supported(int Cin, int Cout, int ks, int stride);
 // backward need not write dz (ResNet identity blocks).
 // Linear-layer (GEMM) epilogues, launch_gemm only:
 //   kEpiBias      y = conv + bias (bf16 bias, added in f32 before the one rounding);
-//   kEpiGelu      u = bf16(conv + bias) is written to ea.aux (the GELU's saved input) and
-//                 y = gelu(u) (erf form, torch's F.gelu default);
 //   kEpiGeluGrad  the output is the gradient of a GELU output whose input is ea.bx (= u):
 //                 y = bf16(conv) * gelu'(u) and stats[slot][0][c] += sum(y) (the bias gradient
 //                 of the layer that produced u).
 enum ConvEpi : int {
     kEpiFwdStats = 1, kEpiAccum = 2, kEpiBwdCoef = 4, kEpiBwdBits = 8, kEpiBiasRelu = 16, kEpiGate = 32,
-    kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGelu = 512, kEpiGeluGrad = 1024
+    kEpiAccMask = 64, kEpiAccEven = 128, kEpiBias = 256, kEpiGeluGrad = 1024
     // (round 6: the BN normalise-on-load A operand, 2048, is gone -- +2.56 ms/step on ResNet-50,
-    // profiles/r5_prebn.md)
+    // profiles/r5_prebn.md; the FC1 bias + GELU forward epilogue, 512, too -- slower end to end than
+    // hipBLASLt + the GELU pass, profiles/r5t34_bert_g*.log)
 };
 // In-launch BN finalize of a statistics epilogue (kEpiFwdStats / kEpiBwdCoef / kEpiBwdBits): every
 // workgroup waits for its slot atomics, arrives on a two-level counter (per blockIdx % 8 shard,
@@ -241,8 +235,7 @@ struct EpiArgs {
     // ~25 spilled SGPRs: the compiler loads all kernel arguments up front)
     const BNFin *fin = nullptr;
     const uint8_t *amask = nullptr;  // kEpiAccMask: ReLU mask of `old`, one byte per 8 channels
-    uint16_t *aux = nullptr;         // kEpiGelu: the pre-activation output [M, K] bf16
-    const uint16_t *bias = nullptr;  // kEpiBiasRelu / kEpiBias / kEpiGelu: bf16 [K]
+    const uint16_t *bias = nullptr;  // kEpiBiasRelu / kEpiBias: bf16 [K]
     double *stats = nullptr;         // kStatSlots x [2][K] f64 (zeroed; consumed + re-zeroed by the BN)
     const uint16_t *bx = nullptr;    // bwd: the BN's input x, same [M, K] layout as the output
     const float *fcoef = nullptr;    // bwd coef: forward [scale(K); shift(K)]
@@ -267,7 +260,7 @@ void launch_conv_dgrad_s2(const uint16_t *dy, const uint16_t *wt, uint16_t *dx, 
 // 7x1, 1x3, 3x1, 5x5): the same implicit GEMM, K = KH*KW*Cin tap-major; epilogue none or
 // kEpiFwdStats.  Cin, Cout multiples of 64.
 // Linear layer y[M, N] = x[M, K] w[N, K]^T (+ epilogue) on the same MFMA kernel (a 1x1 conv over
-// M "pixels"): epi 0, kEpiBias, kEpiGelu, kEpiGeluGrad, kEpiAccum (y += product).  K, N % 64.
+// M "pixels"): epi 0, kEpiBias, kEpiGeluGrad, kEpiAccum (y += product).  K, N % 64.
 bool gemm_supported(int M, int K, int N);
 void launch_gemm(const uint16_t *x, const uint16_t *w, uint16_t *y, int M, int K, int N, const EpiArgs &ea, int epi,
                  hipStream_t s, int variant = -1);
@@ -351,17 +344,16 @@ void launch_stem_forward(const uint16_t *x4, const uint16_t *wp, uint16_t *y, do
 // dw [64][7][7][3] bf16; part: stem_wgrad_workspace(...) floats.
 int stem_wgrad_splits(int N, int H, int W);
 int64_t stem_wgrad_workspace(int N, int H, int W, int splits);
+// The stem weight gradient with the dy operand formed while staging from the stem's BN + ReLU +
+// MaxPool backward (stem.hip BNP): y = the conv output (BN input), dyp / arg = the pooled gradient and
+// window argmax, fcoef = forward [scale; shift], bcoef = bn_bwd_finalize's [k1; k2; k3] -- the BN input
+// gradient is never materialised.  Row-kernel shapes only (stem_wgrad_bnp_supported).
+bool stem_wgrad_bnp_supported(int N, int H, int W);
+void launch_stem_wgrad_bnp(const uint16_t *y, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
+                           int splits, const uint16_t *dyp, const uint8_t *arg, const float *fcoef,
+                           const float *bcoef, hipStream_t s);
 void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
                        int splits, hipStream_t s);
-// Fused stem backward: given the pooled gradient dyp + argmax of BN+ReLU+MaxPool over the conv
-// output y (fcoef = forward [scale; shift]), write dgamma, dbeta of the BN and the conv weight
-// gradient dw [64][7][7][3] bf16 -- the BN input gradient is never materialised.
-// ws: stem_bwd_workspace(splits) floats.
-int64_t stem_bwd_workspace(int splits);
-void launch_stem_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *y, const float *fcoef,
-                          const float *mean, const float *invstd, const float *gamma, const uint16_t *x4, int N, int H,
-                          int W, bool training, int splits, float *ws, float *dgamma, float *dbeta, uint16_t *dw,
-                          hipStream_t s);
 
 // Fused NHWC batch-norm(+residual)(+ReLU), bf16 activations, f32 statistics
 // (see bn.hip).  x/y/res/dy/dx/dres are [rows, C] bf16 with C contiguous.
@@ -443,7 +435,7 @@ void launch_bn_pool_forward(const uint16_t *x, const float *gamma, const float *
 void launch_bn_pool_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *x, const float *fcoef,
                              const float *mean, const float *invstd, const float *gamma, BNShape sh, int H, int W,
                              bool training, float *partial, float *dgamma, float *dbeta, float *coef, uint16_t *dx,
-                             hipStream_t s, const uint16_t *xarg = nullptr, double *sums = nullptr);
+                             hipStream_t s, const uint16_t *xarg = nullptr, double *sums = nullptr, bool apply = true);
 
 // Conv bias (+ ReLU) on NHWC bf16 [rows, C] (bias_act.hip): forward in place; backward
 // dz = dy * (y > 0) (relu) and dbias[c] = sum over rows (f32, deterministic: per-block partials
@@ -477,7 +469,6 @@ void launch_global_avgpool_backward(const uint16_t *dy, uint16_t *dx, int64_t N,
 // dgamma/dbeta (f32) through [blocks][2][D] f32 partials.
 bool layernorm_supported(int D);
 int layernorm_bwd_blocks(int64_t rows);
-void set_layernorm_bwd_rows_per_wave(int r);
 void launch_layernorm_forward(const uint16_t *x, const uint16_t *r, const float *gamma, const float *beta, uint16_t *y,
                               uint16_t *s, float *mean, float *rstd, int64_t rows, int D, float eps, hipStream_t st,
                               float p = 0.f, uint32_t seed = 0);
@@ -500,9 +491,6 @@ void launch_attention_forward(const uint16_t *qkv, uint16_t *out, float *lse, in
 // dqkv [B, S, 3, H, 64] (every element written)
 void launch_attention_backward(const uint16_t *qkv, const uint16_t *out, const float *lse, const uint16_t *dout,
                                uint16_t *dqkv, int B, int S, int H, float scale, uint32_t seed, float p_drop,
-                               hipStream_t s, float *bsum = nullptr);
-// rows of the backward's optional column-sum partials (bsum: [rows][3 * H * 64] f32, every entry written):
-// the column sums of dqkv as stored -- the bias gradient of the projection that produced qkv
-int attention_bwd_partial_rows(int B, int S);
+                               hipStream_t s);
 
 }  // namespace kfk

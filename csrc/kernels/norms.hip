@@ -336,8 +336,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint4 *__restrict__
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float x0 = __uint_as_float(a[k] << 16), x1 = __uint_as_float(a[k] & 0xffff0000u);
-                o[k] = static_cast<uint32_t>(f32_to_bf16(x0 * gelu_cdf_fast(x0))) |
-                       (static_cast<uint32_t>(f32_to_bf16(x1 * gelu_cdf_fast(x1))) << 16);
+                o[k] = pack_bf16x2(x0 * gelu_cdf_fast(x0), x1 * gelu_cdf_fast(x1));
             }
             y[i0 + h * stride] = make_uint4(o[0], o[1], o[2], o[3]);
         }

@@ -182,8 +182,7 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_fwd_kernel(const uint4 *__r
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            o[k] = static_cast<uint32_t>(f32_to_bf16(best[2 * k])) |
-                   (static_cast<uint32_t>(f32_to_bf16(best[2 * k + 1])) << 16);
+            o[k] = pack_bf16x2(best[2 * k], best[2 * k + 1]);
         y[i] = make_uint4(o[0], o[1], o[2], o[3]);
         arg[i] = make_uint2(a[0] | (a[1] << 8) | (a[2] << 16) | (a[3] << 24),
                             a[4] | (a[5] << 8) | (a[6] << 16) | (a[7] << 24));
@@ -229,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void maxpool3s2_bwd_kernel(const uint4 *__r
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k])) | (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1])) << 16);
+            o[k] = pack_bf16x2(acc[2 * k], acc[2 * k + 1]);
         dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -266,8 +265,7 @@ __global__ __launch_bounds__(kBlock) void avgpool3s1_kernel(const uint4 *__restr
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k] * inv9)) |
-                   (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1] * inv9)) << 16);
+            o[k] = pack_bf16x2(acc[2 * k] * inv9, acc[2 * k + 1] * inv9);
         y[i] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }
@@ -303,8 +301,7 @@ __global__ __launch_bounds__(kBlock) void gap_fwd_kernel(const uint4 *__restrict
         uint32_t o[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            o[k] = static_cast<uint32_t>(f32_to_bf16(acc[2 * k] * inv)) |
-                   (static_cast<uint32_t>(f32_to_bf16(acc[2 * k + 1] * inv)) << 16);
+            o[k] = pack_bf16x2(acc[2 * k] * inv, acc[2 * k + 1] * inv);
         y[i] = make_uint4(o[0], o[1], o[2], o[3]);
     }
 }

@@ -55,6 +55,8 @@ __device__ __forceinline__ int fdiv(int p, uint64_t m) {
 
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
 // two f32 -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32 on gfx950
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
@@ -647,12 +649,107 @@ __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float *__r
 // pixel 2 (ow0 + q) + kw0 + p: 4 channels = 8 bytes) -- no im2col image at all.
 constexpr int kDyRow = 128 * kARow;  // dy row image: 128 ow x 128 B
 
+// BNP (round 6): the dy operand is not read but FORMED while staging -- the gradient of the stem's
+// conv output through BN(batch stats) + ReLU + MaxPool(3, 2, 1):
+//     g  = sum of dyp over the (<= 2x2) pooled windows whose argmax is this element  (the pool gather)
+//     dz = g if y * fscale + fshift > 0 else 0                                         (the ReLU gate)
+//     dx = k1 * dz + k2 * y + k3                      (BN backward, k = bn_bwd_finalize's coefficients)
+// with y the conv output (read where the plain kernel reads dy: same layout, same bytes).  The
+// same f32 expressions as bn.hip's bn_bwd_apply_kernel<PoolGrad>, so dx rounds to the same bf16 and
+// the weight gradient equals the layered path's; but the 411 MB BN input gradient of a 256-image
+// batch is never written nor read back (the layered pass was 256 us + a 167 us weight gradient).
+// The pooled gradient and argmax rows are staged through a 2-slot LDS ring (pooled row p in slot
+// p & 1; conv row h needs rows h >> 1 and (h + 1) >> 1) and gathered from there: each pooled byte
+// is read from HBM once.  (Gathering the <= 4 candidates per pixel from global memory instead --
+// 8 dependent loads per 16-byte chunk at one workgroup per CU -- ran the kernel at 418 us.)
+struct StemBnp {
+    const uint4 *dyp;    // pooled gradient [N, PH, PW, 64]
+    const uint2 *arg;    // window argmax bytes [N, PH, PW, 64]
+    const float *fcoef;  // forward BN [scale(64); shift(64)]
+    const float *bcoef;  // backward BN [k1(64); k2(64); k3(64)]
+    int PH, PW;
+};
+constexpr int kPoolD = 64 * 128;               // slot: dyp row [PW <= 64][64] bf16 ...
+constexpr int kPoolSlot = kPoolD + 64 * 64;    // ... + argmax row [PW][64] bytes
+
+__device__ __forceinline__ void unpack8f(const uint4 &v, float (&f)[8]) {
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = __uint_as_float(u[i] << 16);
+        f[2 * i + 1] = __uint_as_float(u[i] & 0xffff0000u);
+    }
+}
+
+// g = the pooled gradient gathered back to conv-output pixel (h, w), 8 channels cv * 8.., from the LDS
+// ring: the windows (oh, ow) with oh in {h >> 1, (h + 1) >> 1} and ow in {w >> 1, (w + 1) >> 1}, in
+// bn.hip PoolGrad's order, each adding its dyp where its argmax byte names (h, w).  PoolGrad adds a 0
+// for a window that cannot cover (h, w); here such windows are skipped -- at compile time for the
+// column (ODDW: w is odd, so two columns) and by the wave-uniform row parity (HODD) -- which gives the
+// same sum (adding +0 to a sum that starts at +0 changes nothing): 2.25 windows per pixel, not 4.
+template <bool ODDW>
+__device__ __forceinline__ void pool_grad8(const uint8_t *pool, int PH, int PW, int h, bool hodd, int w, int cv,
+                                           float (&g)[8]) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g[k] = 0.f;
+    const int oh_lo = h >> 1, ow_lo = w >> 1;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int oh = oh_lo + rr;
+        if (rr == 1 && !(hodd && oh < PH)) break;  // wave-uniform
+        const uint8_t *slot = pool + (oh & 1) * kPoolSlot;
+#pragma unroll
+        for (int cc = 0; cc < (ODDW ? 2 : 1); ++cc) {
+            int ow = ow_lo + cc;
+            // the last odd column of an even-width map has no right window: read window ow_lo, never match
+            const bool ok = cc == 0 || ow < PW;
+            const uint32_t kk = ok ? static_cast<uint32_t>((h + 1 - 2 * oh) * 3 + (w + 1 - 2 * ow)) : 0xffu;
+            ow = ok ? ow : ow_lo;
+            const int e = ow * 8 + cv;
+            const uint4 dv = *reinterpret_cast<const uint4 *>(slot + e * 16);
+            const uint2 am = *reinterpret_cast<const uint2 *>(slot + kPoolD + e * 8);
+            float d[8];
+            unpack8f(dv, d);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
+                g[k] += ak == kk ? d[k] : 0.f;
+            }
+        }
+    }
+}
+
+// the forward / backward BN coefficients [fs; fh; k1; k2; k3] x 64 channels, staged once into LDS
+// (register-resident they cost 40 VGPRs across the MFMA loop and pushed the kernel into spills)
+constexpr int kBnpCoef = 5 * kCout;
+
+// dx (8 channels cv * 8.., bf16) of one conv-output pixel from its y vector and gathered pooled gradient;
+// kc = the LDS coefficient table
+__device__ __forceinline__ uint4 bnp_dx(const float *kc, int cv, const uint4 &yv, float (&g)[8]) {
+    float xv[8];
+    unpack8f(yv, xv);
+    float o[8];
+    // (scalar reads of the table, not a [5][8] array: the array was promoted to LDS)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float *t = kc + cv * 8 + k;
+        g[k] = (xv[k] * t[0] + t[kCout]) > 0.f ? g[k] : 0.f;
+        o[k] = t[2 * kCout] * g[k] + t[3 * kCout] * xv[k] + t[4 * kCout];
+    }
+    return make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
+                      pack_bf16x2(o[6], o[7]));
+}
+
+template <bool BNP>
 __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__restrict__ dy,
                                                               const uint16_t *__restrict__ x4,
-                                                              float *__restrict__ part, StemGeo g, int rows_per_wg) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kRowBytes + 2 * kDyRow];
+                                                              float *__restrict__ part, StemGeo g, int rows_per_wg,
+                                                              StemBnp bp) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kRing * kRowBytes + 2 * kDyRow + (BNP ? kBnpCoef * 4 + 2 * kPoolSlot : 0)];
     uint8_t *ring = lds;
     uint8_t *dyimg = lds + kRing * kRowBytes;
+    float *kc = reinterpret_cast<float *>(lds + kRing * kRowBytes + 2 * kDyRow);  // BNP only
+    uint8_t *pool = lds + kRing * kRowBytes + 2 * kDyRow + kBnpCoef * 4;       // BNP only: the pooled-row ring
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // wave = kh
     const int R = g.N * g.OH;
     const int r_begin = blockIdx.x * rows_per_wg;
@@ -661,6 +758,10 @@ __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__
     // zero both dy images once (rows >= OW stay zero: the K padding)
     for (int v = tid; v < 2 * kDyRow / 16; v += 448)
         reinterpret_cast<uint4 *>(dyimg)[v] = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (BNP) {
+        if (tid < kBnpCoef) kc[tid] = tid < 2 * kCout ? bp.fcoef[tid] : bp.bcoef[tid - 2 * kCout];
+    }
+    lds_barrier();  // the zero fill (and table) before any dy row lands in the images
 
     // input-row loader (as the forward): thread t < kRowPx owns padded pixel t
     const int px = tid - kRowPad;
@@ -675,25 +776,69 @@ __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__
         if (!ok) v = make_uint2(0u, 0u);
         if (tid < kRowPx) *reinterpret_cast<uint2 *>(ring + ((ih + kRing) & (kRing - 1)) * kRowBytes + tid * 8) = v;
     };
-    // dy row loader: chunk v = tid + 448 u (u = 0, 1) of the OW x 8 16-byte chunks
-    auto dy_load = [&](int r, uint4 (&d)[2]) {
+    // dy row loader: two of the OW x 8 16-byte chunks (ow, channel group c) per thread -- chunks tid and
+    // tid + 448; BNP: (2 j, c) and (2 j + 1, c) for j = tid >> 3, c = tid & 7 (an even and an odd column:
+    // the pool gather is specialised by column parity; OW <= 112).  Two named registers, not a [2] array:
+    // with the BNP staging below the arrays stayed in scratch.
+    const int cv0 = BNP ? (tid >> 3) * 16 + (tid & 7) : tid, cv1 = BNP ? cv0 + 8 : tid + 448;
+    const int dv0 = cv0 < g.OW * 8 ? cv0 : g.OW * 8 - 1;  // clamped (masked at the store)
+    const int dv1 = cv1 < g.OW * 8 ? cv1 : g.OW * 8 - 1;
+    auto dy_load = [&](int r, uint4 &d0, uint4 &d1) {
         const uint4 *src = reinterpret_cast<const uint4 *>(dy + static_cast<int64_t>(r) * g.OW * kCout);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            int v = tid + 448 * u;
-            v = v < g.OW * 8 ? v : g.OW * 8 - 1;  // clamped (masked at the store)
-            d[u] = src[v];
+        d0 = src[dv0];
+        d1 = src[dv1];
+    };
+    // BNP: pooled row p of image n (PW x 8 16-byte chunks of dyp, 8-byte chunks of argmax: chunk v = tid +
+    // 448 u) -> registers -> its LDS slot p & 1
+    struct PRow {  // native vectors: HIP's uint4 struct copies were left in scratch across the step
+        u32x4 d0, d1;
+        u32x2 a0, a1;
+    };
+    const u32x4 *dyp4 = reinterpret_cast<const u32x4 *>(bp.dyp);
+    const u32x2 *arg2 = reinterpret_cast<const u32x2 *>(bp.arg);
+    const int pv1 = tid + 448 < bp.PW * 8 ? tid + 448 : bp.PW * 8 - 1;  // chunk tid + 448, clamped
+    auto prow_load = [&](int nn, int p, PRow &pr) {
+        const int64_t base = (static_cast<int64_t>(nn) * bp.PH + p) * bp.PW * 8;
+        const int v0 = tid < bp.PW * 8 ? tid : bp.PW * 8 - 1;
+        pr.d0 = dyp4[base + v0];
+        pr.a0 = arg2[base + v0];
+        pr.d1 = dyp4[base + pv1];
+        pr.a1 = arg2[base + pv1];
+    };
+    auto prow_store = [&](int p, const PRow &pr) {
+        uint8_t *slot = pool + (p & 1) * kPoolSlot;
+        if (tid < bp.PW * 8) {
+            *reinterpret_cast<u32x4 *>(slot + tid * 16) = pr.d0;
+            *reinterpret_cast<u32x2 *>(slot + kPoolD + tid * 8) = pr.a0;
+        }
+        if (tid + 448 < bp.PW * 8) {
+            *reinterpret_cast<u32x4 *>(slot + (tid + 448) * 16) = pr.d1;
+            *reinterpret_cast<u32x2 *>(slot + kPoolD + (tid + 448) * 8) = pr.a1;
         }
     };
-    auto dy_store = [&](int buf, const uint4 (&d)[2]) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int v = tid + 448 * u;
-            if (v < g.OW * 8) {
-                const int ow = v >> 3, c = v & 7;
-                *reinterpret_cast<uint4 *>(dyimg + buf * kDyRow + ow * kARow + ((c >> 1) ^ hswz<kARow>(ow)) * 32 +
-                                           (c & 1) * 16) = d[u];
+    // stage dy row hh (conv row hh of the current image; BNP: formed from y = d and the pooled ring)
+    auto dy_put = [&](int buf, int v, const uint4 &val) {
+        const int ow = v >> 3, c = v & 7;
+        *reinterpret_cast<uint4 *>(dyimg + buf * kDyRow + ow * kARow + ((c >> 1) ^ hswz<kARow>(ow)) * 32 + (c & 1) * 16) =
+            val;
+    };
+    auto dy_store = [&](int buf, const uint4 &d0, const uint4 &d1, int hh) {
+        if constexpr (BNP) {
+            const bool hodd = hh & 1;
+            const int c = tid & 7, ow0 = cv0 >> 3;
+            if (cv0 < g.OW * 8) {
+                float gg[8];
+                pool_grad8<false>(pool, bp.PH, bp.PW, hh, hodd, ow0, c, gg);
+                dy_put(buf, cv0, bnp_dx(kc, c, d0, gg));
             }
+            if (cv1 < g.OW * 8) {
+                float gg[8];
+                pool_grad8<true>(pool, bp.PH, bp.PW, hh, hodd, ow0 + 1, c, gg);
+                dy_put(buf, cv1, bnp_dx(kc, c, d1, gg));
+            }
+        } else {
+            if (cv0 < g.OW * 8) dy_put(buf, cv0, d0);
+            if (cv1 < g.OW * 8) dy_put(buf, cv1, d1);
         }
     };
 
@@ -720,30 +865,51 @@ __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__
     // still filling would make the compiler wait for that load.
     struct Q {
         uint2 a, b;
-        uint4 d[2];
+        uint4 d0, d1;
     };
     auto rclamp = [&](int rr) { return rr < R ? rr : R - 1; };
     bool fresh = true;
     int buf = 0;
     auto step = [&](int r, Q &qa, Q &qb, Q &qc) {
         if (fresh) {
-            uint4 dcur[2];
-            dy_load(r, dcur);
-            dy_load(rclamp(r + 1), qa.d);
-            dy_load(rclamp(r + 2), qb.d);
+            uint4 dc0, dc1;
+            if constexpr (BNP) {
+                // pooled rows oh >> 1 and the next: those of conv rows oh and oh + 1 (later ones are
+                // loaded one step ahead, below)
+                const int p0 = oh >> 1;
+                PRow a, b;
+                prow_load(n, p0, a);
+                if (p0 + 1 < bp.PH) prow_load(n, p0 + 1, b);
+                prow_store(p0, a);
+                if (p0 + 1 < bp.PH) prow_store(p0 + 1, b);
+                lds_barrier();
+            }
+            dy_load(r, dc0, dc1);
+            dy_load(rclamp(r + 1), qa.d0, qa.d1);
+            dy_load(rclamp(r + 2), qb.d0, qb.d1);
 #pragma unroll
             for (int kh = 0; kh < kKH; ++kh) row_store(2 * oh - 3 + kh, row_value(n, 2 * oh - 3 + kh));
             qa.a = row_value(n, 2 * oh + 4);
             qa.b = row_value(n, 2 * oh + 5);
             qb.a = row_value(n, 2 * oh + 6);
             qb.b = row_value(n, 2 * oh + 7);
-            dy_store(buf, dcur);
+            dy_store(buf, dc0, dc1, oh);
             lds_barrier();
         }
         const bool next_same = r + 1 < r_end && oh + 1 < g.OH;
+        // BNP: at an odd conv row, pooled row (oh + 3) / 2 -- first needed by conv row oh + 2 -- into the
+        // slot of row (oh - 1) / 2, whose last reader (conv row oh) is staged.  Issued first: the wait for
+        // it at this step's end leaves the later row prefetches in flight
+        PRow pn;
+        const int pnext = (oh + 3) >> 1;
+        const bool pload = BNP && (oh & 1) && next_same && pnext < bp.PH;
+        if constexpr (BNP) {
+            if (pload) prow_load(n, pnext, pn);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         qc.a = row_value(n, 2 * oh + 8);  // the new input rows of output row oh + 3
         qc.b = row_value(n, 2 * oh + 9);
-        dy_load(rclamp(r + 3), qc.d);
+        dy_load(rclamp(r + 3), qc.d0, qc.d1);
 
         if (wave < kKH) {
             const int kh = wave;
@@ -772,7 +938,10 @@ __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__
         if (next_same) {  // rows of output row oh + 1 and its dy row, into the free slots / buffer
             row_store(2 * oh + 4, qa.a);
             row_store(2 * oh + 5, qa.b);
-            dy_store(buf ^ 1, qa.d);
+            if constexpr (BNP) {
+                if (pload) prow_store(pnext, pn);
+            }
+            dy_store(buf ^ 1, qa.d0, qa.d1, oh + 1);
         }
         lds_barrier();
         buf ^= 1;
@@ -802,296 +971,6 @@ __global__ __launch_bounds__(448) void stem_wgrad_rows_kernel(const uint16_t *__
                     const int co = i * 16 + (lane >> 4) * 4 + q;
                     dst[co * kKPad + wave * 32 + j * 16 + (lane & 15)] = acc[i][j][q];
                 }
-    }
-}
-
-// ------------------------------------------------- fused backward: pool + BN + weight gradient
-// The stem's forward is conv -> BN(batch stats) -> ReLU -> MaxPool(3,2,1), and the image needs
-// no gradient, so the BN input gradient dx = k1*dz + k2*y + k3 (dz = ReLU'-gated gradient
-// scattered back through the pool argmax, y = conv output, k = per-channel BN-backward
-// coefficients that depend on sum(dz) and sum(dz*y)) is only ever consumed by the weight
-// gradient.  By linearity
-//     dW[co][k] = k1[co] * S1[co][k] + k2[co] * S2[co][k] + k3[co] * S3[k],
-//     S1 = sum_p dz[p] (x) A[p],   S2 = sum_p y[p] (x) A[p],   S3 = sum_p A[p]   (A = im2col row)
-// so ONE pass over the pixels gathers dz, accumulates sum(dz), sum(dz*y) and the three MFMA
-// products (S3 via a constant ones-row A fragment), and a tiny finalize applies the BN
-// backward -- dx (411 MB at batch 256) is never written nor re-read, and the separate BN
-// reduce / apply passes disappear.
-constexpr int kPart1 = kCout * kKPad;                      // S1 or S2 floats
-constexpr int kPartStride = 2 * kPart1 + kKPad + 2 * kCout;  // S1 | S2 | S3 | sum dz | sum dz*y
-
-__global__ __launch_bounds__(256) void stem_bwd_kernel(const uint16_t *__restrict__ dyp,
-                                                       const uint8_t *__restrict__ arg,
-                                                       const uint16_t *__restrict__ y,
-                                                       const float *__restrict__ fcoef,
-                                                       const uint16_t *__restrict__ x4, float *__restrict__ part,
-                                                       StemGeo g, int PH, int PW, int kps) {
-    constexpr int kA2 = kBK * kARow;                      // second A image (y) after the first (dz)
-    constexpr int kStage = 2 * kA2 + kBK * kIRow;         // 48 KB
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kStage];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int split = blockIdx.x;
-    const int p_begin = split * kps * kBK;
-    int nsteps = (g.M - p_begin + kBK - 1) / kBK;
-    if (nsteps > kps) nsteps = kps;
-
-    // staging: pixel spx = tid >> 2; channels 16 ssub + [0, 16) (two 8-channel vectors);
-    //          im2col window slots q = ssub + 4 i (kh = q / 8, kw = q % 8)
-    const int spx = tid >> 2, ssub = tid & 3;
-    float sc[2][8], sh[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[u][k] = fcoef[16 * ssub + 8 * u + k];
-            sh[u][k] = fcoef[kCout + 16 * ssub + 8 * u + k];
-        }
-    float sdz[2][8], sdzy[2][8];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sdz[u][k] = sdzy[u][k] = 0.f;
-
-    struct Regs {
-        uint4 dz[2], yv[2];
-        uint2 im[14];
-    };
-    auto gload = [&](Regs &R, int ks) {
-        const int p = p_begin + ks * kBK + spx;
-        const bool ok = p < g.M;
-        int n = 0, h = 0, w = 0;
-        if (ok) {
-            n = fdiv(p, g.m_hw);
-            const int rem = p - n * g.OH * g.OW;
-            h = fdiv(rem, g.m_ow);
-            w = rem - h * g.OW;
-        }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int cv = 2 * ssub + u;
-            float gz[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) gz[k] = 0.f;
-            uint4 yq = make_uint4(0u, 0u, 0u, 0u);
-            if (ok) {
-                yq = *reinterpret_cast<const uint4 *>(y + static_cast<int64_t>(p) * kCout + cv * 8);
-                // pool windows (oh, ow) with 2 oh - 1 <= h <= 2 oh + 1 (same for w): the gradient
-                // of window o reaches this pixel iff its argmax is this pixel's window offset
-                const int oh_lo = h >> 1, oh_hi = (h + 1) >> 1, ow_lo = w >> 1, ow_hi = (w + 1) >> 1;
-#pragma unroll
-                for (int a = 0; a < 2; ++a) {
-                    const int oh = a ? oh_hi : oh_lo;
-                    if ((a && oh_hi == oh_lo) || oh >= PH) continue;
-                    const int kh = h + 1 - 2 * oh;
-#pragma unroll
-                    for (int b = 0; b < 2; ++b) {
-                        const int ow = b ? ow_hi : ow_lo;
-                        if ((b && ow_hi == ow_lo) || ow >= PW) continue;
-                        const uint32_t kk = static_cast<uint32_t>(kh * 3 + (w + 1 - 2 * ow));
-                        const int64_t o = ((static_cast<int64_t>(n) * PH + oh) * PW + ow) * kCout + cv * 8;
-                        const uint2 am = *reinterpret_cast<const uint2 *>(arg + o);
-                        float d[8];
-                        unpack8(*reinterpret_cast<const uint4 *>(dyp + o), d);
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
-                            if (ak == kk) gz[k] += d[k];
-                        }
-                    }
-                }
-            }
-            float yf[8];
-            unpack8(yq, yf);
-            uint32_t pk[4];
-#pragma unroll
-            for (int k = 0; k < 8; k += 2) {
-                const float z0 = (yf[k] * sc[u][k] + sh[u][k]) > 0.f ? gz[k] : 0.f;
-                const float z1 = (yf[k + 1] * sc[u][k + 1] + sh[u][k + 1]) > 0.f ? gz[k + 1] : 0.f;
-                sdz[u][k] += z0;
-                sdz[u][k + 1] += z1;
-                sdzy[u][k] += z0 * yf[k];
-                sdzy[u][k + 1] += z1 * yf[k + 1];
-                pk[k >> 1] = static_cast<uint32_t>(f32_to_bf16(z0)) | (static_cast<uint32_t>(f32_to_bf16(z1)) << 16);
-            }
-            R.dz[u] = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-            R.yv[u] = yq;
-        }
-        const int ih0 = h * 2 - 3, iw0 = w * 2 - 3;
-        const int base = ((n * g.H + ih0) * g.W + iw0) * 4;
-#pragma unroll
-        for (int i = 0; i < 14; ++i) {
-            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
-            const bool in = ok && static_cast<unsigned>(ih0 + kh) < static_cast<unsigned>(g.H) &&
-                            static_cast<unsigned>(iw0 + kw) < static_cast<unsigned>(g.W);
-            R.im[i] = in ? *reinterpret_cast<const uint2 *>(x4 + (base + (kh * g.W + kw) * 4)) : make_uint2(0u, 0u);
-        }
-    };
-    auto swrite = [&](const Regs &R, int buf) {
-        uint8_t *a1 = lds + buf * kStage;
-        uint8_t *a2 = a1 + kA2;
-        uint8_t *ib = a2 + kA2;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int c = 2 * ssub + u;  // 16-byte chunk of the 128-byte row
-            const int o = spx * kARow + ((c >> 1) ^ hswz<kARow>(spx)) * 32 + (c & 1) * 16;
-            *reinterpret_cast<uint4 *>(a1 + o) = R.dz[u];
-            *reinterpret_cast<uint4 *>(a2 + o) = R.yv[u];
-        }
-#pragma unroll
-        for (int i = 0; i < 14; ++i) {
-            const int q = ssub + 4 * i, kh = q >> 3, kw = q & 7;
-            const int byte = kh * 64 + kw * 8;
-            const int grp = (byte >> 5) ^ hswz<kIRow>(spx);
-            *reinterpret_cast<uint2 *>(ib + spx * kIRow + grp * 32 + (byte & 31)) = R.im[i];
-        }
-    };
-
-    const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
-    const int row0 = 8 * fg + fq;
-    int aoff[4], boff[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        aoff[i] = row0 * kARow + 32 * (i ^ hswz<kARow>(row0)) + 8 * fp;
-        boff[i] = row0 * kIRow + 32 * ((wave * 4 + i) ^ hswz<kIRow>(row0)) + 8 * fp;
-    }
-    const int jmax = wave == 3 ? 2 : 4;
-    // ones-row A fragment: row 0 of the 16x32 operand all ones -> S3 = column sums of B
-    bf16x8 ones;
-    {
-        const short one = (lane & 15) == 0 ? static_cast<short>(0x3f80) : static_cast<short>(0);
-        const s16x8 v = {one, one, one, one, one, one, one, one};
-        ones = __builtin_bit_cast(bf16x8, v);
-    }
-    f32x4 acc1[4][4], acc2[4][4], acc3[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        acc3[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc1[i][j] = acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    auto compute = [&](int buf) {
-        const uint8_t *a1 = lds + buf * kStage;
-        const uint8_t *a2 = a1 + kA2;
-        const uint8_t *ib = a2 + kA2;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            bf16x8 f1[4], f2[4], bfr[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                f1[i] = tr_frag(a1 + aoff[i] + 32 * s * kARow, a1 + aoff[i] + (32 * s + 4) * kARow);
-                f2[i] = tr_frag(a2 + aoff[i] + 32 * s * kARow, a2 + aoff[i] + (32 * s + 4) * kARow);
-                bfr[i] = tr_frag(ib + boff[i] + 32 * s * kIRow, ib + boff[i] + (32 * s + 4) * kIRow);
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (j < jmax) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[i], bfr[j], acc1[i][j], 0, 0, 0);
-                        acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f2[i], bfr[j], acc2[i][j], 0, 0, 0);
-                    }
-                    acc3[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, bfr[j], acc3[j], 0, 0, 0);
-                }
-            }
-        }
-    };
-
-    Regs R;
-    if (nsteps > 0) {
-        gload(R, 0);
-        swrite(R, 0);
-    }
-    __syncthreads();
-    for (int ks = 0; ks < nsteps; ++ks) {
-        if (ks + 1 < nsteps) gload(R, ks + 1);
-        compute(ks & 1);
-        if (ks + 1 < nsteps) swrite(R, (ks + 1) & 1);
-        __syncthreads();
-    }
-
-    // ---- partials of this split: S1, S2 [co][k < 224], S3 [k], sum dz, sum dz*y [co]
-    float *dst = part + static_cast<int64_t>(split) * kPartStride;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (j < jmax)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int co = i * 16 + (lane >> 4) * 4 + r;
-                    const int k = wave * 64 + j * 16 + (lane & 15);
-                    dst[co * kKPad + k] = acc1[i][j][r];
-                    dst[kPart1 + co * kKPad + k] = acc2[i][j][r];
-                }
-    if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (j < jmax) dst[2 * kPart1 + wave * 64 + j * 16 + lane] = acc3[j][0];
-    }
-    // per-channel sums: the 64 pixel-threads of each channel group meet in LDS
-    float *red = reinterpret_cast<float *>(lds);  // [64 spx][2][64 ch]; the loop's last barrier passed
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int c = 16 * ssub + 8 * u + k;
-            red[(spx * 2) * kCout + c] = sdz[u][k];
-            red[(spx * 2 + 1) * kCout + c] = sdzy[u][k];
-        }
-    __syncthreads();
-    if (tid < 2 * kCout) {
-        const int which = tid / kCout, c = tid % kCout;
-        float t = 0.f;
-        for (int q = 0; q < kBK; ++q) t += red[(q * 2 + which) * kCout + c];
-        dst[2 * kPart1 + kKPad + which * kCout + c] = t;
-    }
-}
-
-// tot[e] = sum over splits of part[split][e]; block = 16 elements x 16 split groups
-__global__ __launch_bounds__(256) void stem_bwd_fold_kernel(const float *__restrict__ part, int splits,
-                                                            float *__restrict__ tot) {
-    __shared__ float red[256];
-    const int t = threadIdx.x, o = t & 15, sg = t >> 4;
-    const int e = blockIdx.x * 16 + o;
-    float s = 0.f;
-    if (e < kPartStride)
-        for (int sp = sg; sp < splits; sp += 16) s += part[static_cast<int64_t>(sp) * kPartStride + e];
-    red[t] = s;
-    __syncthreads();
-    if (sg == 0 && e < kPartStride) {
-        for (int q = 1; q < 16; ++q) s += red[o + 16 * q];
-        tot[e] = s;
-    }
-}
-
-// BN backward coefficients per channel (as bn.hip's bn_bwd_finalize) and
-// dW[co][kh][kw][c] = k1 S1 + k2 S2 + k3 S3, rounded to bf16 in [64][7][7][3] order.
-__global__ __launch_bounds__(256) void stem_bwd_finalize_kernel(const float *__restrict__ tot,
-                                                                const float *__restrict__ mean,
-                                                                const float *__restrict__ invstd,
-                                                                const float *__restrict__ gamma, int64_t rows,
-                                                                int training, float *__restrict__ dgamma,
-                                                                float *__restrict__ dbeta, uint16_t *__restrict__ dw) {
-    const int co = blockIdx.x;
-    const double db = tot[2 * kPart1 + kKPad + co];
-    const double sxy = tot[2 * kPart1 + kKPad + kCout + co];
-    const double dg = static_cast<double>(invstd[co]) * (sxy - static_cast<double>(mean[co]) * db);
-    if (threadIdx.x == 0) {
-        dgamma[co] = static_cast<float>(dg);
-        dbeta[co] = static_cast<float>(db);
-    }
-    const float a = (gamma ? gamma[co] : 1.f) * invstd[co];
-    float k2 = 0.f, k3 = 0.f;
-    if (training) {
-        const float inv_m = 1.f / static_cast<float>(rows);
-        k2 = -a * static_cast<float>(dg) * invstd[co] * inv_m;
-        k3 = -a * static_cast<float>(db) * inv_m - k2 * mean[co];
-    }
-    for (int e = threadIdx.x; e < 147; e += blockDim.x) {
-        const int kh = e / 21, r2 = e - kh * 21, kw = r2 / 3, c = r2 - kw * 3;
-        const int k = kh * 32 + kw * 4 + c;
-        const float v = a * tot[co * kKPad + k] + k2 * tot[kPart1 + co * kKPad + k] + k3 * tot[2 * kPart1 + k];
-        dw[co * 147 + e] = f32_to_bf16(v);
     }
 }
 
@@ -1169,6 +1048,28 @@ int stem_wgrad_splits(int N, int H, int W) {
     return splits < 1 ? 1 : splits;
 }
 
+bool stem_wgrad_bnp_supported(int N, int H, int W) {
+    const StemGeo g = make_geo(N, H, W);
+    return g.W <= kRowPx - 8 && g.OW <= 112;  // one even and one odd column per thread
+}
+
+void launch_stem_wgrad_bnp(const uint16_t *y, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
+                           int splits, const uint16_t *dyp, const uint8_t *arg, const float *fcoef,
+                           const float *bcoef, hipStream_t s) {
+    const StemGeo g = make_geo(N, H, W);
+    check_geo(g);
+    if (!(g.W <= kRowPx - 8 && g.OW <= 112)) throw std::invalid_argument("stem_wgrad_bnp: image too wide for the row kernel");
+    const int R = g.N * g.OH;
+    if (splits < 1) splits = 1;
+    if (splits > R) splits = R;
+    const int rpw = (R + splits - 1) / splits;
+    splits = (R + rpw - 1) / rpw;
+    StemBnp bp{reinterpret_cast<const uint4 *>(dyp), reinterpret_cast<const uint2 *>(arg), fcoef, bcoef,
+               (g.OH + 2 - 3) / 2 + 1, (g.OW + 2 - 3) / 2 + 1};
+    stem_wgrad_rows_kernel<true><<<splits, 448, 0, s>>>(y, x4, part, g, rpw, bp);
+    stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
+}
+
 void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, float *part, int N, int H, int W,
                        int splits, hipStream_t s) {
     const StemGeo g = make_geo(N, H, W);
@@ -1180,7 +1081,7 @@ void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, flo
         if (splits > R) splits = R;
         const int rpw = (R + splits - 1) / splits;
         splits = (R + rpw - 1) / rpw;
-        stem_wgrad_rows_kernel<<<splits, 448, 0, s>>>(dy, x4, part, g, rpw);
+        stem_wgrad_rows_kernel<false><<<splits, 448, 0, s>>>(dy, x4, part, g, rpw, StemBnp{});
         stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
         return;
     }
@@ -1191,28 +1092,6 @@ void launch_stem_wgrad(const uint16_t *dy, const uint16_t *x4, uint16_t *dw, flo
     splits = (ksteps + kps - 1) / kps;  // no empty split
     stem_wgrad_kernel<<<splits, 256, 0, s>>>(dy, x4, part, g, kps);
     stem_wgrad_reduce_kernel<<<(kCout * 147 + 15) / 16, 256, 0, s>>>(part, splits, dw);
-}
-
-
-int64_t stem_bwd_workspace(int splits) { return static_cast<int64_t>(splits + 1) * kPartStride; }
-
-void launch_stem_backward(const uint16_t *dyp, const uint8_t *arg, const uint16_t *y, const float *fcoef,
-                          const float *mean, const float *invstd, const float *gamma, const uint16_t *x4, int N, int H,
-                          int W, bool training, int splits, float *ws, float *dgamma, float *dbeta, uint16_t *dw,
-                          hipStream_t s) {
-    const StemGeo g = make_geo(N, H, W);
-    check_geo(g);
-    const int PH = pool_out(g.OH), PW = pool_out(g.OW);
-    const int ksteps = (g.M + kBK - 1) / kBK;
-    if (splits < 1) splits = 1;
-    if (splits > ksteps) splits = ksteps;
-    const int kps = (ksteps + splits - 1) / splits;
-    splits = (ksteps + kps - 1) / kps;  // no empty split
-    float *tot = ws + static_cast<int64_t>(splits) * kPartStride;
-    stem_bwd_kernel<<<splits, 256, 0, s>>>(dyp, arg, y, fcoef, x4, ws, g, PH, PW, kps);
-    stem_bwd_fold_kernel<<<(kPartStride + 15) / 16, 256, 0, s>>>(ws, splits, tot);
-    stem_bwd_finalize_kernel<<<kCout, 256, 0, s>>>(tot, mean, invstd, gamma, g.M, training ? 1 : 0, dgamma, dbeta,
-                                                   dw);
 }
 
 }  // namespace kfk

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kXBlock) void xent_bwd_kernel(const uint32_t *__res
         float a = __expf(__uint_as_float(w << 16) - l), b = __expf(__uint_as_float(w & 0xffff0000u) - l);
         if (2 * i == lab) a -= 1.f;
         if (2 * i + 1 == lab) b -= 1.f;
-        drow[i] = static_cast<uint32_t>(f32_to_bf16(a * g)) | (static_cast<uint32_t>(f32_to_bf16(b * g)) << 16);
+        drow[i] = pack_bf16x2(a * g, b * g);
     }
 }
 
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kXBlock) void xent_bwd_vec_kernel(const uint16_t *_
             float a = e < V ? __expf(f[2 * k] - l) : 0.f, b = e + 1 < V ? __expf(f[2 * k + 1] - l) : 0.f;
             if (e == lab) a -= 1.f;
             if (e + 1 == lab) b -= 1.f;
-            w[k] = static_cast<uint32_t>(f32_to_bf16(a * g)) | (static_cast<uint32_t>(f32_to_bf16(b * g)) << 16);
+            w[k] = pack_bf16x2(a * g, b * g);
         }
         return make_uint4(w[0], w[1], w[2], w[3]);
     };

@@ -28,7 +28,6 @@ class BertLayer(nn.Module):
         # parameters and state_dict keys, torch composition off the GPU fast path
         self.ln1 = AddLayerNorm(d, eps=1e-12)
         self.fc1 = nn.Linear(d, ffn)
-        self.fc1._kf_gelu_out = True  # its only consumer is the GELU: u and gelu(u) from one GEMM (ops/linear.py)
         self.fc2 = nn.Linear(ffn, d)
         self.ln2 = AddLayerNorm(d, eps=1e-12)
         self.dropout = dropout
@@ -42,8 +41,7 @@ class BertLayer(nn.Module):
         qkv = self.qkv(x)
         if mask is None:
             # fused HIP attention straight from / into the projections' layouts (SDPA off that path)
-            # qkv's only consumer: the attention backward also forms the projection's bias gradient
-            a = self_attention(qkv, self.heads, p, bias_link=True)
+            a = self_attention(qkv, self.heads, p)
         else:
             q, k, v = qkv.view(B, S, 3, self.heads, D // self.heads).permute(2, 0, 3, 1, 4)
             a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=p)

@@ -167,9 +167,8 @@ class ResNet(nn.Module):
             from ..parallel.mixed import shadow
 
             sums = _sums(self.bn1, x.device) if self.training else None
-            if stem_ops.FUSED_BACKWARD and self.training and self.bn1.track_running_stats and \
-                    self.bn1.momentum is not None:
-                # conv + BN + ReLU + MaxPool as one node: fused one-pass backward
+            if self.training and stem_ops.block_eligible(x, self.bn1):
+                # conv + BN + ReLU + MaxPool as one node: the weight gradient forms dx while staging
                 x = stem_ops.stem_block(x, shadow(self.conv1.weight), self.bn1, sums)
             else:
                 x = self.bn1.forward_pool(stem_ops.stem_conv(x, shadow(self.conv1.weight), sums), sums=sums)

@@ -21,33 +21,25 @@ import torch.nn.functional as F
 from .._lib import hip, hip_available
 from . import dropout_seed
 
-# module switch (tests / A/B): the qkv bias gradient from the attention backward's column sums.  Off: measured
-# slower end to end than the projection's own two-stage column sum (BERT-base + GNS 15.70-15.76 -> 15.78-15.80
-# ms/step, same box, r5t38)
-_BIAS_LINK = False
+# (round 6: the qkv bias gradient from column sums inside the attention backward is gone -- measured slower
+# end to end than the projection's own two-stage column sum, BERT-base + GNS 15.70-15.76 -> 15.78-15.80
+# ms/step on one box, r5t38)
 
 
 class _AttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, heads, p, seed, blink=None):
+    def forward(ctx, qkv, heads, p, seed):
         scale = 1.0 / math.sqrt(64.0)
         out, lse = hip().attention_forward(qkv, heads, scale, seed, p)
         ctx.save_for_backward(qkv, out, lse)
         ctx.heads, ctx.p, ctx.seed, ctx.scale = heads, p, seed, scale
-        ctx.blink = blink
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        bl = ctx.blink
-        dqkv, db = hip().attention_backward(qkv, out, lse, dout.contiguous(), ctx.heads, ctx.scale, ctx.seed, ctx.p,
-                                            bl.dtype if bl is not None else None)
-        if bl is not None:
-            # the qkv projection's bias gradient, from the kernel's column sums (ops.linear.BiasLink: that
-            # layer's backward checks it receives exactly this dqkv and skips its own column-sum pass)
-            bl.value, bl.ptr = db, dqkv.data_ptr()
-        return dqkv, None, None, None, None
+        dqkv = hip().attention_backward(qkv, out, lse, dout.contiguous(), ctx.heads, ctx.scale, ctx.seed, ctx.p)
+        return dqkv, None, None, None
 
 
 def eligible(qkv: torch.Tensor, heads: int) -> bool:
@@ -55,17 +47,14 @@ def eligible(qkv: torch.Tensor, heads: int) -> bool:
             and qkv.shape[2] == 3 * heads * 64 and hip_available() and hip().attention_supported(int(qkv.shape[1]), 64))
 
 
-def self_attention(qkv: torch.Tensor, heads: int, p: float = 0.0, bias_link: bool = False) -> torch.Tensor:
+def self_attention(qkv: torch.Tensor, heads: int, p: float = 0.0) -> torch.Tensor:
     """softmax(Q K^T / sqrt(64)) V with dropout ``p`` on the probabilities, per head;
-    ``qkv``: [B, S, 3*H*dh] -> [B, S, H*dh].  ``bias_link``: the caller guarantees ``qkv`` is an
-    :func:`ops.linear.linear` output consumed only here -- the backward then also forms that layer's
-    bias gradient (column sums inside the attention backward kernel)."""
+    ``qkv``: [B, S, 3*H*dh] -> [B, S, H*dh]."""
     B, S, D3 = qkv.shape
     if eligible(qkv, heads):
         seed = int(torch.randint(0, 2**31 - 1, (1,)).item())  # CPU generator: no device sync
         dropout_seed.base(qkv.device)  # registers the device seed word (graph replays advance it)
-        bl = getattr(qkv, "_kf_blink", None) if bias_link and _BIAS_LINK else None
-        return _AttnFn.apply(qkv, heads, float(p), seed, bl)
+        return _AttnFn.apply(qkv, heads, float(p), seed)
     dh = D3 // (3 * heads)
     q, k, v = qkv.view(B, S, 3, heads, dh).permute(2, 0, 3, 1, 4)
     a = F.scaled_dot_product_attention(q, k, v, dropout_p=p)

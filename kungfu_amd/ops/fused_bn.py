@@ -121,7 +121,7 @@ class _BNActPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, mean, invstd, weight, coef, arg, xarg = ctx.saved_tensors
-        dx, dw, db = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training, xarg)
+        dx, dw, db, _ = hip().bn_pool_backward(dy, arg, x, mean, invstd, weight, coef, ctx.training, xarg)
         dw, db = _param_grads(ctx, dw, db)
         return dx, dw, db, None, None, None, None, None, None, None
 

@@ -69,10 +69,9 @@ class GeluLink:
 
 _RES_LINK = True  # module switch (tests / A/B)
 _GELU_GEMM = True  # module switch (tests / A/B): FC2's data gradient + GELU backward on gemm.hip
-# module switch (tests / A/B): FC1's forward + GELU on one gemm.hip launch (linear(..., gelu_out=True)).  Off:
-# measured slower end to end (BERT-base + GNS 15.58-15.69 -> 15.90-15.94 ms/step, same box, r5t34) -- our
-# 256 x 256 NT GEMM stays behind hipBLASLt's stream-K kernel at this shape by more than the GELU pass it saves
-_GELU_FWD = False
+# (round 6: FC1's forward + GELU on one gemm.hip launch is gone -- measured slower end to end, BERT-base +
+# GNS 15.58-15.69 -> 15.90-15.94 ms/step on one box, r5t34: the 256 x 256 NT GEMM stays behind hipBLASLt's
+# stream-K kernel at that shape by more than the GELU pass it saves)
 
 
 def residual_link(x: torch.Tensor):
@@ -122,7 +121,7 @@ def _gelu_gemm_ok(M: int, in_f: int, out_f: int) -> bool:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, target=None, rlink=None, glink=None, gelu_out=False):
+    def forward(ctx, x, w, b, target=None, rlink=None, glink=None):
         ctx.save_for_backward(x, w)
         ctx.target = target
         ctx.rlink = rlink
@@ -139,14 +138,6 @@ class _LinearFn(torch.autograd.Function):
         out_f, in_f = w.shape
         M = x.numel() // in_f
         ctx.wt = None
-        ctx.gelu_h = None
-        if (gelu_out and _GELU_FWD and b is not None and b.dtype == torch.bfloat16 and x.is_contiguous()
-                and out_f % 256 == 0 and hip().gemm_nt_supported(M, out_f, in_f)):
-            # the consumer is a GELU (BERT's FC1): u and h = gelu(u) from ONE gemm.hip launch; ops.linear.gelu
-            # then hands out this h instead of running its own pass (u stays the saved GELU input)
-            u, h = hip().gemm_nt_gelu(x.view(M, in_f), w, b, 256)
-            ctx.gelu_h = h.view(*x.shape[:-1], out_f)
-            return u.view(*x.shape[:-1], out_f)
         if _gemm_ok(M, in_f, out_f) and x.is_contiguous() and (b is None or b.dtype == torch.bfloat16):
             if target is not None and _gemm_ok(M, out_f, in_f):
                 ctx.wt = _wt_cache(target, w)
@@ -191,7 +182,11 @@ class _LinearFn(torch.autograd.Function):
                 # g first (a 25 MB D2D copy per BERT-base product, measured slower than the add it
                 # replaces).  g is the AddLayerNorm's own backward output; when it also went out as
                 # the residual branch's gradient (no dropout) that branch's backward consumed it
-                # earlier on this stream
+                # earlier on this stream -- but its weight gradient may still be reading it on the side
+                # stream: wait for that first
+                from ..parallel.mixed import SideStream
+
+                SideStream.before_write(g)
                 dx = g.addmm_(dy2, w).view(x.shape)
             else:
                 dx = torch.mm(dy2, w).view(x.shape)
@@ -222,6 +217,7 @@ class _LinearFn(torch.autograd.Function):
                 dy2.record_stream(side)
                 x2.record_stream(side)
                 SideStream._pending.append(ev)
+                SideStream.note_reads(ev, dy2, x2)
             else:
                 wg()
             space.sink.put_direct(i)
@@ -238,7 +234,7 @@ class _LinearFn(torch.autograd.Function):
                 db = hip().colsum(dy2, ctx.b_dtype)
             else:
                 db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -250,8 +246,7 @@ def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
     return hip_available() and hip().conv_wgrad_supported(int(in_f), int(out_f), 1, 1)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target=None,
-           gelu_out: bool = False) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target=None) -> torch.Tensor:
     """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible.  ``grad_target``
     ``(space, index)``: ``w`` is the bf16 shadow of that flat-space parameter -- its gradient is
     reduced straight into the parameter's f32 gradient slot (``space.sink.put_direct``)."""
@@ -260,11 +255,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target
         if rl is not None and (rl.armed or x.dtype != torch.bfloat16):
             rl = None  # one linear consumer per link
         gl = getattr(x, "_kf_glink", None)
-        y = _LinearFn.apply(x, w, b, grad_target, rl, gl, gelu_out)
+        y = _LinearFn.apply(x, w, b, grad_target, rl, gl)
         if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
             y._kf_blink = y.grad_fn.blink
-        if y.grad_fn is not None and getattr(y.grad_fn, "gelu_h", None) is not None:
-            y._kf_gelu_h, y.grad_fn.gelu_h = y.grad_fn.gelu_h, None
         return y
     return F.linear(x, w, b)
 
@@ -279,11 +272,7 @@ class _GeluFn(torch.autograd.Function):
         ctx.save_for_backward(u)
         ctx.blink = blink
         ctx.glink = glink
-        h = getattr(u, "_kf_gelu_h", None)
-        if h is not None:  # formed by u's producing GEMM (linear(..., gelu_out=True))
-            u._kf_gelu_h = None
-            return h
-        return F.gelu(u)  # norms.hip gelu_forward measured 0.6 % slower end to end (r4t20): not used
+        return F.gelu(u)  # a HIP erf-GELU forward measured 0.6 % slower end to end (r4t20): torch's
 
     @staticmethod
     def backward(ctx, dy):

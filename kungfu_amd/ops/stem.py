@@ -21,9 +21,9 @@ import torch
 from .._lib import hip, hip_available
 
 _ENABLED = os.environ.get("KUNGFU_STEM", "1") != "0"
-# One-pass fused stem backward (``_StemBlockFn``); off by default until it beats the layered
-# BN-pool backward + weight-gradient kernels (tools/bench_stem.py).
-FUSED_BACKWARD = False  # one-pass fused stem backward: measured slower (r3); kept for its test
+# Stem conv + BN + ReLU + MaxPool as one autograd node whose weight gradient forms the BN input
+# gradient while staging (``_StemBlockFn``) instead of the layered BN-pool backward + weight gradient.
+FUSED_BACKWARD = True
 
 
 def set_enabled(on: bool) -> bool:
@@ -78,9 +78,12 @@ def stem_conv(x: torch.Tensor, w: torch.Tensor, stats: Optional[torch.Tensor] = 
 
 
 class _StemBlockFn(torch.autograd.Function):
-    """maxpool3x3s2p1(relu(bn(conv7x7s2p3(x)))) as ONE autograd node: the backward is the
-    fused stem kernel (pool-gradient gather + BN backward + conv weight gradient in one pass,
-    ``stem.hip: stem_bwd_kernel``) -- the BN input gradient is never materialised."""
+    """maxpool3x3s2p1(relu(bn(conv7x7s2p3(x)))) as ONE autograd node.  Backward: the BN+ReLU+pool
+    backward runs only its statistics + finalize (``bn_pool_backward(apply=False)``: the BN
+    gamma/beta gradients and the coefficients k1, k2, k3 of ``dx = k1 dz + k2 y + k3``), then the
+    stem weight-gradient kernel FORMS dx while staging its dy operand (``stem_wgrad_bnp``: pool
+    gather + ReLU gate + BN backward from dyp, the argmax bytes and y) -- the BN input gradient
+    (411 MB at batch 256) is never written nor read back."""
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, running_mean, running_var, momentum, eps, training, nbt, sums):
@@ -93,9 +96,9 @@ class _StemBlockFn(torch.autograd.Function):
             wb = wb.contiguous(memory_format=torch.channels_last)
         st = sums if training else None
         y = H.stem_forward(x4, H.stem_pack_weight(wb), st)
-        yp, mean, invstd, coef, arg, _ = H.bn_pool_forward(y, gamma, beta, running_mean, running_var, momentum, eps,
-                                                         training, nbt, st)
-        ctx.save_for_backward(x4, y, mean, invstd, gamma, coef, arg)
+        yp, mean, invstd, coef, arg, xarg = H.bn_pool_forward(y, gamma, beta, running_mean, running_var, momentum,
+                                                              eps, training, nbt, st)
+        ctx.save_for_backward(x4, y, mean, invstd, gamma, coef, arg, xarg)
         ctx.training = training
         ctx.wdtype = w.dtype
         ctx.direct = _direct(gamma, beta)
@@ -105,12 +108,24 @@ class _StemBlockFn(torch.autograd.Function):
     def backward(ctx, dyp):
         from .fused_bn import _param_grads
 
-        x4, y, mean, invstd, gamma, coef, arg = ctx.saved_tensors
-        dw, dg, db = hip().stem_backward(dyp, arg, y, coef, mean, invstd, gamma, x4, ctx.training)
+        x4, y, mean, invstd, gamma, coef, arg, xarg = ctx.saved_tensors
+        H = hip()
+        if not dyp.is_contiguous(memory_format=torch.channels_last):
+            dyp = dyp.contiguous(memory_format=torch.channels_last)
+        _, dg, db, bcoef = H.bn_pool_backward(dyp, arg, y, mean, invstd, gamma, coef, ctx.training, xarg,
+                                              apply=False)
+        dw = H.stem_wgrad_bnp(y, x4, dyp, arg, coef, bcoef)
         dg, db = _param_grads(ctx, dg, db)
         if dw.dtype != ctx.wdtype:
             dw = dw.to(ctx.wdtype)
         return None, dw, dg, db, None, None, None, None, None, None, None
+
+
+def block_eligible(x: torch.Tensor, bn) -> bool:
+    """The fused stem node applies: training with batch statistics and an image the row kernel
+    takes (``stem_wgrad_bnp_supported``)."""
+    return (FUSED_BACKWARD and bn.training and bn.track_running_stats and bn.momentum is not None
+            and hip().stem_wgrad_bnp_supported(x.shape[0], x.shape[2], x.shape[3]))
 
 
 def stem_block(x: torch.Tensor, w: torch.Tensor, bn, sums: Optional[torch.Tensor]) -> torch.Tensor:

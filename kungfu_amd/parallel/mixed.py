@@ -147,8 +147,7 @@ def _linear_forward(self, x):
     # reduces its splits straight into the weight's flat f32 gradient slot
     w = shadow(self.weight)
     return linear(x, w, shadow(self.bias) if self.bias is not None else None,
-                  grad_target=direct_target(self.weight) if w is not self.weight else None,
-                  gelu_out=getattr(self, "_kf_gelu_out", False))
+                  grad_target=direct_target(self.weight) if w is not self.weight else None)
 
 
 class SideStream:
@@ -165,6 +164,24 @@ class SideStream:
 
     _streams: Dict[int, torch.cuda.Stream] = {}
     _pending: list = []
+    # storage base pointer -> the event after the last side-stream kernel reading it: an in-place write
+    # on the main stream into such a storage (ops.linear's ``g.addmm_``: with no dropout the
+    # AddLayerNorm's skip gradient IS the gradient the side-stream weight gradient of FC2 reads) must
+    # wait for that event first (:meth:`before_write`)
+    _reads: Dict[int, torch.cuda.Event] = {}
+
+    @classmethod
+    def note_reads(cls, ev: torch.cuda.Event, *ts: torch.Tensor) -> None:
+        for t in ts:
+            cls._reads[t.untyped_storage().data_ptr()] = ev
+
+    @classmethod
+    def before_write(cls, t: torch.Tensor) -> None:
+        """Make the current stream wait for side-stream kernels still reading ``t``'s storage."""
+        if cls._reads:
+            ev = cls._reads.pop(t.untyped_storage().data_ptr(), None)
+            if ev is not None:
+                torch.cuda.current_stream().wait_event(ev)
 
     @classmethod
     def stream(cls, dev: torch.device) -> torch.cuda.Stream:
@@ -189,6 +206,7 @@ class SideStream:
             t.record_stream(side)  # main may free them while the side stream still reads
         out.record_stream(main)  # consumed on the main stream after the join
         cls._pending.append(ev)
+        cls.note_reads(ev, *inputs)
         return out
 
     @classmethod
@@ -199,6 +217,7 @@ class SideStream:
         for ev in cls._pending:
             s.wait_event(ev)
         cls._pending = []
+        cls._reads = {}
 
 
 class ImmediateSink:

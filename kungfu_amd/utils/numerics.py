@@ -38,14 +38,17 @@ def bn_param_grads_f64(dz: torch.Tensor, x: torch.Tensor, mean: torch.Tensor, in
     """(dgamma, dbeta) in float64 of ``z = act(gamma * (x - mean) * invstd + beta)``.
 
     ``kind``: ``"relu"`` -- act = ReLU, ``gate`` = the forward coefficients [scale(C); shift(C)]
-    (relu' recomputed as x * scale + shift > 0, as the kernels do, in f32); ``"mask"`` -- the
+    (relu' recomputed as x * scale + shift > 0, as the kernels do with one f32 FMA: its sign is the
+    sign of the exact value, computed here in f64 -- x is bf16, so x * scale is exact in f64 and the
+    one rounding of the sum keeps its sign; a separately rounded f32 product flips gates of
+    elements whose BN output rounds to about zero); ``"mask"`` -- the
     ReLU gate is the 1-bit mask ``gate`` (a BN + residual + ReLU tail); ``"plain"`` -- no
     activation (``dz`` already is the gradient at the BN output)."""
     xr, dr = _rows(x), _rows(dz).double()
     C = xr.shape[1]
     if kind == "relu":
-        sc, sh = gate[:C].float(), gate[C:2 * C].float()
-        on = torch.addcmul(sh, xr.float(), sc) > 0
+        sc, sh = gate[:C].float().double(), gate[C:2 * C].float().double()
+        on = xr.double() * sc + sh > 0
         dr = dr * on
     elif kind == "mask":
         dr = dr * unpack_mask(gate, xr.shape[0], C)

@@ -412,11 +412,13 @@ def test_stem_conv_matches_torch(H, shape, xdtype):
 
 
 @needs_gpu
-@pytest.mark.parametrize("shape", [(4, 64, 64), (2, 37, 50)])
+@pytest.mark.parametrize("shape", [(4, 64, 64), (2, 37, 50), (2, 224, 224)])
 def test_stem_block_fused_backward_matches_fp32(shape):
-    """conv7x7/2 -> BN -> ReLU -> MaxPool as one node (fused one-pass backward: pool gather,
-    BN backward and weight gradient, no BN input gradient): outputs, running stats and the
-    weight / gamma / beta gradients vs an f32 torch reference, no worse than the layered path."""
+    """conv7x7/2 -> BN -> ReLU -> MaxPool as one node (the weight-gradient kernel forms the BN
+    input gradient while staging: pool gather + ReLU gate + BN backward, never materialised):
+    outputs, running stats and the weight / gamma / beta gradients vs an f32 torch reference, no
+    worse than the layered path; gamma / beta bit-identical to the layered path (same statistics
+    kernels) and the weight gradient within bf16 rounding of it (the same f32 dx expression)."""
     import torch.nn.functional as F
 
     from kungfu_amd.ops.fused_bn import BatchNormAct2d
@@ -448,9 +450,10 @@ def test_stem_block_fused_backward_matches_fp32(shape):
     bn_f, w_f = make()
     y_f = stem_block(x, w_f, bn_f, _sums(bn_f, x.device))
     y_f.backward(dy.bfloat16().contiguous(memory_format=torch.channels_last))
-    # layered HIP path (stem conv node + BN-pool node)
+    # layered HIP path (stem conv node + BN-pool node), the statistics from the conv epilogue as well
     bn_l, w_l = make()
-    y_l = bn_l.forward_pool(stem_conv(x, w_l, None))
+    s_l = _sums(bn_l, x.device)
+    y_l = bn_l.forward_pool(stem_conv(x, w_l, s_l), sums=s_l)
     y_l.backward(dy.bfloat16().contiguous(memory_format=torch.channels_last))
 
     def r(a, b):
@@ -464,6 +467,8 @@ def test_stem_block_fused_backward_matches_fp32(shape):
                           (bn_f.bias.grad, bn_l.bias.grad, bn_r.bias.grad, "beta")]:
         ef, el = r(a, c), r(b, c)
         assert ef <= max(1.5 * el, 2e-2), (what, ef, el)
+    assert torch.equal(bn_f.weight.grad, bn_l.weight.grad) and torch.equal(bn_f.bias.grad, bn_l.bias.grad)
+    assert r(w_f.grad, w_l.grad) < 2e-3, r(w_f.grad, w_l.grad)
 
 
 @needs_gpu
@@ -1716,29 +1721,6 @@ def test_bert_layer_residual_link_matches_autograd_add(p, monkeypatch):
     for n in gp0:
         a, b = gp0[n], gp1[n]
         assert ((a - b).norm() / b.norm().clamp_min(1e-12)).item() < 2e-2, n
-
-
-@needs_gpu
-@pytest.mark.parametrize("n", [16384 * 3072, 8 * 1000 + 8, 8])
-def test_gelu_forward_matches_torch(n):
-    """norms.hip gelu_forward (one-exponential erf) vs torch's erf GELU in fp32: within one bf16
-    ulp of the exact value everywhere, identical to torch's rounding for > 99 % of the elements."""
-    import torch.nn.functional as F
-
-    from kungfu_amd._lib import hip
-
-    torch.manual_seed(5)
-    u = (torch.randn(n, device="cuda") * 3).bfloat16()
-    u[:8] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 8.0, -8.0, 30.0, -30.0], device="cuda").bfloat16()
-    y = hip().gelu_forward(u).float()
-    ref = F.gelu(u.float())
-    err = (y - ref).abs()
-    # within one bf16 ulp of the exact value (a value near a rounding midpoint may round the other way)
-    assert (err <= ref.abs() * 2 ** -7 + 1e-30).all(), err.max()
-    # the A-S erf's 1.5e-7 absolute error is a 1e-4 relative error of Phi in the far negative tail:
-    # 0.35 % of N(0, 9) inputs round to the neighbouring bf16 value (r4t20)
-    same = (y == ref.bfloat16().float()).float().mean().item()
-    assert same > 0.99, same
 
 
 @needs_gpu

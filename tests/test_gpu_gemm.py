@@ -19,7 +19,7 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("M,K,N", [(4096, 768, 2304), (1000, 768, 768), (2048, 3072, 768), (520, 256, 192)])
 @pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3])
-def test_gemm_plain_bias_gelu(M, K, N, variant):
+def test_gemm_plain_bias(M, K, N, variant):
     H = _hip()
     if variant in (0, 3) and N % 256:
         pytest.skip("256-wide tile")
@@ -32,11 +32,6 @@ def test_gemm_plain_bias_gelu(M, K, N, variant):
     assert y.shape == (M, N) and _rel(y, ref) < 1e-2
     yb = H.gemm(x, w, b, variant=variant)[0]
     assert _rel(yb, ref + b.float()) < 1e-2
-    g, u = H.gemm(x, w, b, True, variant=variant)
-    assert _rel(u, ref + b.float()) < 1e-2
-    # gelu applied to the bf16 pre-activation, as torch's bf16 F.gelu does
-    assert _rel(g, F.gelu(u.float())) < 1e-2
-    assert (g.float() - F.gelu(u.float())).abs().max().item() < 0.05
 
 
 @pytest.mark.parametrize("M,K,N", [(4096, 3072, 768), (1000, 768, 3072), (520, 768, 64)])
@@ -117,7 +112,10 @@ def test_gemm_nt_rejects_bad_shapes():
 def test_linear_gemm_path_matches_library_path():
     """ops.linear with KUNGFU_LINEAR_GEMM (forward + data gradient on gemm_nt, W^T from the
     per-step multi-tensor flip of the bf16 shadow weights) vs the hipBLASLt path: same loss and
-    flat gradients up to bf16 rounding, over two optimizer steps (the W^T cache must refresh)."""
+    flat gradients up to bf16 rounding, over two optimizer steps (the W^T cache must refresh).  lr 1e-4:
+    at 1e-3 the first AdamW step (a ~lr-sized move of EVERY weight, whatever its gradient) takes the loss
+    from 11.4 to 16.6 and the second-step comparison measures that jump's sensitivity to one bf16 ulp
+    (2e-3 apart, r6t10), not the GEMM path."""
     import kungfu_amd as kf
     from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
     from kungfu_amd.ops import linear as lin
@@ -132,7 +130,7 @@ def test_linear_gemm_path_matches_library_path():
             m = BertForPreTraining(layers=2).cuda()
             for l in m.layers:
                 l.dropout = 0.0
-            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
+            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-4),
                                                         named_parameters=m.named_parameters())
             enable_bf16_shadow(m, opt)
             g = torch.Generator(device="cuda").manual_seed(1)
@@ -302,83 +300,3 @@ def test_bert_vocab_head_and_tied_direct_landing_match_stock():
         for n in x:
             assert y[n].abs().sum().item() > 0, n
             assert _rel(y[n], x[n]) < 2e-2, (n, _rel(y[n], x[n]))
-
-
-def test_gemm_nt_gelu_matches_fp32():
-    """gemm_nt_gelu: u = a . b^T + bias and h = gelu(u) (erf, of the bf16 u) against fp32 references."""
-    H = _hip()
-    torch.manual_seed(6)
-    for M, K, N, bn in ((4096, 768, 3072, 256), (1000, 256, 768, 192), (300, 128, 256, 128)):
-        a = torch.randn(M, K, device="cuda").bfloat16()
-        b = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
-        bias = torch.randn(N, device="cuda").bfloat16()
-        u, h = H.gemm_nt_gelu(a, b, bias, bn)
-        ref = a.float() @ b.float().t() + bias.float()
-        assert _rel(u, ref) < 1e-2
-        assert (h.float() - F.gelu(u.float())).abs().max().item() < 2e-2
-        assert _rel(h, F.gelu(u.float())) < 5e-3
-
-
-def test_bert_fc1_gelu_gemm_matches_library_path():
-    """BERT with FC1 + GELU on one gemm.hip launch (ops.linear._GELU_FWD) vs hipBLASLt + torch GELU:
-    losses and the flat gradient over two AdamW steps."""
-    import kungfu_amd as kf
-    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
-    from kungfu_amd.ops import linear as lin
-    from kungfu_amd.parallel.mixed import enable_bf16_shadow
-
-    kf.init()
-
-    def run(on):
-        old, lin._GELU_FWD = lin._GELU_FWD, on
-        try:
-            torch.manual_seed(0)
-            m = BertForPreTraining(layers=2).cuda()
-            for l in m.layers:
-                l.dropout = 0.0
-            opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-3),
-                                                        named_parameters=m.named_parameters())
-            enable_bf16_shadow(m, opt)
-            g = torch.Generator(device="cuda").manual_seed(1)
-            batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
-            losses, grads = [], []
-            for _ in range(2):
-                opt.zero_grad()
-                with torch.autocast("cuda", dtype=torch.bfloat16):
-                    loss = pretraining_loss(m, batch)
-                loss.backward()
-                opt.reducer.synchronize()
-                grads.append(opt.space.flat_grad.clone())
-                losses.append(loss.item())
-                opt.step()
-            torch.cuda.synchronize()
-            return losses, grads
-        finally:
-            lin._GELU_FWD = old
-
-    la, ga = run(False)
-    lb, gb = run(True)
-    for x, y in zip(la, lb):
-        assert abs(x - y) < 2e-3 * abs(x), (la, lb)
-    for x, y in zip(ga, gb):
-        assert _rel(y, x) < 3e-2, _rel(y, x)
-
-
-@pytest.mark.parametrize("S", [128, 64])
-def test_attention_backward_bias_sums_match_colsum(S):
-    """attention_backward(..., bias_dtype): the dqkv column sums formed inside the kernel equal the
-    two-stage column sum of the returned dqkv (f32 rounding), and dqkv itself is unchanged."""
-    H = _hip()
-    torch.manual_seed(7)
-    B, NH = 6, 12
-    qkv = (torch.randn(B, S, 3 * NH * 64, device="cuda") * 0.5).bfloat16()
-    out, lse = H.attention_forward(qkv, NH, 0.125, 11, 0.1)
-    dout = torch.randn(B, S, NH * 64, device="cuda").bfloat16()
-    d0, none = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1)
-    assert none is None
-    d1, db = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1, torch.float32)
-    assert torch.equal(d0, d1)
-    ref = d1.float().reshape(-1, 3 * NH * 64).sum(0)
-    torch.testing.assert_close(db, ref, rtol=1e-4, atol=1e-3)
-    _, dbb = H.attention_backward(qkv, out, lse, dout, NH, 0.125, 11, 0.1, torch.bfloat16)
-    assert dbb.dtype == torch.bfloat16 and _rel(dbb, ref) < 1e-2

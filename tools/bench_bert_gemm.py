@@ -44,12 +44,11 @@ for name, cin, cout in SHAPES:
             err = (y.float() - ref.float()).abs().max().item()
             us = timeit(lambda: H_.gemm(x, w, variant=v))
             usb = timeit(lambda: H_.gemm(x, w, b, variant=v))
-            usg = timeit(lambda: H_.gemm(x, w, b, True, variant=v))
         except Exception as e:  # noqa: BLE001
             res.append("v%d:-" % v)
             continue
-        res.append("v%d:%.0fus/%.0fTF(bias %.0f gelu %.0f)%s" % (v, us, flop / us / 1e6, usb, usg,
-                                                              "" if err < 0.5 else "(err %.2f)" % err))
+        res.append("v%d:%.0fus/%.0fTF(bias %.0f)%s" % (v, us, flop / us / 1e6, usb,
+                                                    "" if err < 0.5 else "(err %.2f)" % err))
     u = torch.randn(T, cout, device="cuda").bfloat16()
     st = torch.zeros(H_.conv_stat_slots * 2 * cout, dtype=torch.float64, device="cuda")
     res.append("geluG:%.0fus" % timeit(lambda: H_.gemm(x, w, gelu_u=u, stats=st)))

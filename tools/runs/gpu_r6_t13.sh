@@ -1,0 +1,20 @@
+#!/bin/bash
+# r6 t13: hardware (v_cvt_pk_bf16_f32) vs integer-trick bf16 rounding, same tree otherwise (build_ab/*.so)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
+SO=kungfu_amd/_hip.cpython-310-x86_64-linux-gnu.so
+j() { python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["config"]["final_loss"])'; }
+for i in 1 2; do
+  for V in hw soft; do
+    cp build_ab/_hip_$V.so $SO
+    timeout -k 10 300 python bench.py --steps 30 --warmup 8 > $O/r6t13_${V}_$i.log 2>&1 || { tail -5 $O/r6t13_${V}_$i.log; exit 1; }
+    echo "r50 $V run $i: $(tail -1 $O/r6t13_${V}_$i.log | j)"
+  done
+done
+for V in hw soft; do
+  cp build_ab/_hip_$V.so $SO
+  timeout -k 10 300 python bench.py --model bert_base --optimizer gns --steps 20 --warmup 5 > $O/r6t13_bert_${V}.log 2>&1 || { tail -5 $O/r6t13_bert_${V}.log; exit 1; }
+  echo "bert $V: $(tail -1 $O/r6t13_bert_${V}.log | j)"
+done
+cp build_ab/_hip_hw.so $SO
