@@ -261,7 +261,6 @@ def main():
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
     p.add_argument("--bucket-mb", type=float, default=None)
-    p.add_argument("--stem-fused", type=int, default=1, help="TEMP A/B: fused stem backward node")
     p.add_argument("--bf16-shadow", type=int, default=1,
                    help="1: bf16 compute weights from one cast of the flat f32 master + direct bucket gradients")
     p.add_argument("--lr", type=float, default=0.01,
@@ -302,8 +301,6 @@ def main():
     if a.adam < 0:
         a.adam = 1 if bert else 0
     _setup_env()
-    from kungfu_amd.ops import stem as _stem_ops
-    _stem_ops.FUSED_BACKWARD = bool(a.stem_fused)
     if a.emulate_comm:
         if a.gpus not in (None, 1) or world_env not in (None, 1) or a.device != "cuda":
             print("bench.py: --emulate-comm models an N-rank job on ONE GPU", file=sys.stderr, flush=True)

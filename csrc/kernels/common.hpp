@@ -42,27 +42,20 @@ inline int grid_for(size_t n_vec) {
 
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(static_cast<uint32_t>(h) << 16); }
 
-// f32 -> bf16, round to nearest even, on gfx950's conversion instruction (v_cvt_pk_bf16_f32: one VALU
-// op for TWO values through pack_bf16x2, against 3-4 integer ops per value for the bit-trick rounding
-// these kernels used through round 5 -- the same bits for every finite input; NaN stays NaN)
-typedef __attribute__((ext_vector_type(2))) float kf_f32x2;
-typedef __attribute__((ext_vector_type(2))) __bf16 kf_bf16x2;
-#ifdef KFK_SOFT_BF16  // TEMP A/B
+// f32 -> bf16, round to nearest even (finite inputs; NaN payloads are not preserved).  Integer
+// rounding, NOT gfx950's v_cvt_pk_bf16_f32: the same bits for every finite input
+// (tools/diag/cvt_check.hip, 2^26 patterns), but the instruction measured far slower in the kernels
+// -- the NT GEMM with it 6.5x slower (101.7 vs 15.7 ms over 108 launches), ResNet-50 21.17 vs
+// 20.35 ms/step, BERT-base 26.8 vs 15.95 ms/step (tools/runs/gpu_r6_t13.sh / t14, same box).
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     uint32_t u = __float_as_uint(f);
     u += 0x7fffu + ((u >> 16) & 1u);
     return static_cast<uint16_t>(u >> 16);
 }
+// (lo, hi) -> one 32-bit word, lo in the low half
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
     return static_cast<uint32_t>(f32_to_bf16(lo)) | (static_cast<uint32_t>(f32_to_bf16(hi)) << 16);
 }
-#else
-__device__ __forceinline__ uint16_t f32_to_bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
-// (lo, hi) -> one 32-bit word, lo in the low half
-__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
-    return __builtin_bit_cast(uint32_t, __builtin_convertvector((kf_f32x2{lo, hi}), kf_bf16x2));
-}
-#endif
 
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
     _Float16 x;

@@ -58,7 +58,10 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
-// two f32 -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32 on gfx950
+// two f32 -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32 on gfx950.  Shadows
+// common.hpp's integer-rounding pack_bf16x2 inside this file: here (stem forward epilogue, the BNP dx)
+// the instruction measured faster (r6t15: ResNet-50 20.24-20.27 vs 20.35-20.42 ms/step with attention /
+// stem / stem3 on it), while in gemm.hip's epilogues it measured 6.5x slower (r6t14)
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
     const bf16x2 v = __builtin_convertvector(f32x2{a, b}, bf16x2);
     return __builtin_bit_cast(uint32_t, v);
@@ -681,12 +684,28 @@ __device__ __forceinline__ void unpack8f(const uint4 &v, float (&f)[8]) {
     }
 }
 
+// 16-bit lane masks of the argmax bytes equal to kk: for the 4 bytes of a (channels 4 q .. 4 q + 3),
+// lo = [ch 0 | ch 1] and hi = [ch 2 | ch 3] as 0xffff / 0 halves (SWAR zero-byte test of a ^ kk, then
+// v_perm_b32's sign-replicating selectors 8..11 spread each byte's flag; ~8 ops for 4 channels against
+// 8 compares + 8 selects)
+__device__ __forceinline__ void argmax_masks(uint32_t a, uint32_t kk, uint32_t &lo, uint32_t &hi) {
+    const uint32_t x = a ^ (kk * 0x01010101u);
+    const uint32_t z = ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);  // 0x80 in each zero byte
+    const uint32_t zs = z << 8;  // flags of bytes 0 / 2 at bits 15 / 31
+    // perm(src0 = z, src1 = zs): sel 8 = zs bit 15 (byte 0), 9 = zs bit 31 (byte 2), 10 = z bit 15 (byte 1),
+    // 11 = z bit 31 (byte 3)
+    lo = __builtin_amdgcn_perm(z, zs, 0x0a0a0808u);
+    hi = __builtin_amdgcn_perm(z, zs, 0x0b0b0909u);
+}
+
 // g = the pooled gradient gathered back to conv-output pixel (h, w), 8 channels cv * 8.., from the LDS
 // ring: the windows (oh, ow) with oh in {h >> 1, (h + 1) >> 1} and ow in {w >> 1, (w + 1) >> 1}, in
 // bn.hip PoolGrad's order, each adding its dyp where its argmax byte names (h, w).  PoolGrad adds a 0
 // for a window that cannot cover (h, w); here such windows are skipped -- at compile time for the
-// column (ODDW: w is odd, so two columns) and by the wave-uniform row parity (HODD) -- which gives the
+// column (ODDW: w is odd, so two columns) and by the wave-uniform row parity (hodd) -- which gives the
 // same sum (adding +0 to a sum that starts at +0 changes nothing): 2.25 windows per pixel, not 4.
+// The window offset of (h, w) in window (oh, ow), kk = (h + 1 - 2 oh) * 3 + (w + 1 - 2 ow), is a
+// constant per (row parity, window row, column parity, window column).
 template <bool ODDW>
 __device__ __forceinline__ void pool_grad8(const uint8_t *pool, int PH, int PW, int h, bool hodd, int w, int cv,
                                            float (&g)[8]) {
@@ -698,23 +717,24 @@ __device__ __forceinline__ void pool_grad8(const uint8_t *pool, int PH, int PW, 
         const int oh = oh_lo + rr;
         if (rr == 1 && !(hodd && oh < PH)) break;  // wave-uniform
         const uint8_t *slot = pool + (oh & 1) * kPoolSlot;
+        const uint32_t krow = hodd ? (rr ? 0u : 6u) : 3u;  // 3 (h + 1 - 2 oh)
 #pragma unroll
         for (int cc = 0; cc < (ODDW ? 2 : 1); ++cc) {
             int ow = ow_lo + cc;
             // the last odd column of an even-width map has no right window: read window ow_lo, never match
             const bool ok = cc == 0 || ow < PW;
-            const uint32_t kk = ok ? static_cast<uint32_t>((h + 1 - 2 * oh) * 3 + (w + 1 - 2 * ow)) : 0xffu;
+            const uint32_t kk = ok ? krow + (ODDW ? (cc ? 0u : 2u) : 1u) : 0xffu;
             ow = ok ? ow : ow_lo;
             const int e = ow * 8 + cv;
             const uint4 dv = *reinterpret_cast<const uint4 *>(slot + e * 16);
             const uint2 am = *reinterpret_cast<const uint2 *>(slot + kPoolD + e * 8);
+            uint32_t m0, m1, m2, m3;
+            argmax_masks(am.x, kk, m0, m1);
+            argmax_masks(am.y, kk, m2, m3);
             float d[8];
-            unpack8f(dv, d);
+            unpack8f(make_uint4(dv.x & m0, dv.y & m1, dv.z & m2, dv.w & m3), d);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint32_t ak = ((k < 4 ? am.x : am.y) >> (8 * (k & 3))) & 0xffu;
-                g[k] += ak == kk ? d[k] : 0.f;
-            }
+            for (int k = 0; k < 8; ++k) g[k] += d[k];
         }
     }
 }

@@ -492,6 +492,52 @@ def test_linear_side_stream_wgrad_joined_without_bucket_engine(monkeypatch):
 
 
 @needs_gpu
+def test_bert_side_stream_wgrad_vs_inplace_residual_gradient(monkeypatch):
+    """Round 6 race: with no dropout, an AddLayerNorm's skip gradient IS the gradient FC2's side-stream
+    weight gradient reads, and FC1's backward adds its data gradient into it in place (``g.addmm_``).
+    ``SideStream.before_write`` makes that write wait for the side-stream readers of the storage.
+    Without it, FC2's weight gradients differed by 25-29 % from the single-stream run
+    (tools/diag/linear_gemm_ab.py, r6t12; 6 % of the whole flat gradient).  Here: flat gradients over
+    two AdamW steps equal with and without the side stream, up to the embedding scatter-add's f32
+    atomic-order noise (1e-5 / 1e-3 relative at steps 1 / 2)."""
+    import kungfu_amd as kf
+    from kungfu_amd.models.bert import BertForPreTraining, pretraining_loss, synthetic_pretraining_batch
+    from kungfu_amd.ops import linear as lin
+    from kungfu_amd.parallel import mixed
+
+    kf.init()
+
+    def run(side):
+        monkeypatch.setattr(lin, "_WGRAD_SIDE", side)
+        torch.manual_seed(0)
+        m = BertForPreTraining(layers=2).cuda()
+        for l in m.layers:
+            l.dropout = 0.0
+        opt = kf.optimizers.SynchronousSGDOptimizer(torch.optim.AdamW(m.parameters(), lr=1e-4),
+                                                    named_parameters=m.named_parameters())
+        mixed.enable_bf16_shadow(m, opt)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        batch = synthetic_pretraining_batch(16, 128, device="cuda", generator=g)
+        grads = []
+        for _ in range(2):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = pretraining_loss(m, batch)
+            loss.backward()
+            opt.reducer.synchronize()
+            grads.append(opt.space.flat_grad.clone())
+            opt.step()
+        torch.cuda.synchronize()
+        mixed.disable(m)
+        return grads
+
+    g0, g1 = run(False), run(True)
+    for a, b, tol in zip(g0, g1, (1e-5, 1e-3)):
+        rel = ((a - b).norm() / a.norm()).item()
+        assert rel < tol, rel
+
+
+@needs_gpu
 def test_linear_direct_f32_wgrad_into_flat_slot(monkeypatch):
     """bf16-shadow linear layers (S-SGD engine, bucket reducer): the split-K weight gradient
     reduced straight into the flat f32 gradient slot (ops/linear.py, sink.put_direct) equals the
