@@ -257,7 +257,11 @@ def main():
     p.add_argument("--optimizer", default="ssgd", choices=["ssgd", "sma", "pair", "ada", "gns", "local"])
     p.add_argument("--force-comm", type=int, default=1,
                    help="1: S-SGD buckets go through the communicator even with one GPU (RCCL 1-rank all-reduce)")
-    p.add_argument("--comm-dtype", default="f32", choices=["f32", "bf16"], help="gradient dtype on the wire")
+    p.add_argument("--comm-dtype", default="auto", choices=["auto", "f32", "bf16"],
+                   help="gradient dtype on the wire (S-SGD / GNS).  auto: bf16 when gradients cross ranks on GPUs "
+                        "(N > 1, or the --emulate-comm model of it), f32 otherwise -- emulated 8 ranks: BERT-base "
+                        "18.41-18.55 -> 17.26-17.29 ms/step, ResNet-50 21.09-21.20 -> 21.06-21.08 "
+                        "(profiles/r6_multirank_defaults.md)")
     p.add_argument("--overlap", type=int, default=1, help="S-SGD: all-reduce buckets during backward")
     p.add_argument("--fused-bn", type=int, default=-1, help="1: HIP fused BN(+add)+ReLU; -1: auto")
     p.add_argument("--bucket-mb", type=float, default=None)
@@ -354,6 +358,8 @@ def main():
     else:
         base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
         opt_desc = "SGD momentum=0.9 wd=1e-4"
+    if a.comm_dtype == "auto":
+        a.comm_dtype = "bf16" if cuda and (size > 1 or a.emulate_comm) else "f32"
     comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else None
     if a.optimizer == "ssgd":
         opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),
@@ -362,7 +368,8 @@ def main():
     elif a.optimizer == "gns":  # S-SGD + gradient-noise-scale monitor (K5 every step)
         opt = kf.optimizers.MonitorGradientNoiseScaleOptimizer(base, device_batch_size=a.batch,
                                                                named_parameters=model.named_parameters(),
-                                                               monitor_single=bool(a.force_comm))
+                                                               monitor_single=bool(a.force_comm),
+                                                               comm_dtype=comm_dtype)
     elif a.optimizer == "local":  # diagnostics only: fused flat SGD, no gradient exchange
         from kungfu_amd.optimizers.core import KungFuOptimizer
 
@@ -414,12 +421,14 @@ def main():
     if a.graph < 0:
         # ResNet-50 / Inception-v3 with S-SGD.  N = 1: one whole-step graph.  N > 1 (and the 1-GPU
         # model of it, --emulate-comm): graph SEGMENTS cut at every bucket launch with the collectives
-        # issued eagerly between replays (parallel/graphs.py; KUNGFU_GRAPH_SEGMENTED) -- emulated 8-rank
-        # ResNet-50 21.15-21.18 vs eager 21.19-21.22 ms/step (r5t6; one graph with the collectives
-        # inside: 21.55-21.59), and the host no longer enqueues ~460-900 kernels per rank per step
-        # (Inception-v3: 17.4 ms of host time per 20.9 ms step eagerly, r5t5).  BERT: replay measured
+        # issued eagerly between replays (parallel/graphs.py) for ResNet-50 -- emulated 8-rank
+        # 21.15-21.18 vs eager 21.19-21.22 ms/step (r5t6; one graph with the collectives inside:
+        # 21.55-21.59) -- but EAGER for Inception-v3, whose segments measured slower (emulated 8-rank
+        # 20.45 vs 20.32-20.34 ms, r6t11; r5: 20.92-20.95 vs 20.81-20.83).  BERT: replay measured
         # 2.4 % slower (r4t31); VGG-16: +0.4 % only (r4_host_overhead.md)
-        a.graph = 0 if (bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local")) else 1
+        multi = size > 1 or bool(a.emulate_comm)
+        a.graph = 0 if (bert or a.model == "vgg16" or a.optimizer not in ("ssgd", "local")
+                        or (a.model == "inception_v3" and multi)) else 1
     if a.graph and cuda:
         from kungfu_amd.parallel.graphs import GraphedStep
 

@@ -52,8 +52,11 @@ def _gns_update_host(sq_small: float, sq_big: float, b: float, B: float, alpha: 
 class _GradientNoiseScale(_SynchronousSGD):
     def __init__(self, optimizer, device_batch_size: int, named_parameters=None, monitor_interval: int = 1,
                  alpha: float = 0.6, verbose: bool = False, fused: bool = True, monitor_single: bool = False,
-                 flat=None):
-        super().__init__(optimizer, named_parameters, op="avg", fused=fused, force_comm=monitor_single, flat=flat)
+                 flat=None, comm_dtype: Optional[torch.dtype] = None):
+        # comm_dtype: the gradient dtype on the wire (sync_sgd.SynchronousSGDOptimizer); |g_big|^2 is
+        # then taken of the bf16-averaged gradient (a ~2^-9 relative perturbation of the estimate)
+        super().__init__(optimizer, named_parameters, op="avg", fused=fused, force_comm=monitor_single, flat=flat,
+                         comm_dtype=comm_dtype)
         self.device_batch_size = float(device_batch_size)
         self.interval = max(1, int(monitor_interval))
         self.alpha = alpha
@@ -136,9 +139,10 @@ class _GradientNoiseScale(_SynchronousSGD):
 def MonitorGradientNoiseScaleOptimizer(optimizer, device_batch_size: int, named_parameters=None,
                                        monitor_interval: int = 1, alpha: float = 0.6, verbose: bool = False,
                                        fused: bool = True, name=None, use_locking=False, monitor_single: bool = False,
-                                       flat=None):
+                                       flat=None, comm_dtype: Optional[torch.dtype] = None):
     return _GradientNoiseScale(optimizer, device_batch_size, named_parameters, monitor_interval=monitor_interval,
-                               alpha=alpha, verbose=verbose, fused=fused, monitor_single=monitor_single, flat=flat)
+                               alpha=alpha, verbose=verbose, fused=fused, monitor_single=monitor_single, flat=flat,
+                               comm_dtype=comm_dtype)
 
 
 class _GradVariance(_SynchronousSGD):
