@@ -203,6 +203,273 @@ __global__ void bn_fin_desc_kernel(const BNFin *__restrict__ fp, double *sums, i
     }
 }
 
+// The epilogue of one output tile (shared by conv_kernel and conv_rows_kernel): the f32
+// accumulators (C^T fragments: lane -> pixel row lane & 15, channels 4 (lane >> 4) + r) go through
+// the LDS as a bf16 tile, then 16-byte row stores with the fused epilogue applied on the way; the
+// per-channel statistics accumulate in s1 / s2 (this thread's fixed 8-channel group).  The caller
+// has waited for its LDS-DMA and passed a barrier (the LDS is reused).
+template <int WM, int WN, int TM, int TN, int EPI>
+__device__ __forceinline__ void conv_store_tile(const f32x4 (&acc)[TM][TN], uint8_t *lds, uint16_t *__restrict__ y,
+                                                const Geo &g, const EpiArgs &ea, int m0, int n0, int tid,
+                                                float (&s1)[8], float (&s2)[8]) {
+    constexpr int WTM = 16 * TM, WTN = 16 * TN;
+    constexpr int BM = WTM * WM, BN = WTN * WN, NT = 64 * WM * WN;
+    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
+    constexpr bool GATE = (EPI & kEpiGate) != 0;
+    constexpr bool GELUG = (EPI & kEpiGeluGrad) != 0;
+    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias)) != 0;
+    constexpr int NSUM = (GATE || GELUG) ? 1 : 2;  // the gates need sum(y) only (a bias gradient)
+    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
+    constexpr int GROUPS = NT / VPR;
+    constexpr int ITER = BM * VPR / NT;  // 16-byte output vectors per thread per tile
+    static_assert(ITER * NT == BM * VPR, "whole store iterations");
+    constexpr bool LD_OLD = (EPI & kEpiAccum) != 0;
+    constexpr bool LD_BX = GATE || GELUG || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int cv = tid % (BN / 8);  // the epilogue's fixed 8-channel group of this thread
+    (void)STATS, (void)NSUM, (void)GROUPS, (void)LD_OLD, (void)LD_BX, (void)lane, (void)wm, (void)wn, (void)CROW,
+        (void)BIAS, (void)ITER;
+
+    // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
+    // C^T map (16x16): pixel row = lane & 15, channel col = (lane >> 4) * 4 + r.
+    float bcol[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            bcol[j][r] = 0.f;
+            if constexpr (BIAS) {
+                const int c = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
+                if (c < g.K) bcol[j][r] = bf16_to_f32(ea.bias[c]);
+            }
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int row = wm * WTM + i * 16 + (lane & 15);
+            const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
+            uint32_t h[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = acc[i][j][r];
+                if constexpr (BIAS) v += bcol[j][r];
+                if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
+                h[r] = f32_to_bf16(v);
+            }
+            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        }
+    __syncthreads();
+    // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
+    // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
+    static_assert(NT % VPR == 0, "fixed channel group per thread");
+    // The global reads of the epilogue (old value, BN input, masks) of U rows are all issued
+    // before any of them is consumed: one load round trip per U rows instead of per row (the
+    // loop is otherwise a chain of dependent HBM latencies -- the stores to y may alias later
+    // reads as far as the compiler knows).
+    // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
+    // the 256x256 tile, whose 16 coefficient registers would otherwise spill).  (Round 6: issuing
+    // every row's epilogue reads behind the prologue staging instead -- operands in registers when
+    // the K loop ends -- took the 4-wave tiles to one wave per SIMD and spilled the 8-wave ones:
+    // ResNet-50 20.40 -> 21.45 ms/step, profiles/r6_conv_pmc.md.)
+    constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
+    const bool col_ok = n0 + cv * 8 < g.K;  // this thread's 8 channels exist (Cout % BN != 0)
+    float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
+    if constexpr ((EPI & kEpiBwdCoef) != 0) {
+        if (col_ok)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            sc[k] = ea.fcoef[n0 + cv * 8 + k];
+            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
+        }
+    }
+    for (int it0 = 0; it0 < ITER; it0 += U) {
+        uint4 val[U], old[U], bxv[U];
+        uint32_t amb[U], bmb[U];
+        int64_t ee[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int v = tid + (it0 + u) * NT;
+            const int row = v / VPR;
+            const int m = m0 + row;
+            ok[u] = m < g.M && col_ok;
+            int pix = m;
+            if (g.scat) {
+                const int t = m / g.OW, ow = m - t * g.OW;
+                const int n = t / g.OH, a = t - n * g.OH;
+                pix = (n * g.dh + 2 * a + g.pr) * g.dw + 2 * ow + g.pc;
+            }
+            const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
+            ee[u] = e;
+            val[u] = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
+            old[u] = bxv[u] = make_uint4(0u, 0u, 0u, 0u);
+            amb[u] = 0u;
+            bmb[u] = 0xffu;
+            if (ok[u]) {
+                if constexpr (LD_OLD) {
+                    bool here = true;
+                    if constexpr ((EPI & kEpiAccEven) != 0) {
+                        // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
+                        const int t = m / g.OW, ow = m - t * g.OW;
+                        here = ((ow | (t % g.OH)) & 1) == 0;
+                    }
+                    if (here) old[u] = *reinterpret_cast<const uint4 *>(y + e);
+                    if constexpr ((EPI & kEpiAccMask) != 0) amb[u] = ea.amask[e >> 3];  // 8 channels, 8-aligned e
+                }
+                if constexpr (LD_BX) bxv[u] = *reinterpret_cast<const uint4 *>(ea.bx + e);
+                if constexpr ((EPI & kEpiBwdBits) != 0) bmb[u] = ea.bmask[e >> 3];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            uint4 v = val[u];
+            if constexpr (LD_OLD) {
+                uint4 o0 = old[u];
+                if constexpr ((EPI & kEpiAccMask) != 0) {
+                    const uint32_t mb = amb[u];
+                    uint32_t *ow = reinterpret_cast<uint32_t *>(&o0);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        ow[k] &= (((mb >> (2 * k)) & 1u) ? 0xffffu : 0u) | (((mb >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
+                }
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(&v);
+                const uint32_t *b = reinterpret_cast<const uint32_t *>(&o0);
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float lo = bf16_to_f32(static_cast<uint16_t>(a[k] & 0xffffu)) +
+                                     bf16_to_f32(static_cast<uint16_t>(b[k] & 0xffffu));
+                    const float hi = bf16_to_f32(static_cast<uint16_t>(a[k] >> 16)) +
+                                     bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
+                    o[k] = pack_bf16x2(lo, hi);
+                }
+                v = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            if constexpr (GATE) {
+                // gradient of a ReLU output: keep y where bx > 0 (NaN passes), sum the kept values
+                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bxv[u]);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
+                                          (!(__uint_as_float(bw[k] & 0xffff0000u) <= 0.f) ? 0xffff0000u : 0u);
+                    vw[k] &= keep;
+                }
+            }
+            if constexpr (GELUG) {
+                // gradient of gelu(u): dy * (Phi(u) + u * phi(u)), torch's GeluBackward in f32
+                float f[8], uf[8];
+                unpack_bf16x8(v, f);
+                unpack_bf16x8(bxv[u], uf);
+                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    float d[2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float t = uf[2 * k + h];
+                        const float cdf = 0.5f * (1.f + erff(t * 0.70710678118654752f));
+                        const float pdf = __expf(-0.5f * t * t) * 0.39894228040143268f;
+                        d[h] = f[2 * k + h] * (cdf + t * pdf);
+                    }
+                    vw[k] = pack_bf16x2(d[0], d[1]);
+                }
+            }
+            *reinterpret_cast<uint4 *>(y + ee[u]) = v;
+            if constexpr (STATS) {
+                float f[8];
+                unpack_bf16x8(v, f);
+                if constexpr (GATE || GELUG) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s1[k] += f[k];
+                } else if constexpr ((EPI & kEpiFwdStats) != 0) {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        s1[k] += f[k];
+                        s2[k] += f[k] * f[k];
+                    }
+                } else {
+                    // BN backward sums of the BN whose input is ea.bx:
+                    //   dz = grad * relu'(.) ; s1 += dz ; s2 += dz * x
+                    float xv[8];
+                    unpack_bf16x8(bxv[u], xv);
+                    const uint32_t mbits = bmb[u];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        bool on;
+                        if constexpr ((EPI & kEpiBwdBits) != 0) on = (mbits >> k) & 1u;
+                        else on = xv[k] * sc[k] + sh[k] > 0.f;
+                        const float dz = on ? f[k] : 0.f;
+                        s1[k] += dz;
+                        s2[k] += dz * xv[k];
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Per-channel statistics of a workgroup (s1 / s2 of every thread) -> f64 atomics into stats slot
+// `slot_sel % kStatSlots`, then the optional in-launch finalize.
+template <int WM, int WN, int TM, int TN, int EPI, int LDS_BYTES>
+__device__ __forceinline__ void conv_stats_flush(uint8_t *lds, const Geo &g, const EpiArgs &ea, int n0, int tid,
+                                                 const float (&s1)[8], const float (&s2)[8], int slot_sel, int nwg,
+                                                 int orig) {
+    constexpr int WTM = 16 * TM, WTN = 16 * TN;
+    constexpr int BM = WTM * WM, BN = WTN * WN, NT = 64 * WM * WN;
+    constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
+    constexpr bool GATE = (EPI & kEpiGate) != 0;
+    constexpr bool GELUG = (EPI & kEpiGeluGrad) != 0;
+    constexpr bool BIAS = (EPI & (kEpiBiasRelu | kEpiBias)) != 0;
+    constexpr int NSUM = (GATE || GELUG) ? 1 : 2;  // the gates need sum(y) only (a bias gradient)
+    constexpr int VPR = BN / 8;  // 16-byte vectors per C row
+    constexpr int GROUPS = NT / VPR;
+    constexpr int ITER = BM * VPR / NT;  // 16-byte output vectors per thread per tile
+    static_assert(ITER * NT == BM * VPR, "whole store iterations");
+    constexpr bool LD_OLD = (EPI & kEpiAccum) != 0;
+    constexpr bool LD_BX = GATE || GELUG || (EPI & (kEpiBwdCoef | kEpiBwdBits)) != 0;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int wm = wave / WN, wn = wave % WN;
+    const int cv = tid % (BN / 8);  // the epilogue's fixed 8-channel group of this thread
+    (void)STATS, (void)NSUM, (void)GROUPS, (void)LD_OLD, (void)LD_BX, (void)lane, (void)wm, (void)wn, (void)CROW,
+        (void)BIAS, (void)ITER;
+    {
+        // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
+        float *red = reinterpret_cast<float *>(lds);
+        __syncthreads();
+        const int grp = tid / VPR;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            red[grp * BN + cv * 8 + k] = s1[k];
+            if constexpr (NSUM == 2) red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
+        }
+        __syncthreads();
+        for (int col = tid; col < BN; col += NT) {
+            double t1 = 0, t2 = 0;
+#pragma unroll 4
+            for (int p = 0; p < GROUPS; ++p) {
+                t1 += red[p * BN + col];
+                if constexpr (NSUM == 2) t2 += red[(GROUPS + p) * BN + col];
+            }
+            double *sl = ea.stats + (slot_sel % kStatSlots) * 2 * g.K;  // spread atomics over slots
+            if (n0 + col < g.K) {
+                atomicAdd(sl + n0 + col, t1);
+                if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
+            }
+        }
+        if constexpr (NSUM == 2) {
+            if (ea.fin != nullptr)
+                bn_finalize_last(ea.fin, ea.stats, g.K, nwg, orig, tid, NT, reinterpret_cast<double *>(lds),
+                                 LDS_BYTES / 8 - 2);
+        }
+    }
+}
+
 // WM x WN waves (wave tile 64x64), STAGES-deep global_load_lds ring.
 // KS = 3 or 1: square window; KS = 0xHW (>= 16): an H x W window (Inception's 1x7 / 7x1 / 1x3 /
 // 3x1 / 5x5, and the parity phases of a stride-2 3x3 data gradient, launch_conv_dgrad_s2).  The
@@ -442,216 +709,263 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     }
     wait_vmcnt<0>();
     __syncthreads();  // all ds_reads of the last tile done before the LDS is reused
-
-    // ---- epilogue: bf16 tile through LDS, then 16-byte row stores
-    // C^T map (16x16): pixel row = lane & 15, channel col = (lane >> 4) * 4 + r.
-    float bcol[TN][4];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            bcol[j][r] = 0.f;
-            if constexpr (BIAS) {
-                const int c = n0 + wn * WTN + j * 16 + (lane >> 4) * 4 + r;
-                if (c < g.K) bcol[j][r] = bf16_to_f32(ea.bias[c]);
-            }
-        }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int row = wm * WTM + i * 16 + (lane & 15);
-            const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
-            uint32_t h[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float v = acc[i][j][r];
-                if constexpr (BIAS) v += bcol[j][r];
-                if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
-                h[r] = f32_to_bf16(v);
-            }
-            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        }
-    __syncthreads();
-    // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
-    // multiple of VPR), so per-channel statistics accumulate in registers across its rows.
-    static_assert(NT % VPR == 0, "fixed channel group per thread");
-    // The global reads of the epilogue (old value, BN input, masks) of U rows are all issued
-    // before any of them is consumed: one load round trip per U rows instead of per row (the
-    // loop is otherwise a chain of dependent HBM latencies -- the stores to y may alias later
-    // reads as far as the compiler knows).
-    // U rows in flight (none to batch without global reads; 2 for the BN-coefficient epilogue on
-    // the 256x256 tile, whose 16 coefficient registers would otherwise spill).  (Round 6: issuing
-    // every row's epilogue reads behind the prologue staging instead -- operands in registers when
-    // the K loop ends -- took the 4-wave tiles to one wave per SIMD and spilled the 8-wave ones:
-    // ResNet-50 20.40 -> 21.45 ms/step, profiles/r6_conv_pmc.md.)
-    constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
-    const bool col_ok = n0 + cv * 8 < g.K;  // this thread's 8 channels exist (Cout % BN != 0)
-    float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
-    if constexpr ((EPI & kEpiBwdCoef) != 0) {
-        if (col_ok)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[k] = ea.fcoef[n0 + cv * 8 + k];
-            sh[k] = ea.fcoef[g.K + n0 + cv * 8 + k];
-        }
-    }
-    for (int it0 = 0; it0 < ITER; it0 += U) {
-        uint4 val[U], old[U], bxv[U];
-        uint32_t amb[U], bmb[U];
-        int64_t ee[U];
-        bool ok[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int v = tid + (it0 + u) * NT;
-            const int row = v / VPR;
-            const int m = m0 + row;
-            ok[u] = m < g.M && col_ok;
-            int pix = m;
-            if (g.scat) {
-                const int t = m / g.OW, ow = m - t * g.OW;
-                const int n = t / g.OH, a = t - n * g.OH;
-                pix = (n * g.dh + 2 * a + g.pr) * g.dw + 2 * ow + g.pc;
-            }
-            const int64_t e = static_cast<int64_t>(pix) * g.K + n0 + cv * 8;
-            ee[u] = e;
-            val[u] = *reinterpret_cast<const uint4 *>(lds + row * CROW + cv * 16);
-            old[u] = bxv[u] = make_uint4(0u, 0u, 0u, 0u);
-            amb[u] = 0u;
-            bmb[u] = 0xffu;
-            if (ok[u]) {
-                if constexpr (LD_OLD) {
-                    bool here = true;
-                    if constexpr ((EPI & kEpiAccEven) != 0) {
-                        // only the even pixels hold a partial sum (a stride-2 1x1 data gradient)
-                        const int t = m / g.OW, ow = m - t * g.OW;
-                        here = ((ow | (t % g.OH)) & 1) == 0;
-                    }
-                    if (here) old[u] = *reinterpret_cast<const uint4 *>(y + e);
-                    if constexpr ((EPI & kEpiAccMask) != 0) amb[u] = ea.amask[e >> 3];  // 8 channels, 8-aligned e
-                }
-                if constexpr (LD_BX) bxv[u] = *reinterpret_cast<const uint4 *>(ea.bx + e);
-                if constexpr ((EPI & kEpiBwdBits) != 0) bmb[u] = ea.bmask[e >> 3];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            uint4 v = val[u];
-            if constexpr (LD_OLD) {
-                uint4 o0 = old[u];
-                if constexpr ((EPI & kEpiAccMask) != 0) {
-                    const uint32_t mb = amb[u];
-                    uint32_t *ow = reinterpret_cast<uint32_t *>(&o0);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k)
-                        ow[k] &= (((mb >> (2 * k)) & 1u) ? 0xffffu : 0u) | (((mb >> (2 * k + 1)) & 1u) ? 0xffff0000u : 0u);
-                }
-                const uint32_t *a = reinterpret_cast<const uint32_t *>(&v);
-                const uint32_t *b = reinterpret_cast<const uint32_t *>(&o0);
-                uint32_t o[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float lo = bf16_to_f32(static_cast<uint16_t>(a[k] & 0xffffu)) +
-                                     bf16_to_f32(static_cast<uint16_t>(b[k] & 0xffffu));
-                    const float hi = bf16_to_f32(static_cast<uint16_t>(a[k] >> 16)) +
-                                     bf16_to_f32(static_cast<uint16_t>(b[k] >> 16));
-                    o[k] = pack_bf16x2(lo, hi);
-                }
-                v = make_uint4(o[0], o[1], o[2], o[3]);
-            }
-            if constexpr (GATE) {
-                // gradient of a ReLU output: keep y where bx > 0 (NaN passes), sum the kept values
-                const uint32_t *bw = reinterpret_cast<const uint32_t *>(&bxv[u]);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t keep = (!(__uint_as_float(bw[k] << 16) <= 0.f) ? 0xffffu : 0u) |
-                                          (!(__uint_as_float(bw[k] & 0xffff0000u) <= 0.f) ? 0xffff0000u : 0u);
-                    vw[k] &= keep;
-                }
-            }
-            if constexpr (GELUG) {
-                // gradient of gelu(u): dy * (Phi(u) + u * phi(u)), torch's GeluBackward in f32
-                float f[8], uf[8];
-                unpack_bf16x8(v, f);
-                unpack_bf16x8(bxv[u], uf);
-                uint32_t *vw = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    float d[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const float t = uf[2 * k + h];
-                        const float cdf = 0.5f * (1.f + erff(t * 0.70710678118654752f));
-                        const float pdf = __expf(-0.5f * t * t) * 0.39894228040143268f;
-                        d[h] = f[2 * k + h] * (cdf + t * pdf);
-                    }
-                    vw[k] = pack_bf16x2(d[0], d[1]);
-                }
-            }
-            *reinterpret_cast<uint4 *>(y + ee[u]) = v;
-            if constexpr (STATS) {
-                float f[8];
-                unpack_bf16x8(v, f);
-                if constexpr (GATE || GELUG) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s1[k] += f[k];
-                } else if constexpr ((EPI & kEpiFwdStats) != 0) {
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        s1[k] += f[k];
-                        s2[k] += f[k] * f[k];
-                    }
-                } else {
-                    // BN backward sums of the BN whose input is ea.bx:
-                    //   dz = grad * relu'(.) ; s1 += dz ; s2 += dz * x
-                    float xv[8];
-                    unpack_bf16x8(bxv[u], xv);
-                    const uint32_t mbits = bmb[u];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        bool on;
-                        if constexpr ((EPI & kEpiBwdBits) != 0) on = (mbits >> k) & 1u;
-                        else on = xv[k] * sc[k] + sh[k] > 0.f;
-                        const float dz = on ? f[k] : 0.f;
-                        s1[k] += dz;
-                        s2[k] += dz * xv[k];
-                    }
-                }
-            }
-        }
-    }
+    conv_store_tile<WM, WN, TM, TN, EPI>(acc, lds, y, g, ea, m0, n0, tid, s1, s2);
     }  // m-tile loop
-    if constexpr (STATS) {
-        // reduce the NT / VPR threads of each channel group, then f64 atomics into a slot
-        float *red = reinterpret_cast<float *>(lds);
-        __syncthreads();
-        const int grp = tid / VPR;
+    if constexpr (STATS) conv_stats_flush<WM, WN, TM, TN, EPI, LDS_BYTES>(lds, g, ea, n0, tid, s1, s2, mt_last + wg, nwg, orig);
+}
+
+// Row-image 3x3 / stride-1 / pad-1 convolution (forward, and the stride-1 data gradient on
+// flipped weights): the same GEMM as conv_kernel<3>, M = output pixels, N = Cout, K = 9 * Cin, but
+// the A operand is staged ONCE per 64-channel chunk as an image instead of once per tap.
+//   * Padded pixel index G(n, ihp, iwp) = (n (H + 2) + ihp)(W + 2) + iwp (ihp = ih + 1, iwp = iw + 1):
+//     output pixel m = (n, oh, ow) reads, at tap (kh, kw), the input at G(m) + kh (W + 2) + kw with
+//     G(m) = (n (H + 2) + oh)(W + 2) + ow.  A tile of BM consecutive output pixels therefore reads one
+//     CONTIGUOUS range of padded indices, [G(m0), G(m_last) + 2 (W + 2) + 2] (image boundaries
+//     included: their pad rows are part of the range and read zeros).
+//   * That range is staged as IMG rows of 128 bytes (one pixel's 64 channels; padding pixels and
+//     rows past the range get the out-of-range buffer offset, i.e. zeros) with the 16-byte chunk
+//     swizzle of conv_kernel (chunk ^ (row & 7)); the tap shift is only an address offset of the
+//     per-lane fragment reads (ds_read_b128 takes per-lane addresses).
+//   * K-steps run chunk-major, tap-minor: only B (BN weight rows of one tap and chunk) goes through
+//     the BST-deep ring per step; the image of chunk c + 1 is staged with B of its first tap, into
+//     the other of IMGB image buffers (IMGB = 1 when Cin = 64: one chunk).
+// Why: conv_kernel re-stages the A tile for each of the 9 taps -- 9x the bytes through the LDS-DMA
+// path; at 56 x 56 (64 -> 64) its K-step is 512 MFMA cycles per SIMD against 40 KB of staging, and
+// the kernel ran at 23 % MFMA busy (profiles/r6_conv3x3_rows.md).  Here the staged bytes per tile
+// fall from 9 (BM + BN) to about 1.1 BM + 9 BN rows per chunk.
+// The epilogue and the statistics flush are conv_kernel's (conv_store_tile / conv_stats_flush).
+template <int WM, int WN, int BST, int EPI, int TM, int TN, int IMG, int IMGB, bool PERSIST>
+__global__ __launch_bounds__(64 * WM * WN) void conv_rows_kernel(const uint16_t *__restrict__ x,
+                                                                 const uint16_t *__restrict__ w,
+                                                                 uint16_t *__restrict__ y, Geo g, EpiArgs ea) {
+    constexpr int WTM = 16 * TM, WTN = 16 * TN;
+    constexpr int BM = WTM * WM, BN = WTN * WN, NW = WM * WN, NT = 64 * NW;
+    constexpr int B_BYTES = BN * kRowBytes, IMG_BYTES = IMG * kRowBytes;
+    constexpr int B_INST = BN / 8 / NW;  // LDS-DMA pieces per wave per B stage (8 rows each)
+    constexpr int I_INST = IMG / 8 / NW;  // ... per image
+    static_assert(B_INST >= 1 && B_INST * NW * 8 == BN && I_INST * NW * 8 == IMG, "staging split");
+    constexpr int CROW = BN * 2 + 16;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
+    constexpr int NSUM = (EPI & (kEpiGate | kEpiGeluGrad)) ? 1 : 2;
+    constexpr int RED_BYTES = STATS ? NSUM * (NT / (BN / 8)) * BN * 4 : 0;
+    constexpr int EPI_BYTES = BM * CROW > RED_BYTES ? BM * CROW : RED_BYTES;
+    constexpr int MAIN_BYTES = IMGB * IMG_BYTES + BST * B_BYTES;
+    constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[LDS_BYTES];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nwg = gridDim.x, orig = blockIdx.x;
+    const int q = nwg >> 3, rr = nwg & 7, xcd = orig & 7;
+    const int wg = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (orig >> 3);
+    const int mt_first = wg / g.ntiles, nt = wg - mt_first * g.ntiles;
+    const int n0 = nt * BN;
+    const int mstride = PERSIST ? nwg / g.ntiles : g.mtiles;
+    float s1[8], s2[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            red[grp * BN + cv * 8 + k] = s1[k];
-            if constexpr (NSUM == 2) red[(GROUPS + grp) * BN + cv * 8 + k] = s2[k];
+    for (int k = 0; k < 8; ++k) s1[k] = s2[k] = 0.f;
+    const int Wp = g.W + 2, HWp = (g.H + 2) * Wp;
+    const int csteps = g.C / kBK;  // Cin % 64 == 0 (launcher)
+    const int ksteps = 9 * csteps;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(x), 0, static_cast<int>(kBufOOB), kBufFlags);
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t *>(w), 0, static_cast<int>(kBufOOB), kBufFlags);
+    const int srow = lane >> 3;
+    const int schunk = (lane & 7) ^ srow;  // staged rows start at multiples of 8: row & 7 = srow
+    const int wm = wave / WN, wn = wave % WN;
+    int mt_last = mt_first;
+    for (int mt = mt_first; mt < g.mtiles; mt += mstride) {
+        mt_last = mt;
+        const int m0 = mt * BM;
+        if (mt != mt_first) __syncthreads();
+        auto gidx = [&](int m) {
+            const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
+            return n * HWp + oh * Wp + ow;
+        };
+        const int base = gidx(m0);
+        const int mlast = (m0 + BM < g.M ? m0 + BM : g.M) - 1;
+        const int nslots = gidx(mlast) - base + 2 * Wp + 3;
+        // image staging: element offset of slot s's pixel (this lane's chunk), or -1 (zeros)
+        // (decoded once, then stepped by 8 slots per piece: Wp >= 9, so at most one column wrap;
+        // integer divisions per piece were ~1.5 k VALU instructions per wave and tile)
+        int i_off[I_INST];
+        {
+            const int s0 = wave * I_INST * 8 + srow;
+            int n = (base + s0) / HWp, r = base + s0 - n * HWp;
+            int ihp = r / Wp, iwp = r - ihp * Wp;
+#pragma unroll
+            for (int j = 0; j < I_INST; ++j) {
+                const int s = s0 + j * 8;
+                const bool ok = s < nslots && n < g.N && ihp >= 1 && ihp <= g.H && iwp >= 1 && iwp <= g.W;
+                i_off[j] = ok ? ((n * g.H + ihp - 1) * g.W + iwp - 1) * g.C + schunk * 8 : -1;
+                iwp += 8;
+                if (iwp >= Wp) {
+                    iwp -= Wp;
+                    if (++ihp == g.H + 2) {
+                        ihp = 0;
+                        ++n;
+                    }
+                }
+            }
         }
+        int b_off[B_INST];
+#pragma unroll
+        for (int j = 0; j < B_INST; ++j) b_off[j] = (n0 + (wave * B_INST + j) * 8 + srow) * 9 * g.C + schunk * 8;
+        // fragment rows: slot of tap (0, 0) relative to the image (rows past M read a valid slot)
+        int frel[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int m = m0 + wm * WTM + i * 16 + (lane & 15);
+            frel[i] = gidx(m < g.M ? m : g.M - 1) - base;
+        }
+        auto stage = [&](int ks) {
+            const int cc = ks / 9, tap = ks - cc * 9;
+            if (tap == 0) {
+                uint8_t *ib = lds + (IMGB == 1 ? 0 : (cc & 1)) * IMG_BYTES;
+#pragma unroll
+                for (int j = 0; j < I_INST; ++j) {
+                    const uint32_t vo = i_off[j] >= 0 ? static_cast<uint32_t>(i_off[j] + cc * kBK) * 2u : kBufOOB;
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(ib + (wave * I_INST + j) * 1024), 16, vo, 0,
+                                                             0, 0);
+                }
+            }
+            uint8_t *bb = lds + IMGB * IMG_BYTES + (ks % BST) * B_BYTES;
+#pragma unroll
+            for (int j = 0; j < B_INST; ++j) {
+                const uint32_t vo = static_cast<uint32_t>(b_off[j] + tap * g.C + cc * kBK) * 2u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, lds_ptr(bb + (wave * B_INST + j) * 1024), 16, vo, 0, 0,
+                                                         0);
+            }
+        };
+        f32x4 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        auto mfma_block = [&](const bf16x8 (&af)[TM], const bf16x8 (&bfr)[TN]) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        };
+#pragma unroll
+        for (int p = 0; p < BST - 1; ++p)
+            if (p < ksteps) stage(p);
+        for (int ks = 0; ks < ksteps; ++ks) {
+            // B of step ks (and every older load: its chunk's image) landed
+            if (ks + BST - 1 <= ksteps) wait_vmcnt<B_INST * (BST - 2)>();
+            else wait_vmcnt<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            const int cc = ks / 9, tap = ks - cc * 9;
+            const int kh = tap / 3, kw = tap - kh * 3;
+            const int toff = kh * Wp + kw;
+            const uint8_t *ib = lds + (IMGB == 1 ? 0 : (cc & 1)) * IMG_BYTES;
+            const uint8_t *bb = lds + IMGB * IMG_BYTES + (ks % BST) * B_BYTES;
+            bf16x8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int sl = frel[i] + toff;
+                af0[i] = *reinterpret_cast<const bf16x8 *>(ib + img_off(sl, lane >> 4));
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int rb = wn * WTN + j * 16 + (lane & 15);
+                bf0[j] = *reinterpret_cast<const bf16x8 *>(bb + img_off(rb, lane >> 4));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int sl = frel[i] + toff;
+                af1[i] = *reinterpret_cast<const bf16x8 *>(ib + img_off(sl, 4 + (lane >> 4)));
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int rb = wn * WTN + j * 16 + (lane & 15);
+                bf1[j] = *reinterpret_cast<const bf16x8 *>(bb + img_off(rb, 4 + (lane >> 4)));
+            }
+            mfma_block(af0, bf0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + BST - 1 < ksteps) stage(ks + BST - 1);  // into the slot read in step ks - 1
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_block(af1, bf1);
+        }
+        wait_vmcnt<0>();
         __syncthreads();
-        for (int col = tid; col < BN; col += NT) {
-            double t1 = 0, t2 = 0;
-#pragma unroll 4
-            for (int p = 0; p < GROUPS; ++p) {
-                t1 += red[p * BN + col];
-                if constexpr (NSUM == 2) t2 += red[(GROUPS + p) * BN + col];
-            }
-            double *sl = ea.stats + ((mt_last + wg) % kStatSlots) * 2 * g.K;  // spread atomics over slots
-            if (n0 + col < g.K) {
-                atomicAdd(sl + n0 + col, t1);
-                if constexpr (NSUM == 2) atomicAdd(sl + g.K + n0 + col, t2);
-            }
+        conv_store_tile<WM, WN, TM, TN, EPI>(acc, lds, y, g, ea, m0, n0, tid, s1, s2);
+    }  // m-tile loop
+    if constexpr (STATS)
+        conv_stats_flush<WM, WN, TM, TN, EPI, LDS_BYTES>(lds, g, ea, n0, tid, s1, s2, mt_last + wg, nwg, orig);
+}
+
+// Largest image (padded-index range) any BM-pixel tile of this stride-1 3x3 geometry reads.
+inline int conv_rows_slots(const Geo &g, int BM) {
+    const int Wp = g.W + 2, HWp = (g.H + 2) * Wp;
+    auto gidx = [&](int m) {
+        const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
+        return n * HWp + oh * Wp + ow;
+    };
+    // the range depends on the tile only through m0 mod (OH * OW): one period of tile positions
+    const int per_img = g.OH * g.OW;
+    int a = per_img, b = BM;
+    while (b) {
+        const int t = a % b;
+        a = b;
+        b = t;
+    }
+    const int64_t period = static_cast<int64_t>(per_img / a) * BM;  // lcm(per_img, BM) pixels
+    int worst = 0;
+    for (int m0 = 0; m0 < g.M && m0 < period; m0 += BM) {
+        const int ml = (m0 + BM < g.M ? m0 + BM : g.M) - 1;
+        const int s = gidx(ml) - gidx(m0) + 2 * Wp + 3;
+        worst = s > worst ? s : worst;
+    }
+    return worst;
+}
+
+template <int WM, int WN, int BST, int EPI, int TM, int TN, int IMG, int IMGB>
+void launch_rows_epi(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, hipStream_t s) {
+    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
+    g.mtiles = (g.M + BM - 1) / BM;
+    g.ntiles = g.K / BN;
+    constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate)) != 0;
+    if constexpr (STATS) {
+        constexpr int LDS = IMGB * IMG * 128 + BST * BN * 128;
+        constexpr int OCC = (160 * 1024) / LDS < 4 ? (160 * 1024) / LDS : 4;
+        const int per_n = 256 * (OCC < 1 ? 1 : OCC) / g.ntiles;
+        if (per_n >= 1 && g.mtiles > 2 * per_n) {
+            conv_rows_kernel<WM, WN, BST, EPI, TM, TN, IMG, IMGB, true><<<per_n * g.ntiles, 64 * WM * WN, 0, s>>>(
+                x, w, y, g, ea);
+            return;
         }
-        if constexpr (NSUM == 2) {
-            if (ea.fin != nullptr)
-                bn_finalize_last(ea.fin, ea.stats, g.K, nwg, orig, tid, NT, reinterpret_cast<double *>(lds),
-                                 LDS_BYTES / 8 - 2);
-        }
+    }
+    if (ea.fin) {
+        EpiArgs e2 = ea;
+        e2.fin = nullptr;
+        conv_rows_kernel<WM, WN, BST, EPI, TM, TN, IMG, IMGB, false><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+            x, w, y, g, e2);
+        bn_fin_desc_kernel<<<(g.K + 255) / 256, 256, 0, s>>>(ea.fin, ea.stats, g.K);
+        return;
+    }
+    conv_rows_kernel<WM, WN, BST, EPI, TM, TN, IMG, IMGB, false><<<g.mtiles * g.ntiles, 64 * WM * WN, 0, s>>>(
+        x, w, y, g, ea);
+}
+
+// The epilogues of a stride-1 3x3 conv in ResNet / VGG (forward statistics, BN-backward sums with
+// the coefficients or the ReLU bits, accumulate, plain); false = not on this kernel.
+template <int WM, int WN, int BST, int TM, int TN, int IMG, int IMGB>
+bool launch_rows_variant(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const EpiArgs &ea, int epi,
+                         hipStream_t s) {
+    constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
+    if (g.K % BN || g.C % kBK || (IMGB == 1 && g.C != kBK) || g.W < 7 || conv_rows_slots(g, BM) > IMG) return false;
+    switch (epi) {
+    case 0: launch_rows_epi<WM, WN, BST, 0, TM, TN, IMG, IMGB>(x, w, y, g, ea, s); return true;
+    case kEpiFwdStats: launch_rows_epi<WM, WN, BST, kEpiFwdStats, TM, TN, IMG, IMGB>(x, w, y, g, ea, s); return true;
+    case kEpiBwdCoef: launch_rows_epi<WM, WN, BST, kEpiBwdCoef, TM, TN, IMG, IMGB>(x, w, y, g, ea, s); return true;
+    case kEpiBwdBits: launch_rows_epi<WM, WN, BST, kEpiBwdBits, TM, TN, IMG, IMGB>(x, w, y, g, ea, s); return true;
+    default: return false;
     }
 }
 
