@@ -71,6 +71,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 __device__ __forceinline__ int wm_of(int wave, int wn) { return wave / wn; }
 
+
 __device__ __forceinline__ void unpack_bf16x8(const uint4 &v, float (&f)[8]) {
     const uint32_t *u = reinterpret_cast<const uint32_t *>(&v);
 #pragma unroll
@@ -251,15 +252,19 @@ __device__ __forceinline__ void conv_store_tile(const f32x4 (&acc)[TM][TN], uint
         for (int j = 0; j < TN; ++j) {
             const int row = wm * WTM + i * 16 + (lane & 15);
             const int col = wn * WTN + j * 16 + (lane >> 4) * 4;
-            uint32_t h[4];
+            float v4[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 float v = acc[i][j][r];
                 if constexpr (BIAS) v += bcol[j][r];
                 if constexpr ((EPI & kEpiBiasRelu) != 0) v = !(v <= 0.f) ? v : 0.f;  // NaN stays NaN (torch.relu)
-                h[r] = f32_to_bf16(v);
+                v4[r] = v;
             }
-            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+            // (integer rounding: v_cvt_pk_bf16_f32 here measured ResNet-50 20.24 -> 20.72 ms/step, the 56 x 56
+            // 3x3 conv 99 -> 163 us, r6t25 / profiles/r6_conv3x3_rows.md)
+            *reinterpret_cast<uint2 *>(lds + row * CROW + col * 2) =
+                make_uint2(f32_to_bf16(v4[0]) | (static_cast<uint32_t>(f32_to_bf16(v4[1])) << 16),
+                           f32_to_bf16(v4[2]) | (static_cast<uint32_t>(f32_to_bf16(v4[3])) << 16));
         }
     __syncthreads();
     // Store loop: thread -> 16-byte vectors (row, cv) with a FIXED 8-channel group cv (NT is a
