@@ -359,7 +359,9 @@ def main():
         base = torch.optim.SGD(model.parameters(), lr=a.lr, momentum=0.9, weight_decay=1e-4)
         opt_desc = "SGD momentum=0.9 wd=1e-4"
     if a.comm_dtype == "auto":
-        a.comm_dtype = "bf16" if cuda and (size > 1 or a.emulate_comm) else "f32"
+        # elastic: every rank must pick the same wire dtype whatever the size it started at (a rank
+        # that joins at 2 and one that started alone would otherwise reduce bf16 against f32 and hang)
+        a.comm_dtype = "bf16" if cuda and (size > 1 or a.emulate_comm or a.elastic) else "f32"
     comm_dtype = torch.bfloat16 if a.comm_dtype == "bf16" else None
     if a.optimizer == "ssgd":
         opt = kf.optimizers.SynchronousSGDOptimizer(base, named_parameters=model.named_parameters(),

@@ -115,6 +115,13 @@ int conv_tile_rules() {
     return v;
 }
 
+// KUNGFU_CONV_T224 (dev knob, default 1): 224x256 tiles for one- or two-round grids of 256x256 tiles
+// (launch_ks); 0 = always 256x256
+int conv_t224() {
+    static const int v = dev_knob("KUNGFU_CONV_T224", 1);
+    return v;
+}
+
 // Staggered staging issue in the 8-wave tiles: the two waves sharing a SIMD issue their LDS-DMA
 // pieces in different phases of the K-step (one before its fragment reads, one between its MFMA
 // clusters) instead of stalling on staging issue together.  ResNet-50 +0.8 % (21.43-21.49 ->

@@ -56,6 +56,7 @@ struct Geo {
 const void *zero_page();
 void check_buf_extent(const Geo &g);
 int conv_tile_rules();
+int conv_t224();
 int conv_stagger();
 int conv_prio();
 // the square-window launchers (conv_k1.hip / conv_k3.hip): tile variant < 0 = the per-shape default
@@ -279,7 +280,9 @@ __device__ __forceinline__ void conv_store_tile(const f32x4 (&acc)[TM][TN], uint
     // every row's epilogue reads behind the prologue staging instead -- operands in registers when
     // the K loop ends -- took the 4-wave tiles to one wave per SIMD and spilled the 8-wave ones:
     // ResNet-50 20.40 -> 21.45 ms/step, profiles/r6_conv_pmc.md.)
-    constexpr int U = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
+    constexpr int U0 = !(LD_OLD || LD_BX) ? 1 : ((EPI & kEpiBwdCoef) && TM * TN >= 32) ? 2 : (ITER >= 4 ? 4 : ITER);
+    constexpr int U = ITER % U0 == 0 ? U0 : (ITER % 2 == 0 ? 2 : 1);  // whole groups (ITER = 14 on the 224-row tile)
+    static_assert(ITER % U == 0, "whole row groups");
     const bool col_ok = n0 + cv * 8 < g.K;  // this thread's 8 channels exist (Cout % BN != 0)
     float sc[8], sh[8];  // bwd coef: the forward BN's [scale; shift] of this thread's 8 channels
     if constexpr ((EPI & kEpiBwdCoef) != 0) {
@@ -502,10 +505,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     constexpr int TAPS = KH * KW;
     constexpr int A_BYTES = BM * kRowBytes, B_BYTES = BN * kRowBytes;
     constexpr int STAGE = A_BYTES + B_BYTES;
-    constexpr int A_INST = BM / 8 / NW;  // glds instructions per wave per A tile (8 rows each)
+    // A pieces (8 rows each): A_INST per wave; when BM / 8 is not a multiple of the wave count (the
+    // 224-row tile) the pieces interleave over the waves (piece j * NW + wave) and the last round is
+    // partial -- per-wave load counts then differ, so only the 2-stage ring (vmcnt(0) waits) allows it
+    constexpr int A_PIECES = BM / 8;
+    constexpr int A_INST = (A_PIECES + NW - 1) / NW;  // glds instructions per wave per A tile (at most)
+    constexpr bool A_EVEN = A_INST * NW == A_PIECES;
     constexpr int B_INST = BN / 8 / NW;
     constexpr int LOADS = A_INST + B_INST;
-    static_assert(A_INST >= 1 && B_INST >= 1 && A_INST * NW * 8 == BM && B_INST * NW * 8 == BN, "tile split");
+    static_assert(A_INST >= 1 && B_INST >= 1 && A_PIECES * 8 == BM && B_INST * NW * 8 == BN, "tile split");
+    static_assert(A_EVEN || STAGES == 2, "uneven A split needs the 2-stage ring");
     constexpr int CROW = BN * 2 + 16;  // padded bytes per C row of the epilogue tile
     constexpr bool STATS = (EPI & (kEpiFwdStats | kEpiBwdCoef | kEpiBwdBits | kEpiGate | kEpiGeluGrad)) != 0;
     constexpr bool GATE = (EPI & kEpiGate) != 0;
@@ -554,11 +563,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
     uint32_t a_ok[A_INST];
 #pragma unroll
     for (int j = 0; j < A_INST; ++j) {
-        const int r = (wave * A_INST + j) * 8 + srow;
+        const int piece = A_EVEN ? wave * A_INST + j : j * NW + wave;
+        const int r = piece * 8 + srow;
         const int m = m0 + r;
         a_off[j] = 0;
         a_ok[j] = 0;
-        if (m < g.M) {
+        if (m < g.M && piece < A_PIECES) {
             const int ow = m % g.OW, t = m / g.OW, oh = t % g.OH, n = t / g.OH;
             const int ih0 = oh * g.stride - g.ph, iw0 = ow * g.stride - g.pw;
             a_off[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + schunk * 8;
@@ -605,14 +615,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_kernel(const uint16_t *__re
         uint8_t *bbase = abase + A_BYTES;
 #pragma unroll
         for (int j = 0; j < A_INST; ++j) {
+            const int piece = A_EVEN ? wave * A_INST + j : j * NW + wave;
+            if (!A_EVEN && piece >= A_PIECES) break;  // wave-uniform
             const bool ok = ((a_ok[j] >> tap) & 1u) && cin_ok;
 #if KUNGFU_CONV_BUFLD
             const uint32_t vo = ok ? static_cast<uint32_t>(a_off[j] + toff) * 2u : kBufOOB;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(abase + (wave * A_INST + j) * 1024), 16, vo, 0, 0,
-                                                     0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, lds_ptr(abase + piece * 1024), 16, vo, 0, 0, 0);
 #else
             const uint16_t *src = ok ? x + static_cast<uint32_t>(a_off[j] + toff) : zero;
-            __builtin_amdgcn_global_load_lds(src, abase + (wave * A_INST + j) * 1024, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(src, abase + piece * 1024, 16, 0, 0);
 #endif
         }
 #pragma unroll
@@ -1062,6 +1073,13 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
             // 512 outputs that are not on 256x256 tiles (128->128@28 101 -> 88, 512->512@7 76 -> 71)
             if ((epi & kEpiAccum) != 0 || (KS == 3 && g.stride == 1 && variant != 7)) variant = 0;
         }
+        if (variant == 7 && g.M % 224 == 0 && conv_t224()) {
+            // a one- or two-round grid of 256x256 tiles: 224x256 tiles when their rounds cost >= 5 %
+            // less (ResNet-50's 14 x 14 layers, M = 50,176: 196 tiles leave 60 of 256 CUs idle, 224
+            // tiles of 7/8 the work fill 224 of them)
+            const int64_t t7 = ((static_cast<int64_t>(g.M) + 255) / 256) * (g.K / 256), t8 = (g.M / 224) * (g.K / 256);
+            if (t7 <= 512 && ((t8 + 255) / 256) * 224 < 0.95 * ((t7 + 255) / 256) * 256) variant = 8;
+        }
     }
     // the per-shape defaults only (round 6: the tuning-only tiles -- 256x64 3-stage, 512x64, 128x64,
     // 256x256 of 128x64 waves, the 2- and 4-wave 64x128 -- never won a default, see
@@ -1074,8 +1092,10 @@ void launch_ks(const uint16_t *x, const uint16_t *w, uint16_t *y, Geo g, const E
     case 2: launch_variant<KS, 4, 1, 2>(x, w, y, g, ea, epi, s); break;                          // 256x64
     case 7: if (g.K % 256) throw std::invalid_argument("conv variant 7: Cout % 256");
             launch_variant<KS, 4, 2, 2, 4, 8>(x, w, y, g, ea, epi, s); break;                  // 256x256, 8w, 64x128
+    case 8: if (g.K % 256) throw std::invalid_argument("conv variant 8: Cout % 256");
+            launch_variant<KS, 2, 4, 2, 7, 4>(x, w, y, g, ea, epi, s); break;                  // 224x256, 8w, 112x64
     case 11: launch_variant<KS, 4, 1, 2, 4, 2>(x, w, y, g, ea, epi, s); break;                // 256x32 (Cout <= 32)
-    default: throw std::invalid_argument("conv: tile variant must be -1, 0, 1, 2, 7 or 11");
+    default: throw std::invalid_argument("conv: tile variant must be -1, 0, 1, 2, 7, 8 or 11");
     }
 }
 
