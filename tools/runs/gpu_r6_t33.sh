@@ -1,0 +1,14 @@
+#!/bin/bash
+# r6 t33: unlinked bias gradients beside the weight gradient on the side stream: BERT tests, then the BERT bench A/B
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
+true; rc=0
+true
+show() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2],d['ms_per_step'],d['value'],d['config']['final_loss'])" $1 $2; }
+for r in 1 2 3; do
+  timeout -k 10 300 python tools/bench_switch.py kungfu_amd.ops.linear:_BIAS_SIDE=False -- --model bert_base --optimizer gns --steps 30 --warmup 8 --comm-probe 0 > $O/r6t33_main_$r.log 2>&1 || { tail -5 $O/r6t33_main_$r.log; exit 1; }
+  show $O/r6t33_main_$r.log bias_main
+  timeout -k 10 300 python bench.py --model bert_base --optimizer gns --steps 30 --warmup 8 --comm-probe 0 > $O/r6t33_side_$r.log 2>&1 || { tail -5 $O/r6t33_side_$r.log; exit 1; }
+  show $O/r6t33_side_$r.log bias_side
+done
