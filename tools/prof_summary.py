@@ -22,7 +22,7 @@ CATEGORIES = [
     ("BN finalize (ours)", r"kfk::.*(bn_sums_finalize|bn_bwd_finalize|bn_stats_finalize|bn_eval_coef|stem_bwd_finalize)"),
     ("fused BN (ours)", r"kfk::.*bn_"),
     ("conv MFMA 1x1 (ours)", r"kfk::.*conv_kernel<1,"),
-    ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,"),
+    ("conv MFMA 3x3 (ours)", r"kfk::.*conv3x3|kfk::.*conv_kernel<3,|kfk::.*conv_rows_kernel"),
     ("conv MFMA rect KHxKW (ours)", r"kfk::.*conv_kernel<1\d\d,"),
     ("conv MFMA stride-2 dgrad phases (ours)", r"kfk::.*conv_kernel<\d\d,"),
     ("conv weight flip (ours)", r"kfk::.*conv_flip"),
