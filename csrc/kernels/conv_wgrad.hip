@@ -967,9 +967,19 @@ constexpr RowsEx kRowsEx[] = {{32, 2}, {32, 3}, {32, 4}, {64, 3}, {64, 4}};
 bool rows_supported(int Cin, int Cout, int ks, int stride) {
     return ks == 3 && stride == 1 && Cin % 64 == 0 && Cout % 64 == 0;
 }
-// default for the narrow channel counts (tools/bench_wgrad.py): wide tiles keep the tap-tiled kernel
-bool rows_default(int Cin, int Cout, int ks, int stride) {
-    return rows_supported(Cin, Cout, ks, stride) && Cin <= 128 && Cout <= 128;
+// KUNGFU_WGRAD_PLAN (dev knob): 2 (default) = the round-6 plan rules below, 1 = the round-5 ones
+int wgrad_plan_rules() {
+    static const int v = dev_knob("KUNGFU_WGRAD_PLAN", 2);
+    return v;
+}
+
+// default for the narrow channel counts (tools/bench_wgrad.py), and (round 6) for every channel
+// count on maps of at most 200,704 output pixels: ResNet-50's 14 x 14 256->256 and 7 x 7 512->512
+// measured 113 -> 93 us on it (r6t36, profiles/r6_wgrad_plan.md); wide tiles on larger maps (VGG-16's
+// 56 x 56 and up) keep the tap-tiled kernel
+bool rows_default(int Cin, int Cout, int ks, int stride, int64_t P) {
+    if (!rows_supported(Cin, Cout, ks, stride)) return false;
+    return (Cin <= 128 && Cout <= 128) || (wgrad_plan_rules() >= 2 && P <= 200704);
 }
 
 RGeo rows_segments(int N, int H, int W, int Cin, int Cout) {
@@ -1094,13 +1104,16 @@ bool conv_wgrad_supported(int Cin, int Cout, int ks, int stride) {
 WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int stride, int variant, int splits) {
     WgradPlan pl;
     const int64_t work = static_cast<int64_t>(Cin) * Cout * ks * ks;
-    if (variant < 0 && rows_default(Cin, Cout, ks, stride)) variant = kRowsVariant;
+    if (variant < 0 && rows_default(Cin, Cout, ks, stride, static_cast<int64_t>(N) * H * W)) variant = kRowsVariant;
     if (variant == kRowsVariant) {
         if (!rows_supported(Cin, Cout, ks, stride)) throw std::invalid_argument("conv_wgrad: rows variant needs 3x3/s1");
         pl.variant = variant;
         const RGeo rg = rows_segments(N, H, W, Cin, Cout);
         const int ct = rg.mtiles * rg.ntiles;
-        if (splits < 0) splits = std::max(1, (512 + ct / 2) / ct);  // 2 workgroups of 9 waves per CU
+        // one workgroup of 9 waves per CU (round 6; two per CU through round 5): half the split
+        // partials to reduce -- 56 x 56 64->64 119 -> 89 us, 28 x 28 128->128 108 -> 84 (r6t36)
+        const int per = wgrad_plan_rules() >= 2 ? 256 : 512;
+        if (splits < 0) splits = std::max(1, (per + ct / 2) / ct);
         splits = std::max(1, std::min(splits, std::max(1, rg.nseg / 4)));
         pl.kps = (rg.nseg + splits - 1) / splits;
         pl.splits = (rg.nseg + pl.kps - 1) / pl.kps;
@@ -1113,9 +1126,15 @@ WgradPlan conv_wgrad_plan(int N, int H, int W, int Cin, int Cout, int ks, int st
         // tools/bench_wgrad_1x1.py: 256x256 for the large long-K linear-layer products (BERT-base
         // 768x3072 at 16 K tokens: 133 -> 87 us); ResNet's 1x1 shapes keep 256x128 (their split-K
         // partials of 256x256 tiles cost more than the extra MFMA density saves)
-        if (Cout % 256 == 0 && Cin % 256 == 0 && work >= 1500000 && ks == 1) variant = 7;
+        const int64_t P1 = static_cast<int64_t>(N) * ((H + 2 * ((ks - 1) / 2) - ks) / stride + 1) *
+                           ((W + 2 * ((ks - 1) / 2) - ks) / stride + 1);
+        // (round 6: and the wide 1x1 products on >= 200,704 output pixels -- 28 x 28 512->256 103 -> 77 us,
+        // 56 x 56 256->512 / s2 103 -> 90; ResNet-50 20.09-20.13 -> 20.07 ms/step, r6t36 / r6t37)
+        if (Cout % 256 == 0 && Cin % 256 == 0 && ks == 1 && (work >= 1500000 || (wgrad_plan_rules() >= 2 && P1 >= 200704)))
+            variant = 7;
         else if (Cout % 256 == 0 && Cin % 128 == 0) variant = 4;
-        else if (Cout % 128 == 0 && Cin % 256 == 0 && work >= 131072) variant = 5;
+        else if (Cout % 128 == 0 && Cin % 256 == 0 && work >= (wgrad_plan_rules() >= 2 ? 32768 : 131072)) variant = 5;
+        // (round 6: 128x256 from 32 K outputs -- 56 x 56 256->128 158 -> 111 us, 28 x 28 512->128 73 -> 60, r6t36)
         else if (Cout % 128 == 0 && Cin % 128 == 0) variant = 0;
         else if (Cout % 128 == 0) variant = 1;
         else if (Cin % 128 == 0) variant = 2;

@@ -113,6 +113,7 @@ KNOBS: Dict[str, Knob] = {
     "KUNGFU_SELF_IP": _l("this worker's IP (single mode)"),
     # -- dev A/B knobs (need KUNGFU_DEV_KNOBS=1) ----------------------------------------------
     "KUNGFU_CONV_TILE_RULES": _d("2", "1 = the round-2 conv tile defaults"),
+    "KUNGFU_WGRAD_PLAN": _d("2", "1: the round-5 weight-gradient plan rules (tile variant, row-image kernel, split counts)"),
     "KUNGFU_CONV_T224": _d("1", "0: no 224x256 conv tiles (one- or two-round grids of 256x256 tiles keep them)"),
     "KUNGFU_CONV_ROWS": _d("1", "0: stride-1 3x3 convs with Cin = Cout = 64 on the tap-wise kernel, not the row-image one"),
     "KUNGFU_VGG_FUSED": _d("1", "VGG-16 conv/ReLU/pool stack as one autograd node (0: the per-layer modules)"),
