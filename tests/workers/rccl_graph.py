@@ -99,7 +99,11 @@ for phase in phases:
         body(phase)
     torch.cuda.synchronize()
     g = track(torch.cuda.CUDAGraph())
-    with torch.cuda.graph(g, stream=cap):
+    # relaxed, as GraphedStep's segment captures: in the default "global" mode a HIP call from any
+    # other thread during the capture (the native RCCL watchdog's hipEventQuery on earlier
+    # collectives) invalidates it -- phase two failed that way in a suite run (r6s2c); "thread_local"
+    # fails inside RCCL's own enqueue (r6t41)
+    with torch.cuda.graph(g, stream=cap, capture_error_mode="relaxed"):
         body(phase)
     print("RCCL_GRAPH phase %s captured rank=%d" % (phase, r), flush=True)
     for i in range(3):

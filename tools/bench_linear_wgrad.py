@@ -1,9 +1,15 @@
 """BERT-base linear weight gradients at 16 K tokens: dW[out, in] = dy^T . x accumulated into an f32
 slot (what the engine's direct path does, ops/linear.py) -- ours (split-K MFMA + reduce into the slot)
 vs hipBLASLt (torch.mm with out_dtype=float32, or bf16 mm + f32 add)."""
+import os
+import sys
+
 import torch
 
-from kungfu_amd._lib import hip
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kungfu_amd._lib import hip  # noqa: E402
+
+SWEEP = "--sweep" in sys.argv  # every tile variant x split count of the split-K kernel
 
 
 def _as_nhwc(t2):
@@ -56,7 +62,28 @@ def main():
                 tot[lab] = tot.get(lab, 0.0) + us * (12 if name != "out" else 12)
             except Exception as e:  # noqa: BLE001
                 row.append("%s ERR %s" % (lab, str(e)[:80]))
-        print("  ".join(row), flush=True)
+        if SWEEP:
+            res = []
+            for v in range(hip().conv_wgrad_variants()):
+                seen = set()
+                for sp in (4, 8, 16, 32, 64, 128, 256):
+                    try:
+                        sp2 = hip().conv_wgrad_plan(1, 1, T, fin, fout, 1, 1, v, sp)[1]
+                    except Exception:  # noqa: BLE001
+                        break
+                    if sp2 in seen:
+                        continue
+                    seen.add(sp2)
+
+                    def f(v=v, sp2=sp2):
+                        slot.zero_()
+                        hip().conv_wgrad(_as_nhwc(dy), _as_nhwc(x), 1, 1,
+                                         out=slot.as_strided((fout, fin, 1, 1), (fin, 1, fin, fin)),
+                                         accumulate=True, atomics=False, variant=v, splits=sp2)
+                    res.append((timeit(f, n=10), v, sp2))
+            res.sort()
+            print("   plan %s | best: %s" % (hip().conv_wgrad_plan(1, 1, T, fin, fout, 1, 1),
+                                             " ".join("v%d/s%d %.1f" % (v, sp, t) for t, v, sp in res[:5])), flush=True)
     print("per step (x12 layers):", {k: round(v, 1) for k, v in tot.items()})
 
 
