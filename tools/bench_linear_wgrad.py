@@ -62,6 +62,7 @@ def main():
                 tot[lab] = tot.get(lab, 0.0) + us * (12 if name != "out" else 12)
             except Exception as e:  # noqa: BLE001
                 row.append("%s ERR %s" % (lab, str(e)[:80]))
+        print("  ".join(row), flush=True)
         if SWEEP:
             res = []
             for v in range(hip().conv_wgrad_variants()):
