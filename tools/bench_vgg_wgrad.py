@@ -39,7 +39,7 @@ for Hh, C, K in SHAPES:
     flop = 2.0 * N * Hh * Hh * K * C * 9
     res = ["default:%.0fus/%.0fTF" % ((lambda us: (us, flop / us / 1e6))(timeit(lambda: H_.conv_wgrad(dy, x, 3, 1))))]
     for v in range(H_.conv_wgrad_variants()):
-        for sp in (-1, 64, 128, 256, 512):
+        for sp in (-1, 16, 32, 64, 128, 256, 512):
             try:
                 us = timeit(lambda: H_.conv_wgrad(dy, x, 3, 1, variant=v, splits=sp))
             except Exception:  # noqa: BLE001
