@@ -973,13 +973,12 @@ int wgrad_plan_rules() {
     return v;
 }
 
-// default for the narrow channel counts (tools/bench_wgrad.py), and (round 6) for every channel
-// count on maps of at most 200,704 output pixels: ResNet-50's 14 x 14 256->256 and 7 x 7 512->512
-// measured 113 -> 93 us on it (r6t36, profiles/r6_wgrad_plan.md); wide tiles on larger maps (VGG-16's
-// 56 x 56 and up) keep the tap-tiled kernel
-bool rows_default(int Cin, int Cout, int ks, int stride, int64_t P) {
+// default for the narrow channel counts (tools/bench_wgrad.py), and (round 6) for every stride-1 3x3:
+// ResNet-50's 14 x 14 256->256 and 7 x 7 512->512 measured 113 -> 93 us on it (r6t36), VGG-16's
+// 56 x 56 128->256 / 256->256 673 -> 766 / 688 -> 788 TF/s (r6t43, profiles/r6_wgrad_plan.md)
+bool rows_default(int Cin, int Cout, int ks, int stride, int64_t /*P*/) {
     if (!rows_supported(Cin, Cout, ks, stride)) return false;
-    return (Cin <= 128 && Cout <= 128) || (wgrad_plan_rules() >= 2 && P <= 200704);
+    return (Cin <= 128 && Cout <= 128) || wgrad_plan_rules() >= 2;
 }
 
 RGeo rows_segments(int N, int H, int W, int Cin, int Cout) {
