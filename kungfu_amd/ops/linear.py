@@ -87,7 +87,6 @@ _DIRECT_WGRAD = True  # module switch (tests)
 # direct weight gradients on the side stream (module switch): BERT-base + GNS 16.57-16.61 -> 16.45 ms/step
 # on one box, two interleaved rounds (r5t30); the conv weight gradients measured the other way (mixed.SideStream)
 _WGRAD_SIDE = True
-_BIAS_SIDE = True  # module switch (tests / A/B): unlinked bias gradients beside the weight gradient
 # set_gemm_enabled(True): forward (x W^T + b) and data gradient (dy W, with W^T from the flat space's
 # per-step multi-tensor transpose) on gemm.hip's pipelined NT GEMM instead of hipBLASLt -- measured
 # slower (profiles/r4_gemm_nt.md), so off and not an environment knob any more (round 5)
@@ -122,10 +121,9 @@ def _gelu_gemm_ok(M: int, in_f: int, out_f: int) -> bool:
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, target=None, rlink=None, glink=None, btarget=None):
+    def forward(ctx, x, w, b, target=None, rlink=None, glink=None):
         ctx.save_for_backward(x, w)
         ctx.target = target
-        ctx.btarget = btarget
         ctx.rlink = rlink
         ctx.glink = ctx.wt_g = None
         if glink is not None and target is not None and rlink is None:
@@ -193,11 +191,6 @@ class _LinearFn(torch.autograd.Function):
             else:
                 dx = torch.mm(dy2, w).view(x.shape)
         tgt = ctx.target
-        bl = ctx.blink
-        linked_db = bl is not None and bl.value is not None and bl.ptr == dy2.data_ptr()
-        bt = ctx.btarget
-        side_db = (bt is not None and not linked_db and ctx.has_b and ctx.needs_input_grad[2] and _BIAS_SIDE
-                   and dy2.dtype == torch.bfloat16 and hasattr(bt[0].sink, "put_direct"))
         if ctx.needs_input_grad[1] and tgt is not None and _DIRECT_WGRAD and hasattr(tgt[0].sink, "put_direct"):
             # the split-K partials are reduced straight into the weight's flat f32 gradient slot
             # (deterministic, accumulating): no bf16 weight gradient, no landing pass
@@ -208,11 +201,6 @@ class _LinearFn(torch.autograd.Function):
                 hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1,
                                  out=gv.as_strided((out_f, in_f, 1, 1), (in_f, 1, in_f, in_f)),
                                  accumulate=True, atomics=False)  # deterministic partials + reduce (atomics: -3 %, r4t29)
-                if side_db:
-                    # the bias gradient (column sums of dy) beside the weight gradient, straight into
-                    # the bias's flat f32 slot: off the critical path (r6t33: QKV's two-stage column
-                    # sum waited 60 us per layer for CUs held by these weight gradients)
-                    bt[0].grad_view(bt[1]).add_(hip().colsum(dy2, torch.float32))
 
             if _WGRAD_SIDE and dy2.is_cuda and not torch.cuda.is_current_stream_capturing():
                 # on the side stream: the split-K kernel and its (memory-bound) reduce overlap the next
@@ -233,15 +221,10 @@ class _LinearFn(torch.autograd.Function):
             else:
                 wg()
             space.sink.put_direct(i)
-            if side_db:
-                bt[0].sink.put_direct(bt[1])
-        else:
-            side_db = False
-            if ctx.needs_input_grad[1]:
-                dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
-        if side_db:
-            pass  # landed in the flat slot with the weight gradient
-        elif linked_db and ctx.needs_input_grad[2]:
+        elif ctx.needs_input_grad[1]:
+            dw = hip().conv_wgrad(_as_nhwc(dy2), _as_nhwc(x2), 1, 1).view(out_f, in_f)
+        bl = ctx.blink
+        if bl is not None and bl.value is not None and bl.ptr == dy2.data_ptr() and ctx.needs_input_grad[2]:
             db = bl.value  # produced by the consuming LayerNorm's backward pass
             bl.value, bl.ptr = None, 0
         elif ctx.has_b and ctx.needs_input_grad[2]:
@@ -251,7 +234,7 @@ class _LinearFn(torch.autograd.Function):
                 db = hip().colsum(dy2, ctx.b_dtype)
             else:
                 db = dy2.sum(0, dtype=torch.float32).to(ctx.b_dtype)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None
 
 
 def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -263,19 +246,16 @@ def eligible(x: torch.Tensor, w: torch.Tensor) -> bool:
     return hip_available() and hip().conv_wgrad_supported(int(in_f), int(out_f), 1, 1)
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target=None,
-           bias_target=None) -> torch.Tensor:
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor = None, grad_target=None) -> torch.Tensor:
     """``F.linear(x, w, b)`` with the MFMA split-K weight gradient when eligible.  ``grad_target``
     ``(space, index)``: ``w`` is the bf16 shadow of that flat-space parameter -- its gradient is
-    reduced straight into the parameter's f32 gradient slot (``space.sink.put_direct``).
-    ``bias_target``: the same for ``b``; a bias gradient that no consumer hands over (``BiasLink``)
-    is then summed beside the weight gradient and added into its slot there."""
+    reduced straight into the parameter's f32 gradient slot (``space.sink.put_direct``)."""
     if eligible(x, w) and (b is None or b.dtype in (torch.bfloat16, torch.float32)):
         rl = getattr(x, "_kf_rlink", None)
         if rl is not None and (rl.armed or x.dtype != torch.bfloat16):
             rl = None  # one linear consumer per link
         gl = getattr(x, "_kf_glink", None)
-        y = _LinearFn.apply(x, w, b, grad_target, rl, gl, bias_target if grad_target is not None else None)
+        y = _LinearFn.apply(x, w, b, grad_target, rl, gl)
         if y.grad_fn is not None and getattr(y.grad_fn, "blink", None) is not None:
             y._kf_blink = y.grad_fn.blink
         return y

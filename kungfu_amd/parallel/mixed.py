@@ -146,9 +146,8 @@ def _linear_forward(self, x):
     # bf16 shadow weights: the weight gradient takes the split-K MFMA kernel (ops/linear.py), which
     # reduces its splits straight into the weight's flat f32 gradient slot
     w = shadow(self.weight)
-    b = shadow(self.bias) if self.bias is not None else None
-    return linear(x, w, b, grad_target=direct_target(self.weight) if w is not self.weight else None,
-                  bias_target=direct_target(self.bias) if b is not None and b is not self.bias else None)
+    return linear(x, w, shadow(self.bias) if self.bias is not None else None,
+                  grad_target=direct_target(self.weight) if w is not self.weight else None)
 
 
 class SideStream:
