@@ -3,5 +3,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out; mkdir -p $O
-bash tools/gpu_prof.sh r6s2 resnet50 bert_base > $O/r6s2_prof.log 2>&1 || { tail -5 $O/r6s2_prof.log; exit 1; }
-head -20 $O/r6s2_resnet50_summary.md
+bash tools/gpu_prof.sh ${TAG:-r6s2} resnet50 bert_base > $O/${TAG:-r6s2}_prof.log 2>&1 || { tail -5 $O/${TAG:-r6s2}_prof.log; exit 1; }
+head -20 $O/${TAG:-r6s2}_resnet50_summary.md
